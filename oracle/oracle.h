@@ -1,0 +1,98 @@
+/* ORACLE — test infrastructure only (tests/, __graft_entry__.smoke(), bench.py
+ * cpu_baseline).  C ABI of the CPU restatement of the reference BlockSolver /
+ * LinearSolverCSparse / OptimizationAlgorithmLevenberg path.  Never linked into
+ * the product library.  Type and statistics layouts deliberately mirror
+ * include/g2o_hip.h so that tests can feed both the same arrays. */
+#ifndef G2O_ORACLE_H
+#define G2O_ORACLE_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* vertex types */
+#define ORACLE_V_SE3_EXPMAP 1 /* est: tx ty tz qx qy qz qw (world->cam, SE3Quat::toVector order) */
+#define ORACLE_V_XYZ 2        /* est: x y z */
+#define ORACLE_V_SE3_QUAT 3   /* est: x y z qx qy qz qw (toVectorQT) */
+#define ORACLE_V_SE2 4        /* est: x y theta */
+/* edge types */
+#define ORACLE_E_SE3_PROJECT_XYZ 1 /* v0 = point, v1 = camera; meas u v; info 2x2; params fx fy cx cy */
+#define ORACLE_E_SE3_QUAT 2        /* meas x y z qx qy qz qw; info 6x6 */
+#define ORACLE_E_SE2 3             /* meas x y theta; info 3x3 */
+
+typedef struct {
+  int iteration;
+  int numVertices;
+  int numEdges;
+  double chi2;
+  double lambda;
+  double timeResiduals;
+  double timeQuadraticForm;
+  int levenbergIterations;
+  double timeSchurComplement;
+  double timeSymbolicDecomposition;
+  double timeNumericDecomposition;
+  double timeLinearSolution;
+  double timeLinearSolver;
+  double timeUpdate;
+  double timeIteration;
+  long long hessianDimension;
+  long long hessianPoseDimension;
+  long long hessianLandmarkDimension;
+  long long choleskyNNZ;
+} oracle_batch_stats;
+
+typedef struct {
+  int max_trials_after_failure; /* 10 */
+  double user_lambda_init;      /* 0 -> tau * max diag */
+  int threads;                  /* OpenMP threads for assembly / Schur (1 = deterministic) */
+  int use_ref_csparse;          /* 1: cs_amd + cs_chol from oracle/_ref (if loaded); 0: restated */
+  int block_ordering;           /* 1: AMD on block pattern (lm_fixP_L), 0: scalar (lm_var) */
+} oracle_config;
+
+typedef struct OracleGraph OracleGraph;
+
+OracleGraph* oracle_graph_new(void);
+void oracle_graph_free(OracleGraph* g);
+int oracle_add_vertices(OracleGraph* g, int type, int n, const int* ids, const double* est, const int* fixed,
+                        const int* marginalized);
+int oracle_add_edges(OracleGraph* g, int type, int n, const int* v0, const int* v1, const double* meas,
+                     const double* info /* D*D row-major per edge */, const double* params /* or NULL */);
+int oracle_load_g2o(OracleGraph* g, const char* path, int marginalize_xyz);
+int oracle_save_g2o(OracleGraph* g, const char* path);
+int oracle_num_vertices(OracleGraph* g);
+int oracle_num_edges(OracleGraph* g);
+/* estimates in insertion order of the given type; returns count */
+int oracle_get_estimates(OracleGraph* g, int type, double* out, int* ids_out);
+/* minimal state vector (SE3: toVectorMQT / SE3Quat minimal, SE2 x y th, XYZ) concatenated in vertex-id order */
+int oracle_minimal_state(OracleGraph* g, double* out);
+
+int oracle_initialize(OracleGraph* g);
+double oracle_chi2(OracleGraph* g); /* computeActiveErrors + activeRobustChi2 */
+int oracle_optimize(OracleGraph* g, const oracle_config* cfg, int iterations, oracle_batch_stats* stats);
+
+/* Stage export (small problems only): runs buildStructure, computeActiveErrors,
+ * buildSystem, setLambda(lambda), solve at the current state.  Dense outputs:
+ *   b[n], x[n], Hschur[np*np] (full symmetric, or Hpp when no Schur),
+ *   bschur[np]; sizes returned in dims[0]=n, dims[1]=np (pose scalars),
+ *   dims[2]=nl (landmark scalars).  Any output pointer may be NULL. */
+int oracle_stage(OracleGraph* g, const oracle_config* cfg, double lambda, double* b, double* x, double* Hschur,
+                 double* bschur, long long* dims);
+/* Dense Hessian blocks: Hpp[np*np] (full sym), Hll[nl*3] (diag blocks, col-major per landmark),
+ * Hpl[np*nl] dense.  Small problems only. */
+int oracle_hessian_dense(OracleGraph* g, double* Hpp, double* Hll_diag, double* Hpl);
+
+/* Jacobians of one edge at the current estimates (analytic + numeric), for unit tests. */
+int oracle_edge_jacobians(OracleGraph* g, int edge_index, double* err, double* Ji_an, double* Jj_an,
+                          double* Ji_num, double* Jj_num);
+
+/* Sparse Cholesky pin: solve A x = b, A given as upper CCS (n, Ap, Ai, Ax).  mode 0 = restated
+ * up-looking LL^T with natural ordering, 1 = restated with cs_amd ordering (needs _ref),
+ * 2 = reference CSparse cs_cholsol (needs _ref).  Returns 1 on success, 0 not PD, -1 unavailable. */
+int oracle_ccs_cholsol(int n, const int* Ap, const int* Ai, const double* Ax, double* b, int mode);
+int oracle_ref_available(void);
+const char* oracle_ref_path(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,310 @@
+"""g2o_amd — MI355X-native BlockSolver<p,l> backend for g2o.
+
+Python mirror of the reference's operator/plugin interface for this path
+(``g2o::SparseOptimizer`` + ``OptimizationAlgorithmLevenberg`` + the ``Solver``
+plugin, see ``include/g2o_hip.h``) over the C ABI of ``libg2o_hip.so``.
+The library is hand-written HIP for gfx950; there is no CPU fallback: every
+compute call fails loudly when the library or a GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from . import synth  # noqa: F401
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libg2o_hip.so")
+
+
+class BatchStats(C.Structure):
+    """G2OBatchStatistics (core/batch_stats.h:42-72) + lambda."""
+    _fields_ = [
+        ("iteration", C.c_int), ("numVertices", C.c_int), ("numEdges", C.c_int),
+        ("chi2", C.c_double), ("lambda_", C.c_double),
+        ("timeResiduals", C.c_double), ("timeQuadraticForm", C.c_double),
+        ("levenbergIterations", C.c_int),
+        ("timeSchurComplement", C.c_double), ("timeSymbolicDecomposition", C.c_double),
+        ("timeNumericDecomposition", C.c_double), ("timeLinearSolution", C.c_double),
+        ("timeLinearSolver", C.c_double), ("timeUpdate", C.c_double), ("timeIteration", C.c_double),
+        ("hessianDimension", C.c_longlong), ("hessianPoseDimension", C.c_longlong),
+        ("hessianLandmarkDimension", C.c_longlong), ("choleskyNNZ", C.c_longlong),
+    ]
+
+
+class Config(C.Structure):
+    _fields_ = [("max_trials_after_failure", C.c_int), ("user_lambda_init", C.c_double), ("verbose", C.c_int)]
+
+
+EXPORTS = [
+    "g2ohip_graph_create", "g2ohip_graph_destroy", "g2ohip_add_vertices", "g2ohip_add_edges",
+    "g2ohip_load_g2o", "g2ohip_save_g2o", "g2ohip_num_vertices", "g2ohip_num_edges",
+    "g2ohip_get_estimates", "g2ohip_set_estimates", "g2ohip_minimal_state", "g2ohip_set_algorithm",
+    "g2ohip_initialize", "g2ohip_chi2", "g2ohip_optimize", "g2ohip_optimize_step",
+    "g2ohip_solver_build_structure", "g2ohip_solver_build_system", "g2ohip_solver_set_lambda",
+    "g2ohip_solver_restore_diagonal", "g2ohip_solver_solve", "g2ohip_solver_vector_size",
+    "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
+    "g2ohip_discard_top", "g2ohip_stage", "g2ohip_linear_solve_ccs", "g2ohip_comm_unique_id",
+    "g2ohip_set_comm", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing", "g2ohip_kernel_ms",
+    "g2ohip_kernel_count", "g2ohip_kernel_bytes", "g2ohip_kernel_flops", "g2ohip_last_error",
+    "g2ohip_version",
+]
+
+
+def build(arch: str = "gfx950") -> None:
+    """Compile libg2o_hip.so in-tree with hipcc (cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", HERE, f"ARCH={arch}", "-j8"], check=True)
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run g2o_amd.build() (hipcc --offload-arch=gfx950)")
+    L = C.CDLL(LIB_PATH)
+    P, I, D, LL = C.c_void_p, C.c_int, C.c_double, C.c_longlong
+    sig = {
+        "g2ohip_graph_create": ([I], P),
+        "g2ohip_graph_destroy": ([P], None),
+        "g2ohip_add_vertices": ([P, I, I, P, P, P, P], I),
+        "g2ohip_add_edges": ([P, I, I, P, P, P, P, P], I),
+        "g2ohip_load_g2o": ([P, C.c_char_p, I], I),
+        "g2ohip_save_g2o": ([P, C.c_char_p], I),
+        "g2ohip_num_vertices": ([P], I),
+        "g2ohip_num_edges": ([P], I),
+        "g2ohip_get_estimates": ([P, I, P, P], I),
+        "g2ohip_set_estimates": ([P, I, P], I),
+        "g2ohip_minimal_state": ([P, P], I),
+        "g2ohip_set_algorithm": ([P, C.c_char_p], I),
+        "g2ohip_initialize": ([P], I),
+        "g2ohip_chi2": ([P], D),
+        "g2ohip_optimize": ([P, P, I, P], I),
+        "g2ohip_optimize_step": ([P, P, I, P], I),
+        "g2ohip_solver_build_structure": ([P], I),
+        "g2ohip_solver_build_system": ([P], I),
+        "g2ohip_solver_set_lambda": ([P, D, I], I),
+        "g2ohip_solver_restore_diagonal": ([P], I),
+        "g2ohip_solver_solve": ([P], I),
+        "g2ohip_solver_vector_size": ([P], LL),
+        "g2ohip_solver_get_x": ([P, P], I),
+        "g2ohip_solver_get_b": ([P, P], I),
+        "g2ohip_update": ([P, P], I),
+        "g2ohip_push": ([P], I),
+        "g2ohip_pop": ([P], I),
+        "g2ohip_discard_top": ([P], I),
+        "g2ohip_stage": ([P, D, P, P, P, P, P], I),
+        "g2ohip_linear_solve_ccs": ([I, I, P, P, P, P, P, I, P], I),
+        "g2ohip_comm_unique_id": ([P], I),
+        "g2ohip_set_comm": ([P, P, I, I], I),
+        "g2ohip_symbolic_analyze": ([I, I, I, P, P, P, P], I),
+        "g2ohip_enable_kernel_timing": ([P, I], None),
+        "g2ohip_kernel_ms": ([P, C.c_char_p], D),
+        "g2ohip_kernel_count": ([P, C.c_char_p], LL),
+        "g2ohip_kernel_bytes": ([P, C.c_char_p], D),
+        "g2ohip_kernel_flops": ([P, C.c_char_p], D),
+        "g2ohip_last_error": ([], C.c_char_p),
+        "g2ohip_version": ([], C.c_char_p),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def last_error() -> str:
+    return lib().g2ohip_last_error().decode()
+
+
+class G2OHipError(RuntimeError):
+    pass
+
+
+def _check(code, what):
+    if code < 0:
+        raise G2OHipError(f"{what} failed ({code}): {last_error()}")
+    return code
+
+
+def symbolic_analyze(nblocks: int, bdim: int, bi, bj):
+    """Host-only symbolic analysis (ordering + supernodes); returns (perm, stats dict)."""
+    bi = np.ascontiguousarray(bi, np.int32)
+    bj = np.ascontiguousarray(bj, np.int32)
+    perm = np.zeros(nblocks * bdim, np.int32)
+    st = np.zeros(4)
+    n = lib().g2ohip_symbolic_analyze(nblocks, bdim, len(bi), _p(bi), _p(bj), _p(perm), _p(st))
+    _check(n, "symbolic_analyze")
+    return perm, dict(nnzL=st[0], flops=st[1], supernodes=int(st[2]), levels=int(st[3]))
+
+
+def linear_solve_ccs(n, Ap, Ai, Ax, b, block_dim=1, device=0):
+    """LinearSolver::solve on an upper-CCS matrix (LinearSolverCCS contract)."""
+    Ap = np.ascontiguousarray(Ap, np.int32)
+    Ai = np.ascontiguousarray(Ai, np.int32)
+    Ax = np.ascontiguousarray(Ax, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    x = np.zeros(n)
+    nb = n // block_dim
+    ends = np.arange(1, nb + 1, dtype=np.int32) * block_dim
+    r = lib().g2ohip_linear_solve_ccs(device, n, _p(Ap), _p(Ai), _p(Ax), _p(b), _p(x), nb, _p(ends))
+    _check(r, "linear_solve_ccs")
+    return bool(r), x
+
+
+class SparseOptimizer:
+    """g2o::SparseOptimizer with a device-resident ``lm_hip_*`` algorithm
+    (sparse_optimizer.h; optimization_algorithm_levenberg.h)."""
+
+    def __init__(self, device: int = 0):
+        self.h = lib().g2ohip_graph_create(device)
+        if not self.h:
+            raise G2OHipError(f"g2ohip_graph_create failed: {last_error()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().g2ohip_graph_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    # ---- OptimizableGraph ----
+    def add_vertices(self, vs):
+        ids = np.ascontiguousarray(vs.ids, np.int32)
+        est = np.ascontiguousarray(vs.est, np.float64)
+        fx = np.ascontiguousarray(vs.fixed, np.int32)
+        mg = np.ascontiguousarray(vs.marginalized, np.int32)
+        _check(lib().g2ohip_add_vertices(self.h, vs.vtype, len(ids), _p(ids), _p(est), _p(fx), _p(mg)),
+               "add_vertices")
+
+    def add_edges(self, es):
+        v0 = np.ascontiguousarray(es.v0, np.int32)
+        v1 = np.ascontiguousarray(es.v1, np.int32)
+        meas = np.ascontiguousarray(es.meas, np.float64)
+        info = np.ascontiguousarray(es.info, np.float64)
+        par = None if es.params is None else np.ascontiguousarray(es.params, np.float64)
+        _check(lib().g2ohip_add_edges(self.h, es.etype, len(v0), _p(v0), _p(v1), _p(meas), _p(info), _p(par)),
+               "add_edges")
+
+    def add_problem(self, prob):
+        for vs in prob.vertices:
+            self.add_vertices(vs)
+        for es in prob.edges:
+            self.add_edges(es)
+        return self
+
+    def load(self, path: str, marginalize_xyz: bool = True):
+        _check(lib().g2ohip_load_g2o(self.h, path.encode(), int(marginalize_xyz)), "load")
+
+    def save(self, path: str):
+        _check(lib().g2ohip_save_g2o(self.h, path.encode()), "save")
+
+    def set_algorithm(self, name: str):
+        _check(lib().g2ohip_set_algorithm(self.h, name.encode()), "set_algorithm")
+
+    def initialize_optimization(self):
+        _check(lib().g2ohip_initialize(self.h), "initializeOptimization")
+
+    def chi2(self) -> float:
+        return lib().g2ohip_chi2(self.h)
+
+    def optimize(self, iterations: int, max_trials: int = 10, lambda_init: float = 0.0, verbose: bool = False):
+        cfg = Config(max_trials, lambda_init, int(verbose))
+        stats = (BatchStats * max(iterations, 1))()
+        n = _check(lib().g2ohip_optimize(self.h, C.byref(cfg), iterations, stats), "optimize")
+        return n, [stats[i] for i in range(n)]
+
+    def optimize_step(self, iteration: int, max_trials: int = 10, lambda_init: float = 0.0, stats: bool = True):
+        cfg = Config(max_trials, lambda_init, 0)
+        st = BatchStats()
+        r = _check(lib().g2ohip_optimize_step(self.h, C.byref(cfg), iteration, C.byref(st) if stats else None),
+                   "optimize_step")
+        return r, st
+
+    def minimal_state(self) -> np.ndarray:
+        n = _check(lib().g2ohip_minimal_state(self.h, None), "minimal_state")
+        out = np.zeros(n)
+        lib().g2ohip_minimal_state(self.h, _p(out))
+        return out
+
+    def estimates(self, vtype: int) -> np.ndarray:
+        n = _check(lib().g2ohip_get_estimates(self.h, vtype, None, None), "get_estimates")
+        out = np.zeros((n, synth.EST_DIM[vtype]))
+        lib().g2ohip_get_estimates(self.h, vtype, _p(out), None)
+        return out
+
+    # ---- Solver plugin (core/solver.h) ----
+    def build_structure(self):
+        _check(lib().g2ohip_solver_build_structure(self.h), "buildStructure")
+
+    def build_system(self):
+        _check(lib().g2ohip_solver_build_system(self.h), "buildSystem")
+
+    def set_lambda(self, lam: float, backup: bool = True):
+        _check(lib().g2ohip_solver_set_lambda(self.h, lam, int(backup)), "setLambda")
+
+    def restore_diagonal(self):
+        _check(lib().g2ohip_solver_restore_diagonal(self.h), "restoreDiagonal")
+
+    def solve(self) -> bool:
+        return bool(_check(lib().g2ohip_solver_solve(self.h), "solve"))
+
+    def vector_size(self) -> int:
+        return int(lib().g2ohip_solver_vector_size(self.h))
+
+    def x(self) -> np.ndarray:
+        out = np.zeros(self.vector_size())
+        _check(lib().g2ohip_solver_get_x(self.h, _p(out)), "x")
+        return out
+
+    def b(self) -> np.ndarray:
+        out = np.zeros(self.vector_size())
+        _check(lib().g2ohip_solver_get_b(self.h, _p(out)), "b")
+        return out
+
+    def stage(self, lam: float):
+        dims = np.zeros(3, np.int64)
+        _check(lib().g2ohip_stage(self.h, 0.0, None, None, None, None, _p(dims)), "stage")
+        n, npose = int(dims[0]), int(dims[1])
+        b, x, H, bs = np.zeros(n), np.zeros(n), np.zeros((npose, npose)), np.zeros(npose)
+        ok = _check(lib().g2ohip_stage(self.h, lam, _p(b), _p(x), _p(H), _p(bs), _p(dims)), "stage")
+        return dict(ok=ok, b=b, x=x, Hschur=H, bschur=bs, n=n, np=npose, nl=int(dims[2]))
+
+    # ---- multi-GPU ----
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (C.c_ubyte * 128)()
+        _check(lib().g2ohip_comm_unique_id(buf), "comm_unique_id")
+        return bytes(buf)
+
+    def set_comm(self, uid: bytes, rank: int, nranks: int):
+        buf = (C.c_ubyte * 128).from_buffer_copy(uid)
+        _check(lib().g2ohip_set_comm(self.h, buf, rank, nranks), "set_comm")
+
+    # ---- measurement ----
+    def enable_kernel_timing(self, on: bool = True):
+        lib().g2ohip_enable_kernel_timing(self.h, int(on))
+
+    def kernel_ms(self, name: str) -> float:
+        return lib().g2ohip_kernel_ms(self.h, name.encode())
+
+    def kernel_count(self, name: str) -> int:
+        return lib().g2ohip_kernel_count(self.h, name.encode())
+
+    def kernel_bytes(self, name: str) -> float:
+        return lib().g2ohip_kernel_bytes(self.h, name.encode())
+
+    def kernel_flops(self, name: str) -> float:
+        return lib().g2ohip_kernel_flops(self.h, name.encode())

@@ -1,0 +1,297 @@
+// extern "C" entry points of libg2o_hip.so (include/g2o_hip.h).
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <vector>
+#include <cstring>
+#include <string>
+
+#include "../../include/g2o_hip.h"
+#include "engine.hpp"
+
+struct g2ohip_graph {
+  g2ohip::Engine* e;
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return G2OHIP_ERR_DEVICE;
+  }
+}
+bool algorithm_known(const std::string& n) {
+  // {gn,lm}_hip_{var,fix6_3,fix3_3,fix6_6} (cf. solver_csparse.cpp:51-84 name parsing)
+  if (n.size() < 7) return false;
+  const std::string m = n.substr(0, 3), rest = n.substr(3);
+  if (m != "lm_" && m != "gn_") return false;
+  return rest == "hip_var" || rest == "hip_fix6_3" || rest == "hip_fix3_3" || rest == "hip_fix6_6";
+}
+}  // namespace
+
+extern "C" {
+
+g2ohip_graph* g2ohip_graph_create(int device) {
+  try {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= device) {
+      g_err = "no HIP device " + std::to_string(device) + " (libg2o_hip requires a gfx950 GPU)";
+      return nullptr;
+    }
+    return new g2ohip_graph{new g2ohip::Engine(device)};
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return nullptr;
+  }
+}
+void g2ohip_graph_destroy(g2ohip_graph* g) {
+  if (!g) return;
+  delete g->e;
+  delete g;
+}
+int g2ohip_add_vertices(g2ohip_graph* g, int type, int n, const int* ids, const double* est, const int* fixed,
+                        const int* marginalized) {
+  if (!g || (n > 0 && (!ids || !est))) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->add_vertices(type, n, ids, est, fixed, marginalized); });
+}
+int g2ohip_add_edges(g2ohip_graph* g, int type, int n, const int* v0, const int* v1, const double* meas,
+                     const double* info, const double* params) {
+  if (!g || (n > 0 && (!v0 || !v1 || !meas || !info))) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->add_edges(type, n, v0, v1, meas, info, params); });
+}
+int g2ohip_load_g2o(g2ohip_graph* g, const char* path, int marginalize_xyz) {
+  if (!g || !path) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->load(path, marginalize_xyz); });
+}
+int g2ohip_save_g2o(g2ohip_graph* g, const char* path) {
+  if (!g || !path) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->save(path); });
+}
+int g2ohip_num_vertices(g2ohip_graph* g) { return g ? (int)g->e->hg.verts.size() : G2OHIP_ERR_ARG; }
+int g2ohip_num_edges(g2ohip_graph* g) { return g ? (int)g->e->hg.ev0.size() : G2OHIP_ERR_ARG; }
+int g2ohip_get_estimates(g2ohip_graph* g, int type, double* out, int* ids_out) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->get_estimates(type, out, ids_out); });
+}
+int g2ohip_set_estimates(g2ohip_graph* g, int type, const double* est) {
+  if (!g || !est) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->set_estimates(type, est); });
+}
+int g2ohip_minimal_state(g2ohip_graph* g, double* out) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->minimal_state(out); });
+}
+int g2ohip_set_algorithm(g2ohip_graph* g, const char* name) {
+  if (!g || !name || !algorithm_known(name)) return G2OHIP_ERR_ARG;
+  g->e->algorithm = name;
+  g->e->levenberg = std::string(name).rfind("lm_", 0) == 0;
+  return G2OHIP_OK;
+}
+int g2ohip_initialize(g2ohip_graph* g) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->initialize(); });
+}
+double g2ohip_chi2(g2ohip_graph* g) {
+  if (!g) return std::nan("");
+  try {
+    return g->e->chi2();
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return std::nan("");
+  }
+}
+int g2ohip_optimize(g2ohip_graph* g, const g2ohip_config* cfg, int iterations, g2ohip_batch_stats* stats) {
+  if (!g || iterations < 0) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->optimize(cfg, iterations, stats); });
+}
+int g2ohip_optimize_step(g2ohip_graph* g, const g2ohip_config* cfg, int iteration, g2ohip_batch_stats* stats) {
+  if (!g || iteration < 0) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->optimize_step(cfg, iteration, stats); });
+}
+int g2ohip_solver_build_structure(g2ohip_graph* g) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->build_structure(); });
+}
+int g2ohip_solver_build_system(g2ohip_graph* g) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->build_system(); });
+}
+int g2ohip_solver_set_lambda(g2ohip_graph* g, double lambda, int backup) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->set_lambda(lambda, backup); });
+}
+int g2ohip_solver_restore_diagonal(g2ohip_graph* g) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->restore_diagonal(); });
+}
+int g2ohip_solver_solve(g2ohip_graph* g) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->solve_sync(); });
+}
+long long g2ohip_solver_vector_size(g2ohip_graph* g) { return g ? g->e->vector_size() : G2OHIP_ERR_ARG; }
+int g2ohip_solver_get_x(g2ohip_graph* g, double* x) {
+  if (!g || !x) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->get_x(x); });
+}
+int g2ohip_solver_get_b(g2ohip_graph* g, double* b) {
+  if (!g || !b) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->get_b(b); });
+}
+int g2ohip_update(g2ohip_graph* g, const double* x_host) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->update_from(x_host); });
+}
+int g2ohip_push(g2ohip_graph* g) { return g ? guarded([&] { return g->e->push(); }) : G2OHIP_ERR_ARG; }
+int g2ohip_pop(g2ohip_graph* g) { return g ? guarded([&] { return g->e->pop(); }) : G2OHIP_ERR_ARG; }
+int g2ohip_discard_top(g2ohip_graph* g) { return g ? guarded([&] { return g->e->discard_top(); }) : G2OHIP_ERR_ARG; }
+int g2ohip_stage(g2ohip_graph* g, double lambda, double* b, double* x, double* Hs, double* bs, long long* dims) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->stage(lambda, b, x, Hs, bs, dims); });
+}
+
+int g2ohip_linear_solve_ccs(int device, int n, const int* Ap, const int* Ai, const double* Ax, const double* b,
+                            double* x, int nblocks, const int* block_ends) {
+  if (n <= 0 || !Ap || !Ai || !Ax || !b || !x) return G2OHIP_ERR_ARG;
+  return guarded([&]() -> int {
+    // Uniform block partition required (BlockSolver<p,l> pose blocks); default 1x1 blocks.
+    int bd = 1;
+    if (nblocks > 0 && block_ends) {
+      bd = block_ends[0];
+      for (int k = 0; k < nblocks; ++k)
+        if (block_ends[k] != (k + 1) * bd) return G2OHIP_ERR_UNSUPPORTED;
+      if (nblocks * bd != n) return G2OHIP_ERR_ARG;
+    }
+    const int nb = n / bd;
+    // collect upper blocks from the scalar CCS
+    std::map<std::pair<int, int>, int> bid;
+    std::vector<int> bi, bj;
+    for (int j = 0; j < n; ++j)
+      for (int p = Ap[j]; p < Ap[j + 1]; ++p) {
+        const int i = Ai[p];
+        if (i > j) continue;
+        auto key = std::make_pair(i / bd, j / bd);
+        if (!bid.count(key)) { bid[key] = (int)bi.size(); bi.push_back(key.first); bj.push_back(key.second); }
+      }
+    for (int k = 0; k < nb; ++k) {
+      auto key = std::make_pair(k, k);
+      if (!bid.count(key)) { bid[key] = (int)bi.size(); bi.push_back(k); bj.push_back(k); }
+    }
+    std::vector<double> vals(bi.size() * bd * bd, 0.0);
+    for (int j = 0; j < n; ++j)
+      for (int p = Ap[j]; p < Ap[j + 1]; ++p) {
+        const int i = Ai[p];
+        if (i > j) continue;
+        const int t = bid[{i / bd, j / bd}];
+        const int r = i % bd, c = j % bd;
+        vals[(size_t)t * bd * bd + c * bd + r] = Ax[p];
+        if (i / bd == j / bd) vals[(size_t)t * bd * bd + r * bd + c] = Ax[p];
+      }
+    HIP_CHECK(hipSetDevice(device));
+    hipStream_t s;
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int ok = 0;
+    {
+      g2ohip::DeviceCholesky ch;
+      ch.setup(nb, bd, bi, bj, s);
+      g2ohip::DevBuf<double> dv, db, dx, dl;
+      g2ohip::DevBuf<int> df;
+      dv.upload(vals, s);
+      db.upload(b, n, s);
+      dx.resize(n);
+      std::vector<double> zero{0.0};
+      dl.upload(zero, s);
+      df.resize(1);
+      df.zero(s);
+      ch.factor(dv.get(), dl.get(), df.get(), s);
+      ch.solve(db.get(), dx.get(), s);
+      int f = 0;
+      HIP_CHECK(hipMemcpyAsync(&f, df.get(), sizeof f, hipMemcpyDeviceToHost, s));
+      dx.download(x, n, s);
+      HIP_CHECK(hipStreamSynchronize(s));
+      ok = f ? 0 : 1;
+    }
+    (void)hipStreamDestroy(s);
+    return ok;
+  });
+}
+
+int g2ohip_comm_unique_id(unsigned char out[128]) {
+  if (!out) return G2OHIP_ERR_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return G2OHIP_ERR_DEVICE;
+  std::memcpy(out, &id, 128);
+  return G2OHIP_OK;
+}
+int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int nranks) {
+  if (!g || !uid || rank < 0 || rank >= nranks) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->set_comm(uid, rank, nranks); });
+}
+
+int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int* perm, double* stats) {
+  if (nblocks <= 0 || bdim <= 0 || nblk < 0 || (nblk > 0 && (!bi || !bj))) return G2OHIP_ERR_ARG;
+  try {
+    g2ohip::BlockPattern P;
+    P.nb = nblocks;
+    P.dim.assign(nblocks, bdim);
+    P.offset.resize(nblocks + 1);
+    for (int k = 0; k <= nblocks; ++k) P.offset[k] = k * bdim;
+    std::vector<std::vector<int>> adj(nblocks);
+    for (int k = 0; k < nblk; ++k) {
+      if (bi[k] < 0 || bj[k] < 0 || bi[k] >= nblocks || bj[k] >= nblocks) return G2OHIP_ERR_ARG;
+      if (bi[k] == bj[k]) continue;
+      adj[bi[k]].push_back(bj[k]);
+      adj[bj[k]].push_back(bi[k]);
+    }
+    P.adjp.assign(nblocks + 1, 0);
+    for (int k = 0; k < nblocks; ++k) {
+      std::sort(adj[k].begin(), adj[k].end());
+      adj[k].erase(std::unique(adj[k].begin(), adj[k].end()), adj[k].end());
+      P.adjp[k + 1] = P.adjp[k] + (int)adj[k].size();
+      P.adji.insert(P.adji.end(), adj[k].begin(), adj[k].end());
+    }
+    g2ohip::Symbolic S = g2ohip::analyze(P);
+    if (perm) std::memcpy(perm, S.perm.data(), sizeof(int) * S.n);
+    if (stats) {
+      stats[0] = S.nnzL;
+      stats[1] = S.flops;
+      stats[2] = (double)S.sn.size();
+      stats[3] = (double)S.num_levels;
+    }
+    return S.n;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return G2OHIP_ERR_STATE;
+  }
+}
+
+void g2ohip_enable_kernel_timing(g2ohip_graph* g, int on) {
+  if (!g) return;
+  g->e->timer.enabled = on != 0;
+  g->e->timer.reset();
+}
+double g2ohip_kernel_ms(g2ohip_graph* g, const char* name) {
+  if (!g || !name) return -1;
+  auto& t = g->e->timer;
+  auto it = t.total_ms.find(name);
+  auto ct = t.count.find(name);
+  if (it == t.total_ms.end() || ct == t.count.end() || ct->second == 0) return 0;
+  return it->second / (double)ct->second;
+}
+long long g2ohip_kernel_count(g2ohip_graph* g, const char* name) {
+  if (!g || !name) return -1;
+  auto ct = g->e->timer.count.find(name);
+  return ct == g->e->timer.count.end() ? 0 : ct->second;
+}
+double g2ohip_kernel_bytes(g2ohip_graph* g, const char* name) { return g && name ? g->e->kernel_bytes(name) : -1; }
+double g2ohip_kernel_flops(g2ohip_graph* g, const char* name) { return g && name ? g->e->kernel_flops(name) : -1; }
+const char* g2ohip_last_error(void) { return g_err.c_str(); }
+const char* g2ohip_version(void) { return "g2o_hip 0.1.0 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,207 @@
+// Host side of the MI355X BlockSolver backend: graph mirror, structure, LM driver.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/g2o_hip.h"
+#include "common.hpp"
+#include "kernels.hpp"
+#include "symbolic.hpp"
+
+namespace g2ohip {
+
+int vertex_dim(int vtype);
+int vertex_est_dim(int vtype);
+int vertex_state_stride(int vtype);
+int edge_dim(int etype);
+int edge_meas_dim(int etype);
+
+// OptimizableGraph mirror (host, authoritative for I/O; the device copy is authoritative
+// during optimize()).
+struct HVertex {
+  int id, type, dim;
+  bool fixed, marg;
+  int local;  // index within its type's state array
+};
+
+struct HostGraph {
+  std::vector<HVertex> verts;
+  std::unordered_map<int, int> idmap;
+  std::vector<double> st[5];            // per type, device layout
+  std::vector<std::vector<int>> by_type = std::vector<std::vector<int>>(5);  // local -> vertex
+  std::vector<int> nopl;                // VertexSE3 oplus counters (per local SE3QUAT vertex)
+  int etype = 0;
+  std::vector<int> ev0, ev1;            // vertex indices
+  std::vector<double> emeas, einfo, eparams;  // raw: meas (as given), info D*D, params 4
+};
+
+void set_state_from_est(int vtype, const double* est, double* st);
+void est_from_state(int vtype, const double* st, double* est);
+void minimal_from_state(int vtype, const double* st, double* out);
+
+// Device-resident multifrontal factor of one block-sparse SPD matrix.
+struct DeviceCholesky {
+  Symbolic sym;
+  int pd = 0;
+  long long nent = 0;
+  DevBuf<long long> dst;
+  DevBuf<unsigned char> isdiag;
+  DevBuf<launch::FrontDesc> fd;
+  DevBuf<int> level_lists, children, relmap, rows, perm;
+  std::vector<int> level_off;  // host offsets into level_lists
+  DevBuf<double> fronts, vecs, rhs_p, x_p;
+  void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
+  void factor(const double* vals, const double* lam, int* fail, hipStream_t s);
+  void solve(const double* rhs, double* x, hipStream_t s);
+};
+
+struct KernelTimer {
+  bool enabled = false;
+  struct Rec { hipEvent_t a, b; std::string name; };
+  std::vector<Rec> pending;
+  std::vector<hipEvent_t> pool;
+  std::map<std::string, double> total_ms;
+  std::map<std::string, long long> count;
+  hipEvent_t get();
+  void begin(const std::string& name, hipStream_t s);
+  void end(hipStream_t s);
+  void collect();  // after a sync
+  void reset() { total_ms.clear(); count.clear(); }
+  ~KernelTimer();
+};
+
+class Engine {
+ public:
+  explicit Engine(int device);
+  ~Engine();
+  HostGraph hg;
+  int device;
+  hipStream_t stream = nullptr;
+  std::string algorithm = "lm_hip_var";
+  bool levenberg = true;
+
+  // ---- graph ops ----
+  int add_vertices(int type, int n, const int* ids, const double* est, const int* fixed, const int* marg);
+  int add_edges(int type, int n, const int* v0, const int* v1, const double* meas, const double* info,
+                const double* params);
+  int load(const char* path, int marginalize_xyz);
+  int save(const char* path);
+  int get_estimates(int type, double* out, int* ids);
+  int set_estimates(int type, const double* est);
+  int minimal_state(double* out);
+
+  // ---- SparseOptimizer / Solver ----
+  int initialize();
+  double chi2();
+  int optimize(const g2ohip_config* cfg, int iterations, g2ohip_batch_stats* stats);
+  // one SparseOptimizer::optimize loop body (iteration 0 rebuilds structure + lambda init);
+  // returns 0 OK, 1 Terminate, 2 Fail, <0 error
+  int optimize_step(const g2ohip_config* cfg, int iteration, g2ohip_batch_stats* stats);
+  int build_structure();
+  int build_system();
+  int set_lambda(double lambda, int backup);
+  int restore_diagonal();
+  int solve_sync();  // 1 ok / 0 not PD
+  long long vector_size() const { return (long long)size_poses + size_landmarks; }
+  int get_x(double* x);
+  int get_b(double* b);
+  int update_from(const double* xh);
+  int push();
+  int pop();
+  int discard_top();
+  int stage(double lambda, double* b, double* x, double* Hs, double* bs, long long* dims);
+
+  // comm
+  int set_comm(const unsigned char* uid, int rank, int nranks);
+  KernelTimer timer;
+  double kernel_bytes(const std::string& name) const;
+  double kernel_flops(const std::string& name) const;
+
+ private:
+  // structure
+  bool initialized = false, structure_built = false, device_state_dirty = true, host_state_stale = false;
+  int family = FAM_NONE;
+  int pd = 0, ld = 0;
+  int num_poses = 0, num_landmarks = 0, size_poses = 0, size_landmarks = 0;
+  std::vector<int> active;       // active vertex indices sorted by id
+  std::vector<int> ivmap;        // hessian order
+  std::vector<int> hidx;         // per vertex: hessian index or -1
+  bool do_schur = false;
+  int vt0 = 0, vt1 = 0;          // vertex types of edge endpoints
+  int ne = 0;
+  // sharding
+  int rank = 0, nranks = 1;
+  void* comm = nullptr;
+  std::vector<int> local_edges;  // edge indices this rank assembles (all when nranks == 1)
+  std::vector<int> local_lm;     // landmark (hessian - num_poses) this rank owns
+
+  // device state
+  DevBuf<double> dstate[5];
+  DevBuf<int> dnopl;
+  std::vector<std::vector<DevBuf<double>>> stack_;  // per push level: per type (buffers reused)
+  int stack_depth_ = 0;
+  bool edges_ready = false;
+  hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};  // schur start, factor start, factor end, solve end
+  bool ev_valid_ = false;
+  DevBuf<int> d_xoff[5];         // per type local -> x offset or -1
+  DevBuf<int> d_hidx[5];         // per type local -> hessian index (-1 fixed)
+  // device edges (local shard, in active-edge order)
+  DevBuf<int> dv0, dv1;
+  DevBuf<double> dmeas, dinfo, dparams;
+  DevBuf<double> dchi;
+  DevBuf<double> dslot0, dslot1;
+  int slot_stride0 = 0, slot_stride1 = 0;
+  DevBuf<long long> doff_dst;
+  DevBuf<unsigned char> doff_tr;
+  bool off_dup = false;
+  DevBuf<double> doffslot;
+  DevBuf<int> doffb_ptr, doffb_edges;
+  DevBuf<long long> doffb_dst;
+  int noffb = 0, off_bsz = 0;
+  // hessian storage
+  int nHpp = 0, nHpl = 0;
+  DevBuf<double> dH;             // [Hpp blocks | Hpl blocks]
+  DevBuf<double> dHll;
+  DevBuf<double> db, dx;
+  // vertex reduction
+  struct VRed { int dim, nv, lanes; DevBuf<int> ptr, code, boff; double* H; };
+  VRed vr_pose, vr_lm;
+  // schur
+  DevBuf<int> d_lm_ptr, d_blk_pose, d_blk_lm;
+  DevBuf<double> dDinv, dW, dS, dbschur;
+  int nS = 0;
+  long long npairs = 0;
+  DevBuf<int> ds_ptr, ds_pairs, ds_hpp, ds_row;
+  DevBuf<unsigned char> ds_diag;
+  std::vector<int> s_bi, s_bj, hpp_bi, hpp_bj;
+  DeviceCholesky chol;
+  // scalars: [0] lambda, [1] chi2, [2] scale, [3] maxdiag
+  DevBuf<double> dscal;
+  DevBuf<int> dfail;
+  DevBuf<double> dpartial, dscale_terms;
+  double lambda_host = 0.0;
+  bool lambda_set = false;
+  // LM state (optimization_algorithm_levenberg.cpp)
+  double current_lambda = -1, ni = 2;
+  int levenberg_iterations = 0;
+  g2ohip_batch_stats* cur_stats = nullptr;
+
+  void ensure_device_state();
+  void sync_host_state();
+  void setup_edges_device();
+  void compute_errors_async();
+  double chi2_sync();
+  double lambda_init();
+  void solve_async();
+  void update_async();
+  void set_lambda_device(double l);
+  void allreduce_sum(double* dptr, size_t n);
+  int lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats* st);
+};
+
+}  // namespace g2ohip

@@ -1,0 +1,644 @@
+// HIP kernels for the BlockSolver<p,l> hot path on gfx950 (MI355X).
+//
+//   k_linearize   BlockSolver::buildSystem edge loop (block_solver.hpp:486-506) fused with
+//                 BaseBinaryEdge::constructQuadraticForm (base_binary_edge.hpp:61-100):
+//                 one lane per edge, J and J^T Omega J in registers, contributions streamed
+//                 to per-edge slots (no atomics, no locks).
+//   k_vertex_reduce  deterministic segmented reduction of the slots into Hpp/Hll diagonal
+//                 blocks and b (replaces the per-vertex omp locks + copyB, :467-517).
+//   k_schur_dinv  landmark pass of BlockSolver::solve (:342-360): Dinv = (Hll+lambda I)^-1,
+//                 W = Hpl Dinv per observation block.
+//   k_schur_pairs Hschur(i,j) = Hpp(i,j) - sum_l W_il Hpl_jl^T and bschur (:361-400) computed
+//                 output-stationary: a group of lanes owns one Schur block and walks its
+//                 precomputed (W, Hpl) pair list; fixed-order tree reduction, no atomics.
+//   k_backsub     x_l = Dinv (b_l - Hpl^T x_p) (:420-446).
+//   k_error/k_oplus  computeActiveErrors (sparse_optimizer.cpp:63-90) and update (:441-454).
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "device_types.hpp"
+#include "kernels.hpp"
+
+namespace g2ohip {
+using namespace dev;
+
+// ------------------------------------------------------------------------------ errors / chi2
+template <class F>
+__global__ void __launch_bounds__(256) k_error(EdgeData d, int ne, double* __restrict__ chi) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  double err[F::D];
+  F::error(d, e, err);
+  double Om[F::D * F::D];
+  load_info<F::D>(d.info + (size_t)e * F::INFO, Om);
+  double s = 0;
+#pragma unroll
+  for (int i = 0; i < F::D; ++i) {
+    double r = 0;
+#pragma unroll
+    for (int j = 0; j < F::D; ++j) r += Om[i * F::D + j] * err[j];
+    s += err[i] * r;
+  }
+  chi[e] = s;
+}
+
+// ------------------------------------------------------------------------------ linearize
+// slot layouts (AoS per edge): packed upper col-major H (d(d+1)/2) followed by b (d)
+template <class F>
+__global__ void __launch_bounds__(256)
+    k_linearize(EdgeData d, int ne, const int* __restrict__ h0, const int* __restrict__ h1, double* __restrict__ slot0,
+                double* __restrict__ slot1, const long long* __restrict__ off_dst, const unsigned char* __restrict__ off_tr,
+                double* __restrict__ off_base) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  constexpr int D = F::D, DA = F::DA, DB = F::DB;
+  constexpr int SA = DA * (DA + 1) / 2 + DA, SB = DB * (DB + 1) / 2 + DB;
+  const bool nfA = h0[d.v0[e]] >= 0, nfB = h1[d.v1[e]] >= 0;
+  if (!nfA && !nfB) return;
+  double err[D], A[D * DA], B[D * DB];
+  F::linearize(d, e, err, A, B);
+  double Om[D * D];
+  load_info<D>(d.info + (size_t)e * F::INFO, Om);
+  double wr[D];
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    double s = 0;
+#pragma unroll
+    for (int c = 0; c < D; ++c) s += Om[r * D + c] * err[c];
+    wr[r] = -s;
+  }
+  double AtO[DA * D];  // A^T Omega
+#pragma unroll
+  for (int i = 0; i < DA; ++i)
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      double s = 0;
+#pragma unroll
+      for (int r = 0; r < D; ++r) s += A[r * DA + i] * Om[r * D + c];
+      AtO[i * D + c] = s;
+    }
+  if (nfA) {
+    double* o = slot0 + (size_t)e * SA;
+    int k = 0;
+#pragma unroll
+    for (int c = 0; c < DA; ++c)
+#pragma unroll
+      for (int r = 0; r <= c; ++r) {
+        double s = 0;
+#pragma unroll
+        for (int t = 0; t < D; ++t) s += AtO[r * D + t] * A[t * DA + c];
+        o[k++] = s;
+      }
+#pragma unroll
+    for (int i = 0; i < DA; ++i) {
+      double s = 0;
+#pragma unroll
+      for (int r = 0; r < D; ++r) s += A[r * DA + i] * wr[r];
+      o[k++] = s;
+    }
+    if (nfB && off_dst[e] >= 0) {
+      double* H = off_base + off_dst[e];
+      if (off_tr[e]) {  // DB x DA col-major: (j,i)
+#pragma unroll
+        for (int i = 0; i < DA; ++i)
+#pragma unroll
+          for (int j = 0; j < DB; ++j) {
+            double s = 0;
+#pragma unroll
+            for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
+            H[i * DB + j] = s;
+          }
+      } else {  // DA x DB col-major: (i,j)
+#pragma unroll
+        for (int j = 0; j < DB; ++j)
+#pragma unroll
+          for (int i = 0; i < DA; ++i) {
+            double s = 0;
+#pragma unroll
+            for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
+            H[j * DA + i] = s;
+          }
+      }
+    }
+  }
+  if (nfB) {
+    double BtO[DB * D];
+#pragma unroll
+    for (int j = 0; j < DB; ++j)
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        double s = 0;
+#pragma unroll
+        for (int r = 0; r < D; ++r) s += B[r * DB + j] * Om[r * D + c];
+        BtO[j * D + c] = s;
+      }
+    double* o = slot1 + (size_t)e * SB;
+    int k = 0;
+#pragma unroll
+    for (int c = 0; c < DB; ++c)
+#pragma unroll
+      for (int r = 0; r <= c; ++r) {
+        double s = 0;
+#pragma unroll
+        for (int t = 0; t < D; ++t) s += BtO[r * D + t] * B[t * DB + c];
+        o[k++] = s;
+      }
+#pragma unroll
+    for (int j = 0; j < DB; ++j) {
+      double s = 0;
+#pragma unroll
+      for (int r = 0; r < D; ++r) s += B[r * DB + j] * wr[r];
+      o[k++] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ vertex reduction
+// One group of LANES lanes per vertex; lane l sums slots l, l+LANES, ... in order; butterfly
+// reduction in a fixed pattern keeps the result bitwise reproducible.
+template <int DIM, int LANES>
+__global__ void __launch_bounds__(256)
+    k_vertex_reduce(int nv, const int* __restrict__ inc_ptr, const int* __restrict__ inc_code,
+                    const double* __restrict__ slot0, const double* __restrict__ slot1, int stride0, int stride1,
+                    double* __restrict__ Hdiag /* [nv][DIM*DIM] */, double* __restrict__ b /* offset per vertex */,
+                    const int* __restrict__ boff) {
+  constexpr int SP = DIM * (DIM + 1) / 2, S = SP + DIM;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int v = gid / LANES, lane = gid % LANES;
+  const bool active = v < nv;
+  double acc[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) acc[k] = 0;
+  if (active) {
+    const int p0 = inc_ptr[v], p1 = inc_ptr[v + 1];
+    for (int p = p0 + lane; p < p1; p += LANES) {
+      const int code = inc_code[p];
+      const int e = code >> 1;
+      const double* s = (code & 1) ? slot1 + (size_t)e * stride1 : slot0 + (size_t)e * stride0;
+#pragma unroll
+      for (int k = 0; k < S; ++k) acc[k] += s[k];
+    }
+  }
+  if (LANES > 1) {
+#pragma unroll
+    for (int m = LANES / 2; m >= 1; m >>= 1)
+#pragma unroll
+      for (int k = 0; k < S; ++k) acc[k] += __shfl_xor(acc[k], m, LANES);
+  }
+  if (!active || lane != 0) return;
+  double* H = Hdiag + (size_t)v * DIM * DIM;
+  int k = 0;
+#pragma unroll
+  for (int c = 0; c < DIM; ++c)
+#pragma unroll
+    for (int r = 0; r <= c; ++r) {
+      H[c * DIM + r] = acc[k];
+      H[r * DIM + c] = acc[k];
+      ++k;
+    }
+  double* bb = b + boff[v];
+#pragma unroll
+  for (int i = 0; i < DIM; ++i) bb[i] = acc[SP + i];
+}
+
+// duplicate off-diagonal blocks: sum per-edge slots in edge order
+__global__ void __launch_bounds__(256) k_offblock_reduce(int nb, int bsz, const int* __restrict__ ptr,
+                                                          const int* __restrict__ edges, const double* __restrict__ slots,
+                                                          double* __restrict__ out, const long long* __restrict__ dst) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int blk = gid / bsz, k = gid % bsz;
+  if (blk >= nb) return;
+  double s = 0;
+  for (int p = ptr[blk]; p < ptr[blk + 1]; ++p) s += slots[(size_t)edges[p] * bsz + k];
+  out[dst[blk] + k] = s;
+}
+
+// ------------------------------------------------------------------------------ Schur
+// Landmark pass: Dinv = (Hll + lambda I)^-1 (cofactor inverse, cf. Eigen's 3x3 inverse used by
+// block_solver.hpp:350), W_a = Hpl_a * Dinv for every observation block a of the landmark.
+template <int PD>
+__global__ void __launch_bounds__(256)
+    k_schur_dinv(int nl, const int* __restrict__ lm_ptr, const double* __restrict__ Hll, const double* __restrict__ Hpl,
+                 const double* __restrict__ lam, double* __restrict__ Dinv, double* __restrict__ W,
+                 int* __restrict__ fail) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nl) return;
+  const double lambda = *lam;
+  const double* Hm = Hll + (size_t)l * 9;
+  double a[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) a[k] = Hm[k];
+  a[0] += lambda; a[4] += lambda; a[8] += lambda;
+  auto m = [&](int r, int c) { return a[c * 3 + r]; };
+  const double c00 = m(1, 1) * m(2, 2) - m(1, 2) * m(2, 1);
+  const double c10 = m(0, 2) * m(2, 1) - m(0, 1) * m(2, 2);
+  const double c20 = m(0, 1) * m(1, 2) - m(0, 2) * m(1, 1);
+  const double det = c00 * m(0, 0) + c10 * m(1, 0) + c20 * m(2, 0);
+  const double inv = 1.0 / det;
+  double Di[9];  // col-major
+  Di[0] = c00 * inv; Di[3] = c10 * inv; Di[6] = c20 * inv;
+  Di[1] = (m(1, 2) * m(2, 0) - m(1, 0) * m(2, 2)) * inv;
+  Di[4] = (m(0, 0) * m(2, 2) - m(0, 2) * m(2, 0)) * inv;
+  Di[7] = (m(0, 2) * m(1, 0) - m(0, 0) * m(1, 2)) * inv;
+  Di[2] = (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0)) * inv;
+  Di[5] = (m(0, 1) * m(2, 0) - m(0, 0) * m(2, 1)) * inv;
+  Di[8] = (m(0, 0) * m(1, 1) - m(0, 1) * m(1, 0)) * inv;
+  if (!(det != 0.0) || !isfinite(inv)) *fail = 1;
+  double* Do = Dinv + (size_t)l * 9;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Do[k] = Di[k];
+  for (int a_ = lm_ptr[l]; a_ < lm_ptr[l + 1]; ++a_) {
+    const double* Bm = Hpl + (size_t)a_ * PD * 3;
+    double* Wo = W + (size_t)a_ * PD * 3;
+    double Bl[PD * 3];
+#pragma unroll
+    for (int k = 0; k < PD * 3; ++k) Bl[k] = Bm[k];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int r = 0; r < PD; ++r)
+        Wo[c * PD + r] = Bl[r] * Di[c * 3] + Bl[PD + r] * Di[c * 3 + 1] + Bl[2 * PD + r] * Di[c * 3 + 2];
+  }
+}
+
+// Output-stationary Schur pair products. G lanes per Schur block.
+template <int PD, int G>
+__global__ void __launch_bounds__(256)
+    k_schur_pairs(int nS, const int* __restrict__ s_ptr, const int2* __restrict__ pairs, const int* __restrict__ s_hpp,
+                  const unsigned char* __restrict__ s_diag, const int* __restrict__ s_row,
+                  const double* __restrict__ Hpp, const double* __restrict__ W, const double* __restrict__ Hpl,
+                  const int* __restrict__ blk_lm, const double* __restrict__ b, int size_poses,
+                  const double* __restrict__ lam, double* __restrict__ S, double* __restrict__ bschur) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = gid / G, lane = gid % G;
+  const bool active = t < nS;
+  double acc[PD * PD];
+  double cb[PD];
+#pragma unroll
+  for (int k = 0; k < PD * PD; ++k) acc[k] = 0;
+#pragma unroll
+  for (int k = 0; k < PD; ++k) cb[k] = 0;
+  const bool diag = active && s_diag[t];
+  if (active) {
+    const int p0 = s_ptr[t], p1 = s_ptr[t + 1];
+    for (int p = p0 + lane; p < p1; p += G) {
+      const int2 pr = pairs[p];
+      const double* Wa = W + (size_t)pr.x * PD * 3;
+      const double* Hb = Hpl + (size_t)pr.y * PD * 3;
+      double wa[PD * 3], hb[PD * 3];
+#pragma unroll
+      for (int k = 0; k < PD * 3; ++k) { wa[k] = Wa[k]; hb[k] = Hb[k]; }
+#pragma unroll
+      for (int c = 0; c < PD; ++c)
+#pragma unroll
+        for (int r = 0; r < PD; ++r)
+          acc[c * PD + r] += wa[r] * hb[c] + wa[PD + r] * hb[PD + c] + wa[2 * PD + r] * hb[2 * PD + c];
+      if (diag) {  // coefficients: B Dinv b_l = W b_l
+        const double* bl = b + size_poses + (size_t)blk_lm[pr.x] * 3;
+        const double b0 = bl[0], b1 = bl[1], b2 = bl[2];
+#pragma unroll
+        for (int r = 0; r < PD; ++r) cb[r] += wa[r] * b0 + wa[PD + r] * b1 + wa[2 * PD + r] * b2;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) {
+#pragma unroll
+    for (int k = 0; k < PD * PD; ++k) acc[k] += __shfl_xor(acc[k], m, G);
+#pragma unroll
+    for (int k = 0; k < PD; ++k) cb[k] += __shfl_xor(cb[k], m, G);
+  }
+  if (!active) return;
+  const int hp = s_hpp[t];
+  const double lambda = *lam;
+  double* So = S + (size_t)t * PD * PD;
+  for (int k = lane; k < PD * PD; k += G) {
+    double h = hp >= 0 ? Hpp[(size_t)hp * PD * PD + k] : 0.0;
+    if (diag && (k % (PD + 1)) == 0) h += lambda;
+    So[k] = h - acc[k];
+  }
+  if (diag && lane < PD) {
+    const int row = s_row[t];
+    bschur[(size_t)row * PD + lane] = b[(size_t)row * PD + lane] - cb[lane];
+  }
+}
+
+// back-substitution: x_l = Dinv_l (b_l - sum_a Hpl_a^T x_pose(a))
+template <int PD>
+__global__ void __launch_bounds__(256)
+    k_backsub(int nl, const int* __restrict__ lm_ptr, const int* __restrict__ blk_pose, const double* __restrict__ Hpl,
+              const double* __restrict__ Dinv, const double* __restrict__ b, int size_poses, double* __restrict__ x) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nl) return;
+  const double* bl = b + size_poses + (size_t)l * 3;
+  double c0 = bl[0], c1 = bl[1], c2 = bl[2];
+  for (int a = lm_ptr[l]; a < lm_ptr[l + 1]; ++a) {
+    const double* Bm = Hpl + (size_t)a * PD * 3;
+    const double* xp = x + (size_t)blk_pose[a] * PD;
+    double s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+    for (int r = 0; r < PD; ++r) {
+      const double xr = -xp[r];
+      s0 += Bm[r] * xr;
+      s1 += Bm[PD + r] * xr;
+      s2 += Bm[2 * PD + r] * xr;
+    }
+    c0 += s0; c1 += s1; c2 += s2;
+  }
+  const double* D = Dinv + (size_t)l * 9;
+  double* xl = x + size_poses + (size_t)l * 3;
+  xl[0] = D[0] * c0 + D[3] * c1 + D[6] * c2;
+  xl[1] = D[1] * c0 + D[4] * c1 + D[7] * c2;
+  xl[2] = D[2] * c0 + D[5] * c1 + D[8] * c2;
+}
+
+// ------------------------------------------------------------------------------ oplus
+__global__ void k_oplus_se3expmap(int n, const int* __restrict__ xoff, const double* __restrict__ x,
+                                  double* __restrict__ st) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n || xoff[v] < 0) return;
+  const double* u = x + xoff[v];
+  double uu[6] = {u[0], u[1], u[2], u[3], u[4], u[5]};
+  double qe[4], te[3];
+  se3_exp(uu, qe, te);
+  double* s = st + (size_t)v * 8;
+  const double q[4] = {s[3], s[4], s[5], s[6]};
+  const double t[3] = {s[0], s[1], s[2]};
+  double rt[3], qn[4];
+  qrot(qe, t, rt);  // exp(u) * T : t' = te + qe * t, q' = qe * q
+  qmul(qe, q, qn);
+  qnormalize_pos(qn);
+  s[0] = te[0] + rt[0]; s[1] = te[1] + rt[1]; s[2] = te[2] + rt[2];
+  s[3] = qn[0]; s[4] = qn[1]; s[5] = qn[2]; s[6] = qn[3];
+}
+
+__global__ void k_oplus_xyz(int n, const int* __restrict__ xoff, const double* __restrict__ x, double* __restrict__ st) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n || xoff[v] < 0) return;
+  const double* u = x + xoff[v];
+  double* s = st + (size_t)v * 3;
+  s[0] += u[0]; s[1] += u[1]; s[2] += u[2];
+}
+
+__global__ void k_oplus_se3quat(int n, const int* __restrict__ xoff, const double* __restrict__ x,
+                                double* __restrict__ st, int* __restrict__ nopl) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n || xoff[v] < 0) return;
+  const double* u = x + xoff[v];
+  // increment = fromVectorMQT(u) (isometry3d_mappings.cpp:106-111)
+  double inc[12];
+  const double qx = u[3], qy = u[4], qz = u[5];
+  double w = 1 - (qx * qx + qy * qy + qz * qz);
+  if (w < 0) {
+    inc[0] = 1; inc[1] = 0; inc[2] = 0; inc[3] = 0; inc[4] = 1; inc[5] = 0; inc[6] = 0; inc[7] = 0; inc[8] = 1;
+  } else {
+    w = sqrt(w);
+    quat_to_R(qx, qy, qz, w, inc);
+  }
+  inc[9] = u[0]; inc[10] = u[1]; inc[11] = u[2];
+  double* s = st + (size_t)v * 12;
+  double X[12], Y[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) X[k] = s[k];
+  iso_mul(X, inc, Y);
+  if (++nopl[v] > 1000) {  // vertex_se3.h:110-113 approximateNearestOrthogonalMatrix
+    nopl[v] = 0;
+    double E[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) E[i * 3 + j] = Y[i] * Y[j] + Y[3 + i] * Y[3 + j] + Y[6 + i] * Y[6 + j] - (i == j ? 1.0 : 0.0);
+    double RE[9];
+    mat3mul(Y, E, RE);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Y[k] = Y[k] - 0.5 * RE[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 12; ++k) s[k] = Y[k];
+}
+
+__global__ void k_oplus_se2(int n, const int* __restrict__ xoff, const double* __restrict__ x, double* __restrict__ st) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n || xoff[v] < 0) return;
+  const double* u = x + xoff[v];
+  double* s = st + (size_t)v * 3;
+  s[0] += u[0];
+  s[1] += u[1];
+  s[2] = normalize_theta(s[2] + u[2]);
+}
+
+// ------------------------------------------------------------------------------ reductions
+// Deterministic two-pass sum: fixed chunking, fixed tree.
+constexpr int RED_BLOCK = 256;
+constexpr int RED_PER_THREAD = 16;
+
+__global__ void __launch_bounds__(RED_BLOCK) k_sum_partial(const double* __restrict__ v, long long n,
+                                                           double* __restrict__ partial) {
+  __shared__ double sh[RED_BLOCK];
+  const long long base = (long long)blockIdx.x * RED_BLOCK * RED_PER_THREAD;
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < RED_PER_THREAD; ++k) {
+    const long long i = base + (long long)k * RED_BLOCK + threadIdx.x;
+    if (i < n) s += v[i];
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int m = RED_BLOCK / 2; m > 0; m >>= 1) {
+    if ((int)threadIdx.x < m) sh[threadIdx.x] += sh[threadIdx.x + m];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+__global__ void __launch_bounds__(RED_BLOCK) k_sum_final(const double* __restrict__ partial, int np,
+                                                         double* __restrict__ out) {
+  __shared__ double sh[RED_BLOCK];
+  double s = 0;
+  for (int i = threadIdx.x; i < np; i += RED_BLOCK) s += partial[i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int m = RED_BLOCK / 2; m > 0; m >>= 1) {
+    if ((int)threadIdx.x < m) sh[threadIdx.x] += sh[threadIdx.x + m];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = sh[0];
+}
+
+// scale terms of OptimizationAlgorithmLevenberg::computeScale (:177-184): x (lambda x + b)
+__global__ void k_scale_terms(long long n, const double* __restrict__ x, const double* __restrict__ b,
+                              const double* __restrict__ lam, double* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double l = *lam;
+  out[i] = x[i] * (l * x[i] + b[i]);
+}
+
+// ------------------------------------------------------------------------------ launchers
+namespace launch {
+
+template <class F>
+static EdgeData mk(const EdgeArgs& a) {
+  return EdgeData{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1};
+}
+
+void error(int family, const EdgeArgs& a, int ne, double* chi, hipStream_t s) {
+  if (ne <= 0) return;
+  const unsigned g = grid_for(ne, 256);
+  switch (family) {
+    case FAM_BA: hipLaunchKernelGGL(k_error<FamilyBA>, g, 256, 0, s, mk<FamilyBA>(a), ne, chi); break;
+    case FAM_SE3: hipLaunchKernelGGL(k_error<FamilySE3>, g, 256, 0, s, mk<FamilySE3>(a), ne, chi); break;
+    case FAM_SE2: hipLaunchKernelGGL(k_error<FamilySE2>, g, 256, 0, s, mk<FamilySE2>(a), ne, chi); break;
+  }
+  KERNEL_CHECK();
+}
+
+void linearize(int family, const EdgeArgs& a, int ne, const int* h0, const int* h1, double* slot0, double* slot1,
+               const long long* off_dst, const unsigned char* off_tr, double* off_base, hipStream_t s) {
+  if (ne <= 0) return;
+  const unsigned g = grid_for(ne, 256);
+  switch (family) {
+    case FAM_BA:
+      hipLaunchKernelGGL(k_linearize<FamilyBA>, g, 256, 0, s, mk<FamilyBA>(a), ne, h0, h1, slot0, slot1, off_dst, off_tr,
+                         off_base);
+      break;
+    case FAM_SE3:
+      hipLaunchKernelGGL(k_linearize<FamilySE3>, g, 256, 0, s, mk<FamilySE3>(a), ne, h0, h1, slot0, slot1, off_dst,
+                         off_tr, off_base);
+      break;
+    case FAM_SE2:
+      hipLaunchKernelGGL(k_linearize<FamilySE2>, g, 256, 0, s, mk<FamilySE2>(a), ne, h0, h1, slot0, slot1, off_dst,
+                         off_tr, off_base);
+      break;
+  }
+  KERNEL_CHECK();
+}
+
+template <int DIM>
+static void vreduce_dim(int nv, int lanes, const int* ptr, const int* code, const double* s0, const double* s1, int st0,
+                        int st1, double* H, double* b, const int* boff, hipStream_t s) {
+  const unsigned g = grid_for((size_t)nv * lanes, 256);
+  switch (lanes) {
+    case 1: hipLaunchKernelGGL((k_vertex_reduce<DIM, 1>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+    case 8: hipLaunchKernelGGL((k_vertex_reduce<DIM, 8>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+    default: hipLaunchKernelGGL((k_vertex_reduce<DIM, 64>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+  }
+  KERNEL_CHECK();
+}
+
+void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, const double* s0, const double* s1,
+                   int st0, int st1, double* H, double* b, const int* boff, hipStream_t s) {
+  if (nv <= 0) return;
+  if (dim == 3) vreduce_dim<3>(nv, lanes, ptr, code, s0, s1, st0, st1, H, b, boff, s);
+  else if (dim == 6) vreduce_dim<6>(nv, lanes, ptr, code, s0, s1, st0, st1, H, b, boff, s);
+  else throw std::runtime_error("vertex_reduce: unsupported dim");
+}
+
+void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const double* slots, double* out,
+                     const long long* dst, hipStream_t s) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(k_offblock_reduce, grid_for((size_t)nb * bsz, 256), 256, 0, s, nb, bsz, ptr, edges, slots, out, dst);
+  KERNEL_CHECK();
+}
+
+void schur_dinv(int nl, const int* lm_ptr, const double* Hll, const double* Hpl, const double* lam, double* Dinv,
+                double* W, int* fail, hipStream_t s) {
+  if (nl <= 0) return;
+  hipLaunchKernelGGL(k_schur_dinv<6>, grid_for(nl, 256), 256, 0, s, nl, lm_ptr, Hll, Hpl, lam, Dinv, W, fail);
+  KERNEL_CHECK();
+}
+
+void schur_pairs(int nS, const int* s_ptr, const int* pairs, const int* s_hpp, const unsigned char* s_diag,
+                 const int* s_row, const double* Hpp, const double* W, const double* Hpl, const int* blk_lm,
+                 const double* b, int size_poses, const double* lam, double* S, double* bschur, hipStream_t s) {
+  if (nS <= 0) return;
+  constexpr int G = 16;
+  hipLaunchKernelGGL((k_schur_pairs<6, G>), grid_for((size_t)nS * G, 256), 256, 0, s, nS, s_ptr,
+                     reinterpret_cast<const int2*>(pairs), s_hpp, s_diag, s_row, Hpp, W, Hpl, blk_lm, b, size_poses, lam,
+                     S, bschur);
+  KERNEL_CHECK();
+}
+
+void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
+             int size_poses, double* x, hipStream_t s) {
+  if (nl <= 0) return;
+  hipLaunchKernelGGL(k_backsub<6>, grid_for(nl, 256), 256, 0, s, nl, lm_ptr, blk_pose, Hpl, Dinv, b, size_poses, x);
+  KERNEL_CHECK();
+}
+
+void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s) {
+  if (n <= 0) return;
+  const unsigned g = grid_for(n, 256);
+  switch (vtype) {
+    case 1: hipLaunchKernelGGL(k_oplus_se3expmap, g, 256, 0, s, n, xoff, x, st); break;
+    case 2: hipLaunchKernelGGL(k_oplus_xyz, g, 256, 0, s, n, xoff, x, st); break;
+    case 3: hipLaunchKernelGGL(k_oplus_se3quat, g, 256, 0, s, n, xoff, x, st, nopl); break;
+    case 4: hipLaunchKernelGGL(k_oplus_se2, g, 256, 0, s, n, xoff, x, st); break;
+  }
+  KERNEL_CHECK();
+}
+
+size_t sum_partials(long long n) { return (size_t)((n + RED_BLOCK * RED_PER_THREAD - 1) / (RED_BLOCK * RED_PER_THREAD)); }
+
+void sum(const double* v, long long n, double* partial, double* out, hipStream_t s) {
+  const int np = (int)sum_partials(n);
+  if (np > 0) hipLaunchKernelGGL(k_sum_partial, np, RED_BLOCK, 0, s, v, n, partial);
+  hipLaunchKernelGGL(k_sum_final, 1, RED_BLOCK, 0, s, partial, np, out);
+  KERNEL_CHECK();
+}
+
+void scale_terms(long long n, const double* x, const double* b, const double* lam, double* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_scale_terms, grid_for(n, 256), 256, 0, s, n, x, b, lam, out);
+  KERNEL_CHECK();
+}
+
+}  // namespace launch
+}  // namespace g2ohip
+
+// ------------------------------------------------------------------------------ small helpers
+namespace g2ohip {
+__global__ void k_set_scalars(double* __restrict__ p, double lam, double lam_rank) {
+  p[0] = lam;
+  p[4] = lam_rank;
+  p[5] = 0.0;
+}
+// max |diag| over nb blocks of dim x dim (col-major), partial per block of threads
+__global__ void __launch_bounds__(256) k_diag_absmax(const double* __restrict__ H, int nb, int dim,
+                                                     double* __restrict__ out) {
+  __shared__ double sh[256];
+  double m = 0.0;
+  for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < (long long)nb * dim; k += (long long)gridDim.x * 256) {
+    const long long blk = k / dim, d = k % dim;
+    m = fmax(m, fabs(H[blk * dim * dim + d * dim + d]));
+  }
+  sh[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
+}
+__global__ void k_max_final(const double* __restrict__ partial, int np, double* __restrict__ out) {
+  double m = 0.0;
+  for (int i = 0; i < np; ++i) m = fmax(m, partial[i]);
+  *out = m;
+}
+namespace launch {
+void set_scalars(double* p, double lam, double lam_rank, hipStream_t s) {
+  hipLaunchKernelGGL(k_set_scalars, 1, 1, 0, s, p, lam, lam_rank);
+  KERNEL_CHECK();
+}
+// writes max|diag| of two block sets into out (partial needs >= 64 doubles)
+void diag_absmax(const double* H1, int nb1, int d1, const double* H2, int nb2, int d2, double* partial, double* out,
+                 hipStream_t s) {
+  const int g = 32;
+  hipLaunchKernelGGL(k_diag_absmax, g, 256, 0, s, H1, nb1, d1, partial);
+  if (H2 && nb2 > 0) hipLaunchKernelGGL(k_diag_absmax, g, 256, 0, s, H2, nb2, d2, partial + g);
+  else hipLaunchKernelGGL(k_diag_absmax, g, 256, 0, s, H1, 0, d1, partial + g);
+  hipLaunchKernelGGL(k_max_final, 1, 1, 0, s, partial, 2 * g, out);
+  KERNEL_CHECK();
+}
+}  // namespace launch
+}  // namespace g2ohip

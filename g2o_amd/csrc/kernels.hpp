@@ -1,0 +1,64 @@
+// Host-side launchers for the kernels in kernels.hip and cholesky.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace g2ohip {
+
+enum Family { FAM_NONE = 0, FAM_BA = 1, FAM_SE3 = 2, FAM_SE2 = 3 };
+
+struct EdgeArgs {
+  const int* v0;
+  const int* v1;
+  const double* meas;
+  const double* info;
+  const double* params;
+  const double* s0;
+  const double* s1;
+};
+
+namespace launch {
+void error(int family, const EdgeArgs& a, int ne, double* chi, hipStream_t s);
+void linearize(int family, const EdgeArgs& a, int ne, const int* h0, const int* h1, double* slot0, double* slot1,
+               const long long* off_dst, const unsigned char* off_tr, double* off_base, hipStream_t s);
+void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, const double* s0, const double* s1,
+                   int st0, int st1, double* H, double* b, const int* boff, hipStream_t s);
+void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const double* slots, double* out,
+                     const long long* dst, hipStream_t s);
+void schur_dinv(int nl, const int* lm_ptr, const double* Hll, const double* Hpl, const double* lam, double* Dinv,
+                double* W, int* fail, hipStream_t s);
+void schur_pairs(int nS, const int* s_ptr, const int* pairs, const int* s_hpp, const unsigned char* s_diag,
+                 const int* s_row, const double* Hpp, const double* W, const double* Hpl, const int* blk_lm,
+                 const double* b, int size_poses, const double* lam, double* S, double* bschur, hipStream_t s);
+void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
+             int size_poses, double* x, hipStream_t s);
+void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s);
+size_t sum_partials(long long n);
+void sum(const double* v, long long n, double* partial, double* out, hipStream_t s);
+void scale_terms(long long n, const double* x, const double* b, const double* lam, double* out, hipStream_t s);
+void set_scalars(double* p, double lam, double lam_rank, hipStream_t s);
+void diag_absmax(const double* H1, int nb1, int d1, const double* H2, int nb2, int d2, double* partial, double* out,
+                 hipStream_t s);
+
+// ---- supernodal multifrontal Cholesky (cholesky.hip) ----
+struct FrontDesc {  // device view of one supernode (see symbolic.hpp)
+  long long front_off;
+  long long vec_off;
+  long long rows_off;
+  int c0, ns, nr, parent;
+  int child_begin, child_end;  // into the children array
+};
+void chol_scatter(long long nent, const double* vals, const long long* dst, const unsigned char* is_diag,
+                  const double* lam, double* fronts, hipStream_t s);
+void chol_level(int nfronts, const int* level_list, const FrontDesc* fd, const int* children, const int* relmap,
+                double* fronts, int* fail, int max_m, hipStream_t s);
+void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]
+void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]
+void chol_forward(int nfronts, const int* level_list, const FrontDesc* fd, const int* children, const int* relmap,
+                  const double* fronts, double* vecs, const double* rhs, hipStream_t s);
+void chol_backward(int nfronts, const int* level_list, const FrontDesc* fd, const int* rows, const double* fronts,
+                   const double* vecs, double* xsol, hipStream_t s);
+}  // namespace launch
+}  // namespace g2ohip

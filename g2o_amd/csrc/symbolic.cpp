@@ -1,0 +1,378 @@
+// Host-side symbolic analysis (see symbolic.hpp).
+#include "symbolic.hpp"
+
+#include <algorithm>
+#include <cassert>
+#include <cstdio>
+#include <numeric>
+#include <stdexcept>
+
+namespace g2ohip {
+namespace {
+
+struct NDState {
+  const BlockPattern& P;
+  std::vector<int> part;   // subgraph id per vertex
+  std::vector<int> order;  // output order (new -> old)
+  std::vector<int> dist, mark;
+  int next_id = 1;
+  int leaf;
+  explicit NDState(const BlockPattern& p, int leaf_) : P(p), part(p.nb, 0), dist(p.nb, -1), mark(p.nb, 0), leaf(leaf_) {}
+
+  // Exact minimum-degree elimination on a small vertex set.
+  void min_degree(const std::vector<int>& vs) {
+    const int n = (int)vs.size();
+    if (n == 0) return;
+    std::vector<int> local(P.nb, -1);
+    for (int k = 0; k < n; ++k) local[vs[k]] = k;
+    std::vector<std::vector<char>> adj(n, std::vector<char>(n, 0));
+    for (int k = 0; k < n; ++k) {
+      int v = vs[k];
+      for (int p = P.adjp[v]; p < P.adjp[v + 1]; ++p) {
+        int u = P.adji[p];
+        if (part[u] == part[v] && local[u] >= 0) adj[k][local[u]] = 1;
+      }
+    }
+    std::vector<char> alive(n, 1);
+    for (int step = 0; step < n; ++step) {
+      int best = -1, bd = 1 << 30;
+      for (int k = 0; k < n; ++k)
+        if (alive[k]) {
+          int d = 0;
+          for (int u = 0; u < n; ++u) d += alive[u] && adj[k][u];
+          if (d < bd) { bd = d; best = k; }
+        }
+      alive[best] = 0;
+      order.push_back(vs[best]);
+      std::vector<int> nb;
+      for (int u = 0; u < n; ++u)
+        if (alive[u] && adj[best][u]) nb.push_back(u);
+      for (int a : nb)
+        for (int b : nb)
+          if (a != b) adj[a][b] = 1;
+    }
+  }
+
+  // BFS restricted to the subgraph `id`; returns level lists.
+  std::vector<std::vector<int>> bfs_levels(int root, int id) {
+    std::vector<std::vector<int>> levels;
+    std::vector<int> cur{root}, touched{root};
+    dist[root] = 0;
+    while (!cur.empty()) {
+      levels.push_back(cur);
+      std::vector<int> nxt;
+      for (int v : cur)
+        for (int p = P.adjp[v]; p < P.adjp[v + 1]; ++p) {
+          int u = P.adji[p];
+          if (part[u] == id && dist[u] < 0) {
+            dist[u] = dist[v] + 1;
+            nxt.push_back(u);
+            touched.push_back(u);
+          }
+        }
+      cur.swap(nxt);
+    }
+    for (int v : touched) dist[v] = -1;
+    return levels;
+  }
+
+  void run(std::vector<int> vs, int id) {
+    if ((int)vs.size() <= leaf) {
+      min_degree(vs);
+      return;
+    }
+    // connected components inside the subgraph
+    {
+      auto lv = bfs_levels(vs[0], id);
+      size_t cnt = 0;
+      for (auto& l : lv) cnt += l.size();
+      if (cnt < vs.size()) {
+        int cid = next_id++;
+        for (auto& l : lv)
+          for (int v : l) part[v] = cid;
+        std::vector<int> a, rest;
+        for (int v : vs) (part[v] == cid ? a : rest).push_back(v);
+        int rid = next_id++;
+        for (int v : rest) part[v] = rid;
+        run(a, cid);
+        run(rest, rid);
+        return;
+      }
+    }
+    // pseudo-peripheral root: repeat BFS from the last level's min-degree vertex
+    int root = vs[0];
+    int depth = 0;
+    for (int it = 0; it < 4; ++it) {
+      auto lv = bfs_levels(root, id);
+      if ((int)lv.size() <= depth) break;
+      depth = (int)lv.size();
+      int best = lv.back()[0], bd = 1 << 30;
+      for (int v : lv.back()) {
+        int d = P.adjp[v + 1] - P.adjp[v];
+        if (d < bd) { bd = d; best = v; }
+      }
+      root = best;
+    }
+    auto lv = bfs_levels(root, id);
+    const int h = (int)lv.size();
+    if (h < 3) {  // nearly complete graph: no useful separator
+      min_degree(vs);
+      return;
+    }
+    const int N = (int)vs.size();
+    std::vector<int> before(h + 1, 0);
+    for (int k = 0; k < h; ++k) before[k + 1] = before[k] + (int)lv[k].size();
+    int kbest = -1;
+    double best = 1e300;
+    for (int k = 1; k < h - 1; ++k) {
+      const int a = before[k], b = N - before[k + 1];
+      if (a < 0.2 * N || b < 0.2 * N) continue;
+      const double cost = (double)lv[k].size() * (1.0 + std::abs(a - b) / (double)N);
+      if (cost < best) { best = cost; kbest = k; }
+    }
+    if (kbest < 0) {  // fall back to the median level
+      for (int k = 1; k < h - 1; ++k)
+        if (before[k + 1] >= N / 2) { kbest = k; break; }
+      if (kbest < 0) kbest = h / 2;
+    }
+    // refine: separator = vertices of level k with a neighbour in level k+1
+    int idA = next_id++, idB = next_id++, idS = next_id++;
+    for (int k = 0; k < h; ++k)
+      for (int v : lv[k]) part[v] = k < kbest ? idA : (k == kbest ? idS : idB);
+    std::vector<int> A, B, S;
+    for (int v : lv[kbest]) {
+      bool touchesB = false;
+      for (int p = P.adjp[v]; p < P.adjp[v + 1] && !touchesB; ++p) touchesB = part[P.adji[p]] == idB;
+      if (touchesB) S.push_back(v);
+      else { part[v] = idA; }
+    }
+    for (int k = 0; k < h; ++k)
+      for (int v : lv[k]) {
+        if (part[v] == idA) A.push_back(v);
+        else if (part[v] == idB) B.push_back(v);
+      }
+    run(A, idA);
+    run(B, idB);
+    std::sort(S.begin(), S.end());
+    for (int v : S) order.push_back(v);
+  }
+};
+
+}  // namespace
+
+std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size) {
+  NDState st(P, std::max(leaf_size, 1));
+  std::vector<int> all(P.nb);
+  std::iota(all.begin(), all.end(), 0);
+  st.run(all, 0);
+  if ((int)st.order.size() != P.nb) throw std::runtime_error("nested_dissection: incomplete order");
+  return st.order;
+}
+
+Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, int relax_max_blocks) {
+  const int nb = P.nb;
+  Symbolic S;
+  S.nb = nb;
+  S.n = nb ? P.offset[nb] : 0;
+  if (nb == 0) return S;
+  if (bperm.empty()) bperm = nested_dissection(P);
+  std::vector<int> bpinv(nb);
+  for (int k = 0; k < nb; ++k) bpinv[bperm[k]] = k;
+
+  auto compute_etree = [&](const std::vector<int>& perm, const std::vector<int>& pinv) {
+    std::vector<int> parent(nb, -1), anc(nb, -1);
+    for (int k = 0; k < nb; ++k) {
+      const int old = perm[k];
+      for (int p = P.adjp[old]; p < P.adjp[old + 1]; ++p) {
+        int i = pinv[P.adji[p]];
+        if (i >= k) continue;
+        while (i != -1 && i < k) {  // Liu's algorithm with path compression (cf. cs_etree.c)
+          int nxt = anc[i];
+          anc[i] = k;
+          if (nxt == -1) parent[i] = k;
+          i = nxt;
+        }
+      }
+    }
+    return parent;
+  };
+  // postorder the etree so supernodes are contiguous
+  {
+    std::vector<int> parent = compute_etree(bperm, bpinv);
+    std::vector<int> head(nb, -1), next(nb, -1), post;
+    post.reserve(nb);
+    for (int j = nb - 1; j >= 0; --j)
+      if (parent[j] != -1) { next[j] = head[parent[j]]; head[parent[j]] = j; }
+    std::vector<int> stack;
+    for (int j = 0; j < nb; ++j) {
+      if (parent[j] != -1) continue;
+      stack.push_back(j);
+      while (!stack.empty()) {
+        int p = stack.back();
+        int i = head[p];
+        if (i == -1) { stack.pop_back(); post.push_back(p); }
+        else { head[p] = next[i]; stack.push_back(i); }
+      }
+    }
+    std::vector<int> nperm(nb);
+    for (int k = 0; k < nb; ++k) nperm[k] = bperm[post[k]];
+    bperm.swap(nperm);
+    for (int k = 0; k < nb; ++k) bpinv[bperm[k]] = k;
+  }
+  std::vector<int> parent = compute_etree(bperm, bpinv);
+  S.bperm = bperm;
+  S.bpinv = bpinv;
+  S.bdim_new.resize(nb);
+  S.boffset_new.assign(nb + 1, 0);
+  for (int k = 0; k < nb; ++k) {
+    S.bdim_new[k] = P.dim[bperm[k]];
+    S.boffset_new[k + 1] = S.boffset_new[k] + S.bdim_new[k];
+  }
+  S.perm.resize(S.n);
+  S.pinv.resize(S.n);
+  for (int k = 0; k < nb; ++k)
+    for (int d = 0; d < S.bdim_new[k]; ++d) {
+      S.perm[S.boffset_new[k] + d] = P.offset[bperm[k]] + d;
+      S.pinv[P.offset[bperm[k]] + d] = S.boffset_new[k] + d;
+    }
+
+  // block structure of L (rows > j), by merging children
+  std::vector<std::vector<int>> st(nb);
+  std::vector<int> nchild(nb, 0), mark(nb, -1);
+  std::vector<std::vector<int>> kids(nb);
+  for (int j = 0; j < nb; ++j)
+    if (parent[j] != -1) { nchild[parent[j]]++; kids[parent[j]].push_back(j); }
+  for (int j = 0; j < nb; ++j) {
+    std::vector<int>& s = st[j];
+    mark[j] = j;
+    const int old = bperm[j];
+    for (int p = P.adjp[old]; p < P.adjp[old + 1]; ++p) {
+      int i = bpinv[P.adji[p]];
+      if (i > j && mark[i] != j) { mark[i] = j; s.push_back(i); }
+    }
+    for (int c : kids[j]) {
+      for (int i : st[c])
+        if (i != j && mark[i] != j) { mark[i] = j; s.push_back(i); }
+    }
+    std::sort(s.begin(), s.end());
+  }
+  // fundamental supernodes
+  std::vector<int> sn_start;
+  for (int j = 0; j < nb; ++j) {
+    bool merge = j > 0 && parent[j - 1] == j && nchild[j] == 1 && st[j - 1].size() == st[j].size() + 1;
+    if (!merge) sn_start.push_back(j);
+  }
+  sn_start.push_back(nb);
+  struct Tmp { int b0, b1; std::vector<int> rows; };  // rows: block rows >= b1
+  std::vector<Tmp> sns;
+  for (size_t s = 0; s + 1 < sn_start.size(); ++s) {
+    Tmp t;
+    t.b0 = sn_start[s];
+    t.b1 = sn_start[s + 1];
+    for (int i : st[t.b1 - 1]) t.rows.push_back(i);  // struct of the last column = rows below
+    sns.push_back(std::move(t));
+  }
+  // relaxed amalgamation: merge a supernode into the next one when it is that one's
+  // (postorder-last) child and the added explicit zeros stay small
+  {
+    std::vector<Tmp> out;
+    for (auto& t : sns) {
+      if (!out.empty()) {
+        Tmp& c = out.back();
+        const int last = c.b1 - 1;
+        if (parent[last] == t.b0) {
+          const double wc = c.b1 - c.b0, wp = t.b1 - t.b0, w = wc + wp;
+          const double rp = (double)t.rows.size(), rc = (double)c.rows.size();
+          const double zeros = wc * (wp + rp - rc);
+          const double total = w * (w + 1) / 2 + w * rp;
+          if (w <= relax_max_blocks && zeros <= relax * total) {
+            c.b1 = t.b1;
+            c.rows = t.rows;
+            continue;
+          }
+        }
+      }
+      out.push_back(std::move(t));
+    }
+    sns.swap(out);
+  }
+  std::vector<std::vector<int>>().swap(st);
+  const int ns_count = (int)sns.size();
+  S.block_sn.assign(nb, -1);
+  for (int s = 0; s < ns_count; ++s)
+    for (int j = sns[s].b0; j < sns[s].b1; ++j) S.block_sn[j] = s;
+  S.sn.resize(ns_count);
+  int64_t roff = 0, foff = 0, voff = 0;
+  for (int s = 0; s < ns_count; ++s) {
+    Supernode& q = S.sn[s];
+    q.b0 = sns[s].b0;
+    q.b1 = sns[s].b1;
+    q.c0 = S.boffset_new[q.b0];
+    q.ns = S.boffset_new[q.b1] - q.c0;
+    q.nr = 0;
+    for (int bi : sns[s].rows) q.nr += S.bdim_new[bi];
+    const int last = q.b1 - 1;
+    q.parent = parent[last] == -1 ? -1 : S.block_sn[parent[last]];
+    q.rows_off = roff;
+    for (int bi : sns[s].rows)
+      for (int d = 0; d < S.bdim_new[bi]; ++d) S.rows.push_back(S.boffset_new[bi] + d);
+    roff += q.nr;
+    const int64_t m = q.ns + q.nr;
+    q.front_off = foff;
+    foff += m * m;
+    q.vec_off = voff;
+    voff += m;
+    S.max_front = std::max<int>(S.max_front, (int)m);
+    for (int k = 0; k < q.ns; ++k) {
+      const double r = (double)(m - k - 1);
+      S.flops += 1 + r + r * (r + 1);  // sqrt, column scale, rank-1 update of the lower trailing part
+    }
+    S.nnzL += (double)q.ns * (q.ns + 1) / 2 + (double)q.ns * q.nr;
+  }
+  S.front_pool = foff;
+  S.vec_pool = voff;
+  // relmap: child's rows -> positions in parent's front
+  S.relmap.assign(roff, -1);
+  for (int s = 0; s < ns_count; ++s) {
+    Supernode& q = S.sn[s];
+    q.rel_off = q.rows_off;
+    if (q.parent < 0) continue;
+    const Supernode& p = S.sn[q.parent];
+    const int* prow = S.rows.data() + p.rows_off;
+    for (int r = 0; r < q.nr; ++r) {
+      const int row = S.rows[q.rows_off + r];
+      int pos;
+      if (row >= p.c0 && row < p.c0 + p.ns) pos = row - p.c0;
+      else {
+        const int* it = std::lower_bound(prow, prow + p.nr, row);
+        if (it == prow + p.nr || *it != row) throw std::runtime_error("symbolic: child row missing in parent");
+        pos = p.ns + (int)(it - prow);
+      }
+      S.relmap[q.rows_off + r] = pos;
+    }
+  }
+  // children lists and levels
+  S.children_ptr.assign(ns_count + 1, 0);
+  for (int s = 0; s < ns_count; ++s)
+    if (S.sn[s].parent >= 0) S.children_ptr[S.sn[s].parent + 1]++;
+  for (int s = 0; s < ns_count; ++s) S.children_ptr[s + 1] += S.children_ptr[s];
+  S.children.assign(S.children_ptr[ns_count], 0);
+  {
+    std::vector<int> fill(S.children_ptr.begin(), S.children_ptr.end() - 1);
+    for (int s = 0; s < ns_count; ++s)
+      if (S.sn[s].parent >= 0) S.children[fill[S.sn[s].parent]++] = s;
+  }
+  int maxlev = 0;
+  for (int s = 0; s < ns_count; ++s) {  // children precede parents (postorder)
+    int lv = 0;
+    for (int k = S.children_ptr[s]; k < S.children_ptr[s + 1]; ++k) lv = std::max(lv, S.sn[S.children[k]].level + 1);
+    S.sn[s].level = lv;
+    maxlev = std::max(maxlev, lv);
+  }
+  S.num_levels = maxlev + 1;
+  S.levels.assign(S.num_levels, {});
+  for (int s = 0; s < ns_count; ++s) S.levels[S.sn[s].level].push_back(s);
+  return S;
+}
+
+}  // namespace g2ohip

@@ -1,0 +1,162 @@
+/*
+ * g2o_hip.h — C ABI of the MI355X-native BlockSolver<p,l> backend (libg2o_hip.so).
+ *
+ * The drop-in boundary is g2o's own plugin interface for this path (paths
+ * relative to the reference tree):
+ *
+ *   Solver (core/solver.h:44-155) ........ g2ohip_solver_*  (buildStructure /
+ *        buildSystem / setLambda / restoreDiagonal / solve / x / b / vectorSize)
+ *   LinearSolver<M>::solve (core/linear_solver.h:42-105) .. g2ohip_linear_solve_ccs
+ *   OptimizationAlgorithmLevenberg::solve (core/optimization_algorithm_levenberg.cpp:58-150)
+ *        + SparseOptimizer::optimize (core/sparse_optimizer.cpp:374-439) ... g2ohip_optimize
+ *   OptimizableGraph::load / save (core/optimizable_graph.cpp:397-679) .. g2ohip_load_g2o / g2ohip_save_g2o
+ *   OptimizationAlgorithmFactory::construct (core/optimization_algorithm_factory.cpp:84-93)
+ *        .. g2ohip_set_algorithm("lm_hip_fix6_3" | "lm_hip_fix3_3" | "lm_hip_fix6_6" | "lm_hip_var" | "gn_hip_*")
+ *   G2OBatchStatistics (core/batch_stats.h:42-72) .. g2ohip_batch_stats
+ *
+ * Plain pointers and sizes only; no torch / HIP types cross the boundary.
+ * Errors follow the reference: no exceptions, int status codes; a solve that
+ * meets a non-positive-definite pivot returns 0 (the reference's `false`,
+ * linear_solver_csparse.h:127-133) so the LM retry logic is unchanged.
+ * Every compute entry point requires a MI355X (gfx950); there is no CPU path.
+ */
+#ifndef G2O_HIP_H
+#define G2O_HIP_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- vertex types (estimate layouts) ---- */
+#define G2OHIP_V_SE3_EXPMAP 1 /* VertexSE3Expmap, types_six_dof_expmap.h:84-102: tx ty tz qx qy qz qw (world->cam) */
+#define G2OHIP_V_XYZ 2        /* VertexSBAPointXYZ, types_sba.h:137: x y z */
+#define G2OHIP_V_SE3_QUAT 3   /* VertexSE3, vertex_se3.h:50: x y z qx qy qz qw (toVectorQT) */
+#define G2OHIP_V_SE2 4        /* VertexSE2, vertex_se2.h:40: x y theta */
+/* ---- edge types ---- */
+#define G2OHIP_E_SE3_PROJECT_XYZ 1 /* EdgeSE3ProjectXYZ, types_six_dof_expmap.h:201-229: v0 point, v1 camera;
+                                      meas u v; info 2x2; params fx fy cx cy */
+#define G2OHIP_E_SE3_QUAT 2        /* EdgeSE3, edge_se3.h: meas x y z qx qy qz qw; info 6x6 */
+#define G2OHIP_E_SE2 3             /* EdgeSE2, edge_se2.h:46-52: meas x y theta; info 3x3 */
+
+/* status codes */
+#define G2OHIP_OK 0
+#define G2OHIP_ERR_ARG (-1)
+#define G2OHIP_ERR_STATE (-2)
+#define G2OHIP_ERR_DEVICE (-3)
+#define G2OHIP_ERR_UNSUPPORTED (-4)
+
+/* G2OBatchStatistics (core/batch_stats.h:42-72) + the current lambda */
+typedef struct {
+  int iteration;
+  int numVertices;
+  int numEdges;
+  double chi2;
+  double lambda;
+  double timeResiduals;
+  double timeQuadraticForm;
+  int levenbergIterations;
+  double timeSchurComplement;
+  double timeSymbolicDecomposition;
+  double timeNumericDecomposition;
+  double timeLinearSolution;
+  double timeLinearSolver;
+  double timeUpdate;
+  double timeIteration;
+  long long hessianDimension;
+  long long hessianPoseDimension;
+  long long hessianLandmarkDimension;
+  long long choleskyNNZ;
+} g2ohip_batch_stats;
+
+/* OptimizationAlgorithmLevenberg properties (optimization_algorithm_levenberg.cpp:48-49) */
+typedef struct {
+  int max_trials_after_failure; /* maxTrialsAfterFailure, default 10 */
+  double user_lambda_init;      /* initialLambda, 0 -> tau * max diag (tau = 1e-5) */
+  int verbose;                  /* SparseOptimizer::setVerbose: per-iteration line on stderr */
+} g2ohip_config;
+
+typedef struct g2ohip_graph g2ohip_graph;
+
+/* ---- graph (OptimizableGraph / SparseOptimizer) ---- */
+g2ohip_graph* g2ohip_graph_create(int device);
+void g2ohip_graph_destroy(g2ohip_graph* g);
+int g2ohip_add_vertices(g2ohip_graph* g, int type, int n, const int* ids, const double* est, const int* fixed,
+                        const int* marginalized);
+int g2ohip_add_edges(g2ohip_graph* g, int type, int n, const int* v0, const int* v1, const double* meas,
+                     const double* info /* n * D*D row-major */, const double* params /* n*4 or NULL */);
+int g2ohip_load_g2o(g2ohip_graph* g, const char* path, int marginalize_xyz);
+int g2ohip_save_g2o(g2ohip_graph* g, const char* path);
+int g2ohip_num_vertices(g2ohip_graph* g);
+int g2ohip_num_edges(g2ohip_graph* g);
+/* estimates of one vertex type in insertion order (syncs device state to host first) */
+int g2ohip_get_estimates(g2ohip_graph* g, int type, double* out, int* ids_out);
+/* overwrite estimates of one vertex type (insertion order) — host-authoritative Solver mode */
+int g2ohip_set_estimates(g2ohip_graph* g, int type, const double* est);
+/* minimal state vector concatenated in vertex-id order (parity checks) */
+int g2ohip_minimal_state(g2ohip_graph* g, double* out);
+
+/* OptimizationAlgorithmFactory::construct by name; default "lm_hip_var" */
+int g2ohip_set_algorithm(g2ohip_graph* g, const char* name);
+/* SparseOptimizer::initializeOptimization(0): active edges/vertices, index mapping */
+int g2ohip_initialize(g2ohip_graph* g);
+/* computeActiveErrors + activeRobustChi2 on the device */
+double g2ohip_chi2(g2ohip_graph* g);
+/* SparseOptimizer::optimize(iterations) with the device-resident LM loop.
+ * stats: array of `iterations` entries or NULL. Returns iterations done, 0 on Fail, <0 on error. */
+int g2ohip_optimize(g2ohip_graph* g, const g2ohip_config* cfg, int iterations, g2ohip_batch_stats* stats);
+/* One iteration of the SparseOptimizer::optimize loop (iteration 0 rebuilds the structure and the
+ * initial lambda, exactly as optimize() does). Returns 0 OK, 1 Terminate, 2 Fail, <0 error. */
+int g2ohip_optimize_step(g2ohip_graph* g, const g2ohip_config* cfg, int iteration, g2ohip_batch_stats* stats);
+
+/* ---- Solver-level plugin (core/solver.h:54-137) for a g2o-side BlockSolverHip adapter ---- */
+int g2ohip_solver_build_structure(g2ohip_graph* g);             /* Solver::buildStructure */
+int g2ohip_solver_build_system(g2ohip_graph* g);                /* Solver::buildSystem */
+int g2ohip_solver_set_lambda(g2ohip_graph* g, double lambda, int backup); /* Solver::setLambda */
+int g2ohip_solver_restore_diagonal(g2ohip_graph* g);            /* Solver::restoreDiagonal */
+int g2ohip_solver_solve(g2ohip_graph* g);                       /* Solver::solve: 1 ok, 0 not PD, <0 error */
+long long g2ohip_solver_vector_size(g2ohip_graph* g);           /* Solver::vectorSize */
+int g2ohip_solver_get_x(g2ohip_graph* g, double* x);            /* Solver::x() (host copy) */
+int g2ohip_solver_get_b(g2ohip_graph* g, double* b);            /* Solver::b() (host copy) */
+/* SparseOptimizer::update(x) + push/pop/discardTop on the device-resident state */
+int g2ohip_update(g2ohip_graph* g, const double* x_host /* NULL: use device x */);
+int g2ohip_push(g2ohip_graph* g);
+int g2ohip_pop(g2ohip_graph* g);
+int g2ohip_discard_top(g2ohip_graph* g);
+
+/* Stage export for parity tests (small problems): after build_system + set_lambda + solve, the
+ * dense reduced system and solution. dims: [n, n_pose_scalars, n_landmark_scalars]. */
+int g2ohip_stage(g2ohip_graph* g, double lambda, double* b, double* x, double* Hschur_dense, double* bschur,
+                 long long* dims);
+
+/* ---- LinearSolver-level plugin (core/linear_solver.h:42-105, LinearSolverCCS) ----
+ * Solve A x = b for symmetric PD A given as UPPER CCS (n, Ap[n+1], Ai, Ax) of scalar entries,
+ * with an optional block partition (nblocks, block_ends[] cumulative end offsets as in
+ * SparseBlockMatrix::rowBlockIndices) used for the block ordering. Returns 1 ok, 0 not PD. */
+int g2ohip_linear_solve_ccs(int device, int n, const int* Ap, const int* Ai, const double* Ax, const double* b,
+                            double* x, int nblocks, const int* block_ends);
+
+/* ---- multi-GPU (landmark sharding + RCCL all-reduce of the reduced camera system) ---- */
+int g2ohip_comm_unique_id(unsigned char out[128]);
+/* this rank keeps landmark shard `rank` of `nranks` (contiguous ranges of the point order) */
+int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int nranks);
+
+/* ---- host-only symbolic analysis (no GPU needed) ----
+ * Block pattern of a symmetric matrix given as upper blocks (bi[k] <= bj[k]) of a uniform block
+ * size bdim: returns n = nblocks*bdim, fills perm[n] (new -> old scalar) and
+ * stats[4] = {nnz(L), factor flops, #supernodes, #levels}. */
+int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int* perm, double* stats);
+
+/* ---- measurement hooks ---- */
+void g2ohip_enable_kernel_timing(g2ohip_graph* g, int on);
+/* per-kernel-class average device time (ms) of the last optimize(); names: "assembly","schur","factor","solve" */
+double g2ohip_kernel_ms(g2ohip_graph* g, const char* name);
+long long g2ohip_kernel_count(g2ohip_graph* g, const char* name);
+/* algorithmic bytes / flops of one launch of the named kernel class (for roofline accounting) */
+double g2ohip_kernel_bytes(g2ohip_graph* g, const char* name);
+double g2ohip_kernel_flops(g2ohip_graph* g, const char* name);
+const char* g2ohip_last_error(void);
+const char* g2ohip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

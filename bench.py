@@ -1,0 +1,220 @@
+"""Benchmark: LM iterations/sec (+ ms per linear solve) of the MI355X BlockSolver
+backend on synthetic BA 1k cameras x 100k points x 1M observations (BASELINE
+config C4), with landmarks sharded over N GPUs (RCCL all-reduce of the reduced
+camera system) when launched with torch.distributed.run.
+
+A "step" is one SparseOptimizer::optimize loop body = one LM outer iteration
+(computeActiveErrors, buildSystem, >=1 trial of setLambda/solve/update/
+restoreDiagonal/computeActiveErrors), all device-resident.  Inputs are resident
+in HBM before the timed region.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_FP64_TFLOPS = 78.6    # MI355X FP64 vector == FP64 matrix (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C4", help="C4 (default, BASELINE metric) or C5/C3/C2/C1")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=2, help="timed oracle LM iterations (after iteration 0)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="OpenMP threads for the CPU baseline (0 = all)")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    return ap.parse_args()
+
+
+def make_problem(cfg):
+    from g2o_amd import synth
+    return synth.by_name(cfg)
+
+
+def dist_setup(n):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def allmax(v, world):
+    if world <= 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bcast_bytes(b, world):
+    if world <= 1:
+        return b
+    import torch.distributed as dist
+    obj = [b]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def cpu_baseline(prob, iters, threads):
+    """The oracle (C++ restatement of BlockSolver + LM) with the reference's own CSparse
+    (oracle/_ref, cs_amd block ordering + LL^T) timed on this host."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle_py
+    nthreads = threads or os.cpu_count() or 1
+    nthreads = min(nthreads, 16)  # the GPU box grants a 16-CPU share
+    g = oracle_py.OracleGraph(prob)
+    cfg = oracle_py.make_config(threads=nthreads, use_ref=True, block_ordering=True)
+    n, st = g.optimize(iters + 1, cfg)
+    timed = st[1:n]
+    if not timed:
+        return None
+    t = sum(s.timeIteration for s in timed)
+    lin = [s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
+    return {
+        "value": len(timed) / t,
+        "unit": "LM it/s",
+        "cores": nthreads,
+        "kind": "port",
+        "ms_per_linear_solve": 1e3 * float(np.median(lin)),
+        "ref_csparse": bool(oracle_py.ref_available()),
+        "sample": f"{len(timed)} LM iterations (after iteration 0) of the same {prob.name} problem: oracle C++ "
+                  f"restatement of BlockSolver/Schur/LM (OpenMP {nthreads} threads for assembly+Schur) with "
+                  f"the reference's vendored CSparse 3.1.0 cs_amd(block)+LL^T ({'loaded' if oracle_py.ref_available() else 'restated'}), single-threaded factorization as in the reference",
+    }
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_setup(args.gpus)
+    import g2o_amd
+
+    t0 = time.time()
+    prob = make_problem(args.config)
+    gen_s = time.time() - t0
+    opt = g2o_amd.SparseOptimizer(local).add_problem(prob)
+    opt.set_algorithm("lm_hip_fix6_3" if prob.landmark_dim else ("lm_hip_fix6_6" if prob.pose_dim == 6 else "lm_hip_fix3_3"))
+    if world > 1:
+        uid = g2o_amd.SparseOptimizer.comm_unique_id() if rank == 0 else None
+        uid = bcast_bytes(uid, world)
+        opt.set_comm(uid, rank, world)
+    try:
+        import torch
+        sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    except Exception:  # torch is plumbing only
+        sync = lambda: None  # noqa: E731
+
+    # warmup: iteration 0 builds the structure (symbolic analysis) and lambda0
+    t0 = time.time()
+    stats = []
+    it = 0
+    for _ in range(max(args.warmup, 1)):
+        r, st = opt.optimize_step(it)
+        stats.append(st)
+        it += 1
+    warm_s = time.time() - t0
+    if not args.no_kernel_timing:
+        opt.enable_kernel_timing(True)
+    barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    timed = []
+    for _ in range(args.steps):
+        r, st = opt.optimize_step(it)
+        timed.append(st)
+        it += 1
+    sync()
+    barrier(world)
+    dt = time.perf_counter() - t0
+    dt = allmax(dt, world)
+    value = args.steps / dt
+    lin_ms = [1e3 * s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
+    trials = sum(s.levenbergIterations for s in timed)
+
+    names = ["linearize", "vreduce", "schur_dinv", "schur_pairs", "chol_factor", "chol_solve", "backsub", "error", "oplus"]
+    kt = {k: {"avg_ms": opt.kernel_ms(k), "count": opt.kernel_count(k)} for k in names}
+    # roofline on the dominant single-dispatch HBM-bound kernel (Schur pair products)
+    dom = "schur_pairs" if prob.landmark_dim else "linearize"
+    avg_ms = kt[dom]["avg_ms"]
+    algo_bytes = opt.kernel_bytes(dom)
+    achieved = algo_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    tf = os.environ.get("G2OHIP_TRAFFIC_JSON")
+    if tf and os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(dom)
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "LM iterations/sec + ms/linear-solve, synthetic BA 1k×100k at 1/2/4/8 GPUs",
+        "value": value,
+        "unit": "LM it/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps,
+        "ms_per_linear_solve": float(np.median(lin_ms)),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (numpy Philox seed 20261015, BAL-style recipe of ba_demo.cpp; SURVEY.md 8d)",
+        "config": {
+            "workload": f"{args.config}: {prob.name} ({prob.num_vertices} vertices, {prob.num_edges} edges), "
+                        f"BlockSolver_6_3 + Schur, landmarks sharded over {world} GPU(s)",
+            "levenberg_trials": trials,
+            "final_chi2": timed[-1].chi2 if timed else None,
+            "parallelism": f"landmark-shard{world}" if world > 1 else "single",
+        },
+        "stages_ms_avg": {k: v["avg_ms"] for k, v in kt.items()},
+        "roofline": {
+            "kernel": dom,
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": achieved / PEAK_HBM_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": algo_bytes,
+            "avg_launch_ms": avg_ms,
+        },
+        "setup_s": {"generate": gen_s, "warmup_incl_structure": warm_s},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(prob, args.cpu_iters, args.cpu_threads)
+        except Exception as ex:  # reported, not fatal
+            out["cpu_baseline"] = {"error": repr(ex)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -209,8 +209,8 @@ int g2ohip_linear_solve_ccs(int device, int n, const int* Ap, const int* Ai, con
       dl.upload(zero, s);
       df.resize(1);
       df.zero(s);
-      ch.factor(dv.get(), dl.get(), df.get(), s);
-      ch.solve(db.get(), dx.get(), s);
+      ch.factor(dv.get(), dl.get(), db.get(), df.get(), s);
+      ch.solve(dx.get(), s);
       int f = 0;
       HIP_CHECK(hipMemcpyAsync(&f, df.get(), sizeof f, hipMemcpyDeviceToHost, s));
       dx.download(x, n, s);

@@ -264,6 +264,52 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     level_off.push_back((int)ll.size());
   }
   level_lists.upload(ll, s);
+  // work lists: per level one extend-add op, then (panel, trailing) ops per 32-wide panel
+  {
+    using launch::Task;
+    const int NB = launch::CHOL_NB, TT = launch::CHOL_TT, EA = launch::CHOL_EA;
+    std::vector<Task> tk;
+    ops.clear();
+    for (auto& lv : sym.levels) {
+      Op ea{0, (int)tk.size(), 0};
+      for (int sn : lv) {
+        const Supernode& q = sym.sn[sn];
+        if (sym.children_ptr[sn + 1] == sym.children_ptr[sn]) continue;
+        const int m = q.ns + q.nr;
+        for (int a = 0; a < m; a += EA) tk.push_back(Task{sn, a, std::min(a + EA, m), 0});
+      }
+      ea.count = (int)tk.size() - ea.off;
+      if (ea.count) ops.push_back(ea);
+      int maxp = 0;
+      for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
+      for (int p = 0; p < maxp; ++p) {
+        Op pa{1, (int)tk.size(), 0};
+        for (int sn : lv) {
+          const Supernode& q = sym.sn[sn];
+          const int k0 = p * NB;
+          if (k0 >= q.ns) continue;
+          const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
+          const int nwg = std::max(1, (m - r0 + 255) / 256);
+          for (int w = 0; w < nwg; ++w) tk.push_back(Task{sn, k0, r0 + w * 256, kb});
+        }
+        pa.count = (int)tk.size() - pa.off;
+        if (pa.count) ops.push_back(pa);
+        Op tr{2, (int)tk.size(), 0};
+        for (int sn : lv) {
+          const Supernode& q = sym.sn[sn];
+          const int k0 = p * NB;
+          if (k0 >= q.ns) continue;
+          const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
+          const int T = (m - r0 + TT - 1) / TT;
+          for (int tj = 0; tj < T; ++tj)
+            for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, k0, ti | (tj << 16), kb});
+        }
+        tr.count = (int)tk.size() - tr.off;
+        if (tr.count) ops.push_back(tr);
+      }
+    }
+    tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
+  }
   children.upload(sym.children.empty() ? std::vector<int>{0} : sym.children, s);
   relmap.upload(sym.relmap.empty() ? std::vector<int>{0} : sym.relmap, s);
   rows.upload(sym.rows.empty() ? std::vector<int>{0} : sym.rows, s);
@@ -271,30 +317,32 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   fronts.resize(std::max<int64_t>(sym.front_pool, 1));
   vecs.resize(std::max<int64_t>(sym.vec_pool, 1));
   rhs_p.resize(std::max(sym.n, 1));
+  y_p.resize(std::max(sym.n, 1));
+  ldiag.resize(std::max(sym.n, 1));
   x_p.resize(std::max(sym.n, 1));
 }
 
-void DeviceCholesky::factor(const double* vals, const double* lam, int* fail, hipStream_t s) {
+void DeviceCholesky::factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s) {
+  launch::chol_permute(sym.n, perm.get(), rhs, rhs_p.get(), s);
+  launch::chol_vec_init((int)sym.sn.size(), fd.get(), rhs_p.get(), vecs.get(), s);
   HIP_CHECK(hipMemsetAsync(fronts.get(), 0, fronts.bytes(), s));
   launch::chol_scatter(nent, vals, dst.get(), isdiag.get(), lam, fronts.get(), s);
-  for (size_t l = 0; l + 1 < level_off.size(); ++l) {
-    const int nf = level_off[l + 1] - level_off[l];
-    launch::chol_level(nf, level_lists.get() + level_off[l], fd.get(), children.get(), relmap.get(), fronts.get(), fail,
-                       sym.max_front, s);
+  for (const Op& op : ops) {
+    const launch::Task* t = tasks.get() + op.off;
+    if (op.kind == 0)
+      launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), fronts.get(), vecs.get(), s);
+    else if (op.kind == 1)
+      launch::chol_panel(op.count, t, fd.get(), fronts.get(), vecs.get(), y_p.get(), ldiag.get(), fail, s);
+    else
+      launch::chol_trail(op.count, t, fd.get(), fronts.get(), s);
   }
 }
 
-void DeviceCholesky::solve(const double* rhs, double* x, hipStream_t s) {
-  launch::chol_permute(sym.n, perm.get(), rhs, rhs_p.get(), s);
-  for (size_t l = 0; l + 1 < level_off.size(); ++l) {
-    const int nf = level_off[l + 1] - level_off[l];
-    launch::chol_forward(nf, level_lists.get() + level_off[l], fd.get(), children.get(), relmap.get(), fronts.get(),
-                         vecs.get(), rhs_p.get(), s);
-  }
+void DeviceCholesky::solve(double* x, hipStream_t s) {
   for (size_t l = level_off.size() - 1; l-- > 0;) {
     const int nf = level_off[l + 1] - level_off[l];
-    launch::chol_backward(nf, level_lists.get() + level_off[l], fd.get(), rows.get(), fronts.get(), vecs.get(),
-                          x_p.get(), s);
+    launch::chol_backward(nf, level_lists.get() + level_off[l], fd.get(), rows.get(), fronts.get(), y_p.get(), ldiag.get(),
+                          x_p.get(), sym.max_front, s);
   }
   launch::chol_ipermute(sym.n, perm.get(), x_p.get(), x, s);
 }
@@ -986,11 +1034,11 @@ void Engine::solve_async() {  // block_solver.hpp:314-447
   if (!do_schur) {
     HIP_CHECK(hipEventRecord(ev_[1], stream));
     timer.begin("chol_factor", stream);
-    chol.factor(dH.get(), dscal.get(), dfail.get(), stream);
+    chol.factor(dH.get(), dscal.get(), db.get(), dfail.get(), stream);
     timer.end(stream);
     HIP_CHECK(hipEventRecord(ev_[2], stream));
     timer.begin("chol_solve", stream);
-    chol.solve(db.get(), dx.get(), stream);
+    chol.solve(dx.get(), stream);
     timer.end(stream);
     HIP_CHECK(hipEventRecord(ev_[3], stream));
     return;
@@ -1010,11 +1058,11 @@ void Engine::solve_async() {  // block_solver.hpp:314-447
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
   HIP_CHECK(hipEventRecord(ev_[1], stream));
   timer.begin("chol_factor", stream);
-  chol.factor(S, dscal.get() + 5, dfail.get(), stream);
+  chol.factor(S, dscal.get() + 5, bschur, dfail.get(), stream);
   timer.end(stream);
   HIP_CHECK(hipEventRecord(ev_[2], stream));
   timer.begin("chol_solve", stream);
-  chol.solve(bschur, dx.get(), stream);
+  chol.solve(dx.get(), stream);
   timer.end(stream);
   HIP_CHECK(hipEventRecord(ev_[3], stream));
   timer.begin("backsub", stream);

@@ -54,10 +54,15 @@ struct DeviceCholesky {
   DevBuf<launch::FrontDesc> fd;
   DevBuf<int> level_lists, children, relmap, rows, perm;
   std::vector<int> level_off;  // host offsets into level_lists
-  DevBuf<double> fronts, vecs, rhs_p, x_p;
+  struct Op { int kind, off, count; };  // kind 0 extend-add, 1 panel, 2 trailing update
+  std::vector<Op> ops;
+  DevBuf<launch::Task> tasks;
+  DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, ldiag;
   void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
-  void factor(const double* vals, const double* lam, int* fail, hipStream_t s);
-  void solve(const double* rhs, double* x, hipStream_t s);
+  // numeric LL^T fused with the forward solve of rhs (y = L^-1 P rhs)
+  void factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s);
+  // backward solve x = P^T L^-T y
+  void solve(double* x, hipStream_t s);
 };
 
 struct KernelTimer {

@@ -50,15 +50,21 @@ struct FrontDesc {  // device view of one supernode (see symbolic.hpp)
   int c0, ns, nr, parent;
   int child_begin, child_end;  // into the children array
 };
+struct Task {  // one workgroup's work item (meaning per kernel, see cholesky.hip)
+  int s, a, b, c;
+};
 void chol_scatter(long long nent, const double* vals, const long long* dst, const unsigned char* is_diag,
                   const double* lam, double* fronts, hipStream_t s);
-void chol_level(int nfronts, const int* level_list, const FrontDesc* fd, const int* children, const int* relmap,
-                double* fronts, int* fail, int max_m, hipStream_t s);
+void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double* vecs, hipStream_t s);
+void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
+                     double* fronts, double* vecs, hipStream_t s);
+void chol_panel(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, double* vecs, double* ysol, double* ldiag,
+                int* fail, hipStream_t s);
+void chol_trail(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, hipStream_t s);
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]
 void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]
-void chol_forward(int nfronts, const int* level_list, const FrontDesc* fd, const int* children, const int* relmap,
-                  const double* fronts, double* vecs, const double* rhs, hipStream_t s);
 void chol_backward(int nfronts, const int* level_list, const FrontDesc* fd, const int* rows, const double* fronts,
-                   const double* vecs, double* xsol, hipStream_t s);
+                   const double* ysol, const double* ldiag, double* xsol, int max_m, hipStream_t s);
+constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 32;
 }  // namespace launch
 }  // namespace g2ohip

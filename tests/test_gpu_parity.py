@@ -1,0 +1,176 @@
+"""GPU parity tests: the HIP backend (through the C ABI) against the oracle.
+
+Tolerance (north_star): state vector and final chi2 within 1e-6 relative of the
+CSparse reference path; the stage-level checks (reduced system, solution) use
+1e-9 because both sides do the same fp64 arithmetic in a different order.
+"""
+import numpy as np
+import pytest
+
+from g2o_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+STATE_RTOL = 1e-6
+CHI2_RTOL = 1e-6
+
+
+def _run_both(g2o_amd_mod, oracle, prob, iters, threads=8):
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    n, st = opt.optimize(iters)
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.optimize(iters, oracle.make_config(threads=threads))
+    return opt, n, st, ref, nr, sr
+
+
+def _check(opt, n, st, ref, nr, sr):
+    assert n == nr
+    for a, b in zip(st, sr):
+        assert abs(a.chi2 - b.chi2) <= CHI2_RTOL * abs(b.chi2), (a.chi2, b.chi2)
+        assert a.levenbergIterations == b.levenbergIterations
+    xg, xr = opt.minimal_state(), ref.minimal_state()
+    rel = np.linalg.norm(xg - xr) / np.linalg.norm(xr)
+    assert rel <= STATE_RTOL, rel
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "C3", "C4", "C5"])
+def test_lm_trajectory_small(g2o_amd_mod, oracle, name):
+    prob = synth.by_name(name, "small")
+    _check(*_run_both(g2o_amd_mod, oracle, prob, 6))
+
+
+def test_ba_sphere2500_full(g2o_amd_mod, oracle):
+    """C1 at its real size (sphere2500 recipe, 2500 poses / 9799 edges)."""
+    prob = synth.by_name("C1")
+    _check(*_run_both(g2o_amd_mod, oracle, prob, 5))
+
+
+@pytest.mark.slow
+def test_c4_full_size_parity(g2o_amd_mod, oracle):
+    """BASELINE config C4 at full size (1k cameras x 100k points x 1M observations)."""
+    prob = synth.by_name("C4")
+    _check(*_run_both(g2o_amd_mod, oracle, prob, 2, threads=16))
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "C4"])
+def test_stage_reduced_system(g2o_amd_mod, oracle, name):
+    prob = synth.by_name(name, "small")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    ref = oracle.OracleGraph(prob)
+    lam = 1e-3
+    g = opt.stage(lam)
+    r = ref.stage(lam)
+    assert g["ok"] == r["ok"] == 1
+    for k in ("b", "bschur", "x"):
+        assert np.linalg.norm(g[k] - r[k]) <= 1e-9 * np.linalg.norm(r[k]), k
+    assert np.linalg.norm(g["Hschur"] - r["Hschur"]) <= 1e-11 * np.linalg.norm(r["Hschur"])
+
+
+def test_solver_plugin_interface(g2o_amd_mod, oracle):
+    """Solver-level contract (core/solver.h): buildStructure / buildSystem / setLambda / solve /
+    x() / b() / restoreDiagonal, driven step by step like OptimizationAlgorithmLevenberg."""
+    prob = synth.by_name("C4", "small")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.initialize_optimization()
+    opt.build_structure()
+    opt.build_system()
+    opt.set_lambda(1e-2, True)
+    assert opt.solve()
+    x = opt.x()
+    b = opt.b()
+    opt.restore_diagonal()
+    r = oracle.OracleGraph(prob).stage(1e-2)
+    assert np.linalg.norm(x - r["x"]) <= 1e-9 * np.linalg.norm(r["x"])
+    assert np.linalg.norm(b - r["b"]) <= 1e-12 * np.linalg.norm(r["b"])
+    # update / push / pop on the device-resident state
+    s0 = opt.minimal_state()
+    lib = g2o_amd_mod.lib()
+    assert lib.g2ohip_push(opt.h) == 0
+    assert lib.g2ohip_update(opt.h, None) == 0
+    assert not np.array_equal(opt.minimal_state(), s0)
+    assert lib.g2ohip_pop(opt.h) == 0
+    assert np.array_equal(opt.minimal_state(), s0)
+
+
+def test_linear_solver_ccs(g2o_amd_mod):
+    rng = np.random.default_rng(3)
+    n = 90
+    A = rng.standard_normal((n, n)) * (rng.random((n, n)) < 0.1)
+    A = A @ A.T + n * np.eye(n)
+    Ap, Ai, Ax = [0], [], []
+    for j in range(n):
+        rows = np.nonzero(A[: j + 1, j])[0]
+        Ai += rows.tolist()
+        Ax += A[rows, j].tolist()
+        Ap.append(len(Ai))
+    b = rng.standard_normal(n)
+    ok, x = g2o_amd_mod.linear_solve_ccs(n, Ap, Ai, Ax, b, block_dim=3)
+    assert ok
+    np.testing.assert_allclose(A @ x, b, rtol=1e-10, atol=1e-10)
+    # not positive definite -> false (linear_solver_csparse.h:127-133)
+    Ax2 = list(Ax)
+    Ax2[Ap[5]:Ap[6]][-1:] = [-1.0]
+    for k in range(Ap[5], Ap[6]):
+        if Ai[k] == 5:
+            Ax2[k] = -50.0
+    ok2, _ = g2o_amd_mod.linear_solve_ccs(n, Ap, Ai, Ax2, b, block_dim=3)
+    assert not ok2
+
+
+def test_g2o_file_roundtrip_parity(g2o_amd_mod, oracle, tmp_path):
+    prob = synth.by_name("C4", "small")
+    path = str(tmp_path / "ba.g2o")
+    oracle.OracleGraph(prob).save(path)
+    opt = g2o_amd_mod.SparseOptimizer(0)
+    opt.load(path, True)
+    ref = oracle.OracleGraph.load(path, True)
+    n, st = opt.optimize(4)
+    nr, sr = ref.optimize(4)
+    _check(opt, n, st, ref, nr, sr)
+    out = str(tmp_path / "out.g2o")
+    opt.save(out)
+    back = oracle.OracleGraph.load(out, True)
+    np.testing.assert_allclose(back.minimal_state(), opt.minimal_state(), rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["translation", "rotation"])
+def test_reference_optimization_slam3d_on_gpu(g2o_amd_mod, kind):
+    """unit_test/slam3d/optimization_slam3d.cpp:38-126 through the HIP backend."""
+    import math
+    ident = np.array([0, 0, 0, 0, 0, 0, 1.0])
+    if kind == "translation":
+        p2 = np.array([10, 10, 10, 0, 0, 0, 1.0])
+    else:
+        R = synth._axis_angle(np.ones((1, 3)) / math.sqrt(3), np.array([math.radians(2)]))
+        p2 = np.concatenate([np.zeros(3), synth.rot_to_quat(R)[0]])
+    vs = synth.VertexSet(synth.V_SE3_QUAT, np.array([0, 1], np.int32), np.stack([ident, p2]),
+                         np.array([1, 0], np.int32), np.zeros(2, np.int32))
+    es = synth.EdgeSet(synth.E_SE3_QUAT, np.array([0], np.int32), np.array([1], np.int32), ident[None], np.eye(6)[None])
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(synth.Problem("t", [vs], [es], 6, 0))
+    assert opt.chi2() > 0
+    n, st = opt.optimize(100)
+    assert n > 0 and st[-1].chi2 < 1e-6
+    est = opt.estimates(synth.V_SE3_QUAT)[1]
+    assert np.linalg.norm(est[:3]) < 1e-12 and np.linalg.norm(est[3:6]) < 1e-12
+
+
+def test_deterministic_bitwise(g2o_amd_mod):
+    prob = synth.by_name("C4", "small")
+    a = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    b = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    a.optimize(4)
+    b.optimize(4)
+    assert np.array_equal(a.minimal_state(), b.minimal_state())
+
+
+def test_full_size_properties_c4(g2o_amd_mod):
+    """Size-independent properties at the bench size: chi2 decreases monotonically and reaches
+    the noise floor (~ #residuals - #dof for unit pixel noise)."""
+    prob = synth.by_name("C4")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    c0 = opt.chi2()
+    n, st = opt.optimize(8)
+    chis = [c0] + [s.chi2 for s in st]
+    assert all(b <= a for a, b in zip(chis, chis[1:]))
+    dof = 2 * prob.num_edges - (6 * 998 + 3 * 100_000)
+    assert abs(chis[-1] / dof - 1.0) < 0.05

@@ -1,0 +1,179 @@
+"""Pins of the oracle (CPU restatement) against what the reference itself fixes.
+
+* unit_test/slam3d/jacobians_slam3d.cpp:56-81, unit_test/slam2d/jacobians_slam2d.cpp:47-72 and
+  test_helper/evaluate_jacobian.h:40-88: analytic vs numeric (BaseBinaryEdge::linearizeOplus,
+  base_binary_edge.hpp:198-266) Jacobians agree within 1e-6.  The same test is applied to
+  EdgeSE3ProjectXYZ (no reference test exists for it; same strategy).
+* unit_test/slam3d/optimization_slam3d.cpp:38-126: two-vertex EdgeSE3 LM converges to chi2 < 1e-6
+  with the free pose at the identity.
+* The restated CSparse factorization is bitwise identical to the reference's vendored CSparse
+  (oracle/_ref, compiled from /root/reference/EXTERNAL/csparse) with the same cs_amd ordering.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from g2o_amd import synth
+
+RNG = np.random.default_rng(20261015)
+
+
+def _eigen_random(n):  # Eigen::Vector3d::Random(): uniform [-1, 1]
+    return RNG.uniform(-1.0, 1.0, size=n)
+
+
+def random_isometry():
+    """unit_test/slam3d/jacobians_slam3d.cpp:46-54 randomIsometry3d()."""
+    aa = _eigen_random(3) + _eigen_random(3)
+    ang = np.linalg.norm(aa)
+    R = synth._axis_angle(aa[None], np.array([ang]))[0]
+    t = _eigen_random(3)
+    q = synth.rot_to_quat(R[None])[0]
+    return np.concatenate([t, q])
+
+
+def random_se2():
+    """unit_test/slam2d/jacobians_slam2d.cpp randomSE2(): x,y uniform, theta uniform(-pi, pi)."""
+    return np.array([RNG.uniform(-1, 1), RNG.uniform(-1, 1), RNG.uniform(-math.pi, math.pi)])
+
+
+def _two_vertex_problem(vt, et, est, meas, D, d):
+    vs = synth.VertexSet(vt, np.array([0, 1], np.int32), np.asarray(est), np.zeros(2, np.int32), np.zeros(2, np.int32))
+    es = synth.EdgeSet(et, np.array([0], np.int32), np.array([1], np.int32), np.asarray(meas)[None],
+                       np.eye(D)[None])
+    return synth.Problem("j", [vs], [es], d, 0)
+
+
+@pytest.mark.parametrize("trials", [2000])
+def test_edge_se3_jacobian_vs_numeric(oracle, trials):
+    worst = 0.0
+    for _ in range(trials):
+        prob = _two_vertex_problem(synth.V_SE3_QUAT, synth.E_SE3_QUAT, [random_isometry(), random_isometry()],
+                                   random_isometry(), 6, 6)
+        g = oracle.OracleGraph(prob)
+        _, Ja, Jb, Na, Nb = g.edge_jacobians(0, 6, 6, 6)
+        worst = max(worst, np.abs(Ja - Na).max(), np.abs(Jb - Nb).max())
+    assert worst < 1e-6, worst  # evaluate_jacobian.h:60 EXPECT_NEAR(n, a, 1e-6)
+
+
+@pytest.mark.parametrize("trials", [2000])
+def test_edge_se2_jacobian_vs_numeric(oracle, trials):
+    worst = 0.0
+    for _ in range(trials):
+        prob = _two_vertex_problem(synth.V_SE2, synth.E_SE2, [random_se2(), random_se2()], random_se2(), 3, 3)
+        g = oracle.OracleGraph(prob)
+        _, Ja, Jb, Na, Nb = g.edge_jacobians(0, 3, 3, 3)
+        worst = max(worst, np.abs(Ja - Na).max(), np.abs(Jb - Nb).max())
+    assert worst < 1e-6, worst
+
+
+def test_edge_se3_project_xyz_jacobian_vs_numeric(oracle):
+    prob = synth.ba(12, 300, 5, 8)
+    g = oracle.OracleGraph(prob)
+    worst = 0.0
+    for k in range(0, 1500, 3):
+        _, Ja, Jb, Na, Nb = g.edge_jacobians(k, 2, 3, 6)
+        # pixel-scale Jacobians (fx = 1000): compare relative to the focal length
+        worst = max(worst, np.abs(Ja - Na).max() / 1000.0, np.abs(Jb - Nb).max() / 1000.0)
+    assert worst < 1e-6, worst
+
+
+def _iso_vec(R, t):
+    return np.concatenate([t, synth.rot_to_quat(R[None])[0]])
+
+
+@pytest.mark.parametrize("kind", ["translation", "rotation"])
+def test_reference_optimization_slam3d(oracle, kind):
+    """unit_test/slam3d/optimization_slam3d.cpp:38-126 (BlockSolverX + LM, 100 iterations)."""
+    ident = _iso_vec(np.eye(3), np.zeros(3))
+    if kind == "translation":
+        p2 = _iso_vec(np.eye(3), np.array([10.0, 10.0, 10.0]))
+    else:
+        R = synth._axis_angle(np.ones((1, 3)) / math.sqrt(3), np.array([math.radians(2)]))[0]
+        p2 = _iso_vec(R, np.zeros(3))
+    vs = synth.VertexSet(synth.V_SE3_QUAT, np.array([0, 1], np.int32), np.stack([ident, p2]),
+                         np.array([1, 0], np.int32), np.zeros(2, np.int32))
+    es = synth.EdgeSet(synth.E_SE3_QUAT, np.array([0], np.int32), np.array([1], np.int32), ident[None], np.eye(6)[None])
+    g = oracle.OracleGraph(synth.Problem("t", [vs], [es], 6, 0))
+    assert g.chi2() > 0.0
+    n, st = g.optimize(100, oracle.make_config(block_ordering=False))
+    assert n > 0
+    assert st[-1].chi2 < 1e-6
+    est = g.estimates(synth.V_SE3_QUAT)[1]
+    assert np.linalg.norm(est[:3]) < 1e-12  # ASSERT_DOUBLE_EQ(0, |t|) in the reference
+    assert np.linalg.norm(est[3:6]) < 1e-12   # rotation == identity
+
+
+def _random_spd_ccs(n, density, rng):
+    A = np.zeros((n, n))
+    mask = rng.random((n, n)) < density
+    A[mask] = rng.standard_normal(mask.sum())
+    A = A @ A.T + n * np.eye(n)
+    Ap, Ai, Ax = [0], [], []
+    for j in range(n):
+        rows = np.nonzero(A[: j + 1, j])[0]
+        Ai.extend(rows.tolist())
+        Ax.extend(A[rows, j].tolist())
+        Ap.append(len(Ai))
+    return A, np.array(Ap), np.array(Ai), np.array(Ax)
+
+
+def test_restated_cholesky_bitwise_equals_reference_csparse(oracle):
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref (reference CSparse) not built")
+    rng = np.random.default_rng(7)
+    for n in (1, 5, 40, 150):
+        A, Ap, Ai, Ax = _random_spd_ccs(n, 0.08, rng)
+        b = rng.standard_normal(n)
+        r1, x1 = oracle.ccs_cholsol(n, Ap, Ai, Ax, b, mode=1)  # restated LL^T, cs_amd order
+        r2, x2 = oracle.ccs_cholsol(n, Ap, Ai, Ax, b, mode=2)  # reference cs_cholsol
+        assert r1 == r2 == 1
+        assert np.array_equal(x1, x2)  # bitwise
+        np.testing.assert_allclose(A @ x1, b, rtol=1e-9, atol=1e-9)
+
+
+def test_restated_cholesky_detects_not_pd(oracle):
+    n = 4
+    A = np.diag([1.0, 2.0, -3.0, 4.0])
+    Ap = np.arange(n + 1)
+    Ai = np.arange(n)
+    r, _ = oracle.ccs_cholsol(n, Ap, Ai, np.diag(A), np.ones(n), mode=0)
+    assert r == 0
+    if oracle.ref_available():
+        r2, _ = oracle.ccs_cholsol(n, Ap, Ai, np.diag(A), np.ones(n), mode=2)
+        assert r2 == 0
+
+
+@pytest.mark.parametrize("name", ["C1", "C2", "C3", "C4"])
+def test_oracle_ordering_independence(oracle, name):
+    """cs_amd block ordering (reference) vs natural ordering: same LM trajectory up to roundoff."""
+    prob = synth.by_name(name, "small")
+    a = oracle.OracleGraph(prob)
+    b = oracle.OracleGraph(prob)
+    na, sa = a.optimize(4, oracle.make_config(use_ref=True))
+    nb, sb = b.optimize(4, oracle.make_config(use_ref=False))
+    assert na == nb
+    for x, y in zip(sa, sb):
+        assert abs(x.chi2 - y.chi2) <= 1e-9 * abs(y.chi2)
+    xa, xb = a.minimal_state(), b.minimal_state()
+    assert np.linalg.norm(xa - xb) <= 1e-9 * np.linalg.norm(xb)
+
+
+def test_g2o_roundtrip(oracle, tmp_path):
+    prob = synth.by_name("C4", "small")
+    g = oracle.OracleGraph(prob)
+    p = str(tmp_path / "ba.g2o")
+    g.save(p)
+    h = oracle.OracleGraph.load(p, marginalize_xyz=True)
+    np.testing.assert_allclose(h.minimal_state(), g.minimal_state(), rtol=0, atol=1e-12)
+    assert abs(h.chi2() - g.chi2()) <= 1e-10 * g.chi2()
+
+
+def test_oracle_deterministic_single_thread(oracle):
+    prob = synth.by_name("C4", "small")
+    a = oracle.OracleGraph(prob)
+    b = oracle.OracleGraph(prob)
+    a.optimize(3)
+    b.optimize(3)
+    assert np.array_equal(a.minimal_state(), b.minimal_state())

@@ -48,7 +48,7 @@ EXPORTS = [
     "g2ohip_solver_restore_diagonal", "g2ohip_solver_solve", "g2ohip_solver_vector_size",
     "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
     "g2ohip_discard_top", "g2ohip_stage", "g2ohip_linear_solve_ccs", "g2ohip_comm_unique_id",
-    "g2ohip_set_comm", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing", "g2ohip_kernel_ms",
+    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing", "g2ohip_kernel_ms",
     "g2ohip_kernel_count", "g2ohip_kernel_bytes", "g2ohip_kernel_flops", "g2ohip_last_error",
     "g2ohip_version",
 ]
@@ -103,6 +103,7 @@ def lib() -> C.CDLL:
         "g2ohip_linear_solve_ccs": ([I, I, P, P, P, P, P, I, P], I),
         "g2ohip_comm_unique_id": ([P], I),
         "g2ohip_set_comm": ([P, P, I, I], I),
+        "g2ohip_set_comm_local": ([P, C.c_char_p, I, I], I),
         "g2ohip_symbolic_analyze": ([I, I, I, P, P, P, P], I),
         "g2ohip_enable_kernel_timing": ([P, I], None),
         "g2ohip_kernel_ms": ([P, C.c_char_p], D),
@@ -292,6 +293,10 @@ class SparseOptimizer:
     def set_comm(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_ubyte * 128).from_buffer_copy(uid)
         _check(lib().g2ohip_set_comm(self.h, buf, rank, nranks), "set_comm")
+
+    def set_comm_local(self, group_key: str, rank: int, nranks: int):
+        """In-process test transport (see g2ohip_set_comm_local); one host thread per rank."""
+        _check(lib().g2ohip_set_comm_local(self.h, group_key.encode(), rank, nranks), "set_comm_local")
 
     # ---- measurement ----
     def enable_kernel_timing(self, on: bool = True):

@@ -233,6 +233,10 @@ int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int
   if (!g || !uid || rank < 0 || rank >= nranks) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->set_comm(uid, rank, nranks); });
 }
+int g2ohip_set_comm_local(g2ohip_graph* g, const char* key, int rank, int nranks) {
+  if (!g || !key || rank < 0 || rank >= nranks) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->set_comm_local(key, rank, nranks); });
+}
 
 int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int* perm, double* stats) {
   if (nblocks <= 0 || bdim <= 0 || nblk < 0 || (nblk > 0 && (!bi || !bj))) return G2OHIP_ERR_ARG;

@@ -11,7 +11,6 @@
 // (chi2, scale, the not-PD flag) once per LM trial.
 #include "engine.hpp"
 
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -359,7 +358,7 @@ Engine::Engine(int dev) : device(dev) {
 }
 Engine::~Engine() {
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
-  if (comm) ncclCommDestroy((ncclComm_t)comm);
+  comm.reset();
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -958,8 +957,7 @@ static EdgeArgs edge_args(const DevBuf<int>& v0, const DevBuf<int>& v1, const De
 
 void Engine::allreduce_sum(double* p, size_t n) {
   if (nranks <= 1 || !comm) return;
-  ncclResult_t r = ncclAllReduce(p, p, n, ncclDouble, ncclSum, (ncclComm_t)comm, stream);
-  if (r != ncclSuccess) throw DeviceError(std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  comm->allreduce_sum(p, n, stream);
 }
 
 void Engine::compute_errors_async() {
@@ -1154,8 +1152,7 @@ double Engine::lambda_init() {  // optimization_algorithm_levenberg.cpp:152-175
   launch::diag_absmax(Hp, num_poses, pd, do_schur ? dHll.get() : nullptr, do_schur ? (int)local_lm.size() : 0, ld,
                       dpartial.get(), dscal.get() + 3, stream);
   if (nranks > 1 && comm) {
-    ncclResult_t r = ncclAllReduce(dscal.get() + 3, dscal.get() + 3, 1, ncclDouble, ncclMax, (ncclComm_t)comm, stream);
-    if (r != ncclSuccess) throw DeviceError("ncclAllReduce(max)");
+    comm->allreduce_max(dscal.get() + 3, 1, stream);
   }
   double m = 0;
   HIP_CHECK(hipMemcpyAsync(&m, dscal.get() + 3, sizeof(double), hipMemcpyDeviceToHost, stream));
@@ -1367,15 +1364,22 @@ int Engine::stage(double lambda, double* b, double* x, double* Hs, double* bs, l
 }
 
 int Engine::set_comm(const unsigned char* uid, int r, int nr) {
-  if (nr <= 1) { rank = 0; nranks = 1; return G2OHIP_OK; }
-  ncclUniqueId id;
-  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
-  std::memcpy(&id, uid, sizeof id);
-  ncclComm_t c;
+  if (nr <= 1) { rank = 0; nranks = 1; comm.reset(); return G2OHIP_OK; }
   HIP_CHECK(hipSetDevice(device));
-  ncclResult_t res = ncclCommInitRank(&c, nr, id, r);
-  if (res != ncclSuccess) return G2OHIP_ERR_DEVICE;
-  comm = c;
+  std::string err;
+  Comm* c = make_rccl_comm(uid, r, nr, err);
+  if (!c) throw DeviceError(err);
+  comm.reset(c);
+  rank = r;
+  nranks = nr;
+  structure_built = false;
+  edges_ready = false;
+  return G2OHIP_OK;
+}
+
+int Engine::set_comm_local(const std::string& key, int r, int nr) {
+  if (nr <= 1) { rank = 0; nranks = 1; comm.reset(); return G2OHIP_OK; }
+  comm.reset(make_local_comm(key, r, nr));
   rank = r;
   nranks = nr;
   structure_built = false;

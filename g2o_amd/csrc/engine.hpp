@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/g2o_hip.h"
+#include "comm.hpp"
 #include "common.hpp"
 #include "kernels.hpp"
 #include "symbolic.hpp"
@@ -123,6 +124,7 @@ class Engine {
 
   // comm
   int set_comm(const unsigned char* uid, int rank, int nranks);
+  int set_comm_local(const std::string& key, int rank, int nranks);
   KernelTimer timer;
   double kernel_bytes(const std::string& name) const;
   double kernel_flops(const std::string& name) const;
@@ -141,7 +143,7 @@ class Engine {
   int ne = 0;
   // sharding
   int rank = 0, nranks = 1;
-  void* comm = nullptr;
+  std::unique_ptr<Comm> comm;
   std::vector<int> local_edges;  // edge indices this rank assembles (all when nranks == 1)
   std::vector<int> local_lm;     // landmark (hessian - num_poses) this rank owns
 

@@ -365,3 +365,20 @@ def by_name(name: str, scale: str = "full") -> Problem:
     if name == "C5":
         return ba(80, 4000) if small else ba(4000, 1_000_000)
     raise KeyError(name)
+
+
+def landmark_shard(prob: Problem, rank: int, nranks: int) -> Problem:
+    """Sub-problem of landmark shard ``rank``: every camera, the contiguous landmark range
+    [P*rank/nranks, P*(rank+1)/nranks) of the landmark order and the observations of those
+    landmarks — the same partition the device engine uses (engine.cpp setup_edges_device)."""
+    cams, pts = prob.vertices
+    e = prob.edges[0]
+    P = pts.ids.size
+    a, b = P * rank // nranks, P * (rank + 1) // nranks
+    keep = slice(a, b)
+    ids = pts.ids[keep]
+    m = (e.v0 >= ids[0]) & (e.v0 <= ids[-1]) if ids.size else np.zeros(e.v0.size, bool)
+    pv = VertexSet(pts.vtype, ids.copy(), pts.est[keep].copy(), pts.fixed[keep].copy(), pts.marginalized[keep].copy())
+    ev = EdgeSet(e.etype, e.v0[m].copy(), e.v1[m].copy(), e.meas[m].copy(), e.info[m].copy(),
+                 None if e.params is None else e.params[m].copy())
+    return Problem(f"{prob.name}/shard{rank}of{nranks}", [cams, pv], [ev], prob.pose_dim, prob.landmark_dim)

@@ -138,6 +138,10 @@ int g2ohip_linear_solve_ccs(int device, int n, const int* Ap, const int* Ai, con
 int g2ohip_comm_unique_id(unsigned char out[128]);
 /* this rank keeps landmark shard `rank` of `nranks` (contiguous ranges of the point order) */
 int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int nranks);
+/* Test transport: `nranks` graphs in ONE process (one host thread each, same GPU) that share
+ * `group_key` reduce through host memory in rank order instead of RCCL. Same sharding, same
+ * call sequence as g2ohip_set_comm; used to test the sharded path on a single-GPU box. */
+int g2ohip_set_comm_local(g2ohip_graph* g, const char* group_key, int rank, int nranks);
 
 /* ---- host-only symbolic analysis (no GPU needed) ----
  * Block pattern of a symmetric matrix given as upper blocks (bi[k] <= bj[k]) of a uniform block

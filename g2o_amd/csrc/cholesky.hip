@@ -5,20 +5,26 @@
 // (csparse_extension.cpp:64-119 cs_chol_workspace; cs_lsolve/cs_ltsolve/cs_ipvec/cs_pvec
 // at :47-52) behind LinearSolver::solve (linear_solver.h:65).  The symbolic
 // analysis (symbolic.cpp) fixes ordering, supernodes and frontal maps once per
-// structure; each LM trial runs
+// structure.  Storage: `fronts` holds each front (m x m col-major, m = ns + nr) as the
+// Schur updates progress; the finished factor columns [L11; L21] (m x ns, ld m) go to `lbuf`,
+// so no kernel ever reads a column another workgroup of the same launch is rewriting.
+// Each LM trial runs
 //   k_permute + k_vec_init   rhs -> P rhs -> front vectors (own rows)
-//   k_chol_scatter           input blocks -> fronts (+ lambda on the diagonal for pose graphs)
+//   k_chol_scatter           input blocks -> fronts (+ lambda on the diagonal)
 //   per level l (all fronts of a level are independent):
 //     k_extend_add     children's update matrices AND update vectors -> parent fronts;
-//                      one workgroup per (front, 32-column slab), children in fixed order
-//     per 32-wide panel p:
-//       k_panel        POTRF of the 32x32 diagonal block in registers of one wave
-//                      (every workgroup of the front recomputes it), forward-solve of the
-//                      block's rhs, TRSM of 256 rows per workgroup fused with the rhs update
-//       k_trail        SYRK/GEMM of the trailing lower triangle in 64x64 tiles on
-//                      v_mfma_f64_16x16x4f64 (4 waves x 2x2 MFMA tiles, K = 32)
-//   k_chol_backward level L-1..0: one workgroup per front, LDS-resident solution slice.
-// Every front entry is written by exactly one workgroup per step in a fixed order: the
+//                      one workgroup per (front, 16-column slab), children in fixed order
+//     k_potrf0         first 32x32 diagonal block of every front + its forward solve
+//     k_step (x panels) one launch per 32-column panel step: every workgroup owns one 64x64
+//                      tile (I, J) of the panel region, solves the panel rows of I and J
+//                      against L_kk (TRSM), updates the tile on v_mfma_f64_16x16x4f64, and the
+//                      (I = 0)-column writers store L21 rows + update the front vector; the
+//                      workgroup of tile (0, 0) then factors the NEXT 32x32 diagonal block —
+//                      one kernel boundary per panel step on the critical path
+//     k_syrk           contribution block U = A22 - L21 L21^T once per front, K = ns
+//   per level L-1..0: k_bwd_gemv (L21^T x, one wave per column) + k_bwd_tri (L11^-T, one
+//                    workgroup per front, LDS-resident solution slice).
+// Every output entry is written by exactly one workgroup per launch in a fixed order: the
 // factor and the solution are bitwise reproducible run to run (no atomics).
 #include <hip/hip_runtime.h>
 
@@ -31,9 +37,10 @@ using launch::FrontDesc;
 using launch::Task;
 
 constexpr int NB = 32;   // panel width
-constexpr int TT = 64;   // trailing tile
-constexpr int PS = 34;   // LDS row stride (doubles) for the P tiles: conflict-free ds_read_b64
-constexpr int EA = 32;   // extend-add column slab
+constexpr int TT = 64;   // update tile
+constexpr int PS = 34;   // LDS row stride (doubles) for the 64 x 32 panel tiles
+constexpr int DS = 33;   // LDS row stride of a 32 x 32 diagonal block
+constexpr int CS = TT + 1;
 
 typedef double dx4 __attribute__((ext_vector_type(4)));
 
@@ -83,27 +90,25 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     while (lo < hi) { const int mid = (lo + hi) >> 1; if (rel[mid] < b) lo = mid + 1; else hi = mid; }
     const int j1 = lo;
     for (int j = j0 + (int)threadIdx.x; j < j1; j += 256) v[rel[j]] += u[j];
-    // (j, i >= j) pairs of the slab flattened over the workgroup, 4 loads in flight per thread
-    const long long tot = (long long)(j1 - j0) * nrc;
-    for (long long p0 = threadIdx.x; p0 < tot; p0 += 1024) {
-      double val[4];
-      long long dsti[4];
+    // lower triangle of the slab, column by column: threads run down the rows (coalesced U reads,
+    // mostly-contiguous F writes), 4 independent loads in flight per thread
+    for (int j = j0; j < j1; ++j) {
+      const double* Uj = U + (size_t)j * mc;
+      double* Fj = F + (size_t)rel[j] * m;
+      for (int i0 = j + (int)threadIdx.x; i0 < nrc; i0 += 1024) {
+        double val[4];
+        int ri[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const long long p = p0 + q * 256;
-        dsti[q] = -1;
-        val[q] = 0.0;
-        if (p < tot) {
-          const int j = j0 + (int)(p / nrc), i = (int)(p % nrc);
-          if (i >= j) {
-            val[q] = U[(size_t)j * mc + i];
-            dsti[q] = (long long)rel[j] * m + rel[i];
-          }
+        for (int q = 0; q < 4; ++q) {
+          const int i = i0 + q * 256;
+          ri[q] = -1;
+          val[q] = 0.0;
+          if (i < nrc) { val[q] = Uj[i]; ri[q] = rel[i]; }
         }
-      }
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (dsti[q] >= 0) F[dsti[q]] += val[q];
+        for (int q = 0; q < 4; ++q)
+          if (ri[q] >= 0) Fj[ri[q]] += val[q];
+      }
     }
     __syncthreads();
   }
@@ -121,183 +126,313 @@ __device__ __forceinline__ double rlane(double v, int l) {
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Factor the 32x32 diagonal block held row-wise by lanes 0..31 (row[c] = A(lane, c), c <= lane;
-// rows >= kb padded with the identity). Column j of L is broadcast through LDS (col, 32 doubles,
-// read back two at a time). On return row[c] = L(lane, c), dinv[lane] = 1 / L(lane, lane).
+// rows >= kb padded with the identity). Fully unrolled (j, c compile-time: no selects); column j
+// of L is broadcast through LDS (col, 32 doubles, read back two at a time, double-buffered so
+// one LDS wait per step). On return row[c] = L(lane, c), dinv[lane] = 1 / L(lane, lane).
 // Returns false if a pivot was not positive (cs_chol's `d <= 0` test).
+// A single wave runs every instruction at 4 cycles: the step body is kept to ~45 instructions.
 __device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col, double* dinv) {
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const double djj = rlane(row[j], j);
     ok &= djj > 0.0;
-    const double ljj = sqrt(djj > 0.0 ? djj : 1.0);
-    const double inv = 1.0 / ljj;
-    const double lrj = lane == j ? ljj : (lane > j ? row[j] * inv : 0.0);
+    const double d = djj > 0.0 ? djj : 1.0;
+    // 1/sqrt(d) by v_rsq_f64 + two Newton steps (relative error ~1e-16), sqrt(d) = d / sqrt(d)
+    double r = __builtin_amdgcn_rsq(d);
+    r = r * (1.5 - 0.5 * d * r * r);
+    r = r * (1.5 - 0.5 * d * r * r);
+    const double ljj = d * r;
+    const double lrj = lane == j ? ljj : row[j] * r;  // lanes < j hold 0 in row[j]
     row[j] = lrj;
-    if (lane == j) dinv[j] = inv;
+    if (lane == j) dinv[j] = r;
     if (j + 1 < NB) {
-      if (lane < NB) col[lane] = lrj;
+      double* cb = col + (j & 1) * NB;
+      if (lane < NB) cb[lane] = lrj;
       lds_fence();
 #pragma unroll
       for (int c = ((j + 1) & ~1); c < NB; c += 2) {
-        const double2 cc = *reinterpret_cast<const double2*>(col + c);
+        const double2 cc = *reinterpret_cast<const double2*>(cb + c);
         if (c > j) row[c] -= lrj * cc.x;
-        if (c + 1 > j) row[c + 1] -= lrj * cc.y;
+        row[c + 1] -= lrj * cc.y;
       }
-      lds_fence();
+      // materialise this step's updates now: left alone, the scheduler defers the FMAs until each
+      // row[c] is next needed and keeps every broadcast column live (512 VGPRs + spills)
+#pragma unroll
+      for (int c = j + 1; c < NB; ++c) asm volatile("" : "+v"(row[c]));
     }
   }
   return ok;
 }
 
-// ---------------------------------------------------------------------------- panel
-// Task: s, a = k0, b = first row of this workgroup's row block, c = kb.
-// Wave 0 factors the (identity-padded) diagonal block in registers and forward-solves the
-// block's rhs; then every wave solves X L_kk^T = P for its 64 rows against the LDS copy of L_kk
-// and applies the rhs update v_i -= X_i y.
-__global__ void __launch_bounds__(256) k_panel(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                               double* __restrict__ fronts, double* __restrict__ vecs,
-                                               double* __restrict__ ysol, double* __restrict__ ldiag,
-                                               int* __restrict__ fail) {
-  __shared__ __attribute__((aligned(16))) double Lk[NB][NB + 2];  // L_kk, row stride 34 (16-B aligned rows)
-  __shared__ __attribute__((aligned(16))) double col[NB];
-  __shared__ double dinv[NB];
-  __shared__ double yv[NB];
-  const Task t = tasks[blockIdx.x];
-  const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr;
-  double* F = fronts + me.front_off;
-  double* v = vecs + me.vec_off;
-  const int k0 = t.a, row0 = t.b, kb = t.c;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r0 = k0 + kb;
-  const int i = row0 + w * 64 + lane;
-  const bool act = i < m;
-  double x[NB];
+// Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid) and
+// forward-solve vy (LDS, kb values) in place. On return D holds L (lower, with diagonal).
+__device__ __forceinline__ void factor_block(double* D, int kb, double* vy, double* col, double* dinv, int lane,
+                                             int* fail) {
+  double row[NB];
 #pragma unroll
-  for (int q = 0; q < NB; ++q) x[q] = (act && q < kb) ? F[(size_t)(k0 + q) * m + i] : 0.0;
-  if (w == 0) {
-    double row[NB];
-#pragma unroll
-    for (int c = 0; c < NB; ++c) {
-      double a = 0.0;
-      if (lane < kb && c <= lane) a = F[(size_t)(k0 + c) * m + k0 + lane];
-      if (lane >= kb && c == lane) a = 1.0;
-      row[c] = a;
-    }
-    const bool ok = chol32(row, lane, col, dinv);
-    if (lane < NB) {
-#pragma unroll
-      for (int c = 0; c < NB; ++c) Lk[lane][c] = row[c];
-    }
-    lds_fence();
-    // L_kk y = v(k0 .. k0+kb)
-    double y = lane < kb ? v[k0 + lane] : 0.0;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const double yj = rlane(y, j) * dinv[j];
-      y = lane == j ? yj : (lane > j ? y - row[j] * yj : y);
-    }
-    if (lane < NB) yv[lane] = y;
-    if (row0 == r0) {  // first workgroup of the front publishes L_kk and y_k
-      // L_kk goes to the (unused) upper triangle of the diagonal block, transposed, and its
-      // diagonal to ldiag: the lower triangle keeps A_kk, which the other workgroups of this
-      // launch may still be reading.
-      if (lane == 0 && !ok) *fail = 1;
-      if (lane < kb) {
-        double dg = 0.0;
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
-          if (c < lane) F[(size_t)(k0 + lane) * m + k0 + c] = row[c];
-          dg = c == lane ? row[c] : dg;
-        }
-        ldiag[me.c0 + k0 + lane] = dg;
-        ysol[me.c0 + k0 + lane] = y;
-      }
-    }
+  for (int c = 0; c < NB; ++c) {
+    const double a = (lane < kb && c <= lane) ? D[lane * DS + c] : 0.0;
+    row[c] = (lane >= kb && c == lane) ? 1.0 : a;
   }
-  __syncthreads();
-  double s2 = 0.0;
+  const bool ok = chol32(row, lane, col, dinv);
+  if (lane == 0 && !ok) *fail = 1;
+  double y = lane < kb ? vy[lane] : 0.0;
 #pragma unroll
-  for (int q = 0; q < NB; ++q) {
-    double s = x[q];
-#pragma unroll
-    for (int u = 0; u + 1 < q; u += 2) {
-      const double2 l2 = *reinterpret_cast<const double2*>(&Lk[q][u]);
-      s -= x[u] * l2.x;
-      s -= x[u + 1] * l2.y;
-    }
-    if (q & 1) s -= x[q - 1] * Lk[q][q - 1];
-    x[q] = s * dinv[q];
-    s2 += x[q] * yv[q];
+  for (int j = 0; j < NB; ++j) {
+    const double yj = rlane(y, j) * dinv[j];
+    y = lane == j ? yj : (lane > j ? y - row[j] * yj : y);
   }
-  if (act) {
+  if (lane < kb) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q)
-      if (q < kb) F[(size_t)(k0 + q) * m + i] = x[q];
-    v[i] -= s2;
+    for (int c = 0; c < NB; ++c)
+      if (c <= lane) D[lane * DS + c] = row[c];
+    vy[lane] = y;
   }
 }
 
-// ---------------------------------------------------------------------------- trailing update (MFMA)
-// Task: s, a = k0, b = ti | tj << 16, c = kb.  C[I,J] -= P_I P_J^T on the lower triangle.
-__global__ void __launch_bounds__(256) k_trail(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                               double* __restrict__ fronts) {
-  __shared__ double sh[2 * TT * PS];  // Pa | Pb, reused as the 64 x 65 result tile
+// D (LDS) -> L block at (r0, r0) of a front's factor columns (ld m), y -> ysol
+__device__ __forceinline__ void publish_block(const double* D, const double* vy, int kb, double* L, int m, int r0,
+                                              double* ysol, int tid) {
+  for (int e = tid; e < NB * NB; e += 256) {
+    const int r = e & (NB - 1), c = e >> 5;
+    if (r < kb && c < kb && r >= c) L[(size_t)(r0 + c) * m + r0 + r] = D[r * DS + c];
+  }
+  if (tid < kb) ysol[r0 + tid] = vy[tid];
+}
+
+// ---------------------------------------------------------------------------- first diagonal block
+// One workgroup per front of the level: A(0:kb, 0:kb) -> L, y(0:kb).
+__global__ void __launch_bounds__(256) k_potrf0(const int* __restrict__ level_list, const FrontDesc* __restrict__ fd,
+                                                const double* __restrict__ fronts, double* __restrict__ lbuf,
+                                                const double* __restrict__ vecs, double* __restrict__ ysol,
+                                                int* __restrict__ fail) {
+  __shared__ double D[NB * DS];
+  __shared__ __attribute__((aligned(16))) double col[2 * NB];
+  __shared__ double dinv[NB], vy[NB];
+  const FrontDesc me = fd[level_list[blockIdx.x]];
+  const int m = me.ns + me.nr, kb = min(NB, me.ns);
+  const double* F = fronts + me.front_off;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < NB * NB; e += 256) {
+    const int r = e & (NB - 1), c = e >> 5;
+    if (r < kb && c < kb && r >= c) D[r * DS + c] = F[(size_t)c * m + r];
+  }
+  if (tid < kb) vy[tid] = vecs[me.vec_off + tid];
+  __syncthreads();
+  if (tid < 64) factor_block(D, kb, vy, col, dinv, tid, fail);
+  __syncthreads();
+  publish_block(D, vy, kb, lbuf + me.l_off, m, 0, ysol + me.c0, tid);
+}
+
+// ---------------------------------------------------------------------------- panel step
+struct MfmaTile {  // 64x64 tile, 4 waves x (2x2) v_mfma_f64_16x16x4f64 tiles, K chunk of 32 in LDS
+  dx4 acc[2][2];
+  __device__ void zero() {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[x][y] = dx4{0.0, 0.0, 0.0, 0.0};
+  }
+  __device__ void step(const double* Pa, const double* Pb, int lane, int w) {
+    const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
+    const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < NB / 4; ++kk) {
+      const int k = kk * 4 + lk;
+      const double a0 = Pa[(wr + lr) * PS + k], a1 = Pa[(wr + 16 + lr) * PS + k];
+      const double b0 = Pb[(wc + lr) * PS + k], b1 = Pb[(wc + 16 + lr) * PS + k];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+  // D layout of v_mfma_f64_16x16x4f64: lane l holds D[(l>>4) + 4*i][l & 15], i = 0..3
+  __device__ void store(double* Ct, int lane, int w) const {
+    const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
+    const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ct[(wr + x * 16 + lk + 4 * i) * CS + wc + y * 16 + lr] = acc[x][y][i];
+  }
+};
+
+// C tile entries owned by a thread: idx = tid + 256 u -> (r = idx % 64, c = idx / 64)
+__device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J0, int climit, int tid, double (&cv)[16]) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
+    const int gi = I0 + r, gj = J0 + c;
+    cv[u] = (gi < m && gj < climit && gi >= gj) ? F[(size_t)gj * m + gi] : 0.0;
+  }
+}
+
+// Task: s; a = k0 | kb << 16; b = ti | tj << 16; c = flags (1: update the tile, 2: factor the
+// next diagonal block). Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
+__global__ void __launch_bounds__(256) k_step(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                              double* __restrict__ fronts, double* __restrict__ lbuf,
+                                              double* __restrict__ vecs, double* __restrict__ ysol,
+                                              int* __restrict__ fail) {
+  __shared__ __attribute__((aligned(16))) double Lk[NB][NB + 2];  // L_kk rows (16-B aligned, stride 34)
+  __shared__ double dv[NB], yk[NB];
+  __shared__ double sh[2 * TT * PS];  // Pa | Pb; reused as the 64 x 65 result tile
+  __shared__ double Dn[NB * DS];      // next diagonal block
+  __shared__ __attribute__((aligned(16))) double col[2 * NB];
+  __shared__ double dinvn[NB], vn[NB];
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr;
+  const int m = me.ns + me.nr, ns = me.ns;
   double* F = fronts + me.front_off;
-  const int k0 = t.a, kb = t.c;
+  double* L = lbuf + me.l_off;
+  double* v = vecs + me.vec_off;
+  const int k0 = t.a & 0xffff, kb = t.a >> 16;
   const int ti = t.b & 0xffff, tj = t.b >> 16;
+  const bool upd = t.c & 1, nextf = t.c & 2, writer = tj == 0;
   const int r0 = k0 + kb;
   const int I0 = r0 + ti * TT, J0 = r0 + tj * TT;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   double* Pa = sh;
   double* Pb = sh + TT * PS;
-  for (int idx = tid; idx < TT * NB; idx += 256) {
-    const int r = idx % TT, k = idx / TT;
-    const bool kin = k < kb;
-    Pa[r * PS + k] = (kin && I0 + r < m) ? F[(size_t)(k0 + k) * m + I0 + r] : 0.0;
-    Pb[r * PS + k] = (kin && J0 + r < m) ? F[(size_t)(k0 + k) * m + J0 + r] : 0.0;
+
+  // ---- stage L_kk, y_k, the raw panel rows of I (and J), prefetch the C tile
+  for (int e = tid; e < NB * NB; e += 256) {
+    const int q = e & (NB - 1), u = e >> 5;
+    Lk[q][u] = (q < kb && u <= q) ? L[(size_t)(k0 + u) * m + k0 + q] : (q == u ? 1.0 : 0.0);
   }
-  __syncthreads();
-  const int lane = tid & 63, w = tid >> 6;
-  const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
-  const int lr = lane & 15, lk = lane >> 4;
-  dx4 acc[2][2];
+  if (tid < NB) yk[tid] = tid < kb ? ysol[me.c0 + k0 + tid] : 0.0;
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = dx4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int kk = 0; kk < NB / 4; ++kk) {
-    const int k = kk * 4 + lk;
-    const double a0 = Pa[(wr + lr) * PS + k], a1 = Pa[(wr + 16 + lr) * PS + k];
-    const double b0 = Pb[(wc + lr) * PS + k], b1 = Pb[(wc + 16 + lr) * PS + k];
-    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+    Pa[r * PS + q] = (q < kb && I0 + r < m) ? F[(size_t)(k0 + q) * m + I0 + r] : 0.0;
+    if (upd) Pb[r * PS + q] = (q < kb && J0 + r < m) ? F[(size_t)(k0 + q) * m + J0 + r] : 0.0;
   }
+  double cv[16];
+  if (upd) load_ctile(F, m, I0, J0, ns, tid, cv);
   __syncthreads();
-  // D layout of v_mfma_f64_16x16x4f64: lane l holds D[(l>>4) + 4*i][l & 15], i = 0..3
-  constexpr int CS = TT + 1;
-  double* Ct = sh;  // [row][col] with stride CS
+  if (tid < NB) dv[tid] = 1.0 / Lk[tid][tid];
+  __syncthreads();
+
+  // ---- TRSM: rows of I (threads 0..63) and of J (64..127) against L_kk
+  if (tid < 64 || (upd && tid < 128)) {
+    double* P = tid < 64 ? Pa + tid * PS : Pb + (tid - 64) * PS;
+    double x[NB];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+    for (int q = 0; q < NB; ++q) x[q] = P[q];
+    double s2 = 0.0;
 #pragma unroll
-    for (int y = 0; y < 2; ++y)
+    for (int q = 0; q < NB; ++q) {
+      double s = x[q];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wr + x * 16 + lk + 4 * i, col = wc + y * 16 + lr;
-        Ct[row * CS + col] = acc[x][y][i];
+      for (int u = 0; u + 1 < q; u += 2) {
+        const double2 l2 = *reinterpret_cast<const double2*>(&Lk[q][u]);
+        s -= x[u] * l2.x;
+        s -= x[u + 1] * l2.y;
       }
+      if (q & 1) s -= x[q - 1] * Lk[q][q - 1];
+      x[q] = s * dv[q];
+      s2 += x[q] * yk[q];
+      asm volatile("" ::: "memory");  // keep the L_kk row reads of step q from being hoisted en masse
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) P[q] = x[q];
+    if (tid < 64 && writer && I0 + tid < m) {  // forward-solve update of the front vector
+      const double nv = v[I0 + tid] - s2;
+      v[I0 + tid] = nv;
+      if (nextf && tid < NB) vn[tid] = nv;
+    }
+  }
   __syncthreads();
-  for (int idx = tid; idx < TT * TT; idx += 256) {
-    const int r = idx % TT, c = idx / TT;
+
+  // ---- writers store the L21 rows of block I
+  if (writer) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+      if (q < kb && I0 + r < m) L[(size_t)(k0 + q) * m + I0 + r] = Pa[r * PS + q];
+    }
+  }
+  if (!upd) return;
+
+  // ---- C[I, J] -= P_I P_J^T (columns inside the supernode, lower triangle)
+  MfmaTile T;
+  T.zero();
+  T.step(Pa, Pb, lane, w);
+  __syncthreads();
+  T.store(sh, lane, w);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
     const int gi = I0 + r, gj = J0 + c;
-    if (gi < m && gj < m && gi >= gj) F[(size_t)gj * m + gi] -= Ct[r * CS + c];
+    if (gi < m && gj < ns && gi >= gj) {
+      const double nvv = cv[u] - sh[r * CS + c];
+      F[(size_t)gj * m + gi] = nvv;
+      if (nextf && r < NB && c < NB) Dn[r * DS + c] = nvv;
+    }
+  }
+  if (!nextf) return;
+
+  // ---- tile (0, 0): factor the next diagonal block and forward-solve its rhs
+  __syncthreads();
+  const int kbn = min(NB, ns - r0);
+  if (tid < 64) factor_block(Dn, kbn, vn, col, dinvn, tid, fail);
+  __syncthreads();
+  publish_block(Dn, vn, kbn, L, m, r0, ysol + me.c0, tid);
+}
+
+// ---------------------------------------------------------------------------- contribution block
+// U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns in 32-wide chunks, the next
+// chunk prefetched into registers. Task: s, b = ti | tj << 16.
+__global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                              double* __restrict__ fronts, const double* __restrict__ lbuf) {
+  __shared__ double sh[2 * TT * PS];
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int m = me.ns + me.nr, ns = me.ns;
+  double* F = fronts + me.front_off;
+  const double* L = lbuf + me.l_off;
+  const int ti = t.b & 0xffff, tj = t.b >> 16;
+  const int I0 = ns + ti * TT, J0 = ns + tj * TT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double cv[16];
+  load_ctile(F, m, I0, J0, m, tid, cv);
+  double* Pa = sh;
+  double* Pb = sh + TT * PS;
+  double pa[8], pb[8];
+  auto fetch = [&](int kc) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), k = kc + (e >> 6);
+      pa[u] = (k < ns && I0 + r < m) ? L[(size_t)k * m + I0 + r] : 0.0;
+      pb[u] = (k < ns && J0 + r < m) ? L[(size_t)k * m + J0 + r] : 0.0;
+    }
+  };
+  MfmaTile T;
+  T.zero();
+  fetch(0);
+  for (int kc = 0; kc < ns; kc += NB) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), k = e >> 6;
+      Pa[r * PS + k] = pa[u];
+      Pb[r * PS + k] = pb[u];
+    }
+    __syncthreads();
+    if (kc + NB < ns) fetch(kc + NB);
+    T.step(Pa, Pb, lane, w);
+    __syncthreads();
+  }
+  T.store(sh, lane, w);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
+    const int gi = I0 + r, gj = J0 + c;
+    if (gi < m && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
   }
 }
 
@@ -312,29 +447,39 @@ __global__ void k_ipermute(int n, const int* __restrict__ perm, const double* __
 
 
 // ---------------------------------------------------------------------------- backward solve
-// x_s = L11^-T (y_s - L21^T x_rows): first the L21^T x_rows GEMV with one thread per column
-// (sequential, cache-line friendly column reads), then 32-column blocks from the last: the
-// in-supernode column dots by 8 threads per column, the 32x32 triangle by one wave in registers.
-__global__ void __launch_bounds__(256) k_chol_backward(const int* __restrict__ level_list, const FrontDesc* __restrict__ fd,
-                                                       const int* __restrict__ rows, const double* __restrict__ fronts,
-                                                       const double* __restrict__ ysol, const double* __restrict__ ldiag,
-                                                       double* __restrict__ xsol) {
-  extern __shared__ __attribute__((aligned(16))) double xs[];  // [m]: own x (being solved) then x_rows
+// Per level (descending), two launches:
+//   k_bwd_gemv  t_s = y_s - L21^T x_rows for every front of the level; one wave per column,
+//               lanes run down the column (coalesced), x_rows gathered from the finished ancestors
+//   k_bwd_tri   x_s = L11^-T t_s per front: 32-column blocks from the last, in-supernode column
+//               dots by 8 threads per column, the 32x32 triangle by one wave in registers.
+// Task (gemv): s, a = first column (4 per workgroup).
+__global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                                  const int* __restrict__ rows, const double* __restrict__ lbuf,
+                                                  const double* __restrict__ ysol, double* __restrict__ xsol) {
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int m = me.ns + me.nr, ns = me.ns;
+  const int lane = threadIdx.x & 63, j = t.a + (int)(threadIdx.x >> 6);
+  if (j >= ns) return;
+  const double* col = lbuf + me.l_off + (size_t)j * m + ns;
+  const int* rw = rows + me.rows_off;
+  double acc = 0.0;
+  for (int i = lane; i < me.nr; i += 64) acc += col[i] * xsol[rw[i]];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) xsol[me.c0 + j] = ysol[me.c0 + j] - acc;
+}
+
+__global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_list, const FrontDesc* __restrict__ fd,
+                                                 const double* __restrict__ lbuf, double* __restrict__ xsol) {
+  extern __shared__ __attribute__((aligned(16))) double xs[];  // [ns]: t_s, solved in place
   __shared__ double red[8][NB];
   const int s = level_list[blockIdx.x];
   const FrontDesc me = fd[s];
   const int m = me.ns + me.nr, ns = me.ns;
-  const double* F = fronts + me.front_off;
-  const int* rw = rows + me.rows_off;
+  const double* L = lbuf + me.l_off;
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < m; i += 256) xs[i] = i < ns ? ysol[me.c0 + i] : xsol[rw[i - ns]];
-  __syncthreads();
-  for (int j = tid; j < ns; j += 256) {
-    const double* col = F + (size_t)j * m + ns;
-    double acc = 0.0;
-    for (int i = 0; i < me.nr; ++i) acc += col[i] * xs[ns + i];
-    xs[j] -= acc;
-  }
+  for (int i = tid; i < ns; i += 256) xs[i] = xsol[me.c0 + i];
   __syncthreads();
   const int nblk = (ns + NB - 1) / NB;
   const int q = tid & (NB - 1), g = tid >> 5;
@@ -342,18 +487,18 @@ __global__ void __launch_bounds__(256) k_chol_backward(const int* __restrict__ l
     const int k0 = bk * NB, kb = min(NB, ns - k0);
     double part = 0.0;
     if (q < kb) {
-      const double* col = F + (size_t)(k0 + q) * m;
-      for (int i = k0 + kb + g; i < ns; i += 8) part += col[i] * xs[i];
+      const double* cl = L + (size_t)(k0 + q) * m;
+      for (int i = k0 + kb + g; i < ns; i += 8) part += cl[i] * xs[i];
     }
     red[g][q] = part;
     __syncthreads();
     if (tid < 64) {
+      // Lc[j] = L(k0 + j, k0 + lane), j >= lane: column k0+lane of the diagonal block
+      const double* cl = L + (size_t)(k0 + min(lane, NB - 1)) * m + k0;
       double Lc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        double a = 0.0;
-        if (lane < kb && j > lane && j < kb) a = F[(size_t)(k0 + j) * m + k0 + lane];  // L(j, lane), upper storage
-        if (lane < kb && j == lane) a = ldiag[me.c0 + k0 + lane];
+        double a = (lane < kb && j >= lane && j < kb) ? cl[j] : 0.0;
         if (lane >= kb && j == lane) a = 1.0;
         Lc[j] = a;
       }
@@ -399,15 +544,21 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
   hipLaunchKernelGGL(k_extend_add, ntasks, 256, 0, s, tasks, fd, children, relmap, fronts, vecs);
   KERNEL_CHECK();
 }
-void chol_panel(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, double* vecs, double* ysol,
-                double* ldiag, int* fail, hipStream_t s) {
-  if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_panel, ntasks, 256, 0, s, tasks, fd, fronts, vecs, ysol, ldiag, fail);
+void chol_potrf0(int nfronts, const int* level_list, const FrontDesc* fd, const double* fronts, double* lbuf,
+                 const double* vecs, double* ysol, int* fail, hipStream_t s) {
+  if (nfronts <= 0) return;
+  hipLaunchKernelGGL(k_potrf0, nfronts, 256, 0, s, level_list, fd, fronts, lbuf, vecs, ysol, fail);
   KERNEL_CHECK();
 }
-void chol_trail(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, hipStream_t s) {
+void chol_step(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, double* lbuf, double* vecs,
+               double* ysol, int* fail, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_trail, ntasks, 256, 0, s, tasks, fd, fronts);
+  hipLaunchKernelGGL(k_step, ntasks, 256, 0, s, tasks, fd, fronts, lbuf, vecs, ysol, fail);
+  KERNEL_CHECK();
+}
+void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
   KERNEL_CHECK();
 }
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s) {
@@ -420,14 +571,20 @@ void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStr
   hipLaunchKernelGGL(k_ipermute, grid_for(n, 256), 256, 0, s, n, perm, in, out);
   KERNEL_CHECK();
 }
-void chol_backward(int nfronts, const int* level_list, const FrontDesc* fd, const int* rows, const double* fronts,
-                   const double* ysol, const double* ldiag, double* xsol, int max_m, hipStream_t s) {
+void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int* rows, const double* lbuf,
+                   const double* ysol, double* xsol, hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_bwd_gemv, ntasks, 256, 0, s, tasks, fd, rows, lbuf, ysol, xsol);
+  KERNEL_CHECK();
+}
+void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, double* xsol,
+                  int max_ns, hipStream_t s) {
   if (nfronts <= 0) return;
-  const size_t bytes = (size_t)max_m * sizeof(double);
-  if (bytes > 150 * 1024) throw DeviceError("front larger than LDS for the backward solve");
+  const size_t bytes = (size_t)max_ns * sizeof(double);
+  if (bytes > 150 * 1024) throw DeviceError("supernode wider than LDS for the backward solve");
   if (bytes > 64 * 1024)
-    HIP_CHECK(hipFuncSetAttribute((const void*)k_chol_backward, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-  hipLaunchKernelGGL(k_chol_backward, nfronts, 256, bytes, s, level_list, fd, rows, fronts, ysol, ldiag, xsol);
+    HIP_CHECK(hipFuncSetAttribute((const void*)k_bwd_tri, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  hipLaunchKernelGGL(k_bwd_tri, nfronts, 256, bytes, s, level_list, fd, lbuf, xsol);
   KERNEL_CHECK();
 }
 

@@ -250,11 +250,14 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   dst.upload(hdst, s);
   isdiag.upload(hdiag, s);
   std::vector<launch::FrontDesc> hfd(sym.sn.size());
+  long long loff = 0;
   for (size_t k = 0; k < sym.sn.size(); ++k) {
     const Supernode& q = sym.sn[k];
-    hfd[k] = launch::FrontDesc{q.front_off, q.vec_off, q.rows_off, q.c0, q.ns, q.nr, q.parent,
+    hfd[k] = launch::FrontDesc{q.front_off, q.vec_off, loff, q.rows_off, q.c0, q.ns, q.nr, q.parent,
                                sym.children_ptr[k], sym.children_ptr[k + 1]};
+    loff += (long long)(q.ns + q.nr) * q.ns;
   }
+  lpool = loff;
   fd.upload(hfd, s);
   std::vector<int> ll;
   level_off.assign(1, 0);
@@ -263,13 +266,15 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     level_off.push_back((int)ll.size());
   }
   level_lists.upload(ll, s);
-  // work lists: per level one extend-add op, then (panel, trailing) ops per 32-wide panel
+  // work lists per level: extend-add, first diagonal block, one step per 32-wide panel,
+  // contribution blocks
   {
     using launch::Task;
     const int NB = launch::CHOL_NB, TT = launch::CHOL_TT, EA = launch::CHOL_EA;
     std::vector<Task> tk;
     ops.clear();
-    for (auto& lv : sym.levels) {
+    for (size_t l = 0; l < sym.levels.size(); ++l) {
+      const auto& lv = sym.levels[l];
       Op ea{0, (int)tk.size(), 0};
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
@@ -279,33 +284,47 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       }
       ea.count = (int)tk.size() - ea.off;
       if (ea.count) ops.push_back(ea);
+      ops.push_back(Op{1, level_off[l], (int)lv.size()});  // k_potrf0 over the level list
       int maxp = 0;
       for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
       for (int p = 0; p < maxp; ++p) {
-        Op pa{1, (int)tk.size(), 0};
+        Op st{2, (int)tk.size(), 0};
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
           const int k0 = p * NB;
           if (k0 >= q.ns) continue;
           const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
-          const int nwg = std::max(1, (m - r0 + 255) / 256);
-          for (int w = 0; w < nwg; ++w) tk.push_back(Task{sn, k0, r0 + w * 256, kb});
+          const int T = (m - r0 + TT - 1) / TT, TJ = (q.ns - r0 + TT - 1) / TT;
+          for (int tj = 0; tj < std::max(TJ, 1); ++tj)
+            for (int ti = tj; ti < T; ++ti) {
+              int flags = tj < TJ ? 1 : 0;
+              if (ti == 0 && tj == 0 && r0 < q.ns) flags |= 2;
+              tk.push_back(Task{sn, k0 | (kb << 16), ti | (tj << 16), flags});
+            }
         }
-        pa.count = (int)tk.size() - pa.off;
-        if (pa.count) ops.push_back(pa);
-        Op tr{2, (int)tk.size(), 0};
-        for (int sn : lv) {
-          const Supernode& q = sym.sn[sn];
-          const int k0 = p * NB;
-          if (k0 >= q.ns) continue;
-          const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
-          const int T = (m - r0 + TT - 1) / TT;
-          for (int tj = 0; tj < T; ++tj)
-            for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, k0, ti | (tj << 16), kb});
-        }
-        tr.count = (int)tk.size() - tr.off;
-        if (tr.count) ops.push_back(tr);
+        st.count = (int)tk.size() - st.off;
+        if (st.count) ops.push_back(st);
       }
+      Op sy{3, (int)tk.size(), 0};
+      for (int sn : lv) {
+        const Supernode& q = sym.sn[sn];
+        const int T = (q.nr + TT - 1) / TT;
+        for (int tj = 0; tj < T; ++tj)
+          for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, 0, ti | (tj << 16), 0});
+      }
+      sy.count = (int)tk.size() - sy.off;
+      if (sy.count) ops.push_back(sy);
+    }
+    // backward-solve gemv tasks per level: (front, 4 columns)
+    bwd_off.assign(1, (int)tk.size());
+    max_ns = 1;
+    for (auto& lv : sym.levels) {
+      for (int sn : lv) {
+        const int ns = sym.sn[sn].ns;
+        max_ns = std::max(max_ns, ns);
+        for (int a = 0; a < ns; a += launch::CHOL_BW) tk.push_back(Task{sn, a, 0, 0});
+      }
+      bwd_off.push_back((int)tk.size());
     }
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
   }
@@ -317,7 +336,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   vecs.resize(std::max<int64_t>(sym.vec_pool, 1));
   rhs_p.resize(std::max(sym.n, 1));
   y_p.resize(std::max(sym.n, 1));
-  ldiag.resize(std::max(sym.n, 1));
+  lbuf.resize(std::max<long long>(lpool, 1));
   x_p.resize(std::max(sym.n, 1));
 }
 
@@ -328,20 +347,22 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
   launch::chol_scatter(nent, vals, dst.get(), isdiag.get(), lam, fronts.get(), s);
   for (const Op& op : ops) {
     const launch::Task* t = tasks.get() + op.off;
-    if (op.kind == 0)
-      launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), fronts.get(), vecs.get(), s);
-    else if (op.kind == 1)
-      launch::chol_panel(op.count, t, fd.get(), fronts.get(), vecs.get(), y_p.get(), ldiag.get(), fail, s);
-    else
-      launch::chol_trail(op.count, t, fd.get(), fronts.get(), s);
+    switch (op.kind) {
+      case 0: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), fronts.get(), vecs.get(), s); break;
+      case 1: launch::chol_potrf0(op.count, level_lists.get() + op.off, fd.get(), fronts.get(), lbuf.get(), vecs.get(),
+                                  y_p.get(), fail, s); break;
+      case 2: launch::chol_step(op.count, t, fd.get(), fronts.get(), lbuf.get(), vecs.get(), y_p.get(), fail, s); break;
+      default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;
+    }
   }
 }
 
 void DeviceCholesky::solve(double* x, hipStream_t s) {
   for (size_t l = level_off.size() - 1; l-- > 0;) {
     const int nf = level_off[l + 1] - level_off[l];
-    launch::chol_backward(nf, level_lists.get() + level_off[l], fd.get(), rows.get(), fronts.get(), y_p.get(), ldiag.get(),
-                          x_p.get(), sym.max_front, s);
+    launch::chol_bwd_gemv(bwd_off[l + 1] - bwd_off[l], tasks.get() + bwd_off[l], fd.get(), rows.get(), lbuf.get(),
+                          y_p.get(), x_p.get(), s);
+    launch::chol_bwd_tri(nf, level_lists.get() + level_off[l], fd.get(), lbuf.get(), x_p.get(), max_ns, s);
   }
   launch::chol_ipermute(sym.n, perm.get(), x_p.get(), x, s);
 }
@@ -1064,8 +1085,8 @@ void Engine::solve_async() {  // block_solver.hpp:314-447
   timer.end(stream);
   HIP_CHECK(hipEventRecord(ev_[3], stream));
   timer.begin("backsub", stream);
-  launch::backsub(nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get() + (size_t)lm_begin * ld,
-                  size_poses, dx.get() + (size_t)lm_begin * ld, stream);
+  launch::backsub(nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get(), size_poses, lm_begin, dx.get(),
+                  stream);
   timer.end(stream);
 }
 

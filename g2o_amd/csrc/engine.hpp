@@ -55,10 +55,13 @@ struct DeviceCholesky {
   DevBuf<launch::FrontDesc> fd;
   DevBuf<int> level_lists, children, relmap, rows, perm;
   std::vector<int> level_off;  // host offsets into level_lists
-  struct Op { int kind, off, count; };  // kind 0 extend-add, 1 panel, 2 trailing update
+  std::vector<int> bwd_off;    // per level: offset of its backward-gemv tasks in `tasks` (+1 end)
+  int max_ns = 0;
+  struct Op { int kind, off, count; };  // kind 0 extend-add, 1 first diagonal block, 2 panel step, 3 contribution block
   std::vector<Op> ops;
   DevBuf<launch::Task> tasks;
-  DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, ldiag;
+  DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, lbuf;
+  long long lpool = 0;
   void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
   // numeric LL^T fused with the forward solve of rhs (y = L^-1 P rhs)
   void factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s);

@@ -327,10 +327,11 @@ __global__ void __launch_bounds__(256)
 template <int PD>
 __global__ void __launch_bounds__(256)
     k_backsub(int nl, const int* __restrict__ lm_ptr, const int* __restrict__ blk_pose, const double* __restrict__ Hpl,
-              const double* __restrict__ Dinv, const double* __restrict__ b, int size_poses, double* __restrict__ x) {
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+              const double* __restrict__ Dinv, const double* __restrict__ b, int size_poses, int lm0,
+              double* __restrict__ x) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;  // local landmark; global index lm0 + l
   if (l >= nl) return;
-  const double* bl = b + size_poses + (size_t)l * 3;
+  const double* bl = b + size_poses + (size_t)(lm0 + l) * 3;
   double c0 = bl[0], c1 = bl[1], c2 = bl[2];
   for (int a = lm_ptr[l]; a < lm_ptr[l + 1]; ++a) {
     const double* Bm = Hpl + (size_t)a * PD * 3;
@@ -346,7 +347,7 @@ __global__ void __launch_bounds__(256)
     c0 += s0; c1 += s1; c2 += s2;
   }
   const double* D = Dinv + (size_t)l * 9;
-  double* xl = x + size_poses + (size_t)l * 3;
+  double* xl = x + size_poses + (size_t)(lm0 + l) * 3;
   xl[0] = D[0] * c0 + D[3] * c1 + D[6] * c2;
   xl[1] = D[1] * c0 + D[4] * c1 + D[7] * c2;
   xl[2] = D[2] * c0 + D[5] * c1 + D[8] * c2;
@@ -560,9 +561,9 @@ void schur_pairs(int nS, const int* s_ptr, const int* pairs, const int* s_hpp, c
 }
 
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
-             int size_poses, double* x, hipStream_t s) {
+             int size_poses, int lm0, double* x, hipStream_t s) {
   if (nl <= 0) return;
-  hipLaunchKernelGGL(k_backsub<6>, grid_for(nl, 256), 256, 0, s, nl, lm_ptr, blk_pose, Hpl, Dinv, b, size_poses, x);
+  hipLaunchKernelGGL(k_backsub<6>, grid_for(nl, 256), 256, 0, s, nl, lm_ptr, blk_pose, Hpl, Dinv, b, size_poses, lm0, x);
   KERNEL_CHECK();
 }
 

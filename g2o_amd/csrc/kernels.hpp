@@ -33,7 +33,7 @@ void schur_pairs(int nS, const int* s_ptr, const int* pairs, const int* s_hpp, c
                  const int* s_row, const double* Hpp, const double* W, const double* Hpl, const int* blk_lm,
                  const double* b, int size_poses, const double* lam, double* S, double* bschur, hipStream_t s);
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
-             int size_poses, double* x, hipStream_t s);
+             int size_poses, int lm0, double* x, hipStream_t s);
 void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s);
 size_t sum_partials(long long n);
 void sum(const double* v, long long n, double* partial, double* out, hipStream_t s);
@@ -46,6 +46,7 @@ void diag_absmax(const double* H1, int nb1, int d1, const double* H2, int nb2, i
 struct FrontDesc {  // device view of one supernode (see symbolic.hpp)
   long long front_off;
   long long vec_off;
+  long long l_off;  // factor columns [L11; L21] (m x ns, ld m) in lbuf
   long long rows_off;
   int c0, ns, nr, parent;
   int child_begin, child_end;  // into the children array
@@ -58,13 +59,17 @@ void chol_scatter(long long nent, const double* vals, const long long* dst, cons
 void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double* vecs, hipStream_t s);
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      double* fronts, double* vecs, hipStream_t s);
-void chol_panel(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, double* vecs, double* ysol, double* ldiag,
-                int* fail, hipStream_t s);
-void chol_trail(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, hipStream_t s);
+void chol_potrf0(int nfronts, const int* level_list, const FrontDesc* fd, const double* fronts, double* lbuf,
+                 const double* vecs, double* ysol, int* fail, hipStream_t s);
+void chol_step(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, double* lbuf, double* vecs,
+               double* ysol, int* fail, hipStream_t s);
+void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s);
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]
 void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]
-void chol_backward(int nfronts, const int* level_list, const FrontDesc* fd, const int* rows, const double* fronts,
-                   const double* ysol, const double* ldiag, double* xsol, int max_m, hipStream_t s);
-constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 32;
+void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int* rows, const double* lbuf,
+                   const double* ysol, double* xsol, hipStream_t s);
+void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, double* xsol,
+                  int max_ns, hipStream_t s);
+constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 16, CHOL_BW = 4;
 }  // namespace launch
 }  // namespace g2ohip

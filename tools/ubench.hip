@@ -1,0 +1,146 @@
+// Micro-benchmarks for the latency-bound Cholesky building blocks (dev tool, not product).
+// Times single-workgroup kernels with hipEvents over many back-to-back launches.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+#include <cmath>
+#include <algorithm>
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+constexpr int NB = 32;
+__device__ __forceinline__ double rlane(double v, int l) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <int NEWTON, int BCAST>
+__device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col, double* dinv) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const double djj = rlane(row[j], j);
+    ok &= djj > 0.0;
+    const double d = djj > 0.0 ? djj : 1.0;
+    double r = __builtin_amdgcn_rsq(d);
+    if (NEWTON >= 1) r = r * (1.5 - 0.5 * d * r * r);
+    if (NEWTON >= 2) r = r * (1.5 - 0.5 * d * r * r);
+    const double ljj = d * r;
+    const double lrj = lane == j ? ljj : row[j] * r;
+    row[j] = lrj;
+    if (lane == j) dinv[j] = r;
+    if (BCAST == 1 && j + 1 < NB) {
+#pragma unroll
+      for (int c = j + 1; c < NB; ++c) row[c] -= lrj * rlane(lrj, c);
+    }
+    if (BCAST == 0 && j + 1 < NB) {
+      double* cb = col + (j & 1) * NB;
+      if (lane < NB) cb[lane] = lrj;
+      lds_fence();
+#pragma unroll
+      for (int c = ((j + 1) & ~1); c < NB; c += 2) {
+        const double2 cc = *reinterpret_cast<const double2*>(cb + c);
+        if (c > j) row[c] -= lrj * cc.x;
+        row[c + 1] -= lrj * cc.y;
+      }
+#pragma unroll
+      for (int c = j + 1; c < NB; ++c) asm volatile("" : "+v"(row[c]));
+    }
+  }
+  return ok;
+}
+
+__global__ void k_rsqacc(const double* x, double* err, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double d = x[i];
+  double r0 = __builtin_amdgcn_rsq(d);
+  double r1 = r0 * (1.5 - 0.5 * d * r0 * r0);
+  double e = 1.0 / sqrt(d);
+  err[2 * i] = fabs(r0 - e) / e;
+  err[2 * i + 1] = fabs(r1 - e) / e;
+}
+__global__ void k_empty(int* p) { if (threadIdx.x == 0 && p[0] == 12345) p[1] = 1; }
+
+// dependent chain of global loads: idx = next[idx]
+__global__ void k_chase(const int* next, int steps, int* out) {
+  int i = threadIdx.x;
+  for (int s = 0; s < steps; ++s) i = next[i];
+  if (i == -7) out[0] = i;
+}
+
+template <int NEWTON, int BCAST>
+__global__ void k_chol(const double* A, double* out, int reps) {
+  __shared__ __attribute__((aligned(16))) double col[2 * NB];
+  __shared__ double dinv[NB];
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x >= 64) return;
+  double row[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) row[c] = (lane < NB && c <= lane) ? A[lane * NB + c] : (c == lane ? 1.0 : 0.0);
+  long long t0 = __builtin_amdgcn_s_memtime();
+  for (int r = 0; r < reps; ++r) {
+    chol32<NEWTON, BCAST>(row, lane, col, dinv);
+#pragma unroll
+    for (int c = 0; c < NB; ++c) row[c] = (lane < NB && c <= lane) ? A[lane * NB + c] + 1e-300 * row[c] : (c == lane ? 1.0 : 0.0);
+  }
+  long long t1 = __builtin_amdgcn_s_memtime();
+  if (lane < NB) out[lane] = row[lane] + dinv[lane];
+  if (lane == 0) out[40] = (double)(t1 - t0);
+}
+
+int main() {
+  int *dp; CK(hipMalloc(&dp, 1 << 20)); CK(hipMemset(dp, 0, 1 << 20));
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  float ms;
+  // 1. empty kernel (1 WG) back-to-back
+  for (int w = 0; w < 10; ++w) hipLaunchKernelGGL(k_empty, 1, 64, 0, 0, dp);
+  CK(hipEventRecord(a)); for (int w = 0; w < 1000; ++w) hipLaunchKernelGGL(k_empty, 1, 64, 0, 0, dp);
+  CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
+  printf("empty kernel back-to-back: %.2f us/launch\n", ms);
+  // 2. pointer chase over 256 MB (HBM) and 1 MB (L2)
+  for (size_t span : {(size_t)1 << 20, (size_t)256 << 20}) {
+    size_t n = span / 4; std::vector<int> h(n);
+    // stride of 4 KB + 64 B across the span, single chain
+    size_t stride = 1024 + 16; size_t cur = 0;
+    for (size_t k = 0; k < n; ++k) { size_t nx = (cur + stride) % n; h[cur] = (int)nx; cur = nx; }
+    int* d; CK(hipMalloc(&d, span)); CK(hipMemcpy(d, h.data(), span, hipMemcpyHostToDevice));
+    const int steps = 2000;
+    hipLaunchKernelGGL(k_chase, 1, 1, 0, 0, d, steps, dp);
+    CK(hipEventRecord(a)); hipLaunchKernelGGL(k_chase, 1, 1, 0, 0, d, steps, dp);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
+    printf("dependent load latency over %zu MB: %.0f ns\n", span >> 20, ms * 1e6 / steps);
+    CK(hipFree(d));
+  }
+  // 3. chol32
+  std::vector<double> A(NB * NB);
+  for (int i = 0; i < NB; ++i) for (int j = 0; j < NB; ++j) A[i * NB + j] = (i == j ? NB : 0.0) + 1.0 / (1 + i + j);
+  double *dA, *dO; CK(hipMalloc(&dA, sizeof(double) * NB * NB)); CK(hipMalloc(&dO, 64 * sizeof(double)));
+  CK(hipMemcpy(dA, A.data(), sizeof(double) * NB * NB, hipMemcpyHostToDevice));
+  const int reps = 200;
+  auto run = [&](auto kern, const char* name) -> int {
+    hipLaunchKernelGGL(kern, 1, 64, 0, 0, dA, dO, reps);
+    CK(hipEventRecord(a)); hipLaunchKernelGGL(kern, 1, 64, 0, 0, dA, dO, reps);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
+    double o[64]; CK(hipMemcpy(o, dO, sizeof o, hipMemcpyDeviceToHost));
+    printf("chol32 %-22s %.2f us per factor; L00 %.17g\n", name, ms * 1e3 / reps, o[0]);
+    return 0;
+  };
+  run(k_chol<2, 0>, "newton2 lds");
+  run(k_chol<1, 0>, "newton1 lds");
+  run(k_chol<0, 0>, "newton0 lds");
+  run(k_chol<1, 1>, "newton1 readlane");
+  run(k_chol<0, 1>, "newton0 readlane");
+  {
+    const int n = 1 << 20; std::vector<double> hx(n); unsigned long long st = 88172645463325252ull;
+    for (int i = 0; i < n; ++i) { st ^= st << 13; st ^= st >> 7; st ^= st << 17; hx[i] = std::ldexp((double)(st >> 11) / 9007199254740992.0 + 0.5, (int)(st % 60) - 30); }
+    double *dx, *de; CK(hipMalloc(&dx, n * 8)); CK(hipMalloc(&de, 2 * n * 8));
+    CK(hipMemcpy(dx, hx.data(), n * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_rsqacc, n / 256, 256, 0, 0, dx, de, n);
+    std::vector<double> he(2 * n); CK(hipMemcpy(he.data(), de, 2 * n * 8, hipMemcpyDeviceToHost));
+    double m0 = 0, m1 = 0; for (int i = 0; i < n; ++i) { m0 = std::max(m0, he[2 * i]); m1 = std::max(m1, he[2 * i + 1]); }
+    printf("v_rsq_f64 max rel err %.3g ; after 1 Newton %.3g\n", m0, m1);
+  }
+  return 0;
+}

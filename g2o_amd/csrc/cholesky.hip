@@ -13,7 +13,7 @@
 //   k_chol_scatter           input blocks -> fronts (+ lambda on the diagonal)
 //   per level l (all fronts of a level are independent):
 //     k_extend_add     children's update matrices AND update vectors -> parent fronts;
-//                      one workgroup per (front, 16-column slab), children in fixed order
+//                      one workgroup per (front, 4-column slab), children in fixed order
 //     k_potrf0         first 32x32 diagonal block of every front + its forward solve
 //     k_step (x panels) one launch per 32-column panel step: every workgroup owns one 64x64
 //                      tile (I, J) of the panel region, solves the panel rows of I and J
@@ -90,17 +90,18 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     while (lo < hi) { const int mid = (lo + hi) >> 1; if (rel[mid] < b) lo = mid + 1; else hi = mid; }
     const int j1 = lo;
     for (int j = j0 + (int)threadIdx.x; j < j1; j += 256) v[rel[j]] += u[j];
-    // lower triangle of the slab, column by column: threads run down the rows (coalesced U reads,
-    // mostly-contiguous F writes), 4 independent loads in flight per thread
-    for (int j = j0; j < j1; ++j) {
+    // lower triangle of the slab: one wave per column, lanes run down the rows (coalesced U
+    // reads, mostly-contiguous F writes), 4 independent loads in flight per lane
+    const int j = j0 + (int)(threadIdx.x >> 6);
+    if (j < j1) {
       const double* Uj = U + (size_t)j * mc;
       double* Fj = F + (size_t)rel[j] * m;
-      for (int i0 = j + (int)threadIdx.x; i0 < nrc; i0 += 1024) {
+      for (int i0 = j + (int)(threadIdx.x & 63); i0 < nrc; i0 += 256) {
         double val[4];
         int ri[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int i = i0 + q * 256;
+          const int i = i0 + q * 64;
           ri[q] = -1;
           val[q] = 0.0;
           if (i < nrc) { val[q] = Uj[i]; ri[q] = rel[i]; }
@@ -126,21 +127,20 @@ __device__ __forceinline__ double rlane(double v, int l) {
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Factor the 32x32 diagonal block held row-wise by lanes 0..31 (row[c] = A(lane, c), c <= lane;
-// rows >= kb padded with the identity). Fully unrolled (j, c compile-time: no selects); column j
-// of L is broadcast through LDS (col, 32 doubles, read back two at a time, double-buffered so
-// one LDS wait per step). On return row[c] = L(lane, c), dinv[lane] = 1 / L(lane, lane).
+// rows >= kb padded with the identity). On return row[c] = L(lane, c), dinv[lane] = 1/L(lane, lane).
 // Returns false if a pivot was not positive (cs_chol's `d <= 0` test).
-// A single wave runs every instruction at 4 cycles: the step body is kept to ~45 instructions.
+// Latency-shaped for one wave: fully unrolled (no selects); column j of L is broadcast through LDS
+// (double-buffered; LDS ops of one wave complete in order, so no waits are placed by hand); the
+// next pivot is formed by its own lane from l_{j+1,j} ahead of the broadcast, so the sequential
+// chain per column is readlane -> rsq + 1 Newton step -> 2 FMAs.
 __device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col, double* dinv) {
   bool ok = true;
+  double djj = rlane(row[0], 0);
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const double djj = rlane(row[j], j);
     ok &= djj > 0.0;
     const double d = djj > 0.0 ? djj : 1.0;
-    // 1/sqrt(d) by v_rsq_f64 + two Newton steps (relative error ~1e-16), sqrt(d) = d / sqrt(d)
-    double r = __builtin_amdgcn_rsq(d);
-    r = r * (1.5 - 0.5 * d * r * r);
+    double r = __builtin_amdgcn_rsq(d);  // ~5e-8 relative; one Newton step -> ~4e-15
     r = r * (1.5 - 0.5 * d * r * r);
     const double ljj = d * r;
     const double lrj = lane == j ? ljj : row[j] * r;  // lanes < j hold 0 in row[j]
@@ -149,7 +149,7 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col,
     if (j + 1 < NB) {
       double* cb = col + (j & 1) * NB;
       if (lane < NB) cb[lane] = lrj;
-      lds_fence();
+      djj = rlane(row[j + 1] - lrj * lrj, j + 1);  // lane j+1 owns both factors
 #pragma unroll
       for (int c = ((j + 1) & ~1); c < NB; c += 2) {
         const double2 cc = *reinterpret_cast<const double2*>(cb + c);
@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(256) k_step(const Task* __restrict__ tasks, co
                                               double* __restrict__ fronts, double* __restrict__ lbuf,
                                               double* __restrict__ vecs, double* __restrict__ ysol,
                                               int* __restrict__ fail) {
-  __shared__ __attribute__((aligned(16))) double Lk[NB][NB + 2];  // L_kk rows (16-B aligned, stride 34)
+  __shared__ __attribute__((aligned(16))) double LkT[NB][NB + 2];  // LkT[u][q] = L_kk(q, u), stride 34
   __shared__ double dv[NB], yk[NB];
   __shared__ double sh[2 * TT * PS];  // Pa | Pb; reused as the 64 x 65 result tile
   __shared__ double Dn[NB * DS];      // next diagonal block
@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(256) k_step(const Task* __restrict__ tasks, co
   // ---- stage L_kk, y_k, the raw panel rows of I (and J), prefetch the C tile
   for (int e = tid; e < NB * NB; e += 256) {
     const int q = e & (NB - 1), u = e >> 5;
-    Lk[q][u] = (q < kb && u <= q) ? L[(size_t)(k0 + u) * m + k0 + q] : (q == u ? 1.0 : 0.0);
+    LkT[u][q] = (q < kb && u <= q) ? L[(size_t)(k0 + u) * m + k0 + q] : (q == u ? 1.0 : 0.0);
   }
   if (tid < NB) yk[tid] = tid < kb ? ysol[me.c0 + k0 + tid] : 0.0;
 #pragma unroll
@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(256) k_step(const Task* __restrict__ tasks, co
   double cv[16];
   if (upd) load_ctile(F, m, I0, J0, ns, tid, cv);
   __syncthreads();
-  if (tid < NB) dv[tid] = 1.0 / Lk[tid][tid];
+  if (tid < NB) dv[tid] = 1.0 / LkT[tid][tid];
   __syncthreads();
 
   // ---- TRSM: rows of I (threads 0..63) and of J (64..127) against L_kk
@@ -322,20 +322,21 @@ __global__ void __launch_bounds__(256) k_step(const Task* __restrict__ tasks, co
     double x[NB];
 #pragma unroll
     for (int q = 0; q < NB; ++q) x[q] = P[q];
+    // column-oriented: x_j is final after one multiply, the updates of the later x_q are
+    // independent, so the dependent chain is 2 operations per column
     double s2 = 0.0;
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      double s = x[q];
+    for (int j = 0; j < NB; ++j) {
+      x[j] *= dv[j];
+      s2 += x[j] * yk[j];
 #pragma unroll
-      for (int u = 0; u + 1 < q; u += 2) {
-        const double2 l2 = *reinterpret_cast<const double2*>(&Lk[q][u]);
-        s -= x[u] * l2.x;
-        s -= x[u + 1] * l2.y;
+      for (int q = ((j + 1) & ~1); q < NB; q += 2) {
+        const double2 l2 = *reinterpret_cast<const double2*>(&LkT[j][q]);
+        if (q > j) x[q] -= x[j] * l2.x;
+        x[q + 1] -= x[j] * l2.y;
       }
-      if (q & 1) s -= x[q - 1] * Lk[q][q - 1];
-      x[q] = s * dv[q];
-      s2 += x[q] * yk[q];
-      asm volatile("" ::: "memory");  // keep the L_kk row reads of step q from being hoisted en masse
+#pragma unroll
+      for (int q = j + 1; q < NB; ++q) asm volatile("" : "+v"(x[q]));  // no deferred updates
     }
 #pragma unroll
     for (int q = 0; q < NB; ++q) P[q] = x[q];
@@ -385,11 +386,13 @@ __global__ void __launch_bounds__(256) k_step(const Task* __restrict__ tasks, co
 }
 
 // ---------------------------------------------------------------------------- contribution block
-// U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns in 32-wide chunks, the next
-// chunk prefetched into registers. Task: s, b = ti | tj << 16.
+// U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns in 64-wide chunks staged in
+// LDS, the next chunk prefetched into registers. Task: s, b = ti | tj << 16.
+constexpr int SK = 64;          // K chunk
+constexpr int SPS = SK + 2;     // LDS row stride
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                               double* __restrict__ fronts, const double* __restrict__ lbuf) {
-  __shared__ double sh[2 * TT * PS];
+  __shared__ double sh[2 * TT * SPS];
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, ns = me.ns;
@@ -401,38 +404,58 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
   double cv[16];
   load_ctile(F, m, I0, J0, m, tid, cv);
   double* Pa = sh;
-  double* Pb = sh + TT * PS;
-  double pa[8], pb[8];
+  double* Pb = sh + TT * SPS;
+  double pa[16], pb[16];
   auto fetch = [&](int kc) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), k = kc + (e >> 6);
       pa[u] = (k < ns && I0 + r < m) ? L[(size_t)k * m + I0 + r] : 0.0;
       pb[u] = (k < ns && J0 + r < m) ? L[(size_t)k * m + J0 + r] : 0.0;
     }
   };
-  MfmaTile T;
-  T.zero();
-  fetch(0);
-  for (int kc = 0; kc < ns; kc += NB) {
+  const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
+  const int lr = lane & 15, lk = lane >> 4;
+  dx4 acc[2][2];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = dx4{0.0, 0.0, 0.0, 0.0};
+  fetch(0);
+  for (int kc = 0; kc < ns; kc += SK) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), k = e >> 6;
-      Pa[r * PS + k] = pa[u];
-      Pb[r * PS + k] = pb[u];
+      Pa[r * SPS + k] = pa[u];
+      Pb[r * SPS + k] = pb[u];
     }
     __syncthreads();
-    if (kc + NB < ns) fetch(kc + NB);
-    T.step(Pa, Pb, lane, w);
+    if (kc + SK < ns) fetch(kc + SK);
+#pragma unroll
+    for (int kk = 0; kk < SK / 4; ++kk) {
+      const int k = kk * 4 + lk;
+      const double a0 = Pa[(wr + lr) * SPS + k], a1 = Pa[(wr + 16 + lr) * SPS + k];
+      const double b0 = Pb[(wc + lr) * SPS + k], b1 = Pb[(wc + 16 + lr) * SPS + k];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
     __syncthreads();
   }
-  T.store(sh, lane, w);
+  double* Ct = sh;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Ct[(wr + x * 16 + lk + 4 * i) * CS + wc + y * 16 + lr] = acc[x][y][i];
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
     const int gi = I0 + r, gj = J0 + c;
-    if (gi < m && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
+    if (gi < m && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - Ct[r * CS + c];
   }
 }
 
@@ -488,7 +511,14 @@ __global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_l
     double part = 0.0;
     if (q < kb) {
       const double* cl = L + (size_t)(k0 + q) * m;
-      for (int i = k0 + kb + g; i < ns; i += 8) part += cl[i] * xs[i];
+      double p4[4] = {0.0, 0.0, 0.0, 0.0};
+      int i = k0 + kb + g;
+      for (; i + 24 < ns; i += 32) {  // 4 independent loads in flight
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p4[u] += cl[i + 8 * u] * xs[i + 8 * u];
+      }
+      for (; i < ns; i += 8) p4[0] += cl[i] * xs[i];
+      part = (p4[0] + p4[1]) + (p4[2] + p4[3]);
     }
     red[g][q] = part;
     __syncthreads();

@@ -70,6 +70,6 @@ void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int
                    const double* ysol, double* xsol, hipStream_t s);
 void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, double* xsol,
                   int max_ns, hipStream_t s);
-constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 16, CHOL_BW = 4;
+constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 4, CHOL_BW = 4;
 }  // namespace launch
 }  // namespace g2ohip

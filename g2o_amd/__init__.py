@@ -17,7 +17,7 @@ import numpy as np
 from . import synth  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libg2o_hip.so")
+LIB_PATH = os.environ.get("G2OHIP_LIB") or os.path.join(HERE, "libg2o_hip.so")
 
 
 class BatchStats(C.Structure):
@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
         "g2ohip_comm_unique_id": ([P], I),
         "g2ohip_set_comm": ([P, P, I, I], I),
         "g2ohip_set_comm_local": ([P, C.c_char_p, I, I], I),
+        "g2ohip_debug_phases": ([P, I], I),
         "g2ohip_symbolic_analyze": ([I, I, I, P, P, P, P], I),
         "g2ohip_enable_kernel_timing": ([P, I], None),
         "g2ohip_kernel_ms": ([P, C.c_char_p], D),

@@ -238,6 +238,14 @@ int g2ohip_set_comm_local(g2ohip_graph* g, const char* key, int rank, int nranks
   return guarded([&] { return g->e->set_comm_local(key, rank, nranks); });
 }
 
+int g2ohip_debug_phases(unsigned long long* out, int max_records) {
+  try {
+    return g2ohip::launch::debug_phases(out, max_records);
+  } catch (...) {
+    return 0;
+  }
+}
+
 int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int* perm, double* stats) {
   if (nblocks <= 0 || bdim <= 0 || nblk < 0 || (nblk > 0 && (!bi || !bj))) return G2OHIP_ERR_ARG;
   try {

@@ -28,12 +28,15 @@
 // factor and the solution are bitwise reproducible run to run (no atomics).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
 namespace g2ohip {
 
 using launch::FrontDesc;
+using launch::StepTask;
 using launch::Task;
 
 constexpr int NB = 32;   // panel width
@@ -43,6 +46,36 @@ constexpr int DS = 33;   // LDS row stride of a 32 x 32 diagonal block
 constexpr int CS = TT + 1;
 
 typedef double dx4 __attribute__((ext_vector_type(4)));
+
+// Load that never branches: the address is selected and the value masked. A guarded load
+// (`ok ? p[i] : 0`) compiles to a branch with its own s_waitcnt, which serialises every load of an
+// unrolled batch; this form keeps the whole batch in flight.
+template <class T>
+__device__ __forceinline__ T ld0(const T* p, int idx, bool ok) {  // front-local index (m^2 < 2^31)
+  const T v = p[ok ? idx : 0];
+  return ok ? v : T(0);
+}
+
+// Optional phase stamps (development build, -DG2OHIP_PHASES): workgroup 0 / thread 0 of each
+// instrumented launch records s_memtime at phase boundaries; read back by g2ohip_debug_phases.
+#ifdef G2OHIP_PHASES
+__device__ unsigned long long g_phase[4096][8];
+__device__ unsigned int g_phase_n;
+#define PH_BEGIN(id)                                                       \
+  const bool ph_on_ = threadIdx.x == 0 && blockIdx.x == 0;                 \
+  unsigned ph_k_ = 0;                                                      \
+  if (ph_on_) {                                                            \
+    ph_k_ = atomicAdd(&g_phase_n, 1u) % 4096u;                             \
+    g_phase[ph_k_][0] = (id);                                              \
+    g_phase[ph_k_][1] = __builtin_amdgcn_s_memtime();                      \
+    for (int q_ = 2; q_ < 8; ++q_) g_phase[ph_k_][q_] = 0;                 \
+  }
+#define PH(i) \
+  if (ph_on_) g_phase[ph_k_][i] = __builtin_amdgcn_s_memtime();
+#else
+#define PH_BEGIN(id)
+#define PH(i)
+#endif
 
 __global__ void __launch_bounds__(256) k_chol_scatter(long long nent, const double* __restrict__ vals,
                                                       const long long* __restrict__ dst,
@@ -63,7 +96,7 @@ __global__ void __launch_bounds__(256) k_vec_init(const FrontDesc* __restrict__ 
   const FrontDesc me = fd[blockIdx.x];
   const int m = me.ns + me.nr;
   double* v = vecs + me.vec_off;
-  for (int i = threadIdx.x; i < m; i += 256) v[i] = i < me.ns ? rhs_p[me.c0 + i] : 0.0;
+  for (int i = threadIdx.x; i < m; i += 256) v[i] = ld0(rhs_p, me.c0 + i, i < me.ns);
 }
 
 // ---------------------------------------------------------------------------- extend-add
@@ -104,7 +137,9 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
           const int i = i0 + q * 64;
           ri[q] = -1;
           val[q] = 0.0;
-          if (i < nrc) { val[q] = Uj[i]; ri[q] = rel[i]; }
+          const bool ok = i < nrc;
+          val[q] = ld0(Uj, i, ok);
+          ri[q] = ok ? ld0(rel, i, ok) : -1;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -133,7 +168,8 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 // (double-buffered; LDS ops of one wave complete in order, so no waits are placed by hand); the
 // next pivot is formed by its own lane from l_{j+1,j} ahead of the broadcast, so the sequential
 // chain per column is readlane -> rsq + 1 Newton step -> 2 FMAs.
-__device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col, double* dinv) {
+// The forward solve L y = b rides along: y holds b(lane) on entry and y(lane) on return.
+__device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, double* col, double* dinv) {
   bool ok = true;
   double djj = rlane(row[0], 0);
 #pragma unroll
@@ -146,6 +182,8 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col,
     const double lrj = lane == j ? ljj : row[j] * r;  // lanes < j hold 0 in row[j]
     row[j] = lrj;
     if (lane == j) dinv[j] = r;
+    const double yj = rlane(y, j) * r;
+    y = lane == j ? yj : (lane > j ? y - lrj * yj : y);
     if (j + 1 < NB) {
       double* cb = col + (j & 1) * NB;
       if (lane < NB) cb[lane] = lrj;
@@ -167,34 +205,37 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col,
 
 // Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid) and
 // forward-solve vy (LDS, kb values) in place. On return D holds L (lower, with diagonal).
+// Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid) and
+// forward-solve vy (LDS, kb values) in place. On return D holds L (lower, with diagonal).
+// Lanes 32..63 run the same instruction stream on the identity: lane 32 + c ends holding column c
+// of L^-1 (right-looking substitution on the broadcast columns of L), written row-major to linv.
 __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, double* col, double* dinv, int lane,
-                                             int* fail) {
+                                             int* fail, double* linv) {
   double row[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
-    const double a = (lane < kb && c <= lane) ? D[lane * DS + c] : 0.0;
-    row[c] = (lane >= kb && c == lane) ? 1.0 : a;
+    const double a = ld0(D, lane * DS + c, lane < kb && c <= lane);
+    row[c] = ((lane >= kb && c == lane) || lane - NB == c) ? 1.0 : a;
   }
-  const bool ok = chol32(row, lane, col, dinv);
+  double y = ld0(vy, lane, lane < kb);
+  const bool ok = chol32(row, y, lane, col, dinv);
   if (lane == 0 && !ok) *fail = 1;
-  double y = lane < kb ? vy[lane] : 0.0;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    const double yj = rlane(y, j) * dinv[j];
-    y = lane == j ? yj : (lane > j ? y - row[j] * yj : y);
-  }
   if (lane < kb) {
 #pragma unroll
     for (int c = 0; c < NB; ++c)
       if (c <= lane) D[lane * DS + c] = row[c];
     vy[lane] = y;
   }
+  if (lane >= NB) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) linv[i * NB + (lane - NB)] = row[i];
+  }
 }
-
-// D (LDS) -> L block at (r0, r0) of a front's factor columns (ld m), y -> ysol
 __device__ __forceinline__ void publish_block(const double* D, const double* vy, int kb, double* L, int m, int r0,
                                               double* ysol, int tid) {
-  for (int e = tid; e < NB * NB; e += 256) {
+#pragma unroll
+  for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+    const int e = tid + 256 * u_;
     const int r = e & (NB - 1), c = e >> 5;
     if (r < kb && c < kb && r >= c) L[(size_t)(r0 + c) * m + r0 + r] = D[r * DS + c];
   }
@@ -206,23 +247,31 @@ __device__ __forceinline__ void publish_block(const double* D, const double* vy,
 __global__ void __launch_bounds__(256) k_potrf0(const int* __restrict__ level_list, const FrontDesc* __restrict__ fd,
                                                 const double* __restrict__ fronts, double* __restrict__ lbuf,
                                                 const double* __restrict__ vecs, double* __restrict__ ysol,
-                                                int* __restrict__ fail) {
+                                                double* __restrict__ linv, int* __restrict__ fail) {
   __shared__ double D[NB * DS];
   __shared__ __attribute__((aligned(16))) double col[2 * NB];
   __shared__ double dinv[NB], vy[NB];
+  PH_BEGIN(1)
   const FrontDesc me = fd[level_list[blockIdx.x]];
   const int m = me.ns + me.nr, kb = min(NB, me.ns);
   const double* F = fronts + me.front_off;
   const int tid = threadIdx.x;
-  for (int e = tid; e < NB * NB; e += 256) {
+#pragma unroll
+  for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+    const int e = tid + 256 * u_;
     const int r = e & (NB - 1), c = e >> 5;
-    if (r < kb && c < kb && r >= c) D[r * DS + c] = F[(size_t)c * m + r];
+    const bool ok = r < kb && c < kb && r >= c;
+    const double a = ld0(F, c * m + r, ok);
+    if (ok) D[r * DS + c] = a;
   }
   if (tid < kb) vy[tid] = vecs[me.vec_off + tid];
   __syncthreads();
-  if (tid < 64) factor_block(D, kb, vy, col, dinv, tid, fail);
+  PH(2)
+  if (tid < 64) factor_block(D, kb, vy, col, dinv, tid, fail, linv + (size_t)me.c0 * (NB * NB));
   __syncthreads();
+  PH(3)
   publish_block(D, vy, kb, lbuf + me.l_off, m, 0, ysol + me.c0, tid);
+  PH(4)
 }
 
 // ---------------------------------------------------------------------------- panel step
@@ -267,93 +316,108 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
   for (int u = 0; u < 16; ++u) {
     const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
     const int gi = I0 + r, gj = J0 + c;
-    cv[u] = (gi < m && gj < climit && gi >= gj) ? F[(size_t)gj * m + gi] : 0.0;
+    cv[u] = ld0(F, gj * m + gi, gi < m && gj < climit && gi >= gj);
   }
 }
 
 // Task: s; a = k0 | kb << 16; b = ti | tj << 16; c = flags (1: update the tile, 2: factor the
 // next diagonal block). Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
-__global__ void __launch_bounds__(256) k_step(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                              double* __restrict__ fronts, double* __restrict__ lbuf,
-                                              double* __restrict__ vecs, double* __restrict__ ysol,
+__global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, double* __restrict__ fronts,
+                                              double* __restrict__ lbuf, double* __restrict__ vecs,
+                                              double* __restrict__ ysol, double* __restrict__ linv,
                                               int* __restrict__ fail) {
-  __shared__ __attribute__((aligned(16))) double LkT[NB][NB + 2];  // LkT[u][q] = L_kk(q, u), stride 34
-  __shared__ double dv[NB], yk[NB];
+  __shared__ double Li[NB * PS];      // L_kk^-1, row-major, stride 34
+  __shared__ double yk[NB];
   __shared__ double sh[2 * TT * PS];  // Pa | Pb; reused as the 64 x 65 result tile
   __shared__ double Dn[NB * DS];      // next diagonal block
   __shared__ __attribute__((aligned(16))) double col[2 * NB];
   __shared__ double dinvn[NB], vn[NB];
-  const Task t = tasks[blockIdx.x];
-  const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr, ns = me.ns;
-  double* F = fronts + me.front_off;
-  double* L = lbuf + me.l_off;
-  double* v = vecs + me.vec_off;
-  const int k0 = t.a & 0xffff, kb = t.a >> 16;
-  const int ti = t.b & 0xffff, tj = t.b >> 16;
-  const bool upd = t.c & 1, nextf = t.c & 2, writer = tj == 0;
+  PH_BEGIN(2)
+  const StepTask t = tasks[blockIdx.x];
+  const int m = t.m, ns = t.ns;
+  double* F = fronts + t.f_off;
+  double* L = lbuf + t.l_off;
+  double* v = vecs + t.v_off;
+  const int k0 = t.k0kb & 0xffff, kb = t.k0kb >> 16;
+  const int ti = t.tile & 0xffff, tj = t.tile >> 16;
+  const bool upd = t.flags & 1, nextf = t.flags & 2, writer = tj == 0;
   const int r0 = k0 + kb;
   const int I0 = r0 + ti * TT, J0 = r0 + tj * TT;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   double* Pa = sh;
   double* Pb = sh + TT * PS;
 
-  // ---- stage L_kk, y_k, the raw panel rows of I (and J), prefetch the C tile
-  for (int e = tid; e < NB * NB; e += 256) {
-    const int q = e & (NB - 1), u = e >> 5;
-    LkT[u][q] = (q < kb && u <= q) ? L[(size_t)(k0 + u) * m + k0 + q] : (q == u ? 1.0 : 0.0);
-  }
-  if (tid < NB) yk[tid] = tid < kb ? ysol[me.c0 + k0 + tid] : 0.0;
+  // ---- stage L_kk^-1, y_k, the raw panel rows of I (and J), prefetch the C tile: every global
+  // load is issued before the first LDS store so the whole batch is in flight at once
+  const double* Lin = linv + (size_t)(t.c0 + k0) * (NB * NB);
+  double lv[NB * NB / 256], pav[8], pbv[8], cv[16];
+#pragma unroll
+  for (int u_ = 0; u_ < NB * NB / 256; ++u_) lv[u_] = Lin[tid + 256 * u_];
+  const double ykv = ld0(ysol, t.c0 + k0 + tid, tid < kb);
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-    Pa[r * PS + q] = (q < kb && I0 + r < m) ? F[(size_t)(k0 + q) * m + I0 + r] : 0.0;
-    if (upd) Pb[r * PS + q] = (q < kb && J0 + r < m) ? F[(size_t)(k0 + q) * m + J0 + r] : 0.0;
+    pav[u] = ld0(F, (k0 + q) * m + I0 + r, q < kb && I0 + r < m);
+    pbv[u] = ld0(F, (k0 + q) * m + J0 + r, upd && q < kb && J0 + r < m);
   }
-  double cv[16];
   if (upd) load_ctile(F, m, I0, J0, ns, tid, cv);
-  __syncthreads();
-  if (tid < NB) dv[tid] = 1.0 / LkT[tid][tid];
-  __syncthreads();
-
-  // ---- TRSM: rows of I (threads 0..63) and of J (64..127) against L_kk
-  if (tid < 64 || (upd && tid < 128)) {
-    double* P = tid < 64 ? Pa + tid * PS : Pb + (tid - 64) * PS;
-    double x[NB];
 #pragma unroll
-    for (int q = 0; q < NB; ++q) x[q] = P[q];
-    // column-oriented: x_j is final after one multiply, the updates of the later x_q are
-    // independent, so the dependent chain is 2 operations per column
+  for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+    const int e = tid + 256 * u_;
+    Li[(e >> 5) * PS + (e & (NB - 1))] = lv[u_];
+  }
+  if (tid < NB) yk[tid] = ykv;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+    Pa[r * PS + q] = pav[u];
+    Pb[r * PS + q] = pbv[u];
+  }
+  __syncthreads();
+  PH(2)
+
+  // ---- TRSM as a product: X = P L_kk^-T on v_mfma_f64_16x16x4f64; wave w owns rows 16w..16w+15
+  // of both panels (A = P rows, B[k][c] = L_kk^-1(c, k))
+  {
+    const int lr = lane & 15, lk = lane >> 4;
+    dx4 xa0 = {0.0, 0.0, 0.0, 0.0}, xa1 = xa0, xb0 = xa0, xb1 = xa0;
+#pragma unroll
+    for (int kk = 0; kk < NB / 4; ++kk) {
+      const int k = kk * 4 + lk;
+      const double a = Pa[(16 * w + lr) * PS + k], b = Pb[(16 * w + lr) * PS + k];
+      const double l0 = Li[lr * PS + k], l1 = Li[(16 + lr) * PS + k];
+      xa0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, l0, xa0, 0, 0, 0);
+      xa1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, l1, xa1, 0, 0, 0);
+      xb0 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, l0, xb0, 0, 0, 0);
+      xb1 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, l1, xb1, 0, 0, 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * w + lk + 4 * i;
+      Pa[r * PS + lr] = xa0[i];
+      Pa[r * PS + 16 + lr] = xa1[i];
+      Pb[r * PS + lr] = xb0[i];
+      Pb[r * PS + 16 + lr] = xb1[i];
+    }
+  }
+  __syncthreads();
+  if (writer && tid < 64 && I0 + tid < m) {  // forward-solve update of the front vector: v_i -= x_i y_k
     double s2 = 0.0;
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      x[j] *= dv[j];
-      s2 += x[j] * yk[j];
-#pragma unroll
-      for (int q = ((j + 1) & ~1); q < NB; q += 2) {
-        const double2 l2 = *reinterpret_cast<const double2*>(&LkT[j][q]);
-        if (q > j) x[q] -= x[j] * l2.x;
-        x[q + 1] -= x[j] * l2.y;
-      }
-#pragma unroll
-      for (int q = j + 1; q < NB; ++q) asm volatile("" : "+v"(x[q]));  // no deferred updates
-    }
-#pragma unroll
-    for (int q = 0; q < NB; ++q) P[q] = x[q];
-    if (tid < 64 && writer && I0 + tid < m) {  // forward-solve update of the front vector
-      const double nv = v[I0 + tid] - s2;
-      v[I0 + tid] = nv;
-      if (nextf && tid < NB) vn[tid] = nv;
-    }
+    for (int q = 0; q < NB; ++q) s2 += Pa[tid * PS + q] * yk[q];
+    const double nv = v[I0 + tid] - s2;
+    v[I0 + tid] = nv;
+    if (nextf && tid < NB) vn[tid] = nv;
   }
-  __syncthreads();
+  PH(3)
 
   // ---- writers store the L21 rows of block I
   if (writer) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-      if (q < kb && I0 + r < m) L[(size_t)(k0 + q) * m + I0 + r] = Pa[r * PS + q];
+      if (q < kb && I0 + r < m) L[(k0 + q) * m + I0 + r] = Pa[r * PS + q];
     }
   }
   if (!upd) return;
@@ -375,20 +439,24 @@ __global__ void __launch_bounds__(256) k_step(const Task* __restrict__ tasks, co
       if (nextf && r < NB && c < NB) Dn[r * DS + c] = nvv;
     }
   }
+  PH(4)
   if (!nextf) return;
 
   // ---- tile (0, 0): factor the next diagonal block and forward-solve its rhs
   __syncthreads();
   const int kbn = min(NB, ns - r0);
-  if (tid < 64) factor_block(Dn, kbn, vn, col, dinvn, tid, fail);
+  __syncthreads();  // vn complete
+  if (tid < 64) factor_block(Dn, kbn, vn, col, dinvn, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB));
   __syncthreads();
-  publish_block(Dn, vn, kbn, L, m, r0, ysol + me.c0, tid);
+  PH(5)
+  publish_block(Dn, vn, kbn, L, m, r0, ysol + t.c0, tid);
+  PH(6)
 }
 
 // ---------------------------------------------------------------------------- contribution block
-// U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns in 64-wide chunks staged in
+// U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns in 32-wide chunks staged in
 // LDS, the next chunk prefetched into registers. Task: s, b = ti | tj << 16.
-constexpr int SK = 64;          // K chunk
+constexpr int SK = 32;          // K chunk
 constexpr int SPS = SK + 2;     // LDS row stride
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                               double* __restrict__ fronts, const double* __restrict__ lbuf) {
@@ -405,13 +473,13 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
   load_ctile(F, m, I0, J0, m, tid, cv);
   double* Pa = sh;
   double* Pb = sh + TT * SPS;
-  double pa[16], pb[16];
+  double pa[SK / 4], pb[SK / 4];
   auto fetch = [&](int kc) {
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < SK / 4; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), k = kc + (e >> 6);
-      pa[u] = (k < ns && I0 + r < m) ? L[(size_t)k * m + I0 + r] : 0.0;
-      pb[u] = (k < ns && J0 + r < m) ? L[(size_t)k * m + J0 + r] : 0.0;
+      pa[u] = ld0(L, k * m + I0 + r, k < ns && I0 + r < m);
+      pb[u] = ld0(L, k * m + J0 + r, k < ns && J0 + r < m);
     }
   };
   const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
@@ -424,7 +492,7 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
   fetch(0);
   for (int kc = 0; kc < ns; kc += SK) {
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < SK / 4; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), k = e >> 6;
       Pa[r * SPS + k] = pa[u];
       Pb[r * SPS + k] = pb[u];
@@ -528,7 +596,7 @@ __global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_l
       double Lc[NB];
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        double a = (lane < kb && j >= lane && j < kb) ? cl[j] : 0.0;
+        double a = ld0(cl, j, lane < kb && j >= lane && j < kb);
         if (lane >= kb && j == lane) a = 1.0;
         Lc[j] = a;
       }
@@ -557,6 +625,23 @@ __global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_l
 
 namespace launch {
 
+int debug_phases(unsigned long long* out, int maxrec) {
+#ifdef G2OHIP_PHASES
+  unsigned n = 0;
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_phase_n), sizeof n));
+  const int cnt = (int)std::min<unsigned>(n, 4096u);
+  const int k = std::min(cnt, maxrec);
+  if (out && k > 0) HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8 * k));
+  const unsigned z = 0;
+  HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_n), &z, sizeof z));
+  return k;
+#else
+  (void)out; (void)maxrec;
+  return 0;
+#endif
+}
+
 void chol_scatter(long long nent, const double* vals, const long long* dst, const unsigned char* is_diag,
                   const double* lam, double* fronts, hipStream_t s) {
   if (nent <= 0) return;
@@ -575,15 +660,15 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
   KERNEL_CHECK();
 }
 void chol_potrf0(int nfronts, const int* level_list, const FrontDesc* fd, const double* fronts, double* lbuf,
-                 const double* vecs, double* ysol, int* fail, hipStream_t s) {
+                 const double* vecs, double* ysol, double* linv, int* fail, hipStream_t s) {
   if (nfronts <= 0) return;
-  hipLaunchKernelGGL(k_potrf0, nfronts, 256, 0, s, level_list, fd, fronts, lbuf, vecs, ysol, fail);
+  hipLaunchKernelGGL(k_potrf0, nfronts, 256, 0, s, level_list, fd, fronts, lbuf, vecs, ysol, linv, fail);
   KERNEL_CHECK();
 }
-void chol_step(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, double* lbuf, double* vecs,
-               double* ysol, int* fail, hipStream_t s) {
+void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
+               double* linv, int* fail, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_step, ntasks, 256, 0, s, tasks, fd, fronts, lbuf, vecs, ysol, fail);
+  hipLaunchKernelGGL(k_step, ntasks, 256, 0, s, tasks, fronts, lbuf, vecs, ysol, linv, fail);
   KERNEL_CHECK();
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {

@@ -220,6 +220,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   for (size_t t = 0; t < bi.size(); ++t)
     if (bi[t] != bj[t]) { P.adji[fill[bi[t]]++] = bj[t]; P.adji[fill[bj[t]]++] = bi[t]; }
   sym = analyze(P);
+  if ((long long)sym.max_front * sym.max_front >= (1LL << 31))
+    throw DeviceError("front too large for 32-bit in-front indexing");
   // scatter map: input block t (bi, bj) col-major bdim x bdim
   nent = (long long)bi.size() * bdim * bdim;
   std::vector<long long> hdst(nent, -1);
@@ -272,6 +274,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     using launch::Task;
     const int NB = launch::CHOL_NB, TT = launch::CHOL_TT, EA = launch::CHOL_EA;
     std::vector<Task> tk;
+    std::vector<launch::StepTask> stk;
     ops.clear();
     for (size_t l = 0; l < sym.levels.size(); ++l) {
       const auto& lv = sym.levels[l];
@@ -288,7 +291,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       int maxp = 0;
       for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
       for (int p = 0; p < maxp; ++p) {
-        Op st{2, (int)tk.size(), 0};
+        Op st{2, (int)stk.size(), 0};
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
           const int k0 = p * NB;
@@ -299,10 +302,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
             for (int ti = tj; ti < T; ++ti) {
               int flags = tj < TJ ? 1 : 0;
               if (ti == 0 && tj == 0 && r0 < q.ns) flags |= 2;
-              tk.push_back(Task{sn, k0 | (kb << 16), ti | (tj << 16), flags});
+              stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0,
+                                             k0 | (kb << 16), ti | (tj << 16), flags});
             }
         }
-        st.count = (int)tk.size() - st.off;
+        st.count = (int)stk.size() - st.off;
         if (st.count) ops.push_back(st);
       }
       Op sy{3, (int)tk.size(), 0};
@@ -327,6 +331,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       bwd_off.push_back((int)tk.size());
     }
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
+    step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
   }
   children.upload(sym.children.empty() ? std::vector<int>{0} : sym.children, s);
   relmap.upload(sym.relmap.empty() ? std::vector<int>{0} : sym.relmap, s);
@@ -337,6 +342,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   rhs_p.resize(std::max(sym.n, 1));
   y_p.resize(std::max(sym.n, 1));
   lbuf.resize(std::max<long long>(lpool, 1));
+  linv.resize((size_t)(sym.n + launch::CHOL_NB) * launch::CHOL_NB * launch::CHOL_NB);  // one 32x32 L_kk^-1 per panel start
   x_p.resize(std::max(sym.n, 1));
 }
 
@@ -350,8 +356,10 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
     switch (op.kind) {
       case 0: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), fronts.get(), vecs.get(), s); break;
       case 1: launch::chol_potrf0(op.count, level_lists.get() + op.off, fd.get(), fronts.get(), lbuf.get(), vecs.get(),
-                                  y_p.get(), fail, s); break;
-      case 2: launch::chol_step(op.count, t, fd.get(), fronts.get(), lbuf.get(), vecs.get(), y_p.get(), fail, s); break;
+                                  y_p.get(), linv.get(), fail, s); break;
+      case 2: launch::chol_step(op.count, step_tasks.get() + op.off, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),
+                                linv.get(), fail, s);
+        break;
       default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;
     }
   }

@@ -60,7 +60,8 @@ struct DeviceCholesky {
   struct Op { int kind, off, count; };  // kind 0 extend-add, 1 first diagonal block, 2 panel step, 3 contribution block
   std::vector<Op> ops;
   DevBuf<launch::Task> tasks;
-  DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, lbuf;
+  DevBuf<launch::StepTask> step_tasks;
+  DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, lbuf, linv;
   long long lpool = 0;
   void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
   // numeric LL^T fused with the forward solve of rhs (y = L^-1 P rhs)

@@ -157,6 +157,9 @@ long long g2ohip_kernel_count(g2ohip_graph* g, const char* name);
 /* algorithmic bytes / flops of one launch of the named kernel class (for roofline accounting) */
 double g2ohip_kernel_bytes(g2ohip_graph* g, const char* name);
 double g2ohip_kernel_flops(g2ohip_graph* g, const char* name);
+/* development builds (-DG2OHIP_PHASES) only: per-launch phase stamps of the Cholesky kernels,
+ * 8 x u64 per record {kernel id, t0, t1..t6}; returns the record count (0 in product builds) */
+int g2ohip_debug_phases(unsigned long long* out, int max_records);
 const char* g2ohip_last_error(void);
 const char* g2ohip_version(void);
 

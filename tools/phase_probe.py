@@ -1,0 +1,43 @@
+"""Development probe: per-phase timing of the Cholesky kernels from s_memtime stamps.
+Run with the phase build:  make -C g2o_amd phases && G2OHIP_LIB=g2o_amd/libg2o_hip_phases.so python tools/phase_probe.py
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import g2o_amd  # noqa: E402
+from g2o_amd import synth  # noqa: E402
+
+CLK = 2.4e3  # s_memtime ticks per microsecond (core clock counter)
+
+
+def main():
+    prob = synth.by_name(sys.argv[1] if len(sys.argv) > 1 else "C4")
+    opt = g2o_amd.SparseOptimizer(0).add_problem(prob)
+    L = g2o_amd.lib()
+    opt.optimize_step(0)
+    buf = (C.c_ulonglong * (8 * 4096))()
+    L.g2ohip_debug_phases(buf, 4096)  # drop warmup records
+    opt.optimize_step(1)
+    n = L.g2ohip_debug_phases(buf, 4096)
+    a = np.frombuffer(buf, dtype=np.uint64, count=8 * n).reshape(n, 8).astype(np.int64)
+    print(f"{n} records")
+    for kid, name, labels in ((1, "k_potrf0", ["stage", "factor", "publish"]),
+                              (2, "k_step", ["stage", "trsm", "write+mfma+rmw", "factor", "publish"])):
+        r = a[a[:, 0] == kid]
+        if not len(r):
+            continue
+        print(f"{name}: {len(r)} launches")
+        t = r[:, 1:]
+        for i, lab in enumerate(labels):
+            d = t[:, i + 1] - t[:, i]
+            ok = (t[:, i + 1] > 0) & (t[:, i] > 0)
+            if ok.any():
+                print(f"   {lab:16s} median {np.median(d[ok]) / CLK:7.2f} us  mean {np.mean(d[ok]) / CLK:7.2f} us  (n={ok.sum()})")
+
+
+if __name__ == "__main__":
+    main()

@@ -178,6 +178,20 @@ __global__ void k_chol6(const double* A, double* out, int reps) {
   if (h == 0) out[i] = acc;
 }
 
+
+// I-cache evictor: ~100 KB of straight-line code, run on every CU
+template <int N>
+__device__ __forceinline__ double chain(double a, double b) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) { a = a * b + (double)(i & 7); asm volatile("" : "+v"(a)); }
+  return a;
+}
+__global__ void k_evict(double* out, double b) {
+  double a = threadIdx.x;
+  a = chain<12000>(a, b);
+  if (a == 12345.678) out[0] = a;
+}
+
 __global__ void k_empty(int* p) { if (threadIdx.x == 0 && p[0] == 12345) p[1] = 1; }
 
 // dependent chain of global loads: idx = next[idx]
@@ -261,6 +275,20 @@ int main() {
     for (int q = 0; q < reps; ++q) hipLaunchKernelGGL(k_chol7, 256, 64, 0, 0, dA, dO, reps);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b)); CK(hipEventElapsedTime(&ms, a, b));
     printf("v7 grid 256: %.2f us\n", ms * 1e3 / reps);
+    // cold I-cache: evictor on every CU between launches; time the chol launch alone via events
+    float tot = 0, tev = 0;
+    hipEvent_t c0, c1; CK(hipEventCreate(&c0)); CK(hipEventCreate(&c1));
+    for (int q = 0; q < 50; ++q) {
+      hipLaunchKernelGGL(k_evict, 1024, 64, 0, 0, dO + 50, 0.999);
+      CK(hipEventRecord(c0)); hipLaunchKernelGGL(k_chol7, 1, 64, 0, 0, dA, dO, reps); CK(hipEventRecord(c1));
+      CK(hipEventSynchronize(c1)); float t; CK(hipEventElapsedTime(&t, c0, c1)); tot += t;
+    }
+    for (int q = 0; q < 50; ++q) {
+      hipLaunchKernelGGL(k_chol7, 1, 64, 0, 0, dA, dO, reps);
+      CK(hipEventRecord(c0)); hipLaunchKernelGGL(k_chol7, 1, 64, 0, 0, dA, dO, reps); CK(hipEventRecord(c1));
+      CK(hipEventSynchronize(c1)); float t; CK(hipEventElapsedTime(&t, c0, c1)); tev += t;
+    }
+    printf("v7 single launch after evictor: %.2f us ; after warm launch: %.2f us\n", tot * 1e3 / 50, tev * 1e3 / 50);
   }
   {
     const int n = 1 << 20; std::vector<double> hx(n); unsigned long long st = 88172645463325252ull;

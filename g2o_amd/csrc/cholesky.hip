@@ -188,11 +188,15 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, d
       double* cb = col + (j & 1) * NB;
       if (lane < NB) cb[lane] = lrj;
       djj = rlane(row[j + 1] - lrj * lrj, j + 1);  // lane j+1 owns both factors
+      // all reads of the broadcast column first (one LDS wait), then the updates
+      const int c0 = (j + 1) & ~1;
+      double2 cc[NB / 2];
 #pragma unroll
-      for (int c = ((j + 1) & ~1); c < NB; c += 2) {
-        const double2 cc = *reinterpret_cast<const double2*>(cb + c);
-        if (c > j) row[c] -= lrj * cc.x;
-        row[c + 1] -= lrj * cc.y;
+      for (int c = c0; c < NB; c += 2) cc[c >> 1] = *reinterpret_cast<const double2*>(cb + c);
+#pragma unroll
+      for (int c = c0; c < NB; c += 2) {
+        if (c > j) row[c] -= lrj * cc[c >> 1].x;
+        row[c + 1] -= lrj * cc[c >> 1].y;
       }
       // materialise this step's updates now: left alone, the scheduler defers the FMAs until each
       // row[c] is next needed and keeps every broadcast column live (512 VGPRs + spills)
@@ -220,10 +224,9 @@ __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, doub
   double y = ld0(vy, lane, lane < kb);
   const bool ok = chol32(row, y, lane, col, dinv);
   if (lane == 0 && !ok) *fail = 1;
-  if (lane < kb) {
+  if (lane < kb) {  // whole row (the upper part is never read back)
 #pragma unroll
-    for (int c = 0; c < NB; ++c)
-      if (c <= lane) D[lane * DS + c] = row[c];
+    for (int c = 0; c < NB; ++c) D[lane * DS + c] = row[c];
     vy[lane] = y;
   }
   if (lane >= NB) {
@@ -542,7 +545,7 @@ __global__ void k_ipermute(int n, const int* __restrict__ perm, const double* __
 //   k_bwd_gemv  t_s = y_s - L21^T x_rows for every front of the level; one wave per column,
 //               lanes run down the column (coalesced), x_rows gathered from the finished ancestors
 //   k_bwd_tri   x_s = L11^-T t_s per front: 32-column blocks from the last, in-supernode column
-//               dots by 8 threads per column, the 32x32 triangle by one wave in registers.
+//               dots by 8 threads per column, the 32x32 triangle as a product with L_kk^-1.
 // Task (gemv): s, a = first column (4 per workgroup).
 __global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                   const int* __restrict__ rows, const double* __restrict__ lbuf,
@@ -562,20 +565,29 @@ __global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks
 }
 
 __global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_list, const FrontDesc* __restrict__ fd,
-                                                 const double* __restrict__ lbuf, double* __restrict__ xsol) {
+                                                 const double* __restrict__ lbuf, const double* __restrict__ linv,
+                                                 double* __restrict__ xsol) {
   extern __shared__ __attribute__((aligned(16))) double xs[];  // [ns]: t_s, solved in place
   __shared__ double red[8][NB];
+  __shared__ double tsh[NB];
   const int s = level_list[blockIdx.x];
   const FrontDesc me = fd[s];
   const int m = me.ns + me.nr, ns = me.ns;
   const double* L = lbuf + me.l_off;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x;
   for (int i = tid; i < ns; i += 256) xs[i] = xsol[me.c0 + i];
   __syncthreads();
   const int nblk = (ns + NB - 1) / NB;
   const int q = tid & (NB - 1), g = tid >> 5;
   for (int bk = nblk - 1; bk >= 0; --bk) {
     const int k0 = bk * NB, kb = min(NB, ns - k0);
+    // column q of L_kk^-1 (row-major in linv), fetched ahead of the dot products
+    double li[NB];
+    if (tid < NB) {
+      const double* Lb = linv + (size_t)(me.c0 + k0) * (NB * NB) + tid;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) li[i] = Lb[i * NB];
+    }
     double part = 0.0;
     if (q < kb) {
       const double* cl = L + (size_t)(k0 + q) * m;
@@ -590,33 +602,18 @@ __global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_l
     }
     red[g][q] = part;
     __syncthreads();
-    if (tid < 64) {
-      // Lc[j] = L(k0 + j, k0 + lane), j >= lane: column k0+lane of the diagonal block
-      const double* cl = L + (size_t)(k0 + min(lane, NB - 1)) * m + k0;
-      double Lc[NB];
+    if (tid < NB) {  // x_blk = L_kk^-T (t_blk - dots): a 32-long dot per lane, no sequential chain
+      double r = 0.0;
+      if (tid < kb) {
+        r = xs[k0 + tid];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        double a = ld0(cl, j, lane < kb && j >= lane && j < kb);
-        if (lane >= kb && j == lane) a = 1.0;
-        Lc[j] = a;
+        for (int gg = 0; gg < 8; ++gg) r -= red[gg][tid];
       }
-      double v = 0.0;
-      if (lane < kb) {
-        double r = xs[k0 + lane];
+      tsh[tid] = r;  // one wave writes and reads tsh: LDS order within the wave suffices
+      double x = 0.0;
 #pragma unroll
-        for (int gg = 0; gg < 8; ++gg) r -= red[gg][lane];
-        v = r;
-      }
-      double dg = 1.0;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) dg = j == lane ? Lc[j] : dg;
-      const double rinv = 1.0 / dg;
-#pragma unroll
-      for (int j = NB - 1; j >= 0; --j) {
-        const double xj = rlane(v, j) * rlane(rinv, j);
-        v = lane == j ? xj : (lane < j ? v - Lc[j] * xj : v);
-      }
-      if (lane < kb) xs[k0 + lane] = v;
+      for (int i = 0; i < NB; ++i) x += li[i] * tsh[i];
+      if (tid < kb) xs[k0 + tid] = x;
     }
     __syncthreads();
   }
@@ -692,14 +689,14 @@ void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int
   hipLaunchKernelGGL(k_bwd_gemv, ntasks, 256, 0, s, tasks, fd, rows, lbuf, ysol, xsol);
   KERNEL_CHECK();
 }
-void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, double* xsol,
-                  int max_ns, hipStream_t s) {
+void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, const double* linv,
+                  double* xsol, int max_ns, hipStream_t s) {
   if (nfronts <= 0) return;
   const size_t bytes = (size_t)max_ns * sizeof(double);
   if (bytes > 150 * 1024) throw DeviceError("supernode wider than LDS for the backward solve");
   if (bytes > 64 * 1024)
     HIP_CHECK(hipFuncSetAttribute((const void*)k_bwd_tri, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-  hipLaunchKernelGGL(k_bwd_tri, nfronts, 256, bytes, s, level_list, fd, lbuf, xsol);
+  hipLaunchKernelGGL(k_bwd_tri, nfronts, 256, bytes, s, level_list, fd, lbuf, linv, xsol);
   KERNEL_CHECK();
 }
 

@@ -370,7 +370,7 @@ void DeviceCholesky::solve(double* x, hipStream_t s) {
     const int nf = level_off[l + 1] - level_off[l];
     launch::chol_bwd_gemv(bwd_off[l + 1] - bwd_off[l], tasks.get() + bwd_off[l], fd.get(), rows.get(), lbuf.get(),
                           y_p.get(), x_p.get(), s);
-    launch::chol_bwd_tri(nf, level_lists.get() + level_off[l], fd.get(), lbuf.get(), x_p.get(), max_ns, s);
+    launch::chol_bwd_tri(nf, level_lists.get() + level_off[l], fd.get(), lbuf.get(), linv.get(), x_p.get(), max_ns, s);
   }
   launch::chol_ipermute(sym.n, perm.get(), x_p.get(), x, s);
 }

@@ -75,8 +75,8 @@ void chol_permute(int n, const int* perm, const double* in, double* out, hipStre
 void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]
 void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int* rows, const double* lbuf,
                    const double* ysol, double* xsol, hipStream_t s);
-void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, double* xsol,
-                  int max_ns, hipStream_t s);
+void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, const double* linv,
+                  double* xsol, int max_ns, hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only
 constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 4, CHOL_BW = 4;
 }  // namespace launch

@@ -966,7 +966,8 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     ds_row.upload(srow, stream);
     ds_diag.upload(sdiag, stream);
     dDinv.resize(std::max(nLloc * 9, 1));
-    dW.resize(std::max<long long>((long long)nHpl * pd * ld, 1));
+    dW.resize(std::max<long long>((long long)nHpl * pd * ld, 1));  // G = Hpl U^-T
+    dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
     chol.setup(num_poses, pd, s_bi, s_bj, stream);
   } else {
@@ -1076,11 +1077,12 @@ void Engine::solve_async() {  // block_solver.hpp:314-447
   double* S = dS.get();
   double* bschur = dS.get() + (size_t)nS * pd * pd;
   timer.begin("schur_dinv", stream);
-  launch::schur_dinv(nLloc, d_lm_ptr.get(), dHll.get(), Hpl, dscal.get(), dDinv.get(), dW.get(), dfail.get() + 1, stream);
+  launch::schur_prep(nLloc, lm_begin, d_lm_ptr.get(), dHll.get(), Hpl, db.get() + size_poses, dscal.get(), dDinv.get(),
+                     dW.get(), dCl.get(), dfail.get() + 1, stream);
   timer.end(stream);
   timer.begin("schur_pairs", stream);
   launch::schur_pairs(nS, ds_ptr.get(), ds_pairs.get(), ds_hpp.get(), ds_diag.get(), ds_row.get(), dH.get(), dW.get(),
-                      Hpl, d_blk_lm.get(), db.get(), size_poses, dscal.get() + 4, S, bschur, stream);
+                      d_blk_lm.get(), dCl.get(), db.get(), dscal.get() + 4, S, bschur, stream);
   timer.end(stream);
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
   HIP_CHECK(hipEventRecord(ev_[1], stream));
@@ -1419,9 +1421,9 @@ int Engine::set_comm_local(const std::string& key, int r, int nr) {
 double Engine::kernel_bytes(const std::string& name) const {
   // algorithmic bytes per launch (SURVEY.md §8d formulas)
   const double npl = nHpl, pb = (double)pd * ld * 8;
-  if (name == "schur_pairs") return (double)nS * pd * pd * 8 * 2 /*Hpp read + S write*/ + npl * pb * 2 /*W, Hpl once*/ +
+  if (name == "schur_pairs") return (double)nS * pd * pd * 8 * 2 /*Hpp read + S write*/ + npl * pb /*G once*/ +
                                     (double)npairs * 8 + size_poses * 16.0;
-  if (name == "schur_dinv") return local_lm.size() * (9 * 8.0 * 2) + npl * pb * 2;
+  if (name == "schur_dinv") return local_lm.size() * (9 * 8.0 * 2 + 3 * 8.0 * 2) + npl * pb * 2;
   if (name == "linearize") return ne * (family == FAM_BA ? (2 + 3 + 4) * 8.0 + 8 + (double)(slot_stride0 + slot_stride1 + pd * ld) * 8 : 0.0);
   if (name == "backsub") return local_lm.size() * (3 * 8.0 * 2 + 72) + npl * (pb + 4) + size_poses * 8.0;
   if (name == "chol_factor") return (double)chol.sym.front_pool * 8 * 2;

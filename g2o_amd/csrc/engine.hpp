@@ -184,7 +184,7 @@ class Engine {
   VRed vr_pose, vr_lm;
   // schur
   DevBuf<int> d_lm_ptr, d_blk_pose, d_blk_lm;
-  DevBuf<double> dDinv, dW, dS, dbschur;
+  DevBuf<double> dDinv, dW, dS, dbschur, dCl;
   int nS = 0;
   long long npairs = 0;
   DevBuf<int> ds_ptr, ds_pairs, ds_hpp, ds_row;

@@ -6,11 +6,11 @@
 //                 to per-edge slots (no atomics, no locks).
 //   k_vertex_reduce  deterministic segmented reduction of the slots into Hpp/Hll diagonal
 //                 blocks and b (replaces the per-vertex omp locks + copyB, :467-517).
-//   k_schur_dinv  landmark pass of BlockSolver::solve (:342-360): Dinv = (Hll+lambda I)^-1,
-//                 W = Hpl Dinv per observation block.
-//   k_schur_pairs Hschur(i,j) = Hpp(i,j) - sum_l W_il Hpl_jl^T and bschur (:361-400) computed
-//                 output-stationary: a group of lanes owns one Schur block and walks its
-//                 precomputed (W, Hpl) pair list; fixed-order tree reduction, no atomics.
+//   k_schur_prep  landmark pass of BlockSolver::solve (:342-360): Dinv = (Hll+lambda I)^-1,
+//                 and the split Hll+lambda I = U U^T, G = Hpl U^-T, c = U^-1 b_l.
+//   k_schur_pairs Hschur(i,j) = Hpp(i,j) - sum_l G_il G_jl^T and bschur = b - sum G c (:361-400)
+//                 computed output-stationary: a group of lanes owns one Schur block and walks its
+//                 precomputed pair list; fixed-order tree reduction, no atomics.
 //   k_backsub     x_l = Dinv (b_l - Hpl^T x_p) (:420-446).
 //   k_error/k_oplus  computeActiveErrors (sparse_optimizer.cpp:63-90) and update (:441-454).
 #include <hip/hip_runtime.h>
@@ -214,13 +214,16 @@ __global__ void __launch_bounds__(256) k_offblock_reduce(int nb, int bsz, const 
 }
 
 // ------------------------------------------------------------------------------ Schur
-// Landmark pass: Dinv = (Hll + lambda I)^-1 (cofactor inverse, cf. Eigen's 3x3 inverse used by
-// block_solver.hpp:350), W_a = Hpl_a * Dinv for every observation block a of the landmark.
+// Landmark pass (block_solver.hpp:341-360): Dinv = (Hll + lambda I)^-1 (cofactor inverse, as
+// Eigen's 3x3 inverse; kept for the back-substitution) and the symmetric split
+//   Hll + lambda I = U U^T (3x3 Cholesky),  G_a = Hpl_a U^-T,  c_l = U^-1 b_l,
+// so that Hpl Dinv Hpl^T = G G^T and Hpl Dinv b_l = G c_l: the pair pass then streams ONE 6x3 block
+// per observation instead of both W = Hpl Dinv and Hpl.
 template <int PD>
 __global__ void __launch_bounds__(256)
-    k_schur_dinv(int nl, const int* __restrict__ lm_ptr, const double* __restrict__ Hll, const double* __restrict__ Hpl,
-                 const double* __restrict__ lam, double* __restrict__ Dinv, double* __restrict__ W,
-                 int* __restrict__ fail) {
+    k_schur_prep(int nl, int lm0, const int* __restrict__ lm_ptr, const double* __restrict__ Hll,
+                 const double* __restrict__ Hpl, const double* __restrict__ bl_all, const double* __restrict__ lam,
+                 double* __restrict__ Dinv, double* __restrict__ G, double* __restrict__ cl_all, int* __restrict__ fail) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= nl) return;
   const double lambda = *lam;
@@ -243,34 +246,57 @@ __global__ void __launch_bounds__(256)
   Di[2] = (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0)) * inv;
   Di[5] = (m(0, 1) * m(2, 0) - m(0, 0) * m(2, 1)) * inv;
   Di[8] = (m(0, 0) * m(1, 1) - m(0, 1) * m(1, 0)) * inv;
-  if (!(det != 0.0) || !isfinite(inv)) *fail = 1;
   double* Do = Dinv + (size_t)l * 9;
 #pragma unroll
   for (int k = 0; k < 9; ++k) Do[k] = Di[k];
+  // U (lower): reciprocal pivots u_ii^-1
+  const double d0 = m(0, 0);
+  const double r0 = 1.0 / sqrt(d0);
+  const double u10 = m(1, 0) * r0, u20 = m(2, 0) * r0;
+  const double d1 = m(1, 1) - u10 * u10;
+  const double r1 = 1.0 / sqrt(d1);
+  const double u21 = (m(2, 1) - u20 * u10) * r1;
+  const double d2 = m(2, 2) - u20 * u20 - u21 * u21;
+  const double r2 = 1.0 / sqrt(d2);
+  if (!(det != 0.0) || !isfinite(inv) || !(d0 > 0.0) || !(d1 > 0.0) || !(d2 > 0.0)) *fail = 1;
+  {  // c_l = U^-1 b_l
+    const double* bl = bl_all + (size_t)(lm0 + l) * 3;
+    const double g0 = bl[0] * r0;
+    const double g1 = (bl[1] - u10 * g0) * r1;
+    const double g2 = (bl[2] - u20 * g0 - u21 * g1) * r2;
+    double* co = cl_all + (size_t)(lm0 + l) * 3;
+    co[0] = g0; co[1] = g1; co[2] = g2;
+  }
   for (int a_ = lm_ptr[l]; a_ < lm_ptr[l + 1]; ++a_) {
-    const double* Bm = Hpl + (size_t)a_ * PD * 3;
-    double* Wo = W + (size_t)a_ * PD * 3;
-    double Bl[PD * 3];
+    const double2* Bm = reinterpret_cast<const double2*>(Hpl + (size_t)a_ * PD * 3);
+    double2* Go = reinterpret_cast<double2*>(G + (size_t)a_ * PD * 3);
+    double h[PD * 3], g[PD * 3];
 #pragma unroll
-    for (int k = 0; k < PD * 3; ++k) Bl[k] = Bm[k];
+    for (int k = 0; k < PD * 3 / 2; ++k) { const double2 v = Bm[k]; h[2 * k] = v.x; h[2 * k + 1] = v.y; }
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < PD; ++r) {  // row r: U g^T = h^T (columns of the col-major 6x3 block)
+      const double g0 = h[r] * r0;
+      const double g1 = (h[PD + r] - u10 * g0) * r1;
+      const double g2 = (h[2 * PD + r] - u20 * g0 - u21 * g1) * r2;
+      g[r] = g0; g[PD + r] = g1; g[2 * PD + r] = g2;
+    }
 #pragma unroll
-      for (int r = 0; r < PD; ++r)
-        Wo[c * PD + r] = Bl[r] * Di[c * 3] + Bl[PD + r] * Di[c * 3 + 1] + Bl[2 * PD + r] * Di[c * 3 + 2];
+    for (int k = 0; k < PD * 3 / 2; ++k) Go[k] = double2{g[2 * k], g[2 * k + 1]};
   }
 }
 
-// Output-stationary Schur pair products. G lanes per Schur block.
-template <int PD, int G>
+// Output-stationary Schur pair products: S(i,j) = Hpp(i,j) (+ lambda on the diagonal)
+//   - sum over the landmarks observed by both cameras of G_a G_b^T, G lanes per Schur block,
+// pairs in landmark order inside each block (deterministic, no atomics).
+template <int PD, int GL>
 __global__ void __launch_bounds__(256)
     k_schur_pairs(int nS, const int* __restrict__ s_ptr, const int2* __restrict__ pairs, const int* __restrict__ s_hpp,
                   const unsigned char* __restrict__ s_diag, const int* __restrict__ s_row,
-                  const double* __restrict__ Hpp, const double* __restrict__ W, const double* __restrict__ Hpl,
-                  const int* __restrict__ blk_lm, const double* __restrict__ b, int size_poses,
-                  const double* __restrict__ lam, double* __restrict__ S, double* __restrict__ bschur) {
+                  const double* __restrict__ Hpp, const double* __restrict__ G, const int* __restrict__ blk_lm,
+                  const double* __restrict__ cl_all, const double* __restrict__ b, const double* __restrict__ lam,
+                  double* __restrict__ S, double* __restrict__ bschur) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int t = gid / G, lane = gid % G;
+  const int t = gid / GL, lane = gid % GL;
   const bool active = t < nS;
   double acc[PD * PD];
   double cb[PD];
@@ -281,45 +307,55 @@ __global__ void __launch_bounds__(256)
   const bool diag = active && s_diag[t];
   if (active) {
     const int p0 = s_ptr[t], p1 = s_ptr[t + 1];
-    for (int p = p0 + lane; p < p1; p += G) {
+    for (int p = p0 + lane; p < p1; p += GL) {
       const int2 pr = pairs[p];
-      const double* Wa = W + (size_t)pr.x * PD * 3;
-      const double* Hb = Hpl + (size_t)pr.y * PD * 3;
-      double wa[PD * 3], hb[PD * 3];
+      const double2* Ga = reinterpret_cast<const double2*>(G + (size_t)pr.x * PD * 3);
+      const double2* Gb = reinterpret_cast<const double2*>(G + (size_t)pr.y * PD * 3);
+      double ga[PD * 3], gb[PD * 3];
 #pragma unroll
-      for (int k = 0; k < PD * 3; ++k) { wa[k] = Wa[k]; hb[k] = Hb[k]; }
+      for (int k = 0; k < PD * 3 / 2; ++k) {
+        const double2 x = Ga[k], y = Gb[k];
+        ga[2 * k] = x.x; ga[2 * k + 1] = x.y;
+        gb[2 * k] = y.x; gb[2 * k + 1] = y.y;
+      }
 #pragma unroll
       for (int c = 0; c < PD; ++c)
 #pragma unroll
         for (int r = 0; r < PD; ++r)
-          acc[c * PD + r] += wa[r] * hb[c] + wa[PD + r] * hb[PD + c] + wa[2 * PD + r] * hb[2 * PD + c];
-      if (diag) {  // coefficients: B Dinv b_l = W b_l
-        const double* bl = b + size_poses + (size_t)blk_lm[pr.x] * 3;
-        const double b0 = bl[0], b1 = bl[1], b2 = bl[2];
+          acc[c * PD + r] += ga[r] * gb[c] + ga[PD + r] * gb[PD + c] + ga[2 * PD + r] * gb[2 * PD + c];
+      if (diag) {  // Hpl Dinv b_l = G c_l
+        const double* cl = cl_all + (size_t)blk_lm[pr.x] * 3;
+        const double c0 = cl[0], c1 = cl[1], c2 = cl[2];
 #pragma unroll
-        for (int r = 0; r < PD; ++r) cb[r] += wa[r] * b0 + wa[PD + r] * b1 + wa[2 * PD + r] * b2;
+        for (int r = 0; r < PD; ++r) cb[r] += ga[r] * c0 + ga[PD + r] * c1 + ga[2 * PD + r] * c2;
       }
     }
   }
 #pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) {
+  for (int m = GL / 2; m >= 1; m >>= 1) {
 #pragma unroll
-    for (int k = 0; k < PD * PD; ++k) acc[k] += __shfl_xor(acc[k], m, G);
+    for (int k = 0; k < PD * PD; ++k) acc[k] += __shfl_xor(acc[k], m, GL);
 #pragma unroll
-    for (int k = 0; k < PD; ++k) cb[k] += __shfl_xor(cb[k], m, G);
+    for (int k = 0; k < PD; ++k) cb[k] += __shfl_xor(cb[k], m, GL);
   }
   if (!active) return;
   const int hp = s_hpp[t];
   const double lambda = *lam;
   double* So = S + (size_t)t * PD * PD;
-  for (int k = lane; k < PD * PD; k += G) {
-    double h = hp >= 0 ? Hpp[(size_t)hp * PD * PD + k] : 0.0;
-    if (diag && (k % (PD + 1)) == 0) h += lambda;
-    So[k] = h - acc[k];
+  // every lane holds the full sums; lane l stores the entries k = l (mod GL) (compile-time k:
+  // a runtime index into acc[] would put it in scratch)
+  const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * PD * PD;
+#pragma unroll
+  for (int k = 0; k < PD * PD; ++k) {
+    if ((k % GL) != lane) continue;
+    const double h = hp >= 0 ? Hh[k] : 0.0;
+    So[k] = ((diag && (k % (PD + 1)) == 0) ? h + lambda : h) - acc[k];
   }
-  if (diag && lane < PD) {
+  if (diag) {
     const int row = s_row[t];
-    bschur[(size_t)row * PD + lane] = b[(size_t)row * PD + lane] - cb[lane];
+#pragma unroll
+    for (int k = 0; k < PD; ++k)
+      if (k == lane) bschur[(size_t)row * PD + k] = b[(size_t)row * PD + k] - cb[k];
   }
 }
 
@@ -542,24 +578,23 @@ void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const do
   KERNEL_CHECK();
 }
 
-void schur_dinv(int nl, const int* lm_ptr, const double* Hll, const double* Hpl, const double* lam, double* Dinv,
-                double* W, int* fail, hipStream_t s) {
+void schur_prep(int nl, int lm0, const int* lm_ptr, const double* Hll, const double* Hpl, const double* bl_all,
+                const double* lam, double* Dinv, double* G, double* cl_all, int* fail, hipStream_t s) {
   if (nl <= 0) return;
-  hipLaunchKernelGGL(k_schur_dinv<6>, grid_for(nl, 256), 256, 0, s, nl, lm_ptr, Hll, Hpl, lam, Dinv, W, fail);
+  hipLaunchKernelGGL(k_schur_prep<6>, grid_for(nl, 256), 256, 0, s, nl, lm0, lm_ptr, Hll, Hpl, bl_all, lam, Dinv, G,
+                     cl_all, fail);
   KERNEL_CHECK();
 }
-
 void schur_pairs(int nS, const int* s_ptr, const int* pairs, const int* s_hpp, const unsigned char* s_diag,
-                 const int* s_row, const double* Hpp, const double* W, const double* Hpl, const int* blk_lm,
-                 const double* b, int size_poses, const double* lam, double* S, double* bschur, hipStream_t s) {
+                 const int* s_row, const double* Hpp, const double* G, const int* blk_lm, const double* cl_all,
+                 const double* b, const double* lam, double* S, double* bschur, hipStream_t s) {
   if (nS <= 0) return;
-  constexpr int G = 16;
-  hipLaunchKernelGGL((k_schur_pairs<6, G>), grid_for((size_t)nS * G, 256), 256, 0, s, nS, s_ptr,
-                     reinterpret_cast<const int2*>(pairs), s_hpp, s_diag, s_row, Hpp, W, Hpl, blk_lm, b, size_poses, lam,
-                     S, bschur);
+  constexpr int GL = 16;
+  hipLaunchKernelGGL((k_schur_pairs<6, GL>), grid_for((size_t)nS * GL, 256), 256, 0, s, nS, s_ptr,
+                     reinterpret_cast<const int2*>(pairs), s_hpp, s_diag, s_row, Hpp, G, blk_lm, cl_all, b, lam, S,
+                     bschur);
   KERNEL_CHECK();
 }
-
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
              int size_poses, int lm0, double* x, hipStream_t s) {
   if (nl <= 0) return;

@@ -27,11 +27,11 @@ void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, 
                    int st0, int st1, double* H, double* b, const int* boff, hipStream_t s);
 void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const double* slots, double* out,
                      const long long* dst, hipStream_t s);
-void schur_dinv(int nl, const int* lm_ptr, const double* Hll, const double* Hpl, const double* lam, double* Dinv,
-                double* W, int* fail, hipStream_t s);
+void schur_prep(int nl, int lm0, const int* lm_ptr, const double* Hll, const double* Hpl, const double* bl_all,
+                const double* lam, double* Dinv, double* G, double* cl_all, int* fail, hipStream_t s);
 void schur_pairs(int nS, const int* s_ptr, const int* pairs, const int* s_hpp, const unsigned char* s_diag,
-                 const int* s_row, const double* Hpp, const double* W, const double* Hpl, const int* blk_lm,
-                 const double* b, int size_poses, const double* lam, double* S, double* bschur, hipStream_t s);
+                 const int* s_row, const double* Hpp, const double* G, const int* blk_lm, const double* cl_all,
+                 const double* b, const double* lam, double* S, double* bschur, hipStream_t s);
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
              int size_poses, int lm0, double* x, hipStream_t s);
 void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s);

@@ -60,6 +60,6 @@ std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size = 48);
 
 // Full symbolic analysis with a given block ordering (bperm: new->old). If bperm is
 // empty, nested dissection is used.
-Symbolic analyze(const BlockPattern& P, std::vector<int> bperm = {}, double relax = 0.25, int relax_max_blocks = 16);
+Symbolic analyze(const BlockPattern& P, std::vector<int> bperm = {}, double relax = 0.25, int relax_max_blocks = 64);
 
 }  // namespace g2ohip

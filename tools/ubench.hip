@@ -192,6 +192,74 @@ __global__ void k_evict(double* out, double b) {
   if (a == 12345.678) out[0] = a;
 }
 
+
+// v8..v10: chol32 as in the product (early pivot, batched LDS column reads), different ways of
+// keeping the per-step updates materialised. MODE 0: volatile asm (product), 1: non-volatile asm,
+// 2: sched_barrier per step, 3: nothing
+template <int MODE>
+__device__ __forceinline__ bool chol32_m(double (&row)[NB], double& y, int lane, double* col, double* dinv) {
+  bool ok = true;
+  double djj = rlane(row[0], 0);
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    ok &= djj > 0.0;
+    const double d = djj > 0.0 ? djj : 1.0;
+    double r = __builtin_amdgcn_rsq(d);
+    r = r * (1.5 - 0.5 * d * r * r);
+    const double ljj = d * r;
+    const double lrj = lane == j ? ljj : row[j] * r;
+    row[j] = lrj;
+    if (lane == j) dinv[j] = r;
+    const double yj = rlane(y, j) * r;
+    y = lane == j ? yj : (lane > j ? y - lrj * yj : y);
+    if (j + 1 < NB) {
+      double* cb = col + (j & 1) * NB;
+      if (lane < NB) cb[lane] = lrj;
+      djj = rlane(row[j + 1] - lrj * lrj, j + 1);
+      const int c0 = (j + 1) & ~1;
+      double2 cc[NB / 2];
+#pragma unroll
+      for (int c = c0; c < NB; c += 2) cc[c >> 1] = *reinterpret_cast<const double2*>(cb + c);
+#pragma unroll
+      for (int c = c0; c < NB; c += 2) {
+        if (c > j) row[c] -= lrj * cc[c >> 1].x;
+        row[c + 1] -= lrj * cc[c >> 1].y;
+      }
+      if (MODE == 0) {
+#pragma unroll
+        for (int c = j + 1; c < NB; ++c) asm volatile("" : "+v"(row[c]));
+      } else if (MODE == 1) {
+#pragma unroll
+        for (int c = j + 1; c < NB; ++c) asm("" : "+v"(row[c]));
+      } else if (MODE == 2) {
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  return ok;
+}
+template <int MODE>
+__global__ void k_cholm(const double* A, double* out, int reps) {
+  __shared__ __attribute__((aligned(16))) double col[2 * NB];
+  __shared__ double dinv[NB];
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x >= 64) return;
+  double row[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) row[c] = (lane < NB && c <= lane) ? A[lane * NB + c] : (c == lane ? 1.0 : 0.0);
+  double y = lane;
+  __syncthreads();
+  long long t0 = __builtin_amdgcn_s_memtime();
+  chol32_m<MODE>(row, y, lane, col, dinv);
+  double acc = y;
+#pragma unroll
+  for (int c = 0; c < NB; ++c) acc += row[c];
+  asm volatile("" : "+v"(acc));
+  long long t1 = __builtin_amdgcn_s_memtime();
+  if (lane < NB) out[lane] = acc;
+  if (lane == 0) out[40] = (double)(t1 - t0);
+}
+
 __global__ void k_empty(int* p) { if (threadIdx.x == 0 && p[0] == 12345) p[1] = 1; }
 
 // dependent chain of global loads: idx = next[idx]
@@ -261,6 +329,20 @@ int main() {
   run(k_chol<0, 1>, "newton0 readlane");
   run(k_chol7, "v7 early pivot");
   run(k_chol6, "v6 half split");
+  auto runm = [&](auto kern, const char* name) -> int {
+    double tk = 0;
+    for (int q = 0; q < 20; ++q) {
+      hipLaunchKernelGGL(kern, 1, 64, 0, 0, dA, dO, reps);
+      double o[64]; CK(hipMemcpy(o, dO, sizeof o, hipMemcpyDeviceToHost));
+      if (q >= 10) tk += o[40];
+    }
+    printf("chol32 %-28s in-kernel %.0f cycles = %.2f us @2.4GHz\n", name, tk / 10, tk / 10 / 2400.0);
+    return 0;
+  };
+  runm(k_cholm<0>, "mode0 volatile asm");
+  runm(k_cholm<1>, "mode1 plain asm");
+  runm(k_cholm<2>, "mode2 sched_barrier");
+  runm(k_cholm<3>, "mode3 nothing");
   {  // alternate two different big kernels: I-cache cold on every launch?
     hipLaunchKernelGGL(k_chol7, 1, 64, 0, 0, dA, dO, reps);
     CK(hipEventRecord(a));

@@ -323,8 +323,8 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
   }
 }
 
-// Task: s; a = k0 | kb << 16; b = ti | tj << 16; c = flags (1: update the tile, 2: factor the
-// next diagonal block). Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
+// Task flags: 1 update the tile (else TRSM + L21 store only), 4 the step's next-diagonal task.
+// Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
 __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, double* __restrict__ fronts,
                                               double* __restrict__ lbuf, double* __restrict__ vecs,
                                               double* __restrict__ ysol, double* __restrict__ linv,
@@ -343,16 +343,91 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   double* v = vecs + t.v_off;
   const int k0 = t.k0kb & 0xffff, kb = t.k0kb >> 16;
   const int ti = t.tile & 0xffff, tj = t.tile >> 16;
-  const bool upd = t.flags & 1, nextf = t.flags & 2, writer = tj == 0;
+  const bool upd = t.flags & 1, writer = tj == 0;
   const int r0 = k0 + kb;
   const int I0 = r0 + ti * TT, J0 = r0 + tj * TT;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   double* Pa = sh;
   double* Pb = sh + TT * PS;
+  const double* Lin = linv + (size_t)(t.c0 + k0) * (NB * NB);
+
+  if (t.flags & 4) {
+    // ---- dedicated next-diagonal task (runs beside the tile tasks of this step): the 32x32 block
+    // D' = A(r0:r0+32, r0:r0+32) - X X^T with X = P(r0:r0+32) L_kk^-T, then its factor, inverse
+    // and forward solve. Only the critical chain of the panel step lives here.
+    const int kbn = min(NB, ns - r0);
+    double lv[NB * NB / 256], pv[NB * NB / 256], cdv[NB * NB / 256];
+#pragma unroll
+    for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+      const int e = tid + 256 * u_, r = e & (NB - 1), c = e >> 5;
+      lv[u_] = Lin[e];
+      pv[u_] = ld0(F, (k0 + c) * m + r0 + r, c < kb);
+      cdv[u_] = ld0(F, (r0 + c) * m + r0 + r, r >= c && r < kbn);
+    }
+    const double ykv = ld0(ysol, t.c0 + k0 + tid, tid < kb);
+    const double vo = ld0(v, r0 + tid, tid < kbn);
+#pragma unroll
+    for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+      const int e = tid + 256 * u_, r = e & (NB - 1), c = e >> 5;
+      Li[c * PS + r] = lv[u_];  // e = row * 32 + col of the row-major inverse: (c, r) = (row, col)
+      Pa[r * PS + c] = pv[u_];
+      Dn[r * DS + c] = cdv[u_];
+    }
+    if (tid < NB) yk[tid] = ykv;
+    __syncthreads();
+    const int lr = lane & 15, lk = lane >> 4;
+    dx4 x0 = {0.0, 0.0, 0.0, 0.0}, x1 = x0;
+    if (w < 2) {  // X rows 16w..16w+15
+#pragma unroll
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        const double a = Pa[(16 * w + lr) * PS + k];
+        x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Li[lr * PS + k], x0, 0, 0, 0);
+        x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Li[(16 + lr) * PS + k], x1, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (w < 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * w + lk + 4 * i;
+        Pa[r * PS + lr] = x0[i];
+        Pa[r * PS + 16 + lr] = x1[i];
+      }
+    }
+    __syncthreads();
+    {  // D' -= X X^T: wave w owns the 16x16 tile (w & 1, w >> 1)
+      const int tr = w & 1, tc = w >> 1;
+      dx4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Pa[(16 * tr + lr) * PS + k], Pa[(16 * tc + lr) * PS + k], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * tr + lk + 4 * i, c = 16 * tc + lr;
+        Dn[r * DS + c] -= acc[i];
+      }
+    }
+    if (tid < NB) {  // rhs of the next block: v - X y_k (same sum, same order as the writer task)
+      double s2 = 0.0;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) s2 += Pa[tid * PS + q] * yk[q];
+      vn[tid] = vo - s2;
+    }
+    __syncthreads();
+    PH(2)
+    if (tid < 64) factor_block(Dn, kbn, vn, col, dinvn, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB));
+    __syncthreads();
+    PH(3)
+    publish_block(Dn, vn, kbn, L, m, r0, ysol + t.c0, tid);
+    PH(4)
+    return;
+  }
 
   // ---- stage L_kk^-1, y_k, the raw panel rows of I (and J), prefetch the C tile: every global
   // load is issued before the first LDS store so the whole batch is in flight at once
-  const double* Lin = linv + (size_t)(t.c0 + k0) * (NB * NB);
   double lv[NB * NB / 256], pav[8], pbv[8], cv[16];
 #pragma unroll
   for (int u_ = 0; u_ < NB * NB / 256; ++u_) lv[u_] = Lin[tid + 256 * u_];
@@ -377,7 +452,6 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     Pb[r * PS + q] = pbv[u];
   }
   __syncthreads();
-  PH(2)
 
   // ---- TRSM as a product: X = P L_kk^-T on v_mfma_f64_16x16x4f64; wave w owns rows 16w..16w+15
   // of both panels (A = P rows, B[k][c] = L_kk^-1(c, k))
@@ -409,11 +483,8 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     double s2 = 0.0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) s2 += Pa[tid * PS + q] * yk[q];
-    const double nv = v[I0 + tid] - s2;
-    v[I0 + tid] = nv;
-    if (nextf && tid < NB) vn[tid] = nv;
+    v[I0 + tid] -= s2;
   }
-  PH(3)
 
   // ---- writers store the L21 rows of block I
   if (writer) {
@@ -436,24 +507,8 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   for (int u = 0; u < 16; ++u) {
     const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
     const int gi = I0 + r, gj = J0 + c;
-    if (gi < m && gj < ns && gi >= gj) {
-      const double nvv = cv[u] - sh[r * CS + c];
-      F[(size_t)gj * m + gi] = nvv;
-      if (nextf && r < NB && c < NB) Dn[r * DS + c] = nvv;
-    }
+    if (gi < m && gj < ns && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
   }
-  PH(4)
-  if (!nextf) return;
-
-  // ---- tile (0, 0): factor the next diagonal block and forward-solve its rhs
-  __syncthreads();
-  const int kbn = min(NB, ns - r0);
-  __syncthreads();  // vn complete
-  if (tid < 64) factor_block(Dn, kbn, vn, col, dinvn, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB));
-  __syncthreads();
-  PH(5)
-  publish_block(Dn, vn, kbn, L, m, r0, ysol + t.c0, tid);
-  PH(6)
 }
 
 // ---------------------------------------------------------------------------- contribution block

@@ -298,13 +298,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           if (k0 >= q.ns) continue;
           const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
           const int T = (m - r0 + TT - 1) / TT, TJ = (q.ns - r0 + TT - 1) / TT;
+          if (r0 < q.ns)  // the next diagonal block first: it is the step's critical chain
+            stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0,
+                                           k0 | (kb << 16), 0, 4});
           for (int tj = 0; tj < std::max(TJ, 1); ++tj)
-            for (int ti = tj; ti < T; ++ti) {
-              int flags = tj < TJ ? 1 : 0;
-              if (ti == 0 && tj == 0 && r0 < q.ns) flags |= 2;
+            for (int ti = tj; ti < T; ++ti)
               stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0,
-                                             k0 | (kb << 16), ti | (tj << 16), flags});
-            }
+                                             k0 | (kb << 16), ti | (tj << 16), tj < TJ ? 1 : 0});
         }
         st.count = (int)stk.size() - st.off;
         if (st.count) ops.push_back(st);

@@ -26,7 +26,7 @@ def main():
     a = np.frombuffer(buf, dtype=np.uint64, count=8 * n).reshape(n, 8).astype(np.int64)
     print(f"{n} records")
     for kid, name, labels in ((1, "k_potrf0", ["stage", "factor", "publish"]),
-                              (2, "k_step", ["stage", "trsm", "write+mfma+rmw", "factor", "publish"])):
+                              (2, "k_step(diag task)", ["stage+trsm+syrk", "factor", "publish"])):
         r = a[a[:, 0] == kid]
         if not len(r):
             continue

@@ -162,11 +162,14 @@ def main():
     avg_ms = kt[dom]["avg_ms"]
     algo_bytes = opt.kernel_bytes(dom)
     achieved = algo_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    # HBM traffic per launch from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs of
+    # this same command, gpu_session.sh; parsed and gfx950-corrected by tools/pmc_traffic.py)
     traffic = None
-    tf = os.environ.get("G2OHIP_TRAFFIC_JSON")
-    if tf and os.path.exists(tf):
+    tf = os.environ.get("G2OHIP_TRAFFIC_JSON") or os.path.join(HERE, "profiles", "traffic.json")
+    if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get(dom)
+            rec = json.load(open(tf)).get(dom)
+            traffic = rec["bytes_per_launch"] if isinstance(rec, dict) else rec
         except Exception:
             traffic = None
     out = {

@@ -1,0 +1,64 @@
+"""Turn rocprofv3 --pmc counter_collection.csv files into per-launch HBM traffic per kernel.
+
+Usage: python tools/pmc_traffic.py OUT.json FETCH_DIR WRITE_DIR
+  FETCH_DIR: a `rocprofv3 --pmc FETCH_SIZE` pass, WRITE_DIR: a `rocprofv3 --pmc WRITE_SIZE` pass
+  (separate passes: FETCH_SIZE needs 3 TCC counters, WRITE_SIZE 2, the TCC block holds 4).
+
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KB; on gfx950
+FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so it is doubled. Traffic
+per launch = mean over the kernel's dispatches of (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes.
+Kernel names are mapped to the bench.py stage names below.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+STAGES = {  # substring of the kernel name -> stage name used by bench.py
+    "k_schur_pairs": "schur_pairs",
+    "k_schur_prep": "schur_dinv",
+    "k_linearize": "linearize",
+    "k_backsub": "backsub",
+    "k_vertex_reduce": "vreduce",
+}
+
+
+def read_counter(d, counter):
+    per = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r.get("Kernel_Name", "")
+            for sub, stage in STAGES.items():
+                if sub in name:
+                    per[stage].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    out, fdir, wdir = sys.argv[1:4]
+    fetch = read_counter(fdir, "FETCH_SIZE")
+    write = read_counter(wdir, "WRITE_SIZE")
+    res = {}
+    for stage in sorted(set(fetch) | set(write)):
+        if not fetch.get(stage) or not write.get(stage):
+            continue
+        f = sum(fetch[stage]) / len(fetch[stage])
+        w = sum(write[stage]) / len(write[stage])
+        res[stage] = {
+            "bytes_per_launch": (2.0 * f + w) * 1024.0,
+            "fetch_size_kb_raw": f,
+            "write_size_kb": w,
+            "launches": len(fetch[stage]),
+            "correction": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)",
+        }
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -155,10 +155,10 @@ def main():
     lin_ms = [1e3 * s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
     trials = sum(s.levenbergIterations for s in timed)
 
-    names = ["linearize", "vreduce", "schur_dinv", "schur_pairs", "chol_factor", "chol_solve", "backsub", "error", "oplus"]
+    names = ["linearize", "vreduce", "schur_dinv", "schur_diag", "schur_rows", "chol_factor", "chol_solve", "backsub", "error", "oplus"]
     kt = {k: {"avg_ms": opt.kernel_ms(k), "count": opt.kernel_count(k)} for k in names}
     # roofline on the dominant single-dispatch HBM-bound kernel (Schur pair products)
-    dom = "schur_pairs" if prob.landmark_dim else "linearize"
+    dom = "schur_rows" if prob.landmark_dim else "linearize"
     avg_ms = kt[dom]["avg_ms"]
     algo_bytes = opt.kernel_bytes(dom)
     achieved = algo_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0

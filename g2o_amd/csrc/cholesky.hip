@@ -31,6 +31,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "device_util.hpp"
 #include "kernels.hpp"
 
 namespace g2ohip {
@@ -46,15 +47,6 @@ constexpr int DS = 33;   // LDS row stride of a 32 x 32 diagonal block
 constexpr int CS = TT + 1;
 
 typedef double dx4 __attribute__((ext_vector_type(4)));
-
-// Load that never branches: the address is selected and the value masked. A guarded load
-// (`ok ? p[i] : 0`) compiles to a branch with its own s_waitcnt, which serialises every load of an
-// unrolled batch; this form keeps the whole batch in flight.
-template <class T>
-__device__ __forceinline__ T ld0(const T* p, int idx, bool ok) {  // front-local index (m^2 < 2^31)
-  const T v = p[ok ? idx : 0];
-  return ok ? v : T(0);
-}
 
 // Optional phase stamps (development build, -DG2OHIP_PHASES): workgroup 0 / thread 0 of each
 // instrumented launch records s_memtime at phase boundaries; read back by g2ohip_debug_phases.

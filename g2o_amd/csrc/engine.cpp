@@ -926,47 +926,119 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       srow_ptr[i + 1] = (int)s_bi.size();
     }
     nS = (int)s_bi.size();
-    auto sfind = [&](int i, int j) -> int {
-      const int* b0 = s_bj.data() + srow_ptr[i];
-      const int* b1 = s_bj.data() + srow_ptr[i + 1];
-      const int* it = std::lower_bound(b0, b1, j);
-      return (int)(it - s_bj.data());
-    };
-    // local pair lists (landmark order inside each Schur block)
-    std::vector<int> cnt(nS + 1, 0);
-    for (int l = 0; l < nLloc; ++l)
-      for (int u = lm_ptr[l]; u < lm_ptr[l + 1]; ++u)
-        for (int v = u; v < lm_ptr[l + 1]; ++v) cnt[sfind(blk_pose[u], blk_pose[v]) + 1]++;
-    for (int t = 0; t < nS; ++t) cnt[t + 1] += cnt[t];
-    npairs = cnt[nS];
-    std::vector<int> pairs(std::max<long long>(2 * npairs, 2), 0);
-    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-    for (int l = 0; l < nLloc; ++l)
-      for (int u = lm_ptr[l]; u < lm_ptr[l + 1]; ++u)
-        for (int v = u; v < lm_ptr[l + 1]; ++v) {
-          const int t = sfind(blk_pose[u], blk_pose[v]);
-          const int p = fill[t]++;
-          pairs[2 * p] = u;
-          pairs[2 * p + 1] = v;
+    // Schur tasks. Diagonal blocks (k_schur_diag): per camera row its observations in landmark order.
+    // Off-diagonal blocks (k_schur_rows): per camera row, chunks of <= SCHUR_SL off-diagonal slots;
+    // per chunk the row's observations (l, i) in landmark order that have partners (l, j) in the
+    // chunk, each staging its own block and those partners; batches of <= SCHUR_SB staged blocks.
+    {
+      constexpr int SB = launch::SCHUR_SB, SL = launch::SCHUR_SL;
+      std::vector<int> rptr(num_poses + 1, 0), robs(std::max(nHpl, 1), 0);
+      for (int a = 0; a < nHpl; ++a) rptr[blk_pose[a] + 1]++;
+      for (int i = 0; i < num_poses; ++i) rptr[i + 1] += rptr[i];
+      {
+        std::vector<int> fill(rptr.begin(), rptr.end() - 1);
+        for (int a = 0; a < nHpl; ++a) robs[fill[blk_pose[a]]++] = a;  // ascending a = landmark order
+      }
+      std::vector<int> obs_lm(std::max(nHpl, 1), 0), sdiag(num_poses);
+      for (int l = 0; l < nLloc; ++l)
+        for (int a = lm_ptr[l]; a < lm_ptr[l + 1]; ++a) obs_lm[a] = l;
+      for (int i = 0; i < num_poses; ++i) sdiag[i] = srow_ptr[i];  // (i, i) is the first block of row i
+      sch_rptr.upload(rptr, stream);
+      sch_robs.upload(robs, stream);
+      sch_obs_lm.upload(obs_lm, stream);
+      sch_sdiag.upload(sdiag, stream);
+
+      std::vector<launch::SchurTask> tasks;
+      std::vector<launch::SchurBatch> batches;
+      std::vector<int> st_obs, st_lm, prs, pp;
+      std::vector<int> camslot(num_poses, -1);
+      struct P3 { int ls, a, b; };
+      std::vector<P3> cur;
+      std::vector<std::pair<int, int>> tmp;
+      npairs = 0;
+      for (int i = 0; i < num_poses; ++i) {
+        const int s_lo = srow_ptr[i], s_hi = srow_ptr[i + 1];
+        for (int k = s_lo; k < s_hi; ++k) camslot[s_bj[k]] = k - s_lo;  // slot 0 = the diagonal block
+        const int noff_total = s_hi - s_lo - 1;
+        for (int ch = 0; ch * SL < noff_total; ++ch) {
+          launch::SchurTask T{};
+          T.row = i;
+          const int off_lo = 1 + ch * SL;
+          T.noff = std::min(SL, noff_total - ch * SL);
+          T.soff = s_lo + off_lo;
+          T.b0 = (int)batches.size();
+          int bst0 = (int)st_obs.size();
+          cur.clear();
+          auto flush = [&]() {
+            const int nst = (int)st_obs.size() - bst0;
+            if (nst == 0) return;
+            launch::SchurBatch B{};
+            B.st0 = bst0;
+            B.nst = nst;
+            B.pr0 = (int)prs.size();
+            std::vector<int> cnt(SL + 1, 0);
+            for (const P3& p : cur) cnt[p.ls + 1]++;
+            for (int k = 0; k < SL; ++k) cnt[k + 1] += cnt[k];
+            for (int k = 0; k <= SL; ++k) pp.push_back(B.pr0 + cnt[k]);
+            std::vector<int> fillp(cnt.begin(), cnt.end() - 1), out(cur.size());
+            for (const P3& p : cur) out[fillp[p.ls]++] = p.a | (p.b << 16);  // stable: landmark order per slot
+            prs.insert(prs.end(), out.begin(), out.end());
+            B.npr = (int)cur.size();
+            npairs += B.npr;
+            batches.push_back(B);
+            cur.clear();
+            bst0 = (int)st_obs.size();
+          };
+          for (int r = rptr[i]; r < rptr[i + 1]; ++r) {
+            const int a = robs[r], l = obs_lm[a];
+            tmp.clear();
+            for (int a2 = a + 1; a2 < lm_ptr[l + 1]; ++a2) {
+              const int sl = camslot[blk_pose[a2]] - off_lo;
+              if (sl >= 0 && sl < T.noff) tmp.push_back({a2, sl});
+            }
+            if (tmp.empty()) continue;
+            const int need = 1 + (int)tmp.size();
+            if ((int)st_obs.size() - bst0 + need > SB) flush();
+            const int posA = (int)st_obs.size() - bst0;
+            st_obs.push_back(a);
+            st_lm.push_back(l);
+            for (auto& [a2, sl] : tmp) {
+              const int posB = (int)st_obs.size() - bst0;
+              st_obs.push_back(a2);
+              st_lm.push_back(l);
+              cur.push_back(P3{sl, posA, posB});
+            }
+          }
+          flush();
+          T.b1 = (int)batches.size();
+          tasks.push_back(T);
         }
-    std::vector<int> shpp(nS, -1), srow(nS);
-    std::vector<unsigned char> sdiag(nS, 0);
+        for (int k = s_lo; k < s_hi; ++k) camslot[s_bj[k]] = -1;
+      }
+      nsch_tasks = (int)tasks.size();
+      nstaged = (long long)st_obs.size();
+      auto nz = [](std::vector<int>& v) -> std::vector<int>& { if (v.empty()) v.push_back(0); return v; };
+      sch_tasks.upload(tasks.empty() ? std::vector<launch::SchurTask>(1) : tasks, stream);
+      batches.push_back(launch::SchurBatch{});  // trailing dummy: k_schur_rows reads one record ahead
+      sch_batches.upload(batches, stream);
+      sch_st_obs.upload(nz(st_obs), stream);
+      sch_st_lm.upload(nz(st_lm), stream);
+      sch_pairs.upload(nz(prs), stream);
+      sch_pp.upload(nz(pp), stream);
+    }
+    std::vector<int> shpp(nS, -1);
+    nHppUsed = 0;
     for (int t = 0; t < nS; ++t) {
-      srow[t] = s_bi[t];
-      sdiag[t] = s_bi[t] == s_bj[t];
-      if (sdiag[t]) shpp[t] = s_bi[t];
+      if (s_bi[t] == s_bj[t]) shpp[t] = s_bi[t];
       else {
         auto it = hppmap.find({s_bi[t], s_bj[t]});
         if (it != hppmap.end()) shpp[t] = it->second;
       }
+      nHppUsed += shpp[t] >= 0;
     }
-    ds_ptr.upload(cnt, stream);
-    ds_pairs.upload(pairs, stream);
     ds_hpp.upload(shpp, stream);
-    ds_row.upload(srow, stream);
-    ds_diag.upload(sdiag, stream);
     dDinv.resize(std::max(nLloc * 9, 1));
-    dW.resize(std::max<long long>((long long)nHpl * pd * ld, 1));  // G = Hpl U^-T
+    dUfac.resize(std::max(nLloc * 6, 1));
     dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
     chol.setup(num_poses, pd, s_bi, s_bj, stream);
@@ -1077,12 +1149,16 @@ void Engine::solve_async() {  // block_solver.hpp:314-447
   double* S = dS.get();
   double* bschur = dS.get() + (size_t)nS * pd * pd;
   timer.begin("schur_dinv", stream);
-  launch::schur_prep(nLloc, lm_begin, d_lm_ptr.get(), dHll.get(), Hpl, db.get() + size_poses, dscal.get(), dDinv.get(),
-                     dW.get(), dCl.get(), dfail.get() + 1, stream);
+  launch::schur_prep(nLloc, lm_begin, dHll.get(), db.get() + size_poses, dscal.get(), dDinv.get(), dUfac.get(),
+                     dCl.get(), dfail.get() + 1, stream);
   timer.end(stream);
-  timer.begin("schur_pairs", stream);
-  launch::schur_pairs(nS, ds_ptr.get(), ds_pairs.get(), ds_hpp.get(), ds_diag.get(), ds_row.get(), dH.get(), dW.get(),
-                      d_blk_lm.get(), dCl.get(), db.get(), dscal.get() + 4, S, bschur, stream);
+  timer.begin("schur_diag", stream);
+  launch::schur_diag(num_poses, sch_rptr.get(), sch_robs.get(), sch_obs_lm.get(), lm_begin, Hpl, dUfac.get(), dCl.get(),
+                     sch_sdiag.get(), ds_hpp.get(), dH.get(), db.get(), dscal.get() + 4, S, bschur, stream);
+  timer.end(stream);
+  timer.begin("schur_rows", stream);
+  launch::schur_rows(nsch_tasks, sch_tasks.get(), sch_batches.get(), sch_st_obs.get(), sch_st_lm.get(), sch_pairs.get(),
+                     sch_pp.get(), Hpl, dUfac.get(), ds_hpp.get(), dH.get(), S, stream);
   timer.end(stream);
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
   HIP_CHECK(hipEventRecord(ev_[1], stream));
@@ -1421,9 +1497,15 @@ int Engine::set_comm_local(const std::string& key, int r, int nr) {
 double Engine::kernel_bytes(const std::string& name) const {
   // algorithmic bytes per launch (SURVEY.md §8d formulas)
   const double npl = nHpl, pb = (double)pd * ld * 8;
-  if (name == "schur_pairs") return (double)nS * pd * pd * 8 * 2 /*Hpp read + S write*/ + npl * pb /*G once*/ +
-                                    (double)npairs * 8 + size_poses * 16.0;
-  if (name == "schur_dinv") return local_lm.size() * (9 * 8.0 * 2 + 3 * 8.0 * 2) + npl * pb * 2;
+  // Schur row pass: Hpl once, U and c per landmark, Hpp blocks present in S, S and bschur written once
+  // Schur row pass (off-diagonal blocks): Hpl of every observation with a partner once, U per
+  // landmark, the off-diagonal Hpp blocks present in S, the off-diagonal S blocks written once
+  if (name == "schur_rows") return npl * pb + local_lm.size() * 6 * 8.0 + (double)(nHppUsed - num_poses) * pd * pd * 8 +
+                                   (double)(nS - num_poses) * pd * pd * 8;
+  // diagonal blocks: Hpl, U and c per observation's landmark, Hpp diagonal, S diagonal + bschur
+  if (name == "schur_diag") return npl * pb + local_lm.size() * 9 * 8.0 + (double)num_poses * pd * pd * 8 * 2 +
+                                   size_poses * 16.0;
+  if (name == "schur_dinv") return local_lm.size() * ((9 + 3) * 8.0 + (9 + 6 + 3) * 8.0);
   if (name == "linearize") return ne * (family == FAM_BA ? (2 + 3 + 4) * 8.0 + 8 + (double)(slot_stride0 + slot_stride1 + pd * ld) * 8 : 0.0);
   if (name == "backsub") return local_lm.size() * (3 * 8.0 * 2 + 72) + npl * (pb + 4) + size_poses * 8.0;
   if (name == "chol_factor") return (double)chol.sym.front_pool * 8 * 2;
@@ -1431,7 +1513,7 @@ double Engine::kernel_bytes(const std::string& name) const {
 }
 double Engine::kernel_flops(const std::string& name) const {
   if (name == "chol_factor") return chol.sym.flops;
-  if (name == "schur_pairs") return (double)npairs * (108 * 2) + (double)nHpl * 36;
+  if (name == "schur_rows") return (double)npairs * (108 * 2) + (double)nstaged * 36;
   return 0;
 }
 

@@ -7,16 +7,19 @@
 //   k_vertex_reduce  deterministic segmented reduction of the slots into Hpp/Hll diagonal
 //                 blocks and b (replaces the per-vertex omp locks + copyB, :467-517).
 //   k_schur_prep  landmark pass of BlockSolver::solve (:342-360): Dinv = (Hll+lambda I)^-1,
-//                 and the split Hll+lambda I = U U^T, G = Hpl U^-T, c = U^-1 b_l.
-//   k_schur_pairs Hschur(i,j) = Hpp(i,j) - sum_l G_il G_jl^T and bschur = b - sum G c (:361-400)
-//                 computed output-stationary: a group of lanes owns one Schur block and walks its
-//                 precomputed pair list; fixed-order tree reduction, no atomics.
+//                 and the split Hll+lambda I = U U^T, c = U^-1 b_l.
+//   k_schur_diag  Hschur(i,i) = Hpp(i,i) + lambda - sum_l G_il G_il^T, bschur = b - sum G c (:361-400),
+//                 G = Hpl U^-T in registers, one wave per camera.
+//   k_schur_rows  Hschur(i,j>i) = Hpp(i,j) - sum_l G_il G_jl^T: one workgroup per camera row (chunk),
+//                 the row's landmarks staged coalesced into LDS in batches; every output has one
+//                 owner and a fixed summation order (no atomics).
 //   k_backsub     x_l = Dinv (b_l - Hpl^T x_p) (:420-446).
 //   k_error/k_oplus  computeActiveErrors (sparse_optimizer.cpp:63-90) and update (:441-454).
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
 #include "device_types.hpp"
+#include "device_util.hpp"
 #include "kernels.hpp"
 
 namespace g2ohip {
@@ -217,13 +220,13 @@ __global__ void __launch_bounds__(256) k_offblock_reduce(int nb, int bsz, const 
 // Landmark pass (block_solver.hpp:341-360): Dinv = (Hll + lambda I)^-1 (cofactor inverse, as
 // Eigen's 3x3 inverse; kept for the back-substitution) and the symmetric split
 //   Hll + lambda I = U U^T (3x3 Cholesky),  G_a = Hpl_a U^-T,  c_l = U^-1 b_l,
-// so that Hpl Dinv Hpl^T = G G^T and Hpl Dinv b_l = G c_l: the pair pass then streams ONE 6x3 block
-// per observation instead of both W = Hpl Dinv and Hpl.
-template <int PD>
+// so that Hpl Dinv Hpl^T = G G^T and Hpl Dinv b_l = G c_l. G is never materialised: the row pass
+// applies U^-T to each observation block as it stages it. Ufac per landmark: r0 r1 r2 u10 u20 u21
+// (r = reciprocal pivots of U).
 __global__ void __launch_bounds__(256)
-    k_schur_prep(int nl, int lm0, const int* __restrict__ lm_ptr, const double* __restrict__ Hll,
-                 const double* __restrict__ Hpl, const double* __restrict__ bl_all, const double* __restrict__ lam,
-                 double* __restrict__ Dinv, double* __restrict__ G, double* __restrict__ cl_all, int* __restrict__ fail) {
+    k_schur_prep(int nl, int lm0, const double* __restrict__ Hll, const double* __restrict__ bl_all,
+                 const double* __restrict__ lam, double* __restrict__ Dinv, double* __restrict__ Ufac,
+                 double* __restrict__ cl_all, int* __restrict__ fail) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= nl) return;
   const double lambda = *lam;
@@ -259,103 +262,253 @@ __global__ void __launch_bounds__(256)
   const double d2 = m(2, 2) - u20 * u20 - u21 * u21;
   const double r2 = 1.0 / sqrt(d2);
   if (!(det != 0.0) || !isfinite(inv) || !(d0 > 0.0) || !(d1 > 0.0) || !(d2 > 0.0)) *fail = 1;
-  {  // c_l = U^-1 b_l
-    const double* bl = bl_all + (size_t)(lm0 + l) * 3;
-    const double g0 = bl[0] * r0;
-    const double g1 = (bl[1] - u10 * g0) * r1;
-    const double g2 = (bl[2] - u20 * g0 - u21 * g1) * r2;
-    double* co = cl_all + (size_t)(lm0 + l) * 3;
-    co[0] = g0; co[1] = g1; co[2] = g2;
-  }
-  for (int a_ = lm_ptr[l]; a_ < lm_ptr[l + 1]; ++a_) {
-    const double2* Bm = reinterpret_cast<const double2*>(Hpl + (size_t)a_ * PD * 3);
-    double2* Go = reinterpret_cast<double2*>(G + (size_t)a_ * PD * 3);
-    double h[PD * 3], g[PD * 3];
-#pragma unroll
-    for (int k = 0; k < PD * 3 / 2; ++k) { const double2 v = Bm[k]; h[2 * k] = v.x; h[2 * k + 1] = v.y; }
-#pragma unroll
-    for (int r = 0; r < PD; ++r) {  // row r: U g^T = h^T (columns of the col-major 6x3 block)
-      const double g0 = h[r] * r0;
-      const double g1 = (h[PD + r] - u10 * g0) * r1;
-      const double g2 = (h[2 * PD + r] - u20 * g0 - u21 * g1) * r2;
-      g[r] = g0; g[PD + r] = g1; g[2 * PD + r] = g2;
-    }
-#pragma unroll
-    for (int k = 0; k < PD * 3 / 2; ++k) Go[k] = double2{g[2 * k], g[2 * k + 1]};
-  }
+  double* U = Ufac + (size_t)l * 6;
+  U[0] = r0; U[1] = r1; U[2] = r2; U[3] = u10; U[4] = u20; U[5] = u21;
+  // c_l = U^-1 b_l
+  const double* bl = bl_all + (size_t)(lm0 + l) * 3;
+  const double g0 = bl[0] * r0;
+  const double g1 = (bl[1] - u10 * g0) * r1;
+  const double g2 = (bl[2] - u20 * g0 - u21 * g1) * r2;
+  double* co = cl_all + (size_t)(lm0 + l) * 3;
+  co[0] = g0; co[1] = g1; co[2] = g2;
 }
 
-// Output-stationary Schur pair products: S(i,j) = Hpp(i,j) (+ lambda on the diagonal)
-//   - sum over the landmarks observed by both cameras of G_a G_b^T, G lanes per Schur block,
-// pairs in landmark order inside each block (deterministic, no atomics).
-template <int PD, int GL>
+// Diagonal blocks of the reduced system (block_solver.hpp:361-400, the j == i terms):
+//   S(i,i) = Hpp(i,i) + lambda I - sum_l G_il G_il^T,   bschur_i = b_i - sum_l G_il c_l,
+// one wave per camera row, lanes stride over the row's observations (landmark order), G formed in
+// registers from Hpl, U_l and c_l; fixed butterfly over the lanes (bitwise reproducible).
 __global__ void __launch_bounds__(256)
-    k_schur_pairs(int nS, const int* __restrict__ s_ptr, const int2* __restrict__ pairs, const int* __restrict__ s_hpp,
-                  const unsigned char* __restrict__ s_diag, const int* __restrict__ s_row,
-                  const double* __restrict__ Hpp, const double* __restrict__ G, const int* __restrict__ blk_lm,
-                  const double* __restrict__ cl_all, const double* __restrict__ b, const double* __restrict__ lam,
-                  double* __restrict__ S, double* __restrict__ bschur) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int t = gid / GL, lane = gid % GL;
-  const bool active = t < nS;
-  double acc[PD * PD];
-  double cb[PD];
+    k_schur_diag(int nrows, const int* __restrict__ rptr, const int* __restrict__ robs,
+                 const int* __restrict__ obs_lm, int lm0, const double* __restrict__ Hpl,
+                 const double* __restrict__ Ufac, const double* __restrict__ cl_all, const int* __restrict__ sdiag,
+                 const int* __restrict__ s_hpp, const double* __restrict__ Hpp, const double* __restrict__ b,
+                 const double* __restrict__ lam, double* __restrict__ S, double* __restrict__ bschur) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= nrows) return;  // wave-uniform
+  double acc[27];  // packed upper of G G^T (21, col-major) | G c (6)
 #pragma unroll
-  for (int k = 0; k < PD * PD; ++k) acc[k] = 0;
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  const int p1 = rptr[row + 1];
+  for (int p = rptr[row] + lane; p < p1; p += 64) {
+    const int a = robs[p], l = obs_lm[a];
+    const double2* h2 = reinterpret_cast<const double2*>(Hpl + (size_t)a * 18);
+    const double2* u2 = reinterpret_cast<const double2*>(Ufac + (size_t)l * 6);
+    double g[18], U[6], c[3];
 #pragma unroll
-  for (int k = 0; k < PD; ++k) cb[k] = 0;
-  const bool diag = active && s_diag[t];
-  if (active) {
-    const int p0 = s_ptr[t], p1 = s_ptr[t + 1];
-    for (int p = p0 + lane; p < p1; p += GL) {
-      const int2 pr = pairs[p];
-      const double2* Ga = reinterpret_cast<const double2*>(G + (size_t)pr.x * PD * 3);
-      const double2* Gb = reinterpret_cast<const double2*>(G + (size_t)pr.y * PD * 3);
-      double ga[PD * 3], gb[PD * 3];
+    for (int k = 0; k < 9; ++k) { const double2 v = h2[k]; g[2 * k] = v.x; g[2 * k + 1] = v.y; }
 #pragma unroll
-      for (int k = 0; k < PD * 3 / 2; ++k) {
-        const double2 x = Ga[k], y = Gb[k];
-        ga[2 * k] = x.x; ga[2 * k + 1] = x.y;
-        gb[2 * k] = y.x; gb[2 * k + 1] = y.y;
-      }
+    for (int k = 0; k < 3; ++k) { const double2 v = u2[k]; U[2 * k] = v.x; U[2 * k + 1] = v.y; }
+    const double* cp = cl_all + (size_t)(lm0 + l) * 3;
+    c[0] = cp[0]; c[1] = cp[1]; c[2] = cp[2];
 #pragma unroll
-      for (int c = 0; c < PD; ++c)
+    for (int r = 0; r < 6; ++r) {  // row r of G = Hpl U^-T
+      const double g0 = g[r] * U[0];
+      const double g1 = (g[6 + r] - U[3] * g0) * U[1];
+      g[12 + r] = (g[12 + r] - U[4] * g0 - U[5] * g1) * U[2];
+      g[r] = g0;
+      g[6 + r] = g1;
+    }
+    int k = 0;
 #pragma unroll
-        for (int r = 0; r < PD; ++r)
-          acc[c * PD + r] += ga[r] * gb[c] + ga[PD + r] * gb[PD + c] + ga[2 * PD + r] * gb[2 * PD + c];
-      if (diag) {  // Hpl Dinv b_l = G c_l
-        const double* cl = cl_all + (size_t)blk_lm[pr.x] * 3;
-        const double c0 = cl[0], c1 = cl[1], c2 = cl[2];
+    for (int cc = 0; cc < 6; ++cc)
 #pragma unroll
-        for (int r = 0; r < PD; ++r) cb[r] += ga[r] * c0 + ga[PD + r] * c1 + ga[2 * PD + r] * c2;
+      for (int r = 0; r <= cc; ++r) acc[k++] += g[r] * g[cc] + g[6 + r] * g[6 + cc] + g[12 + r] * g[12 + cc];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) acc[21 + r] += g[r] * c[0] + g[6 + r] * c[1] + g[12 + r] * c[2];
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+    for (int k = 0; k < 27; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
+  const int sidx = sdiag[row], hp = s_hpp[sidx];
+  const double lambda = *lam;
+  const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * 36;
+  double* So = S + (size_t)sidx * 36;
+  int k = 0;
+#pragma unroll
+  for (int cc = 0; cc < 6; ++cc)
+#pragma unroll
+    for (int r = 0; r <= cc; ++r, ++k) {  // lane k writes (r, cc) and its mirror
+      if (lane != k) continue;
+      const double h0 = hp >= 0 ? Hh[cc * 6 + r] : 0.0;
+      const double v = (r == cc ? h0 + lambda : h0) - acc[k];
+      So[cc * 6 + r] = v;
+      So[r * 6 + cc] = v;
+    }
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+    if (lane == 32 + r) bschur[(size_t)row * 6 + r] = b[(size_t)row * 6 + r] - acc[21 + r];
+}
+
+// Off-diagonal blocks, row-stationary (block_solver.hpp:361-391, j > i): one workgroup per (camera
+// row i, chunk of up to 64 off-diagonal slots of the row's Schur pattern). The row's landmarks are
+// walked in landmark order in batches; a batch stages, coalesced, the 6x3 blocks Hpl_a of the row's
+// own observation a = (l, i) and of the observations (l, j) in the chunk, with U_l, into LDS and
+// turns them into G = Hpl U^-T there. Four threads per slot, each three columns of the block over
+// every second pair of the slot's list (landmark order), the two parities combined by one fixed
+// shuffle: every output has one owner and a fixed summation order (no atomics, bitwise reproducible). The next batch's blocks
+// are in flight while the current one is reduced.
+namespace {
+constexpr int SCH_SB = launch::SCHUR_SB;  // staged observation blocks per batch
+constexpr int SCH_GS = 24;                // doubles per staged block: G (6x3 col-major) | U (6); 16-B aligned
+constexpr int SCH_SL = launch::SCHUR_SL;  // off-diagonal slots per task
+constexpr int SCH_PPB = SCH_SL + 1;       // slot-CSR entries per batch
+constexpr int SCH_NI = (SCH_SB + 255) / 256;
+constexpr int SCH_NH = (SCH_SB * 12 + 255) / 256;  // 16-B chunks per batch: 9 of Hpl + 3 of U per block
+}  // namespace
+
+__global__ void __launch_bounds__(256, 2)
+    k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
+                 const int* __restrict__ st_obs, const int* __restrict__ st_lm, const int* __restrict__ pairs,
+                 const int* __restrict__ pp, const double* __restrict__ Hpl, const double* __restrict__ Ufac,
+                 const int* __restrict__ s_hpp, const double* __restrict__ Hpp, double* __restrict__ S) {
+  __shared__ __attribute__((aligned(16))) double Gs[SCH_SB * SCH_GS];
+  __shared__ int so[SCH_SB], sl[SCH_SB];  // staging indices of the next batch to stage
+  __shared__ int sp[2][SCH_SB];           // pair lists, double-buffered by batch parity
+  __shared__ int spp[2][SCH_PPB];
+  const launch::SchurTask t = tasks[blockIdx.x];
+  const int nb = t.b1 - t.b0;
+  const int tid = threadIdx.x;
+  const int ls = tid >> 2, q = tid & 3;
+  double acc[18];  // 6 x 3: rows 0..5 of columns h3..h3+2
+#pragma unroll
+  for (int k = 0; k < 18; ++k) acc[k] = 0.0;
+  const double2* H2 = reinterpret_cast<const double2*>(Hpl);
+  const double2* U2 = reinterpret_cast<const double2*>(Ufac);
+  // records past the task's end read the next task's (or the trailing dummy) record and go unused
+  auto rec = [&](int k) { return batches[t.b0 + min(k, nb)]; };
+  int ov[SCH_NI], lv[SCH_NI], pv[SCH_NI], ppv = 0;
+  auto idx_load = [&](const launch::SchurBatch B, int k) {
+#pragma unroll
+    for (int u = 0; u < SCH_NI; ++u) {
+      const int i = tid + 256 * u;
+      ov[u] = ld0(st_obs, B.st0 + i, i < B.nst);
+      lv[u] = ld0(st_lm, B.st0 + i, i < B.nst);
+      pv[u] = ld0(pairs, B.pr0 + i, i < B.npr);
+    }
+    ppv = ld0(pp, (t.b0 + k) * SCH_PPB + tid, tid < SCH_PPB) - B.pr0;
+  };
+  auto idx_store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < SCH_NI; ++u) {
+      const int i = tid + 256 * u;
+      if (i < SCH_SB) { so[i] = ov[u]; sl[i] = lv[u]; sp[buf][i] = pv[u]; }
+    }
+    if (tid < SCH_PPB) spp[buf][tid] = ppv;
+  };
+  double2 hv[SCH_NH];
+  auto hpl_load = [&](const launch::SchurBatch B) {  // indices of B sit in so/sl
+    const int n12 = B.nst * 12;
+#pragma unroll
+    for (int u = 0; u < SCH_NH; ++u) {
+      const int idx = tid + 256 * u;
+      const bool ok = idx < n12;
+      const int item = ok ? idx / 12 : 0, ch = ok ? idx - item * 12 : 0;
+      const bool isH = ch < 9;
+      const int gi = isH ? so[item] * 9 + ch : sl[item] * 3 + (ch - 9);
+      const double2 vh = H2[isH && ok ? gi : 0], vu = U2[!isH && ok ? gi : 0];  // two plain loads, no
+      hv[u] = ok ? (isH ? vh : vu) : double2{0.0, 0.0};                        // pointer select
+    }
+  };
+  auto hpl_store = [&](const launch::SchurBatch B) {
+    const int n12 = B.nst * 12;
+#pragma unroll
+    for (int u = 0; u < SCH_NH; ++u) {
+      const int idx = tid + 256 * u;
+      if (idx < n12) {
+        const int item = idx / 12, ch = idx - item * 12;
+        *reinterpret_cast<double2*>(Gs + item * SCH_GS + 2 * ch) = hv[u];
       }
     }
+  };
+  auto transform = [&](const launch::SchurBatch B) {  // G = Hpl U^-T in place, one thread per (block, row)
+    for (int idx = tid; idx < B.nst * 6; idx += 256) {
+      const int item = idx / 6, r = idx - item * 6;
+      double* g = Gs + item * SCH_GS;
+      const double r0 = g[18], r1 = g[19], r2 = g[20], u10 = g[21], u20 = g[22], u21 = g[23];
+      const double g0 = g[r] * r0;
+      const double g1 = (g[6 + r] - u10 * g0) * r1;
+      const double g2 = (g[12 + r] - u20 * g0 - u21 * g1) * r2;
+      g[r] = g0; g[6 + r] = g1; g[12 + r] = g2;
+    }
+  };
+  // thread q of a slot: columns 3h..3h+2 of the block (h = q & 1) over the pairs of parity q >> 1
+  const int h3 = (q & 1) * 3, par = q >> 1;
+  auto compute = [&](int buf) {
+    if (ls >= t.noff) return;
+    const int p1 = spp[buf][ls + 1];
+    for (int p = spp[buf][ls] + par; p < p1; p += 2) {
+      const int pr = sp[buf][p];
+      const double* ga = Gs + (pr & 0xffff) * SCH_GS;
+      const double* gb = Gs + (pr >> 16) * SCH_GS + h3;
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk) {  // one column of G_a and three entries of G_b at a time
+        double A[6], Bm[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const double2 x = *reinterpret_cast<const double2*>(ga + kk * 6 + 2 * k);
+          A[2 * k] = x.x; A[2 * k + 1] = x.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Bm[j] = gb[kk * 6 + j];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int r = 0; r < 6; ++r) acc[j * 6 + r] += A[r] * Bm[j];
+      }
+    }
+  };
+
+  // Invariant at the top of iteration k: Gs holds G of batch k, so/sl the indices of batch k+1,
+  // sp[k&1] and sp[(k+1)&1] the pair lists of k and k+1.
+  launch::SchurBatch B0 = rec(0), B1 = rec(1), B2 = rec(2);
+  if (nb > 0) {
+    idx_load(B0, 0);
+    idx_store(0);
+    __syncthreads();
+    hpl_load(B0);
+    if (nb > 1) idx_load(B1, 1);
+    __syncthreads();  // every lane has read so/sl of batch 0
+    hpl_store(B0);
+    if (nb > 1) idx_store(1);
+    __syncthreads();
+    transform(B0);
+    __syncthreads();
   }
-#pragma unroll
-  for (int m = GL / 2; m >= 1; m >>= 1) {
-#pragma unroll
-    for (int k = 0; k < PD * PD; ++k) acc[k] += __shfl_xor(acc[k], m, GL);
-#pragma unroll
-    for (int k = 0; k < PD; ++k) cb[k] += __shfl_xor(cb[k], m, GL);
+  for (int k = 0; k < nb; ++k) {
+    const int cur = k & 1;
+    if (k + 1 < nb) hpl_load(B1);
+    if (k + 2 < nb) idx_load(B2, k + 2);
+    const launch::SchurBatch B3 = rec(k + 3);
+    compute(cur);
+    __syncthreads();  // Gs, so/sl and the pair list of batch k are free
+    if (k + 1 < nb) {
+      hpl_store(B1);
+      if (k + 2 < nb) idx_store(cur);
+      __syncthreads();
+      transform(B1);
+      __syncthreads();
+    }
+    B0 = B1;
+    B1 = B2;
+    B2 = B3;
   }
-  if (!active) return;
-  const int hp = s_hpp[t];
-  const double lambda = *lam;
-  double* So = S + (size_t)t * PD * PD;
-  // every lane holds the full sums; lane l stores the entries k = l (mod GL) (compile-time k:
-  // a runtime index into acc[] would put it in scratch)
-  const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * PD * PD;
+  // even + odd pairs (fixed order); thread (h, par) stores rows 3 par..3 par+2 of its three columns
 #pragma unroll
-  for (int k = 0; k < PD * PD; ++k) {
-    if ((k % GL) != lane) continue;
-    const double h = hp >= 0 ? Hh[k] : 0.0;
-    So[k] = ((diag && (k % (PD + 1)) == 0) ? h + lambda : h) - acc[k];
-  }
-  if (diag) {
-    const int row = s_row[t];
+  for (int k = 0; k < 18; ++k) acc[k] += __shfl_xor(acc[k], 2, 4);
+  if (ls < t.noff) {
+    const int sidx = t.soff + ls;
+    const int hp = s_hpp[sidx];
+    const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * 36;
+    double* So = S + (size_t)sidx * 36;
 #pragma unroll
-    for (int k = 0; k < PD; ++k)
-      if (k == lane) bschur[(size_t)row * PD + k] = b[(size_t)row * PD + k] - cb[k];
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        if ((r >= 3) != (par == 1)) continue;
+        const int k = (h3 + j) * 6 + r;
+        So[k] = (hp >= 0 ? Hh[k] : 0.0) - acc[j * 6 + r];
+      }
   }
 }
 
@@ -578,21 +731,26 @@ void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const do
   KERNEL_CHECK();
 }
 
-void schur_prep(int nl, int lm0, const int* lm_ptr, const double* Hll, const double* Hpl, const double* bl_all,
-                const double* lam, double* Dinv, double* G, double* cl_all, int* fail, hipStream_t s) {
+void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
+                double* Ufac, double* cl_all, int* fail, hipStream_t s) {
   if (nl <= 0) return;
-  hipLaunchKernelGGL(k_schur_prep<6>, grid_for(nl, 256), 256, 0, s, nl, lm0, lm_ptr, Hll, Hpl, bl_all, lam, Dinv, G,
-                     cl_all, fail);
+  hipLaunchKernelGGL(k_schur_prep, grid_for(nl, 256), 256, 0, s, nl, lm0, Hll, bl_all, lam, Dinv, Ufac, cl_all, fail);
   KERNEL_CHECK();
 }
-void schur_pairs(int nS, const int* s_ptr, const int* pairs, const int* s_hpp, const unsigned char* s_diag,
-                 const int* s_row, const double* Hpp, const double* G, const int* blk_lm, const double* cl_all,
-                 const double* b, const double* lam, double* S, double* bschur, hipStream_t s) {
-  if (nS <= 0) return;
-  constexpr int GL = 16;
-  hipLaunchKernelGGL((k_schur_pairs<6, GL>), grid_for((size_t)nS * GL, 256), 256, 0, s, nS, s_ptr,
-                     reinterpret_cast<const int2*>(pairs), s_hpp, s_diag, s_row, Hpp, G, blk_lm, cl_all, b, lam, S,
-                     bschur);
+void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0, const double* Hpl,
+                const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp, const double* Hpp,
+                const double* b, const double* lam, double* S, double* bschur, hipStream_t s) {
+  if (nrows <= 0) return;
+  hipLaunchKernelGGL(k_schur_diag, grid_for(nrows, 4), 256, 0, s, nrows, rptr, robs, obs_lm, lm0, Hpl, Ufac, cl_all,
+                     sdiag, s_hpp, Hpp, b, lam, S, bschur);
+  KERNEL_CHECK();
+}
+void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs, const int* st_lm,
+                const int* pairs, const int* pp, const double* Hpl, const double* Ufac, const int* s_hpp,
+                const double* Hpp, double* S, hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_schur_rows, ntasks, 256, 0, s, tasks, batches, st_obs, st_lm, pairs, pp, Hpl, Ufac, s_hpp, Hpp,
+                     S);
   KERNEL_CHECK();
 }
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,

@@ -27,11 +27,28 @@ void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, 
                    int st0, int st1, double* H, double* b, const int* boff, hipStream_t s);
 void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const double* slots, double* out,
                      const long long* dst, hipStream_t s);
-void schur_prep(int nl, int lm0, const int* lm_ptr, const double* Hll, const double* Hpl, const double* bl_all,
-                const double* lam, double* Dinv, double* G, double* cl_all, int* fail, hipStream_t s);
-void schur_pairs(int nS, const int* s_ptr, const int* pairs, const int* s_hpp, const unsigned char* s_diag,
-                 const int* s_row, const double* Hpp, const double* G, const int* blk_lm, const double* cl_all,
-                 const double* b, const double* lam, double* S, double* bschur, hipStream_t s);
+void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
+                double* Ufac, double* cl_all, int* fail, hipStream_t s);
+// diagonal blocks + bschur: one wave per camera row over its observations (CSR rptr/robs)
+void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0, const double* Hpl,
+                const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp, const double* Hpp,
+                const double* b, const double* lam, double* S, double* bschur, hipStream_t s);
+// row-stationary off-diagonal Schur pass (k_schur_rows): task = (camera row, <= SCHUR_SL off-diagonal
+// slots), batch = <= SCHUR_SB staged observation blocks of the row's landmarks
+constexpr int SCHUR_SB = 288, SCHUR_SL = 64;
+struct SchurTask {
+  int row, noff;  // camera row, number of off-diagonal slots of this task
+  int b0, b1;     // batches
+  int soff;       // S index of the first off-diagonal slot
+  int pad;
+};
+struct SchurBatch {
+  int st0, nst;  // staged blocks (st_obs / st_lm)
+  int pr0, npr;  // pairs (posA | posB << 16), slot CSR in pp[batch * (SCHUR_SL + 1) ...]
+};
+void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs, const int* st_lm,
+                const int* pairs, const int* pp, const double* Hpl, const double* Ufac, const int* s_hpp,
+                const double* Hpp, double* S, hipStream_t s);
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
              int size_poses, int lm0, double* x, hipStream_t s);
 void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s);

@@ -17,8 +17,9 @@ import sys
 from collections import defaultdict
 
 STAGES = {  # substring of the kernel name -> stage name used by bench.py
-    "k_schur_pairs": "schur_pairs",
+    "k_schur_rows": "schur_rows",
     "k_schur_prep": "schur_dinv",
+    "k_schur_diag": "schur_diag",
     "k_linearize": "linearize",
     "k_backsub": "backsub",
     "k_vertex_reduce": "vreduce",

@@ -384,9 +384,11 @@ Engine::Engine(int dev) : device(dev) {
   dfail.resize(2);
   dfail.zero(stream);
   for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+  for (auto& e : lm_ev_) HIP_CHECK(hipEventCreate(&e));
 }
 Engine::~Engine() {
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+  for (auto& e : lm_ev_) if (e) (void)hipEventDestroy(e);
   comm.reset();
   if (stream) (void)hipStreamDestroy(stream);
 }
@@ -544,6 +546,7 @@ void Engine::ensure_device_state() {
     if (!hg.st[t].empty()) dstate[t].upload(hg.st[t], stream);
   if (!hg.nopl.empty()) dnopl.upload(hg.nopl, stream);
   device_state_dirty = false;
+  ++state_ver;
   host_state_stale = false;
 }
 
@@ -712,6 +715,7 @@ void Engine::setup_edges_device() {
   dchi.resize(std::max(ne, 1));
   dpartial.resize(std::max<size_t>(launch::sum_partials(std::max<long long>(std::max<long long>(ne, vector_size()), 1)) + 64, 128));
   edges_ready = true;
+  ++state_ver;  // the edge set (and so chi2) changed
 }
 
 int Engine::build_structure() {  // block_solver.hpp:102-256
@@ -1073,11 +1077,15 @@ void Engine::compute_errors_async() {
 }
 
 double Engine::chi2_sync() {
+  ensure_device_state();
+  if (chi_ver == state_ver) return chi_cache;  // same device state: computeActiveErrors is deterministic
   compute_errors_async();
   double c = 0;
   HIP_CHECK(hipMemcpyAsync(&c, dscal.get() + 1, sizeof(double), hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
   timer.collect();
+  chi_cache = c;
+  chi_ver = state_ver;
   return c;
 }
 
@@ -1195,6 +1203,7 @@ void Engine::update_async() {  // sparse_optimizer.cpp:441-454
   }
   timer.end(stream);
   host_state_stale = true;
+  ++state_ver;
 }
 
 int Engine::update_from(const double* xh) {
@@ -1238,6 +1247,7 @@ int Engine::pop() {
     if (lvl[t].size())
       HIP_CHECK(hipMemcpyAsync(dstate[t].get(), lvl[t].get(), lvl[t].bytes(), hipMemcpyDeviceToDevice, stream));
   host_state_stale = true;
+  ++state_ver;
   return G2OHIP_OK;
 }
 int Engine::discard_top() {
@@ -1282,21 +1292,19 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   if (st) { st->timeResiduals = wall() - t; t = wall(); }
   double currentChi = currentChi0;
   double tempChi = currentChi;
+  hipEvent_t e0 = lm_ev_[0], e1 = lm_ev_[1], e2 = lm_ev_[2], e3 = lm_ev_[3], q0 = lm_ev_[4], q1 = lm_ev_[5];
+  HIP_CHECK(hipEventRecord(q0, stream));
   build_system();
+  HIP_CHECK(hipEventRecord(q1, stream));  // timeQuadraticForm from events: no host sync here
   if (iteration == 0) {
     current_lambda = cfg.user_lambda_init > 0 ? cfg.user_lambda_init : lambda_init();
     ni = 2;
-  } else {
-    HIP_CHECK(hipStreamSynchronize(stream));
   }
-  if (st) st->timeQuadraticForm = wall() - t;
   const int maxTrials = cfg.max_trials_after_failure > 0 ? cfg.max_trials_after_failure : 10;
   double rho = 0;
   int& qmax = levenberg_iterations;
   qmax = 0;
-  hipEvent_t e0, e1, e2, e3;
-  HIP_CHECK(hipEventCreate(&e0)); HIP_CHECK(hipEventCreate(&e1));
-  HIP_CHECK(hipEventCreate(&e2)); HIP_CHECK(hipEventCreate(&e3));
+  bool first_trial = true;
   do {
     push();
     if (st) st->levenbergIterations++;
@@ -1329,6 +1337,12 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     timer.collect();
     tempChi = hs[1];
     const bool ok2 = f[0] == 0;
+    if (st && first_trial) {
+      float mq = 0;
+      HIP_CHECK(hipEventElapsedTime(&mq, q0, q1));
+      st->timeQuadraticForm = mq * 1e-3;
+    }
+    first_trial = false;
     if (st) {
       float ms01 = 0, ms12 = 0, a = 0, b = 0, c = 0;
       HIP_CHECK(hipEventElapsedTime(&ms01, e0, e1));
@@ -1364,7 +1378,9 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     }
     qmax++;
   } while (rho < 0 && qmax < maxTrials);
-  (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipEventDestroy(e2); (void)hipEventDestroy(e3);
+  // the state left behind has chi2 currentChi (accepted: the last tempChi; rejected: popped back)
+  chi_cache = currentChi;
+  chi_ver = state_ver;
   if (qmax == maxTrials || rho == 0 || !std::isfinite(current_lambda)) return 1;  // Terminate
   return 0;                                                                       // OK
 }

@@ -205,6 +205,11 @@ class Engine {
   bool lambda_set = false;
   // LM state (optimization_algorithm_levenberg.cpp)
   double current_lambda = -1, ni = 2;
+  // chi2 of the device state, cached: every state change bumps state_ver; the LM loop knows the chi2 of
+  // the state it leaves behind (accepted: tempChi, rejected + pop: currentChi) and records it
+  unsigned long long state_ver = 1, chi_ver = 0;
+  double chi_cache = 0.0;
+  hipEvent_t lm_ev_[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int levenberg_iterations = 0;
   g2ohip_batch_stats* cur_stats = nullptr;
 

@@ -48,7 +48,8 @@ EXPORTS = [
     "g2ohip_solver_restore_diagonal", "g2ohip_solver_solve", "g2ohip_solver_vector_size",
     "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
     "g2ohip_discard_top", "g2ohip_stage", "g2ohip_linear_solve_ccs", "g2ohip_comm_unique_id",
-    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing", "g2ohip_kernel_ms",
+    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
+    "g2ohip_kernel_timing_only", "g2ohip_set_stats_level", "g2ohip_kernel_ms",
     "g2ohip_kernel_count", "g2ohip_kernel_bytes", "g2ohip_kernel_flops", "g2ohip_last_error",
     "g2ohip_version",
 ]
@@ -107,6 +108,8 @@ def lib() -> C.CDLL:
         "g2ohip_debug_phases": ([P, I], I),
         "g2ohip_symbolic_analyze": ([I, I, I, P, P, P, P], I),
         "g2ohip_enable_kernel_timing": ([P, I], None),
+        "g2ohip_kernel_timing_only": ([P, C.c_char_p], None),
+        "g2ohip_set_stats_level": ([P, I], None),
         "g2ohip_kernel_ms": ([P, C.c_char_p], D),
         "g2ohip_kernel_count": ([P, C.c_char_p], LL),
         "g2ohip_kernel_bytes": ([P, C.c_char_p], D),
@@ -300,8 +303,14 @@ class SparseOptimizer:
         _check(lib().g2ohip_set_comm_local(self.h, group_key.encode(), rank, nranks), "set_comm_local")
 
     # ---- measurement ----
-    def enable_kernel_timing(self, on: bool = True):
+    def enable_kernel_timing(self, on: bool = True, only: str | None = None):
+        """Per-kernel-class HIP-event timing; ``only`` restricts it to one class."""
+        lib().g2ohip_kernel_timing_only(self.h, (only or "").encode())
         lib().g2ohip_enable_kernel_timing(self.h, int(on))
+
+    def set_stats_level(self, level: int):
+        """G2OBatchStatistics timers: 0 none, 1 timeLinearSolution only, 2 every stage (default)."""
+        lib().g2ohip_set_stats_level(self.h, int(level))
 
     def kernel_ms(self, name: str) -> float:
         return lib().g2ohip_kernel_ms(self.h, name.encode())

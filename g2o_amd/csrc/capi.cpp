@@ -288,6 +288,14 @@ void g2ohip_enable_kernel_timing(g2ohip_graph* g, int on) {
   g->e->timer.enabled = on != 0;
   g->e->timer.reset();
 }
+void g2ohip_kernel_timing_only(g2ohip_graph* g, const char* name) {
+  if (!g) return;
+  g->e->timer.only = name ? name : "";
+}
+void g2ohip_set_stats_level(g2ohip_graph* g, int level) {
+  if (!g) return;
+  g->e->stats_level = level < 0 ? 0 : (level > 2 ? 2 : level);
+}
 double g2ohip_kernel_ms(g2ohip_graph* g, const char* name) {
   if (!g || !name) return -1;
   auto& t = g->e->timer;

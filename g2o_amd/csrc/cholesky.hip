@@ -23,7 +23,7 @@
 //                      one kernel boundary per panel step on the critical path
 //     k_syrk           contribution block U = A22 - L21 L21^T once per front, K = ns
 //   per level L-1..0: k_bwd_gemv (L21^T x, one wave per column) + k_bwd_tri (L11^-T, one
-//                    workgroup per front, LDS-resident solution slice).
+//                    workgroup per front, LDS-resident solution slice, right-looking by blocks).
 // Every output entry is written by exactly one workgroup per launch in a fixed order: the
 // factor and the solution are bitwise reproducible run to run (no atomics).
 #include <hip/hip_runtime.h>
@@ -64,7 +64,23 @@ __device__ unsigned int g_phase_n;
   }
 #define PH(i) \
   if (ph_on_) g_phase[ph_k_][i] = __builtin_amdgcn_s_memtime();
+#define PH_REC (ph_on_ ? g_phase[ph_k_] : nullptr)
+// second record for workgroup 1 (k_step: the first tile task)
+#define PH1_BEGIN(id)                                                      \
+  const bool ph1_on_ = threadIdx.x == 0 && blockIdx.x == 1;                \
+  unsigned ph1_k_ = 0;                                                     \
+  if (ph1_on_) {                                                           \
+    ph1_k_ = atomicAdd(&g_phase_n, 1u) % 4096u;                            \
+    g_phase[ph1_k_][0] = (id);                                             \
+    g_phase[ph1_k_][1] = __builtin_amdgcn_s_memtime();                     \
+    for (int q_ = 2; q_ < 8; ++q_) g_phase[ph1_k_][q_] = 0;                \
+  }
+#define PH1(i) \
+  if (ph1_on_) g_phase[ph1_k_][i] = __builtin_amdgcn_s_memtime();
 #else
+#define PH1_BEGIN(id)
+#define PH1(i)
+#define PH_REC nullptr
 #define PH_BEGIN(id)
 #define PH(i)
 #endif
@@ -154,47 +170,55 @@ __device__ __forceinline__ double rlane(double v, int l) {
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Factor the 32x32 diagonal block held row-wise by lanes 0..31 (row[c] = A(lane, c), c <= lane;
-// rows >= kb padded with the identity). On return row[c] = L(lane, c), dinv[lane] = 1/L(lane, lane).
+// rows >= kb padded with the identity). On return row[c] = L(lane, c).
 // Returns false if a pivot was not positive (cs_chol's `d <= 0` test).
-// Latency-shaped for one wave: fully unrolled (no selects); column j of L is broadcast through LDS
-// (double-buffered; LDS ops of one wave complete in order, so no waits are placed by hand); the
-// next pivot is formed by its own lane from l_{j+1,j} ahead of the broadcast, so the sequential
-// chain per column is readlane -> rsq + 1 Newton step -> 2 FMAs.
-// The forward solve L y = b rides along: y holds b(lane) on entry and y(lane) on return.
-__device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, double* col, double* dinv) {
+// Latency-shaped for one wave, right-looking with a two-column look-ahead: once column j is scaled,
+// columns j+1 and j+2 are updated at once with l_{j+1,j}, l_{j+2,j} broadcast by v_readlane (no LDS
+// on the chain); the rest of column j's rank-1 update goes through LDS and is applied one column
+// later, touching only columns >= j+3, so its reads never stall a pivot. The sequential chain per
+// column is readlane -> rsq + 1 Newton step -> mul -> readlane -> FMA. The forward solve L y = b
+// rides along: y holds b(lane) on entry and y(lane) on return. Entries above a lane's diagonal may
+// collect garbage; they are never read.
+__device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, double* col) {
   bool ok = true;
-  double djj = rlane(row[0], 0);
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
+    // deferred part of column j-1 (columns >= j+2), fetched from LDS first (written one iteration ago)
+    double2 cc[NB / 2];
+    const int c0 = (j + 2) & ~1;
+    if (j >= 1) {
+      const double* cb = col + ((j - 1) & 1) * 2 * NB;
+#pragma unroll
+      for (int c = c0; c < NB; c += 2) cc[c >> 1] = *reinterpret_cast<const double2*>(cb + c);
+    }
+    const double djj = rlane(row[j], j);
     ok &= djj > 0.0;
     const double d = djj > 0.0 ? djj : 1.0;
     double r = __builtin_amdgcn_rsq(d);  // ~5e-8 relative; one Newton step -> ~4e-15
     r = r * (1.5 - 0.5 * d * r * r);
-    const double ljj = d * r;
-    const double lrj = lane == j ? ljj : row[j] * r;  // lanes < j hold 0 in row[j]
-    row[j] = lrj;
-    if (lane == j) dinv[j] = r;
+    // column j of L (or of L^-1 e_c in lanes >= 32); lane j's own row[j] is the pivot d (up to the
+    // non-positive case, which fails the factorisation anyway), so no lane select is needed
+    const double lj = row[j] * r;
+    row[j] = lj;
+    if (j + 1 < NB) {  // look-ahead columns first: they carry the next two pivots
+      row[j + 1] -= lj * rlane(lj, j + 1);
+      if (j + 2 < NB) row[j + 2] -= lj * rlane(lj, j + 2);
+      col[(j & 1) * 2 * NB + lane] = lj;  // every lane writes (lanes >= 32 into the unused half)
+    }
     const double yj = rlane(y, j) * r;
-    y = lane == j ? yj : (lane > j ? y - lrj * yj : y);
-    if (j + 1 < NB) {
-      double* cb = col + (j & 1) * NB;
-      if (lane < NB) cb[lane] = lrj;
-      djj = rlane(row[j + 1] - lrj * lrj, j + 1);  // lane j+1 owns both factors
-      // all reads of the broadcast column first (one LDS wait), then the updates
-      const int c0 = (j + 1) & ~1;
-      double2 cc[NB / 2];
-#pragma unroll
-      for (int c = c0; c < NB; c += 2) cc[c >> 1] = *reinterpret_cast<const double2*>(cb + c);
+    y = lane == j ? yj : (lane > j ? y - lj * yj : y);
+    if (j >= 1) {  // column j-1 onto columns j+2.. (j and j+1 got it at once)
+      const double lp = row[j - 1];
 #pragma unroll
       for (int c = c0; c < NB; c += 2) {
-        if (c > j) row[c] -= lrj * cc[c >> 1].x;
-        row[c + 1] -= lrj * cc[c >> 1].y;
+        if (c > j + 1) row[c] -= lp * cc[c >> 1].x;
+        row[c + 1] -= lp * cc[c >> 1].y;
       }
-      // materialise this step's updates now: left alone, the scheduler defers the FMAs until each
-      // row[c] is next needed and keeps every broadcast column live (512 VGPRs + spills)
-#pragma unroll
-      for (int c = j + 1; c < NB; ++c) asm volatile("" : "+v"(row[c]));
     }
+    // materialise this iteration's updates: left alone, the scheduler defers the FMAs until each
+    // row[c] is next needed and keeps every fetched column live (register blow-up and spills)
+#pragma unroll
+    for (int c = j + 1; c < NB; ++c) asm volatile("" : "+v"(row[c]));
   }
   return ok;
 }
@@ -205,8 +229,8 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, d
 // forward-solve vy (LDS, kb values) in place. On return D holds L (lower, with diagonal).
 // Lanes 32..63 run the same instruction stream on the identity: lane 32 + c ends holding column c
 // of L^-1 (right-looking substitution on the broadcast columns of L), written row-major to linv.
-__device__ __forceinline__ void factor_block(double* D, int kb, double* vy, double* col, double* dinv, int lane,
-                                             int* fail, double* linv) {
+__device__ __forceinline__ void factor_block(double* D, int kb, double* vy, double* col, int lane, int* fail,
+                                             double* linv, unsigned long long* ph = nullptr) {
   double row[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
@@ -214,7 +238,9 @@ __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, doub
     row[c] = ((lane >= kb && c == lane) || lane - NB == c) ? 1.0 : a;
   }
   double y = ld0(vy, lane, lane < kb);
-  const bool ok = chol32(row, y, lane, col, dinv);
+  if (ph) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); ph[5] = __builtin_amdgcn_s_memtime(); }
+  const bool ok = chol32(row, y, lane, col);
+  if (ph) { asm volatile("" : "+v"(row[NB - 1])); ph[6] = __builtin_amdgcn_s_memtime(); }
   if (lane == 0 && !ok) *fail = 1;
   if (lane < kb) {  // whole row (the upper part is never read back)
 #pragma unroll
@@ -244,8 +270,8 @@ __global__ void __launch_bounds__(256) k_potrf0(const int* __restrict__ level_li
                                                 const double* __restrict__ vecs, double* __restrict__ ysol,
                                                 double* __restrict__ linv, int* __restrict__ fail) {
   __shared__ double D[NB * DS];
-  __shared__ __attribute__((aligned(16))) double col[2 * NB];
-  __shared__ double dinv[NB], vy[NB];
+  __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
+  __shared__ double vy[NB];
   PH_BEGIN(1)
   const FrontDesc me = fd[level_list[blockIdx.x]];
   const int m = me.ns + me.nr, kb = min(NB, me.ns);
@@ -262,7 +288,7 @@ __global__ void __launch_bounds__(256) k_potrf0(const int* __restrict__ level_li
   if (tid < kb) vy[tid] = vecs[me.vec_off + tid];
   __syncthreads();
   PH(2)
-  if (tid < 64) factor_block(D, kb, vy, col, dinv, tid, fail, linv + (size_t)me.c0 * (NB * NB));
+  if (tid < 64) factor_block(D, kb, vy, col, tid, fail, linv + (size_t)me.c0 * (NB * NB), PH_REC);
   __syncthreads();
   PH(3)
   publish_block(D, vy, kb, lbuf + me.l_off, m, 0, ysol + me.c0, tid);
@@ -325,9 +351,10 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   __shared__ double yk[NB];
   __shared__ double sh[2 * TT * PS];  // Pa | Pb; reused as the 64 x 65 result tile
   __shared__ double Dn[NB * DS];      // next diagonal block
-  __shared__ __attribute__((aligned(16))) double col[2 * NB];
-  __shared__ double dinvn[NB], vn[NB];
+  __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
+  __shared__ double vn[NB];
   PH_BEGIN(2)
+  PH1_BEGIN(3)
   const StepTask t = tasks[blockIdx.x];
   const int m = t.m, ns = t.ns;
   double* F = fronts + t.f_off;
@@ -410,7 +437,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     }
     __syncthreads();
     PH(2)
-    if (tid < 64) factor_block(Dn, kbn, vn, col, dinvn, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB));
+    if (tid < 64) factor_block(Dn, kbn, vn, col, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB), PH_REC);
     __syncthreads();
     PH(3)
     publish_block(Dn, vn, kbn, L, m, r0, ysol + t.c0, tid);
@@ -445,6 +472,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   }
   __syncthreads();
 
+  PH1(2)
   // ---- TRSM as a product: X = P L_kk^-T on v_mfma_f64_16x16x4f64; wave w owns rows 16w..16w+15
   // of both panels (A = P rows, B[k][c] = L_kk^-1(c, k))
   {
@@ -486,6 +514,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
       if (q < kb && I0 + r < m) L[(k0 + q) * m + I0 + r] = Pa[r * PS + q];
     }
   }
+  PH1(3)
   if (!upd) return;
 
   // ---- C[I, J] -= P_I P_J^T (columns inside the supernode, lower triangle)
@@ -501,6 +530,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     const int gi = I0 + r, gj = J0 + c;
     if (gi < m && gj < ns && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
   }
+  PH1(4)
 }
 
 // ---------------------------------------------------------------------------- contribution block
@@ -591,8 +621,8 @@ __global__ void k_ipermute(int n, const int* __restrict__ perm, const double* __
 // Per level (descending), two launches:
 //   k_bwd_gemv  t_s = y_s - L21^T x_rows for every front of the level; one wave per column,
 //               lanes run down the column (coalesced), x_rows gathered from the finished ancestors
-//   k_bwd_tri   x_s = L11^-T t_s per front: 32-column blocks from the last, in-supernode column
-//               dots by 8 threads per column, the 32x32 triangle as a product with L_kk^-1.
+//   k_bwd_tri   x_s = L11^-T t_s per front: 32-column blocks from the last, the 32x32 triangle as
+//               a product with L_kk^-1, then the block's rows applied to every column above it.
 // Task (gemv): s, a = first column (4 per workgroup).
 __global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                   const int* __restrict__ rows, const double* __restrict__ lbuf,
@@ -615,8 +645,7 @@ __global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_l
                                                  const double* __restrict__ lbuf, const double* __restrict__ linv,
                                                  double* __restrict__ xsol) {
   extern __shared__ __attribute__((aligned(16))) double xs[];  // [ns]: t_s, solved in place
-  __shared__ double red[8][NB];
-  __shared__ double tsh[NB];
+  __shared__ double xb[NB];
   const int s = level_list[blockIdx.x];
   const FrontDesc me = fd[s];
   const int m = me.ns + me.nr, ns = me.ns;
@@ -625,42 +654,37 @@ __global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_l
   for (int i = tid; i < ns; i += 256) xs[i] = xsol[me.c0 + i];
   __syncthreads();
   const int nblk = (ns + NB - 1) / NB;
-  const int q = tid & (NB - 1), g = tid >> 5;
+  // right-looking by 32-column blocks from the last: x_blk = L_kk^-T t_blk (a 32-long dot per lane
+  // with the stored L_kk^-1, four partial chains), then t_c -= L(blk, c)^T x_blk for every column c
+  // above the block: one thread per column reads that column's 32 contiguous entries of the block
   for (int bk = nblk - 1; bk >= 0; --bk) {
     const int k0 = bk * NB, kb = min(NB, ns - k0);
-    // column q of L_kk^-1 (row-major in linv), fetched ahead of the dot products
-    double li[NB];
     if (tid < NB) {
       const double* Lb = linv + (size_t)(me.c0 + k0) * (NB * NB) + tid;
+      double li[NB];
 #pragma unroll
       for (int i = 0; i < NB; ++i) li[i] = Lb[i * NB];
-    }
-    double part = 0.0;
-    if (q < kb) {
-      const double* cl = L + (size_t)(k0 + q) * m;
-      double p4[4] = {0.0, 0.0, 0.0, 0.0};
-      int i = k0 + kb + g;
-      for (; i + 24 < ns; i += 32) {  // 4 independent loads in flight
+      double x4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) p4[u] += cl[i + 8 * u] * xs[i + 8 * u];
-      }
-      for (; i < ns; i += 8) p4[0] += cl[i] * xs[i];
-      part = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+      for (int i = 0; i < NB; ++i) x4[i & 3] += li[i] * (i < kb ? xs[k0 + i] : 0.0);
+      xb[tid] = (x4[0] + x4[1]) + (x4[2] + x4[3]);
     }
-    red[g][q] = part;
     __syncthreads();
-    if (tid < NB) {  // x_blk = L_kk^-T (t_blk - dots): a 32-long dot per lane, no sequential chain
-      double r = 0.0;
-      if (tid < kb) {
-        r = xs[k0 + tid];
+    if (tid < kb) xs[k0 + tid] = xb[tid];
+    const bool vec = kb == NB && ((m | me.l_off) & 1) == 0;  // 16-B aligned column slices
+    for (int c = tid; c < k0; c += 256) {
+      const double* Lc = L + (size_t)c * m + k0;
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      if (vec) {
 #pragma unroll
-        for (int gg = 0; gg < 8; ++gg) r -= red[gg][tid];
+        for (int i = 0; i < NB; i += 2) {
+          const double2 u = *reinterpret_cast<const double2*>(Lc + i);
+          a4[(i >> 1) & 3] += u.x * xb[i] + u.y * xb[i + 1];
+        }
+      } else {
+        for (int i = 0; i < kb; ++i) a4[i & 3] += Lc[i] * xb[i];
       }
-      tsh[tid] = r;  // one wave writes and reads tsh: LDS order within the wave suffices
-      double x = 0.0;
-#pragma unroll
-      for (int i = 0; i < NB; ++i) x += li[i] * tsh[i];
-      if (tid < kb) xs[k0 + tid] = x;
+      xs[c] -= (a4[0] + a4[1]) + (a4[2] + a4[3]);
     }
     __syncthreads();
   }

@@ -166,7 +166,9 @@ hipEvent_t KernelTimer::get() {
   return e;
 }
 void KernelTimer::begin(const std::string& name, hipStream_t s) {
-  if (!enabled) return;
+  open_ = false;
+  if (!enabled || (!only.empty() && name != only)) return;
+  open_ = true;
   Rec r;
   r.a = get();
   r.b = nullptr;
@@ -175,7 +177,8 @@ void KernelTimer::begin(const std::string& name, hipStream_t s) {
   pending.push_back(r);
 }
 void KernelTimer::end(hipStream_t s) {
-  if (!enabled || pending.empty()) return;
+  if (!enabled || !open_ || pending.empty()) return;
+  open_ = false;
   Rec& r = pending.back();
   r.b = get();
   HIP_CHECK(hipEventRecord(r.b, s));
@@ -379,10 +382,8 @@ void DeviceCholesky::solve(double* x, hipStream_t s) {
 Engine::Engine(int dev) : device(dev) {
   HIP_CHECK(hipSetDevice(device));
   HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-  dscal.resize(8);
+  dscal.resize(12);  // [0] lambda [1] chi2 [2] scale [3] maxdiag [4] lambda (rank 0) [5] 0 | [8..9] fail flags (int)
   dscal.zero(stream);
-  dfail.resize(2);
-  dfail.zero(stream);
   for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
   for (auto& e : lm_ev_) HIP_CHECK(hipEventCreate(&e));
 }
@@ -712,7 +713,6 @@ void Engine::setup_edges_device() {
   dmeas.upload(meas, stream);
   dinfo.upload(info, stream);
   dparams.upload(params, stream);
-  dchi.resize(std::max(ne, 1));
   dpartial.resize(std::max<size_t>(launch::sum_partials(std::max<long long>(std::max<long long>(ne, vector_size()), 1)) + 64, 128));
   edges_ready = true;
   ++state_ver;  // the edge set (and so chi2) changed
@@ -1049,7 +1049,6 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
   } else {
     chol.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
   }
-  dscale_terms.resize(std::max<long long>(n, 1));
   HIP_CHECK(hipStreamSynchronize(stream));
   structure_built = true;
   return G2OHIP_OK;
@@ -1070,8 +1069,7 @@ void Engine::compute_errors_async() {
   ensure_device_state();
   EdgeArgs a = edge_args(dv0, dv1, dmeas, dinfo, dparams, dstate[vt0].get(), dstate[vt1].get());
   timer.begin("error", stream);
-  launch::error(family, a, ne, dchi.get(), stream);
-  launch::sum(dchi.get(), ne, dpartial.get(), dscal.get() + 1, stream);
+  launch::error_sum(family, a, ne, dpartial.get(), dscal.get() + 1, stream);
   timer.end(stream);
   if (do_schur) allreduce_sum(dscal.get() + 1, 1);
 }
@@ -1119,9 +1117,9 @@ int Engine::build_system() {  // block_solver.hpp:462-521
   return G2OHIP_OK;
 }
 
-void Engine::set_lambda_device(double l) {
+void Engine::set_lambda_device(double l, bool reset_fail) {
   lambda_host = l;
-  launch::set_scalars(dscal.get(), l, rank == 0 ? l : 0.0, stream);
+  launch::set_scalars(dscal.get(), l, rank == 0 ? l : 0.0, stream, reset_fail);
 }
 
 int Engine::set_lambda(double lambda, int /*backup*/) {  // block_solver.hpp:524-550 (lambda kept virtual)
@@ -1135,20 +1133,21 @@ int Engine::restore_diagonal() {  // :552-565
   return G2OHIP_OK;
 }
 
-void Engine::solve_async() {  // block_solver.hpp:314-447
-  HIP_CHECK(hipMemsetAsync(dfail.get(), 0, sizeof(int) * 2, stream));
-  HIP_CHECK(hipEventRecord(ev_[0], stream));
-  ev_valid_ = true;
+void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
+  if (reset_fail) HIP_CHECK(hipMemsetAsync(failp(), 0, sizeof(int) * 2, stream));
+  const bool sev = stats_level >= 2;  // stage events for G2OBatchStatistics
+  if (sev) HIP_CHECK(hipEventRecord(ev_[0], stream));
+  ev_valid_ = sev;
   if (!do_schur) {
-    HIP_CHECK(hipEventRecord(ev_[1], stream));
+    if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
     timer.begin("chol_factor", stream);
-    chol.factor(dH.get(), dscal.get(), db.get(), dfail.get(), stream);
+    chol.factor(dH.get(), dscal.get(), db.get(), failp(), stream);
     timer.end(stream);
-    HIP_CHECK(hipEventRecord(ev_[2], stream));
+    if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
     timer.begin("chol_solve", stream);
     chol.solve(dx.get(), stream);
     timer.end(stream);
-    HIP_CHECK(hipEventRecord(ev_[3], stream));
+    if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
     return;
   }
   const int lm_begin = local_lm.empty() ? 0 : local_lm.front();
@@ -1158,7 +1157,7 @@ void Engine::solve_async() {  // block_solver.hpp:314-447
   double* bschur = dS.get() + (size_t)nS * pd * pd;
   timer.begin("schur_dinv", stream);
   launch::schur_prep(nLloc, lm_begin, dHll.get(), db.get() + size_poses, dscal.get(), dDinv.get(), dUfac.get(),
-                     dCl.get(), dfail.get() + 1, stream);
+                     dCl.get(), failp() + 1, stream);
   timer.end(stream);
   timer.begin("schur_diag", stream);
   launch::schur_diag(num_poses, sch_rptr.get(), sch_robs.get(), sch_obs_lm.get(), lm_begin, Hpl, dUfac.get(), dCl.get(),
@@ -1169,15 +1168,15 @@ void Engine::solve_async() {  // block_solver.hpp:314-447
                      sch_pp.get(), Hpl, dUfac.get(), ds_hpp.get(), dH.get(), S, stream);
   timer.end(stream);
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
-  HIP_CHECK(hipEventRecord(ev_[1], stream));
+  if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
   timer.begin("chol_factor", stream);
-  chol.factor(S, dscal.get() + 5, bschur, dfail.get(), stream);
+  chol.factor(S, dscal.get() + 5, bschur, failp(), stream);
   timer.end(stream);
-  HIP_CHECK(hipEventRecord(ev_[2], stream));
+  if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
   timer.begin("chol_solve", stream);
   chol.solve(dx.get(), stream);
   timer.end(stream);
-  HIP_CHECK(hipEventRecord(ev_[3], stream));
+  if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
   timer.begin("backsub", stream);
   launch::backsub(nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get(), size_poses, lm_begin, dx.get(),
                   stream);
@@ -1186,9 +1185,9 @@ void Engine::solve_async() {  // block_solver.hpp:314-447
 
 int Engine::solve_sync() {
   if (!structure_built) return G2OHIP_ERR_STATE;
-  solve_async();
+  solve_async(true);
   int f[2] = {0, 0};
-  HIP_CHECK(hipMemcpyAsync(f, dfail.get(), sizeof f, hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipMemcpyAsync(f, failp(), sizeof f, hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
   timer.collect();
   return f[0] ? 0 : 1;
@@ -1233,19 +1232,28 @@ int Engine::push() {  // base_vertex.h:93-95 for all active vertices (stream-ord
   ensure_device_state();
   if ((int)stack_.size() <= stack_depth_) stack_.emplace_back(5);
   auto& lvl = stack_[stack_depth_++];
+  launch::CopyList cl{};
   for (int t = 1; t <= 4; ++t) {
     if (!dstate[t].size()) continue;
     lvl[t].resize(dstate[t].size());
-    HIP_CHECK(hipMemcpyAsync(lvl[t].get(), dstate[t].get(), dstate[t].bytes(), hipMemcpyDeviceToDevice, stream));
+    cl.src[cl.n] = dstate[t].get();
+    cl.dst[cl.n] = lvl[t].get();
+    cl.len[cl.n++] = (long long)dstate[t].size();
   }
+  launch::copy_multi(cl, stream);  // one launch for every vertex type
   return G2OHIP_OK;
 }
 int Engine::pop() {
   if (stack_depth_ == 0) return G2OHIP_ERR_STATE;
   auto& lvl = stack_[--stack_depth_];
+  launch::CopyList cl{};
   for (int t = 1; t <= 4; ++t)
-    if (lvl[t].size())
-      HIP_CHECK(hipMemcpyAsync(dstate[t].get(), lvl[t].get(), lvl[t].bytes(), hipMemcpyDeviceToDevice, stream));
+    if (lvl[t].size()) {
+      cl.src[cl.n] = lvl[t].get();
+      cl.dst[cl.n] = dstate[t].get();
+      cl.len[cl.n++] = (long long)lvl[t].size();
+    }
+  launch::copy_multi(cl, stream);
   host_state_stale = true;
   ++state_ver;
   return G2OHIP_OK;
@@ -1293,9 +1301,9 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   double currentChi = currentChi0;
   double tempChi = currentChi;
   hipEvent_t e0 = lm_ev_[0], e1 = lm_ev_[1], e2 = lm_ev_[2], e3 = lm_ev_[3], q0 = lm_ev_[4], q1 = lm_ev_[5];
-  HIP_CHECK(hipEventRecord(q0, stream));
+  if (st && stats_level >= 2) HIP_CHECK(hipEventRecord(q0, stream));
   build_system();
-  HIP_CHECK(hipEventRecord(q1, stream));  // timeQuadraticForm from events: no host sync here
+  if (st && stats_level >= 2) HIP_CHECK(hipEventRecord(q1, stream));  // timeQuadraticForm from events
   if (iteration == 0) {
     current_lambda = cfg.user_lambda_init > 0 ? cfg.user_lambda_init : lambda_init();
     ni = 2;
@@ -1308,54 +1316,49 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   do {
     push();
     if (st) st->levenbergIterations++;
-    double ts = wall();
-    set_lambda_device(current_lambda);
-    HIP_CHECK(hipEventRecord(e0, stream));
-    solve_async();
-    HIP_CHECK(hipEventRecord(e1, stream));
+    const bool ev1 = st && stats_level >= 1, ev2 = st && stats_level >= 2;
+    set_lambda_device(current_lambda, true);  // also clears the not-PD flags
+    if (ev1) HIP_CHECK(hipEventRecord(e0, stream));
+    solve_async(false);
+    if (ev1) HIP_CHECK(hipEventRecord(e1, stream));
     update_async();
-    HIP_CHECK(hipEventRecord(e2, stream));
-    set_lambda_device(0.0);  // restoreDiagonal
+    if (ev2) HIP_CHECK(hipEventRecord(e2, stream));
+    // computeScale (:177-184) on the device, sum x (lambda x + b), while lambda is still set; the
+    // restoreDiagonal that follows (:113) is the next setLambda (lambda is virtual, never in H)
+    launch::scale_sum(vector_size(), size_poses, dx.get(), db.get(), dscal.get(), dpartial.get(), dscal.get() + 2,
+                      stream);
+    allreduce_sum(dscal.get() + 2, 1);
     compute_errors_async();
-    // computeScale (:177-184) on the device: sum x (lambda x + b)
-    {
-      double* scal = dscal.get();
-      launch::set_scalars(scal, current_lambda, rank == 0 ? current_lambda : 0.0, stream);
-      launch::scale_terms(size_poses, dx.get(), db.get(), scal + 4, dscale_terms.get(), stream);
-      launch::scale_terms(size_landmarks, dx.get() + size_poses, db.get() + size_poses, scal, dscale_terms.get() + size_poses,
-                          stream);
-      launch::sum(dscale_terms.get(), vector_size(), dpartial.get(), scal + 2, stream);
-      allreduce_sum(scal + 2, 1);
-      launch::set_scalars(scal, 0.0, 0.0, stream);
-    }
-    HIP_CHECK(hipEventRecord(e3, stream));
-    double hs[3];
-    int f[2];
+    if (ev2) HIP_CHECK(hipEventRecord(e3, stream));
+    double hs[12];  // lambda, chi2, scale, ... | fail flags (one readback per trial)
     HIP_CHECK(hipMemcpyAsync(hs, dscal.get(), sizeof hs, hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipMemcpyAsync(f, dfail.get(), sizeof f, hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
     timer.collect();
     tempChi = hs[1];
+    int f[2];
+    std::memcpy(f, hs + 8, sizeof f);
     const bool ok2 = f[0] == 0;
-    if (st && first_trial) {
+    if (ev2 && first_trial) {
       float mq = 0;
       HIP_CHECK(hipEventElapsedTime(&mq, q0, q1));
       st->timeQuadraticForm = mq * 1e-3;
     }
     first_trial = false;
-    if (st) {
-      float ms01 = 0, ms12 = 0, a = 0, b = 0, c = 0;
+    if (ev1) {
+      float ms01 = 0;
       HIP_CHECK(hipEventElapsedTime(&ms01, e0, e1));
+      st->timeLinearSolution += ms01 * 1e-3;
+    }
+    if (ev2) {
+      float ms12 = 0, a = 0, b = 0, c = 0;
       HIP_CHECK(hipEventElapsedTime(&ms12, e1, e2));
       HIP_CHECK(hipEventElapsedTime(&a, ev_[0], ev_[1]));
       HIP_CHECK(hipEventElapsedTime(&b, ev_[1], ev_[2]));
       HIP_CHECK(hipEventElapsedTime(&c, ev_[1], ev_[3]));
-      st->timeLinearSolution += ms01 * 1e-3;
       st->timeUpdate = ms12 * 1e-3;
       st->timeSchurComplement = do_schur ? a * 1e-3 : 0.0;
       st->timeNumericDecomposition = b * 1e-3;
       st->timeLinearSolver = c * 1e-3;
-      (void)ts;
     }
     if (!ok2) tempChi = std::numeric_limits<double>::max();
     rho = currentChi - tempChi;
@@ -1378,6 +1381,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     }
     qmax++;
   } while (rho < 0 && qmax < maxTrials);
+  set_lambda_device(0.0);  // restoreDiagonal of the last trial (block_solver.hpp:552-565)
   // the state left behind has chi2 currentChi (accepted: the last tempChi; rejected: popped back)
   chi_cache = currentChi;
   chi_ver = state_ver;

@@ -72,6 +72,8 @@ struct DeviceCholesky {
 
 struct KernelTimer {
   bool enabled = false;
+  std::string only;    // time only this kernel class (empty: all)
+  bool open_ = false;  // a begin() whose end() is pending
   struct Rec { hipEvent_t a, b; std::string name; };
   std::vector<Rec> pending;
   std::vector<hipEvent_t> pool;
@@ -93,6 +95,8 @@ class Engine {
   int device;
   hipStream_t stream = nullptr;
   std::string algorithm = "lm_hip_var";
+  // G2OBatchStatistics timers: 0 none, 1 timeLinearSolution only (2 events per trial), 2 every stage
+  int stats_level = 2;
   bool levenberg = true;
 
   // ---- graph ops ----
@@ -164,7 +168,6 @@ class Engine {
   // device edges (local shard, in active-edge order)
   DevBuf<int> dv0, dv1;
   DevBuf<double> dmeas, dinfo, dparams;
-  DevBuf<double> dchi;
   DevBuf<double> dslot0, dslot1;
   int slot_stride0 = 0, slot_stride1 = 0;
   DevBuf<long long> doff_dst;
@@ -199,8 +202,7 @@ class Engine {
   DeviceCholesky chol;
   // scalars: [0] lambda, [1] chi2, [2] scale, [3] maxdiag
   DevBuf<double> dscal;
-  DevBuf<int> dfail;
-  DevBuf<double> dpartial, dscale_terms;
+  DevBuf<double> dpartial;
   double lambda_host = 0.0;
   bool lambda_set = false;
   // LM state (optimization_algorithm_levenberg.cpp)
@@ -219,9 +221,10 @@ class Engine {
   void compute_errors_async();
   double chi2_sync();
   double lambda_init();
-  void solve_async();
+  void solve_async(bool reset_fail);
+  int* failp() const { return reinterpret_cast<int*>(dscal.get() + 8); }
   void update_async();
-  void set_lambda_device(double l);
+  void set_lambda_device(double l, bool reset_fail = false);
   void allreduce_sum(double* dptr, size_t n);
   int lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats* st);
 };

@@ -17,6 +17,8 @@
 //   k_error/k_oplus  computeActiveErrors (sparse_optimizer.cpp:63-90) and update (:441-454).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 #include "device_types.hpp"
 #include "device_util.hpp"
@@ -664,6 +666,66 @@ __global__ void k_scale_terms(long long n, const double* __restrict__ x, const d
   out[i] = x[i] * (l * x[i] + b[i]);
 }
 
+// computeActiveErrors + activeRobustChi2 fused with the first pass of the deterministic sum: the
+// same fixed chunking and tree as k_sum_partial over a chi2 array, without the array
+template <class F>
+__global__ void __launch_bounds__(RED_BLOCK) k_error_partial(EdgeData d, int ne, double* __restrict__ partial) {
+  __shared__ double sh[RED_BLOCK];
+  const long long base = (long long)blockIdx.x * RED_BLOCK * RED_PER_THREAD;
+  double s = 0;
+  for (int k = 0; k < RED_PER_THREAD; ++k) {
+    const long long e = base + (long long)k * RED_BLOCK + threadIdx.x;
+    if (e < ne) {
+      double err[F::D];
+      F::error(d, (int)e, err);
+      double Om[F::D * F::D];
+      load_info<F::D>(d.info + (size_t)e * F::INFO, Om);
+      double c = 0;
+#pragma unroll
+      for (int i = 0; i < F::D; ++i) {
+        double r = 0;
+#pragma unroll
+        for (int j = 0; j < F::D; ++j) r += Om[i * F::D + j] * err[j];
+        c += err[i] * r;
+      }
+      s += c;
+    }
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int m = RED_BLOCK / 2; m > 0; m >>= 1) {
+    if ((int)threadIdx.x < m) sh[threadIdx.x] += sh[threadIdx.x + m];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+// computeScale (optimization_algorithm_levenberg.cpp:177-184) fused with the first sum pass:
+// x (lambda x + b), lambda = lam[4] (rank-0 share) on the pose part, lam[0] on the landmark part
+__global__ void __launch_bounds__(RED_BLOCK) k_scale_partial(long long n, long long npose, const double* __restrict__ x,
+                                                             const double* __restrict__ b, const double* __restrict__ lam,
+                                                             double* __restrict__ partial) {
+  __shared__ double sh[RED_BLOCK];
+  const double lp = lam[4], ll = lam[0];
+  const long long base = (long long)blockIdx.x * RED_BLOCK * RED_PER_THREAD;
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < RED_PER_THREAD; ++k) {
+    const long long i = base + (long long)k * RED_BLOCK + threadIdx.x;
+    if (i < n) {
+      const double l = i < npose ? lp : ll;
+      s += x[i] * (l * x[i] + b[i]);
+    }
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int m = RED_BLOCK / 2; m > 0; m >>= 1) {
+    if ((int)threadIdx.x < m) sh[threadIdx.x] += sh[threadIdx.x + m];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
 // ------------------------------------------------------------------------------ launchers
 namespace launch {
 
@@ -781,6 +843,25 @@ void sum(const double* v, long long n, double* partial, double* out, hipStream_t
   KERNEL_CHECK();
 }
 
+void error_sum(int family, const EdgeArgs& a, int ne, double* partial, double* out, hipStream_t s) {
+  const int np = (int)sum_partials(ne);
+  if (np > 0) {
+    switch (family) {
+      case FAM_BA: hipLaunchKernelGGL(k_error_partial<FamilyBA>, np, RED_BLOCK, 0, s, mk<FamilyBA>(a), ne, partial); break;
+      case FAM_SE3: hipLaunchKernelGGL(k_error_partial<FamilySE3>, np, RED_BLOCK, 0, s, mk<FamilySE3>(a), ne, partial); break;
+      case FAM_SE2: hipLaunchKernelGGL(k_error_partial<FamilySE2>, np, RED_BLOCK, 0, s, mk<FamilySE2>(a), ne, partial); break;
+    }
+  }
+  hipLaunchKernelGGL(k_sum_final, 1, RED_BLOCK, 0, s, partial, np, out);
+  KERNEL_CHECK();
+}
+void scale_sum(long long n, long long npose, const double* x, const double* b, const double* lam, double* partial,
+               double* out, hipStream_t s) {
+  const int np = (int)sum_partials(n);
+  if (np > 0) hipLaunchKernelGGL(k_scale_partial, np, RED_BLOCK, 0, s, n, npose, x, b, lam, partial);
+  hipLaunchKernelGGL(k_sum_final, 1, RED_BLOCK, 0, s, partial, np, out);
+  KERNEL_CHECK();
+}
 void scale_terms(long long n, const double* x, const double* b, const double* lam, double* out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_scale_terms, grid_for(n, 256), 256, 0, s, n, x, b, lam, out);
@@ -792,10 +873,11 @@ void scale_terms(long long n, const double* x, const double* b, const double* la
 
 // ------------------------------------------------------------------------------ small helpers
 namespace g2ohip {
-__global__ void k_set_scalars(double* __restrict__ p, double lam, double lam_rank) {
+__global__ void k_set_scalars(double* __restrict__ p, double lam, double lam_rank, int reset_fail) {
   p[0] = lam;
   p[4] = lam_rank;
   p[5] = 0.0;
+  if (reset_fail) p[8] = 0.0;  // the two int not-PD flags live in p[8]
 }
 // max |diag| over nb blocks of dim x dim (col-major), partial per block of threads
 __global__ void __launch_bounds__(256) k_diag_absmax(const double* __restrict__ H, int nb, int dim,
@@ -819,9 +901,26 @@ __global__ void k_max_final(const double* __restrict__ partial, int np, double* 
   for (int i = 0; i < np; ++i) m = fmax(m, partial[i]);
   *out = m;
 }
+__global__ void __launch_bounds__(256) k_copy_multi(launch::CopyList cl) {
+  for (int k = 0; k < cl.n; ++k) {  // uniform loop; grid-stride over each buffer
+    const double2* src = reinterpret_cast<const double2*>(cl.src[k]);
+    double2* dst = reinterpret_cast<double2*>(cl.dst[k]);
+    const long long n2 = cl.len[k] / 2;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n2; i += (long long)gridDim.x * 256) dst[i] = src[i];
+    if ((cl.len[k] & 1) && blockIdx.x == 0 && threadIdx.x == 0) cl.dst[k][cl.len[k] - 1] = cl.src[k][cl.len[k] - 1];
+  }
+}
 namespace launch {
-void set_scalars(double* p, double lam, double lam_rank, hipStream_t s) {
-  hipLaunchKernelGGL(k_set_scalars, 1, 1, 0, s, p, lam, lam_rank);
+void copy_multi(const CopyList& cl, hipStream_t s) {
+  if (cl.n <= 0) return;
+  long long mx = 0;
+  for (int k = 0; k < cl.n; ++k) mx = std::max(mx, cl.len[k]);
+  const unsigned g = (unsigned)std::min<long long>(std::max<long long>((mx / 2 + 255) / 256, 1), 1024);
+  hipLaunchKernelGGL(k_copy_multi, g, 256, 0, s, cl);
+  KERNEL_CHECK();
+}
+void set_scalars(double* p, double lam, double lam_rank, hipStream_t s, bool reset_fail) {
+  hipLaunchKernelGGL(k_set_scalars, 1, 1, 0, s, p, lam, lam_rank, reset_fail ? 1 : 0);
   KERNEL_CHECK();
 }
 // writes max|diag| of two block sets into out (partial needs >= 64 doubles)

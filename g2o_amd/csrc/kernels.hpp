@@ -55,7 +55,18 @@ void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* 
 size_t sum_partials(long long n);
 void sum(const double* v, long long n, double* partial, double* out, hipStream_t s);
 void scale_terms(long long n, const double* x, const double* b, const double* lam, double* out, hipStream_t s);
-void set_scalars(double* p, double lam, double lam_rank, hipStream_t s);
+// fused computeActiveErrors + chi2 sum, computeScale + sum (same chunking/tree as sum(): deterministic)
+void error_sum(int family, const EdgeArgs& a, int ne, double* partial, double* out, hipStream_t s);
+void scale_sum(long long n, long long npose, const double* x, const double* b, const double* lam, double* partial,
+               double* out, hipStream_t s);
+void set_scalars(double* p, double lam, double lam_rank, hipStream_t s, bool reset_fail = false);
+struct CopyList {  // up to 4 device-to-device copies of doubles in one launch (vertex push/pop)
+  const double* src[4];
+  double* dst[4];
+  long long len[4];
+  int n;
+};
+void copy_multi(const CopyList& cl, hipStream_t s);
 void diag_absmax(const double* H1, int nb1, int d1, const double* H2, int nb2, int d2, double* partial, double* out,
                  hipStream_t s);
 

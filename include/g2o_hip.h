@@ -151,7 +151,14 @@ int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, cons
 
 /* ---- measurement hooks ---- */
 void g2ohip_enable_kernel_timing(g2ohip_graph* g, int on);
-/* per-kernel-class average device time (ms) of the last optimize(); names: "assembly","schur","factor","solve" */
+/* restrict the kernel timer to one kernel class (NULL or "": every class); each timed class costs two
+ * event records per launch on the stream */
+void g2ohip_kernel_timing_only(g2ohip_graph* g, const char* name);
+/* G2OBatchStatistics timers: 0 none, 1 timeLinearSolution only (2 events per LM trial), 2 (default)
+ * every stage (timeSchurComplement, timeNumericDecomposition, timeLinearSolver, timeUpdate, timeQuadraticForm) */
+void g2ohip_set_stats_level(g2ohip_graph* g, int level);
+/* per-kernel-class average device time (ms) since the timer was enabled; classes: "linearize", "vreduce",
+ * "schur_dinv", "schur_diag", "schur_rows", "chol_factor", "chol_solve", "backsub", "error", "oplus" */
 double g2ohip_kernel_ms(g2ohip_graph* g, const char* name);
 long long g2ohip_kernel_count(g2ohip_graph* g, const char* name);
 /* algorithmic bytes / flops of one launch of the named kernel class (for roofline accounting) */

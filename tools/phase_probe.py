@@ -26,7 +26,14 @@ def main():
     a = np.frombuffer(buf, dtype=np.uint64, count=8 * n).reshape(n, 8).astype(np.int64)
     print(f"{n} records")
     for kid, name, labels in ((1, "k_potrf0", ["stage", "factor", "publish"]),
-                              (2, "k_step(diag task)", ["stage+trsm+syrk", "factor", "publish"])):
+                              (2, "k_step(diag task)", ["stage+trsm+syrk", "factor", "publish"]),
+                              (3, "k_step(tile 0,0)", ["stage", "trsm+L21", "update+store"])):
+        r = a[a[:, 0] == kid]
+        if len(r):
+            d = r[:, 6] - r[:, 5]
+            ok = (r[:, 6] > 0) & (r[:, 5] > 0)
+            if ok.any():
+                print(f"{name}: chol32 alone median {np.median(d[ok]) / CLK:7.2f} us  (n={ok.sum()})")
         r = a[a[:, 0] == kid]
         if not len(r):
             continue

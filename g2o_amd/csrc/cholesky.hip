@@ -341,7 +341,8 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
   }
 }
 
-// Task flags: 1 update the tile (else TRSM + L21 store only), 4 the step's next-diagonal task.
+// Task flags: 1 update the tile (else TRSM + L21 store only), 4 the step's next-diagonal task,
+// 8 the tile may reach into the contribution block (columns >= ns: no separate k_syrk pass).
 // Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
 __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, double* __restrict__ fronts,
                                               double* __restrict__ lbuf, double* __restrict__ vecs,
@@ -457,7 +458,8 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     pav[u] = ld0(F, (k0 + q) * m + I0 + r, q < kb && I0 + r < m);
     pbv[u] = ld0(F, (k0 + q) * m + J0 + r, upd && q < kb && J0 + r < m);
   }
-  if (upd) load_ctile(F, m, I0, J0, ns, tid, cv);
+  const int climit = (t.flags & 8) ? m : ns;  // flag 8: the contribution block is updated here too
+  if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
 #pragma unroll
   for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
     const int e = tid + 256 * u_;
@@ -499,7 +501,10 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     }
   }
   __syncthreads();
-  if (writer && tid < 64 && I0 + tid < m) {  // forward-solve update of the front vector: v_i -= x_i y_k
+  // rows/columns of the next diagonal block, [r0, r0 + kbn): this step's diagonal task reads their
+  // raw values at its start and applies the panel update itself, so tile tasks never write them
+  const int kbn = max(0, min(NB, ns - r0));
+  if (writer && tid < 64 && I0 + tid < m && I0 + tid >= r0 + kbn) {  // forward-solve update: v_i -= x_i y_k
     double s2 = 0.0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) s2 += Pa[tid * PS + q] * yk[q];
@@ -528,7 +533,8 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   for (int u = 0; u < 16; ++u) {
     const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
     const int gi = I0 + r, gj = J0 + c;
-    if (gi < m && gj < ns && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
+    const bool dblk = gi < r0 + kbn && gj < r0 + kbn;
+    if (gi < m && gj < climit && gi >= gj && !dblk) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
   }
   PH1(4)
 }

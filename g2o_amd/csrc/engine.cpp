@@ -13,6 +13,7 @@
 
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -279,6 +280,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     std::vector<Task> tk;
     std::vector<launch::StepTask> stk;
     ops.clear();
+    const char* fe = getenv("G2OHIP_CHOL_FUSED");  // dev A/B: 0 = separate k_syrk pass per level
+    const bool fused_contrib = !fe || atoi(fe) != 0;
     for (size_t l = 0; l < sym.levels.size(); ++l) {
       const auto& lv = sym.levels[l];
       Op ea{0, (int)tk.size(), 0};
@@ -300,20 +303,24 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           const int k0 = p * NB;
           if (k0 >= q.ns) continue;
           const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
-          const int T = (m - r0 + TT - 1) / TT, TJ = (q.ns - r0 + TT - 1) / TT;
+          // fused: every panel step also applies its rank-kb update to the contribution block (the
+          // step is latency-bound on the diagonal chain, the extra tiles run in its shadow)
+          const int T = (m - r0 + TT - 1) / TT, TJ = fused_contrib ? T : (q.ns - r0 + TT - 1) / TT;
+          const int fl = fused_contrib ? 8 : 0;
           if (r0 < q.ns)  // the next diagonal block first: it is the step's critical chain
             stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0,
                                            k0 | (kb << 16), 0, 4});
           for (int tj = 0; tj < std::max(TJ, 1); ++tj)
             for (int ti = tj; ti < T; ++ti)
               stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0,
-                                             k0 | (kb << 16), ti | (tj << 16), tj < TJ ? 1 : 0});
+                                             k0 | (kb << 16), ti | (tj << 16), (tj < TJ ? 1 : 0) | fl});
         }
         st.count = (int)stk.size() - st.off;
         if (st.count) ops.push_back(st);
       }
       Op sy{3, (int)tk.size(), 0};
       for (int sn : lv) {
+        if (fused_contrib) break;
         const Supernode& q = sym.sn[sn];
         const int T = (q.nr + TT - 1) / TT;
         for (int tj = 0; tj < T; ++tj)
@@ -1302,8 +1309,9 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   double tempChi = currentChi;
   hipEvent_t e0 = lm_ev_[0], e1 = lm_ev_[1], e2 = lm_ev_[2], e3 = lm_ev_[3], q0 = lm_ev_[4], q1 = lm_ev_[5];
   if (st && stats_level >= 2) HIP_CHECK(hipEventRecord(q0, stream));
-  build_system();
+  if (built_ver != state_ver || iteration == 0) build_system();  // else enqueued by the previous iteration
   if (st && stats_level >= 2) HIP_CHECK(hipEventRecord(q1, stream));  // timeQuadraticForm from events
+  built_ver = 0;
   if (iteration == 0) {
     current_lambda = cfg.user_lambda_init > 0 ? cfg.user_lambda_init : lambda_init();
     ni = 2;
@@ -1385,6 +1393,13 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   // the state left behind has chi2 currentChi (accepted: the last tempChi; rejected: popped back)
   chi_cache = currentChi;
   chi_ver = state_ver;
+  // the next iteration starts with buildSystem on exactly this state: enqueue it now so the GPU works
+  // while the host returns to the caller (skipped when the loop is about to stop)
+  const bool more = !(qmax == maxTrials || rho == 0 || !std::isfinite(current_lambda));
+  if (more) {
+    build_system();
+    built_ver = state_ver;
+  }
   if (qmax == maxTrials || rho == 0 || !std::isfinite(current_lambda)) return 1;  // Terminate
   return 0;                                                                       // OK
 }

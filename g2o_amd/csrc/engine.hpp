@@ -210,6 +210,9 @@ class Engine {
   // chi2 of the device state, cached: every state change bumps state_ver; the LM loop knows the chi2 of
   // the state it leaves behind (accepted: tempChi, rejected + pop: currentChi) and records it
   unsigned long long state_ver = 1, chi_ver = 0;
+  // buildSystem of the next LM iteration is enqueued as soon as a trial loop ends (it only depends on
+  // the state the loop leaves); built_ver records which state the assembled system belongs to
+  unsigned long long built_ver = 0;
   double chi_cache = 0.0;
   hipEvent_t lm_ev_[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int levenberg_iterations = 0;

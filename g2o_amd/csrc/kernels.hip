@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "device_types.hpp"
@@ -363,7 +364,7 @@ __global__ void __launch_bounds__(256, 2)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
                  const int* __restrict__ st_obs, const int* __restrict__ st_lm, const int* __restrict__ pairs,
                  const int* __restrict__ pp, const double* __restrict__ Hpl, const double* __restrict__ Ufac,
-                 const int* __restrict__ s_hpp, const double* __restrict__ Hpp, double* __restrict__ S) {
+                 const int* __restrict__ s_hpp, const double* __restrict__ Hpp, double* __restrict__ S, int mode) {
   __shared__ __attribute__((aligned(16))) double Gs[SCH_SB * SCH_GS];
   __shared__ int so[SCH_SB], sl[SCH_SB];  // staging indices of the next batch to stage
   __shared__ int sp[2][SCH_SB];           // pair lists, double-buffered by batch parity
@@ -479,16 +480,16 @@ __global__ void __launch_bounds__(256, 2)
   }
   for (int k = 0; k < nb; ++k) {
     const int cur = k & 1;
-    if (k + 1 < nb) hpl_load(B1);
+    if (k + 1 < nb && !(mode & 2)) hpl_load(B1);
     if (k + 2 < nb) idx_load(B2, k + 2);
     const launch::SchurBatch B3 = rec(k + 3);
-    compute(cur);
+    if (!(mode & 1)) compute(cur);
     __syncthreads();  // Gs, so/sl and the pair list of batch k are free
     if (k + 1 < nb) {
       hpl_store(B1);
       if (k + 2 < nb) idx_store(cur);
       __syncthreads();
-      transform(B1);
+      if (!(mode & 4)) transform(B1);
       __syncthreads();
     }
     B0 = B1;
@@ -811,8 +812,9 @@ void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, c
                 const int* pairs, const int* pp, const double* Hpl, const double* Ufac, const int* s_hpp,
                 const double* Hpp, double* S, hipStream_t s) {
   if (ntasks <= 0) return;
+  static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;  // dev A/B only
   hipLaunchKernelGGL(k_schur_rows, ntasks, 256, 0, s, tasks, batches, st_obs, st_lm, pairs, pp, Hpl, Ufac, s_hpp, Hpp,
-                     S);
+                     S, mode);
   KERNEL_CHECK();
 }
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,

@@ -22,8 +22,9 @@
 //                      workgroup of tile (0, 0) then factors the NEXT 32x32 diagonal block —
 //                      one kernel boundary per panel step on the critical path
 //     k_syrk           contribution block U = A22 - L21 L21^T once per front, K = ns
-//   per level L-1..0: k_bwd_gemv (L21^T x, one wave per column) + k_bwd_tri (L11^-T, one
-//                    workgroup per front, LDS-resident solution slice, right-looking by blocks).
+//     (inverse tasks)  in the k_step launches: X = L11^-1 block by block, beside the critical chain
+//   per level L-1..0: k_bwd_gemv (t = y - L21^T x, one wave per column) + k_bwd_x (x = X^T t, one
+//                    wave per column): the backward solve has no sequential chain inside a front.
 // Every output entry is written by exactly one workgroup per launch in a fixed order: the
 // factor and the solution are bitwise reproducible run to run (no atomics).
 #include <hip/hip_runtime.h>
@@ -230,7 +231,7 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, d
 // Lanes 32..63 run the same instruction stream on the identity: lane 32 + c ends holding column c
 // of L^-1 (right-looking substitution on the broadcast columns of L), written row-major to linv.
 __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, double* col, int lane, int* fail,
-                                             double* linv, unsigned long long* ph = nullptr) {
+                                             double* linv, double* X, int ldx, unsigned long long* ph = nullptr) {
   double row[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
@@ -250,6 +251,12 @@ __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, doub
   if (lane >= NB) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) linv[i * NB + (lane - NB)] = row[i];
+    if (lane - NB < kb) {  // diagonal block of X = L11^-1, column-major with leading dimension ldx
+      double* xc = X + (size_t)(lane - NB) * ldx;
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        if (i < kb) xc[i] = row[i];
+    }
   }
 }
 __device__ __forceinline__ void publish_block(const double* D, const double* vy, int kb, double* L, int m, int r0,
@@ -268,7 +275,8 @@ __device__ __forceinline__ void publish_block(const double* D, const double* vy,
 __global__ void __launch_bounds__(256) k_potrf0(const int* __restrict__ level_list, const FrontDesc* __restrict__ fd,
                                                 const double* __restrict__ fronts, double* __restrict__ lbuf,
                                                 const double* __restrict__ vecs, double* __restrict__ ysol,
-                                                double* __restrict__ linv, int* __restrict__ fail) {
+                                                double* __restrict__ linv, double* __restrict__ xinv,
+                                                int* __restrict__ fail) {
   __shared__ double D[NB * DS];
   __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
   __shared__ double vy[NB];
@@ -288,7 +296,7 @@ __global__ void __launch_bounds__(256) k_potrf0(const int* __restrict__ level_li
   if (tid < kb) vy[tid] = vecs[me.vec_off + tid];
   __syncthreads();
   PH(2)
-  if (tid < 64) factor_block(D, kb, vy, col, tid, fail, linv + (size_t)me.c0 * (NB * NB), PH_REC);
+  if (tid < 64) factor_block(D, kb, vy, col, tid, fail, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns, PH_REC);
   __syncthreads();
   PH(3)
   publish_block(D, vy, kb, lbuf + me.l_off, m, 0, ysol + me.c0, tid);
@@ -342,12 +350,13 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
 }
 
 // Task flags: 1 update the tile (else TRSM + L21 store only), 4 the step's next-diagonal task,
-// 8 the tile may reach into the contribution block (columns >= ns: no separate k_syrk pass).
+// 8 the tile may reach into the contribution block (columns >= ns: no separate k_syrk pass),
+// 16 an inverse task: block (tj, ti) of X = L11^-1 (see below).
 // Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
 __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, double* __restrict__ fronts,
                                               double* __restrict__ lbuf, double* __restrict__ vecs,
                                               double* __restrict__ ysol, double* __restrict__ linv,
-                                              int* __restrict__ fail) {
+                                              double* __restrict__ xinv, int* __restrict__ fail) {
   __shared__ double Li[NB * PS];      // L_kk^-1, row-major, stride 34
   __shared__ double yk[NB];
   __shared__ double sh[2 * TT * PS];  // Pa | Pb; reused as the 64 x 65 result tile
@@ -438,11 +447,81 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     }
     __syncthreads();
     PH(2)
-    if (tid < 64) factor_block(Dn, kbn, vn, col, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB), PH_REC);
+    if (tid < 64)
+      factor_block(Dn, kbn, vn, col, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB),
+                   xinv + t.x_off + (size_t)r0 * ns + r0, ns, PH_REC);
     __syncthreads();
     PH(3)
     publish_block(Dn, vn, kbn, L, m, r0, ysol + t.c0, tid);
     PH(4)
+    return;
+  }
+
+  if (t.flags & 16) {
+    // ---- explicit inverse of the supernode's diagonal part, X = L11^-1, for the parallel backward
+    // solve (k_bwd_x). Right-looking over the panel steps: the step of panel s adds the term of block
+    // row s-1 to every pending block (p, j), p >= s, j < s:  W_pj += L_{p,s-1} X_{s-1,j}, kept in X's
+    // own slot; at p = s the block is final: X_sj = -L_ss^-1 W_sj. Every input was written by an
+    // earlier launch; one 32x32x32 product (two when finalising) per task, beside the critical chain.
+    const int j = ti, pp = tj, kq = k0 / NB - 1;
+    const bool fin = pp * NB == k0;
+    const int kbp = min(NB, ns - NB * pp);
+    double* Xf = xinv + t.x_off;
+    double wv[4], lq[4], xq[4], li[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, r = e & (NB - 1), c = e >> 5;
+      wv[u] = ld0(Xf, (NB * j + c) * ns + NB * pp + r, kq > j && r < kbp);  // W_pj so far
+      lq[u] = ld0(L, (NB * kq + c) * m + NB * pp + r, r < kbp);              // L_{p,kq}(r, c)
+      xq[u] = Xf[(NB * j + c) * ns + NB * kq + r];                           // X_{kq,j}(r, c)
+      li[u] = ld0(Lin, e, fin);                                              // L_ss^-1, row-major
+    }
+    double* Ts = Dn;  // 32 x DS
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, r = e & (NB - 1), c = e >> 5;
+      Pa[r * PS + c] = lq[u];
+      Pb[r * PS + c] = xq[u];
+      Ts[r * DS + c] = wv[u];
+      Li[(e >> 5) * PS + (e & (NB - 1))] = li[u];
+    }
+    __syncthreads();
+    const int tr = w & 1, tc = w >> 1;
+    dx4 acc = {0.0, 0.0, 0.0, 0.0};
+    {  // acc = L_{p,kq} X_{kq,j} on the wave's 16x16 tile (B given as rows q of X_{kq,j})
+      const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Pa[(16 * tr + lr) * PS + k], Pb[k * PS + 16 * tc + lr], acc, 0, 0, 0);
+      }
+    }
+    const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += Ts[(16 * tr + lk + 4 * i) * DS + 16 * tc + lr];
+    if (!fin) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * tr + lk + 4 * i, c = 16 * tc + lr;
+        if (r < kbp) Xf[(size_t)(NB * j + c) * ns + NB * pp + r] = acc[i];
+      }
+      return;
+    }
+    __syncthreads();  // every read of Ts done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Ts[(16 * tr + lk + 4 * i) * DS + 16 * tc + lr] = acc[i];
+    __syncthreads();
+    dx4 xo = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < NB / 4; ++kk) {  // X_sj = -L_ss^-1 W_sj
+      const int k = kk * 4 + lk;
+      xo = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[(16 * tr + lr) * PS + k], Ts[k * DS + 16 * tc + lr], xo, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * tr + lk + 4 * i, c = 16 * tc + lr;
+      if (r < kbp) Xf[(size_t)(NB * j + c) * ns + NB * pp + r] = -xo[i];
+    }
     return;
   }
 
@@ -624,15 +703,16 @@ __global__ void k_ipermute(int n, const int* __restrict__ perm, const double* __
 
 
 // ---------------------------------------------------------------------------- backward solve
-// Per level (descending), two launches:
-//   k_bwd_gemv  t_s = y_s - L21^T x_rows for every front of the level; one wave per column,
-//               lanes run down the column (coalesced), x_rows gathered from the finished ancestors
-//   k_bwd_tri   x_s = L11^-T t_s per front: 32-column blocks from the last, the 32x32 triangle as
-//               a product with L_kk^-1, then the block's rows applied to every column above it.
-// Task (gemv): s, a = first column (4 per workgroup).
+// Per level (descending), two launches, both parallel over columns (no sequential chain):
+//   k_bwd_gemv  t_s = y_s - L21^T x_rows for every front of the level; one wave per column, lanes run
+//               down the column (coalesced), x_rows gathered from the finished ancestors
+//   k_bwd_x     x_s = L11^-T t_s = X^T t_s with the explicit inverse X = L11^-1 built during the
+//               factorization (k_step inverse tasks); one wave per column of X
+// Task: s, a = first column (4 per workgroup).
 __global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                   const int* __restrict__ rows, const double* __restrict__ lbuf,
-                                                  const double* __restrict__ ysol, double* __restrict__ xsol) {
+                                                  const double* __restrict__ ysol, const double* __restrict__ xsol,
+                                                  double* __restrict__ tsol) {
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, ns = me.ns;
@@ -644,57 +724,30 @@ __global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks
   for (int i = lane; i < me.nr; i += 64) acc += col[i] * xsol[rw[i]];
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (lane == 0) xsol[me.c0 + j] = ysol[me.c0 + j] - acc;
+  if (lane == 0) tsol[me.c0 + j] = ysol[me.c0 + j] - acc;
 }
 
-__global__ void __launch_bounds__(256) k_bwd_tri(const int* __restrict__ level_list, const FrontDesc* __restrict__ fd,
-                                                 const double* __restrict__ lbuf, const double* __restrict__ linv,
-                                                 double* __restrict__ xsol) {
-  extern __shared__ __attribute__((aligned(16))) double xs[];  // [ns]: t_s, solved in place
-  __shared__ double xb[NB];
-  const int s = level_list[blockIdx.x];
-  const FrontDesc me = fd[s];
-  const int m = me.ns + me.nr, ns = me.ns;
-  const double* L = lbuf + me.l_off;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < ns; i += 256) xs[i] = xsol[me.c0 + i];
-  __syncthreads();
-  const int nblk = (ns + NB - 1) / NB;
-  // right-looking by 32-column blocks from the last: x_blk = L_kk^-T t_blk (a 32-long dot per lane
-  // with the stored L_kk^-1, four partial chains), then t_c -= L(blk, c)^T x_blk for every column c
-  // above the block: one thread per column reads that column's 32 contiguous entries of the block
-  for (int bk = nblk - 1; bk >= 0; --bk) {
-    const int k0 = bk * NB, kb = min(NB, ns - k0);
-    if (tid < NB) {
-      const double* Lb = linv + (size_t)(me.c0 + k0) * (NB * NB) + tid;
-      double li[NB];
+__global__ void __launch_bounds__(256) k_bwd_x(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                               const double* __restrict__ xinv, const double* __restrict__ tsol,
+                                               double* __restrict__ xsol) {
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int ns = me.ns;
+  const int lane = threadIdx.x & 63, j = t.a + (int)(threadIdx.x >> 6);
+  if (j >= ns) return;
+  const double* xc = xinv + me.x_off + (size_t)j * ns;  // column j of X (rows >= j are nonzero)
+  const double* tt = tsol + me.c0;
+  double a4[4] = {0.0, 0.0, 0.0, 0.0};
+  int i = j + lane;
+  for (; i + 192 < ns; i += 256) {
 #pragma unroll
-      for (int i = 0; i < NB; ++i) li[i] = Lb[i * NB];
-      double x4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int i = 0; i < NB; ++i) x4[i & 3] += li[i] * (i < kb ? xs[k0 + i] : 0.0);
-      xb[tid] = (x4[0] + x4[1]) + (x4[2] + x4[3]);
-    }
-    __syncthreads();
-    if (tid < kb) xs[k0 + tid] = xb[tid];
-    const bool vec = kb == NB && ((m | me.l_off) & 1) == 0;  // 16-B aligned column slices
-    for (int c = tid; c < k0; c += 256) {
-      const double* Lc = L + (size_t)c * m + k0;
-      double a4[4] = {0.0, 0.0, 0.0, 0.0};
-      if (vec) {
-#pragma unroll
-        for (int i = 0; i < NB; i += 2) {
-          const double2 u = *reinterpret_cast<const double2*>(Lc + i);
-          a4[(i >> 1) & 3] += u.x * xb[i] + u.y * xb[i + 1];
-        }
-      } else {
-        for (int i = 0; i < kb; ++i) a4[i & 3] += Lc[i] * xb[i];
-      }
-      xs[c] -= (a4[0] + a4[1]) + (a4[2] + a4[3]);
-    }
-    __syncthreads();
+    for (int u = 0; u < 4; ++u) a4[u] += xc[i + 64 * u] * tt[i + 64 * u];
   }
-  for (int j = tid; j < ns; j += 256) xsol[me.c0 + j] = xs[j];
+  for (; i < ns; i += 64) a4[0] += xc[i] * tt[i];
+  double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) xsol[me.c0 + j] = acc;
 }
 
 namespace launch {
@@ -734,15 +787,15 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
   KERNEL_CHECK();
 }
 void chol_potrf0(int nfronts, const int* level_list, const FrontDesc* fd, const double* fronts, double* lbuf,
-                 const double* vecs, double* ysol, double* linv, int* fail, hipStream_t s) {
+                 const double* vecs, double* ysol, double* linv, double* xinv, int* fail, hipStream_t s) {
   if (nfronts <= 0) return;
-  hipLaunchKernelGGL(k_potrf0, nfronts, 256, 0, s, level_list, fd, fronts, lbuf, vecs, ysol, linv, fail);
+  hipLaunchKernelGGL(k_potrf0, nfronts, 256, 0, s, level_list, fd, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
-               double* linv, int* fail, hipStream_t s) {
+               double* linv, double* xinv, int* fail, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_step, ntasks, 256, 0, s, tasks, fronts, lbuf, vecs, ysol, linv, fail);
+  hipLaunchKernelGGL(k_step, ntasks, 256, 0, s, tasks, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
@@ -761,19 +814,15 @@ void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStr
   KERNEL_CHECK();
 }
 void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int* rows, const double* lbuf,
-                   const double* ysol, double* xsol, hipStream_t s) {
+                   const double* ysol, const double* xsol, double* tsol, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_bwd_gemv, ntasks, 256, 0, s, tasks, fd, rows, lbuf, ysol, xsol);
+  hipLaunchKernelGGL(k_bwd_gemv, ntasks, 256, 0, s, tasks, fd, rows, lbuf, ysol, xsol, tsol);
   KERNEL_CHECK();
 }
-void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, const double* linv,
-                  double* xsol, int max_ns, hipStream_t s) {
-  if (nfronts <= 0) return;
-  const size_t bytes = (size_t)max_ns * sizeof(double);
-  if (bytes > 150 * 1024) throw DeviceError("supernode wider than LDS for the backward solve");
-  if (bytes > 64 * 1024)
-    HIP_CHECK(hipFuncSetAttribute((const void*)k_bwd_tri, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-  hipLaunchKernelGGL(k_bwd_tri, nfronts, 256, bytes, s, level_list, fd, lbuf, linv, xsol);
+void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,
+                hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_bwd_x, ntasks, 256, 0, s, tasks, fd, xinv, tsol, xsol);
   KERNEL_CHECK();
 }
 

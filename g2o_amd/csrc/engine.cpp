@@ -256,12 +256,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   dst.upload(hdst, s);
   isdiag.upload(hdiag, s);
   std::vector<launch::FrontDesc> hfd(sym.sn.size());
-  long long loff = 0;
+  long long loff = 0, xoff = 0;
   for (size_t k = 0; k < sym.sn.size(); ++k) {
     const Supernode& q = sym.sn[k];
-    hfd[k] = launch::FrontDesc{q.front_off, q.vec_off, loff, q.rows_off, q.c0, q.ns, q.nr, q.parent,
+    hfd[k] = launch::FrontDesc{q.front_off, q.vec_off, loff, q.rows_off, xoff, q.c0, q.ns, q.nr, q.parent,
                                sym.children_ptr[k], sym.children_ptr[k + 1]};
     loff += (long long)(q.ns + q.nr) * q.ns;
+    xoff += (long long)q.ns * q.ns;  // X = L11^-1, column-major
   }
   lpool = loff;
   fd.upload(hfd, s);
@@ -298,6 +299,10 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
       for (int p = 0; p < maxp; ++p) {
         Op st{2, (int)stk.size(), 0};
+        // task order inside the launch (= dispatch order): every front's next-diagonal task first (the
+        // critical chain must start at once, on a CU of its own), then the tile tasks, then the
+        // inverse tasks (X = L11^-1 for the backward solve), which have the most slack
+        std::vector<launch::StepTask> diag_t, tile_t, inv_t;
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
           const int k0 = p * NB;
@@ -307,14 +312,22 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           // step is latency-bound on the diagonal chain, the extra tiles run in its shadow)
           const int T = (m - r0 + TT - 1) / TT, TJ = fused_contrib ? T : (q.ns - r0 + TT - 1) / TT;
           const int fl = fused_contrib ? 8 : 0;
-          if (r0 < q.ns)  // the next diagonal block first: it is the step's critical chain
-            stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0,
-                                           k0 | (kb << 16), 0, 4});
+          auto mk = [&](int tile, int flags) {
+            return launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns, q.c0,
+                                    k0 | (kb << 16), tile, flags};
+          };
+          if (r0 < q.ns) diag_t.push_back(mk(0, 4));
           for (int tj = 0; tj < std::max(TJ, 1); ++tj)
-            for (int ti = tj; ti < T; ++ti)
-              stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0,
-                                             k0 | (kb << 16), ti | (tj << 16), (tj < TJ ? 1 : 0) | fl});
+            for (int ti = tj; ti < T; ++ti) tile_t.push_back(mk(ti | (tj << 16), (tj < TJ ? 1 : 0) | fl));
+          // inverse tasks: block row p-1's term into every pending block (bp, j), bp >= p, j < p;
+          // block row p is final after this step
+          const int nblk = (q.ns + NB - 1) / NB;
+          for (int bp = p; bp < nblk && p >= 1; ++bp)
+            for (int j = 0; j < p; ++j) inv_t.push_back(mk(j | (bp << 16), 16));
         }
+        stk.insert(stk.end(), diag_t.begin(), diag_t.end());
+        stk.insert(stk.end(), tile_t.begin(), tile_t.end());
+        stk.insert(stk.end(), inv_t.begin(), inv_t.end());
         st.count = (int)stk.size() - st.off;
         if (st.count) ops.push_back(st);
       }
@@ -353,6 +366,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   y_p.resize(std::max(sym.n, 1));
   lbuf.resize(std::max<long long>(lpool, 1));
   linv.resize((size_t)(sym.n + launch::CHOL_NB) * launch::CHOL_NB * launch::CHOL_NB);  // one 32x32 L_kk^-1 per panel start
+  xinv.resize(std::max<long long>(xoff, 1));
+  t_p.resize(std::max(sym.n, 1));
   x_p.resize(std::max(sym.n, 1));
 }
 
@@ -366,9 +381,9 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
     switch (op.kind) {
       case 0: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), fronts.get(), vecs.get(), s); break;
       case 1: launch::chol_potrf0(op.count, level_lists.get() + op.off, fd.get(), fronts.get(), lbuf.get(), vecs.get(),
-                                  y_p.get(), linv.get(), fail, s); break;
+                                  y_p.get(), linv.get(), xinv.get(), fail, s); break;
       case 2: launch::chol_step(op.count, step_tasks.get() + op.off, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),
-                                linv.get(), fail, s);
+                                linv.get(), xinv.get(), fail, s);
         break;
       default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;
     }
@@ -376,11 +391,11 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
 }
 
 void DeviceCholesky::solve(double* x, hipStream_t s) {
-  for (size_t l = level_off.size() - 1; l-- > 0;) {
-    const int nf = level_off[l + 1] - level_off[l];
-    launch::chol_bwd_gemv(bwd_off[l + 1] - bwd_off[l], tasks.get() + bwd_off[l], fd.get(), rows.get(), lbuf.get(),
-                          y_p.get(), x_p.get(), s);
-    launch::chol_bwd_tri(nf, level_lists.get() + level_off[l], fd.get(), lbuf.get(), linv.get(), x_p.get(), max_ns, s);
+  for (size_t l = level_off.size() - 1; l-- > 0;) {  // root level first
+    const int nt = bwd_off[l + 1] - bwd_off[l];
+    launch::chol_bwd_gemv(nt, tasks.get() + bwd_off[l], fd.get(), rows.get(), lbuf.get(), y_p.get(), x_p.get(), t_p.get(),
+                          s);
+    launch::chol_bwd_x(nt, tasks.get() + bwd_off[l], fd.get(), xinv.get(), t_p.get(), x_p.get(), s);
   }
   launch::chol_ipermute(sym.n, perm.get(), x_p.get(), x, s);
 }

@@ -61,7 +61,7 @@ struct DeviceCholesky {
   std::vector<Op> ops;
   DevBuf<launch::Task> tasks;
   DevBuf<launch::StepTask> step_tasks;
-  DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, lbuf, linv;
+  DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, t_p, lbuf, linv, xinv;
   long long lpool = 0;
   void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
   // numeric LL^T fused with the forward solve of rhs (y = L^-1 P rhs)

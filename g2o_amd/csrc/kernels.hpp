@@ -76,6 +76,7 @@ struct FrontDesc {  // device view of one supernode (see symbolic.hpp)
   long long vec_off;
   long long l_off;  // factor columns [L11; L21] (m x ns, ld m) in lbuf
   long long rows_off;
+  long long x_off;  // the front's explicit X = L11^-1 (ns x ns column-major) in xinv
   int c0, ns, nr, parent;
   int child_begin, child_end;  // into the children array
 };
@@ -83,11 +84,11 @@ struct Task {  // one workgroup's work item (meaning per kernel, see cholesky.hi
   int s, a, b, c;
 };
 struct StepTask {  // k_step work item, self-contained so a workgroup needs one dependent load
-  long long f_off, l_off, v_off;
+  long long f_off, l_off, v_off, x_off;
   int m, ns, c0;
   int k0kb;   // k0 | kb << 16
-  int tile;   // ti | tj << 16
-  int flags;  // 1 update the tile, 2 factor the next diagonal block
+  int tile;   // ti | tj << 16 (inverse task: block column j | block row p << 16)
+  int flags;  // 1 update the tile, 4 next-diagonal task, 8 reaches into the contribution block, 16 inverse
 };
 void chol_scatter(long long nent, const double* vals, const long long* dst, const unsigned char* is_diag,
                   const double* lam, double* fronts, hipStream_t s);
@@ -95,16 +96,16 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      double* fronts, double* vecs, hipStream_t s);
 void chol_potrf0(int nfronts, const int* level_list, const FrontDesc* fd, const double* fronts, double* lbuf,
-                 const double* vecs, double* ysol, double* linv, int* fail, hipStream_t s);
+                 const double* vecs, double* ysol, double* linv, double* xinv, int* fail, hipStream_t s);
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
-               double* linv, int* fail, hipStream_t s);
+               double* linv, double* xinv, int* fail, hipStream_t s);
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s);
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]
 void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]
 void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int* rows, const double* lbuf,
-                   const double* ysol, double* xsol, hipStream_t s);
-void chol_bwd_tri(int nfronts, const int* level_list, const FrontDesc* fd, const double* lbuf, const double* linv,
-                  double* xsol, int max_ns, hipStream_t s);
+                   const double* ysol, const double* xsol, double* tsol, hipStream_t s);
+void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,
+                hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only
 constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 4, CHOL_BW = 4;
 }  // namespace launch

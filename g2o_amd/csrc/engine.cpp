@@ -965,6 +965,8 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         std::vector<int> fill(rptr.begin(), rptr.end() - 1);
         for (int a = 0; a < nHpl; ++a) robs[fill[blk_pose[a]]++] = a;  // ascending a = landmark order
       }
+      std::vector<int> gpos(std::max(nHpl, 1), 0);  // observation -> its G block (camera-row order)
+      for (int r = 0; r < nHpl; ++r) gpos[robs[r]] = r;
       std::vector<int> obs_lm(std::max(nHpl, 1), 0), sdiag(num_poses);
       for (int l = 0; l < nLloc; ++l)
         for (int a = lm_ptr[l]; a < lm_ptr[l + 1]; ++a) obs_lm[a] = l;
@@ -976,7 +978,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
 
       std::vector<launch::SchurTask> tasks;
       std::vector<launch::SchurBatch> batches;
-      std::vector<int> st_obs, st_lm, prs, pp;
+      std::vector<int> st_obs, prs, pp;
       std::vector<int> camslot(num_poses, -1);
       struct P3 { int ls, a, b; };
       std::vector<P3> cur;
@@ -1026,12 +1028,10 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
             const int need = 1 + (int)tmp.size();
             if ((int)st_obs.size() - bst0 + need > SB) flush();
             const int posA = (int)st_obs.size() - bst0;
-            st_obs.push_back(a);
-            st_lm.push_back(l);
+            st_obs.push_back(gpos[a]);
             for (auto& [a2, sl] : tmp) {
               const int posB = (int)st_obs.size() - bst0;
-              st_obs.push_back(a2);
-              st_lm.push_back(l);
+              st_obs.push_back(gpos[a2]);
               cur.push_back(P3{sl, posA, posB});
             }
           }
@@ -1048,7 +1048,6 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       batches.push_back(launch::SchurBatch{});  // trailing dummy: k_schur_rows reads one record ahead
       sch_batches.upload(batches, stream);
       sch_st_obs.upload(nz(st_obs), stream);
-      sch_st_lm.upload(nz(st_lm), stream);
       sch_pairs.upload(nz(prs), stream);
       sch_pp.upload(nz(pp), stream);
     }
@@ -1065,6 +1064,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     ds_hpp.upload(shpp, stream);
     dDinv.resize(std::max(nLloc * 9, 1));
     dUfac.resize(std::max(nLloc * 6, 1));
+    dG.resize(std::max<long long>((long long)nHpl * 18, 1));  // G = Hpl U^-T per observation (6x3)
     dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
     chol.setup(num_poses, pd, s_bi, s_bj, stream);
@@ -1183,11 +1183,11 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   timer.end(stream);
   timer.begin("schur_diag", stream);
   launch::schur_diag(num_poses, sch_rptr.get(), sch_robs.get(), sch_obs_lm.get(), lm_begin, Hpl, dUfac.get(), dCl.get(),
-                     sch_sdiag.get(), ds_hpp.get(), dH.get(), db.get(), dscal.get() + 4, S, bschur, stream);
+                     sch_sdiag.get(), ds_hpp.get(), dH.get(), db.get(), dscal.get() + 4, S, bschur, dG.get(), stream);
   timer.end(stream);
   timer.begin("schur_rows", stream);
-  launch::schur_rows(nsch_tasks, sch_tasks.get(), sch_batches.get(), sch_st_obs.get(), sch_st_lm.get(), sch_pairs.get(),
-                     sch_pp.get(), Hpl, dUfac.get(), ds_hpp.get(), dH.get(), S, stream);
+  launch::schur_rows(nsch_tasks, sch_tasks.get(), sch_batches.get(), sch_st_obs.get(), sch_pairs.get(), sch_pp.get(),
+                     dG.get(), ds_hpp.get(), dH.get(), S, stream);
   timer.end(stream);
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
   if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
@@ -1547,13 +1547,12 @@ int Engine::set_comm_local(const std::string& key, int r, int nr) {
 double Engine::kernel_bytes(const std::string& name) const {
   // algorithmic bytes per launch (SURVEY.md §8d formulas)
   const double npl = nHpl, pb = (double)pd * ld * 8;
-  // Schur row pass: Hpl once, U and c per landmark, Hpp blocks present in S, S and bschur written once
-  // Schur row pass (off-diagonal blocks): Hpl of every observation with a partner once, U per
-  // landmark, the off-diagonal Hpp blocks present in S, the off-diagonal S blocks written once
-  if (name == "schur_rows") return npl * pb + local_lm.size() * 6 * 8.0 + (double)(nHppUsed - num_poses) * pd * pd * 8 +
+  // Schur row pass (off-diagonal blocks): G of every observation once, the off-diagonal Hpp blocks
+  // present in S, the off-diagonal S blocks written once
+  if (name == "schur_rows") return npl * pb + (double)(nHppUsed - num_poses) * pd * pd * 8 +
                                    (double)(nS - num_poses) * pd * pd * 8;
-  // diagonal blocks: Hpl, U and c per observation's landmark, Hpp diagonal, S diagonal + bschur
-  if (name == "schur_diag") return npl * pb + local_lm.size() * 9 * 8.0 + (double)num_poses * pd * pd * 8 * 2 +
+  // diagonal blocks: Hpl, U and c per observation's landmark, G written, Hpp diagonal, S diagonal + bschur
+  if (name == "schur_diag") return 2 * npl * pb + local_lm.size() * 9 * 8.0 + (double)num_poses * pd * pd * 8 * 2 +
                                    size_poses * 16.0;
   if (name == "schur_dinv") return local_lm.size() * ((9 + 3) * 8.0 + (9 + 6 + 3) * 8.0);
   if (name == "linearize") return ne * (family == FAM_BA ? (2 + 3 + 4) * 8.0 + 8 + (double)(slot_stride0 + slot_stride1 + pd * ld) * 8 : 0.0);
@@ -1563,7 +1562,7 @@ double Engine::kernel_bytes(const std::string& name) const {
 }
 double Engine::kernel_flops(const std::string& name) const {
   if (name == "chol_factor") return chol.sym.flops;
-  if (name == "schur_rows") return (double)npairs * (108 * 2) + (double)nstaged * 36;
+  if (name == "schur_rows") return (double)npairs * (108 * 2);
   return 0;
 }
 

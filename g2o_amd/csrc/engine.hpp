@@ -187,14 +187,14 @@ class Engine {
   VRed vr_pose, vr_lm;
   // schur
   DevBuf<int> d_lm_ptr, d_blk_pose, d_blk_lm;
-  DevBuf<double> dDinv, dUfac, dS, dCl;
+  DevBuf<double> dDinv, dUfac, dS, dCl, dG;
   int nS = 0, nHppUsed = 0;
   long long npairs = 0, nstaged = 0;  // off-diagonal pair products, staged blocks per Schur pass
   DevBuf<int> ds_hpp;
   // row-stationary Schur pass (k_schur_rows)
   DevBuf<launch::SchurTask> sch_tasks;
   DevBuf<launch::SchurBatch> sch_batches;
-  DevBuf<int> sch_st_obs, sch_st_lm, sch_pairs, sch_pp;
+  DevBuf<int> sch_st_obs, sch_pairs, sch_pp;
   int nsch_tasks = 0;
   // diagonal Schur blocks (k_schur_diag): per camera row its observations in landmark order
   DevBuf<int> sch_rptr, sch_robs, sch_obs_lm, sch_sdiag;

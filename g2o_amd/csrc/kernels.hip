@@ -9,9 +9,9 @@
 //   k_schur_prep  landmark pass of BlockSolver::solve (:342-360): Dinv = (Hll+lambda I)^-1,
 //                 and the split Hll+lambda I = U U^T, c = U^-1 b_l.
 //   k_schur_diag  Hschur(i,i) = Hpp(i,i) + lambda - sum_l G_il G_il^T, bschur = b - sum G c (:361-400),
-//                 G = Hpl U^-T in registers, one wave per camera.
+//                 G = Hpl U^-T in registers (and stored once per observation), one wave per camera.
 //   k_schur_rows  Hschur(i,j>i) = Hpp(i,j) - sum_l G_il G_jl^T: one workgroup per camera row (chunk),
-//                 the row's landmarks staged coalesced into LDS in batches; every output has one
+//                 the row's G blocks staged into LDS by LDS-DMA in batches; every output has one
 //                 owner and a fixed summation order (no atomics).
 //   k_backsub     x_l = Dinv (b_l - Hpl^T x_p) (:420-446).
 //   k_error/k_oplus  computeActiveErrors (sparse_optimizer.cpp:63-90) and update (:441-454).
@@ -223,8 +223,8 @@ __global__ void __launch_bounds__(256) k_offblock_reduce(int nb, int bsz, const 
 // Landmark pass (block_solver.hpp:341-360): Dinv = (Hll + lambda I)^-1 (cofactor inverse, as
 // Eigen's 3x3 inverse; kept for the back-substitution) and the symmetric split
 //   Hll + lambda I = U U^T (3x3 Cholesky),  G_a = Hpl_a U^-T,  c_l = U^-1 b_l,
-// so that Hpl Dinv Hpl^T = G G^T and Hpl Dinv b_l = G c_l. G is never materialised: the row pass
-// applies U^-T to each observation block as it stages it. Ufac per landmark: r0 r1 r2 u10 u20 u21
+// so that Hpl Dinv Hpl^T = G G^T and Hpl Dinv b_l = G c_l. k_schur_diag forms G once per observation
+// (for its own sums and, stored, for k_schur_rows). Ufac per landmark: r0 r1 r2 u10 u20 u21
 // (r = reciprocal pivots of U).
 __global__ void __launch_bounds__(256)
     k_schur_prep(int nl, int lm0, const double* __restrict__ Hll, const double* __restrict__ bl_all,
@@ -285,7 +285,8 @@ __global__ void __launch_bounds__(256)
                  const int* __restrict__ obs_lm, int lm0, const double* __restrict__ Hpl,
                  const double* __restrict__ Ufac, const double* __restrict__ cl_all, const int* __restrict__ sdiag,
                  const int* __restrict__ s_hpp, const double* __restrict__ Hpp, const double* __restrict__ b,
-                 const double* __restrict__ lam, double* __restrict__ S, double* __restrict__ bschur) {
+                 const double* __restrict__ lam, double* __restrict__ S, double* __restrict__ bschur,
+                 double* __restrict__ G) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= nrows) return;  // wave-uniform
   double acc[27];  // packed upper of G G^T (21, col-major) | G c (6)
@@ -310,6 +311,12 @@ __global__ void __launch_bounds__(256)
       g[12 + r] = (g[12 + r] - U[4] * g0 - U[5] * g1) * U[2];
       g[r] = g0;
       g[6 + r] = g1;
+    }
+    {  // every observation lies in exactly one camera row: G is written once, in camera-row order
+       // (consecutive lanes, consecutive blocks), for k_schur_rows
+      double2* go = reinterpret_cast<double2*>(G + (size_t)p * 18);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) go[k] = double2{g[2 * k], g[2 * k + 1]};
     }
     int k = 0;
 #pragma unroll
@@ -345,48 +352,48 @@ __global__ void __launch_bounds__(256)
 
 // Off-diagonal blocks, row-stationary (block_solver.hpp:361-391, j > i): one workgroup per (camera
 // row i, chunk of up to 64 off-diagonal slots of the row's Schur pattern). The row's landmarks are
-// walked in landmark order in batches; a batch stages, coalesced, the 6x3 blocks Hpl_a of the row's
-// own observation a = (l, i) and of the observations (l, j) in the chunk, with U_l, into LDS and
-// turns them into G = Hpl U^-T there. Four threads per slot, each three columns of the block over
-// every second pair of the slot's list (landmark order), the two parities combined by one fixed
-// shuffle: every output has one owner and a fixed summation order (no atomics, bitwise reproducible). The next batch's blocks
-// are in flight while the current one is reduced.
+// walked in landmark order in batches; a batch stages the G blocks (G = Hpl U^-T, written once per
+// observation by k_schur_diag, in camera-row order) of the row's own observation a = (l, i) and of
+// its partners (l, j), j > i, into LDS by LDS-DMA
+// (global_load_lds_dwordx4: 1 KiB lane-linear per wave instruction, no register staging). Two LDS
+// buffers: batch k+1 lands while batch k is reduced. Four threads per slot, each three columns of
+// the block over every second pair of the slot's list (landmark order), the two parities combined by
+// one fixed shuffle: every output has one owner and a fixed summation order (no atomics, bitwise
+// reproducible).
 namespace {
-constexpr int SCH_SB = launch::SCHUR_SB;  // staged observation blocks per batch
-constexpr int SCH_GS = 24;                // doubles per staged block: G (6x3 col-major) | U (6); 16-B aligned
+constexpr int SCH_SB = launch::SCHUR_SB;  // staged G blocks per batch
+constexpr int SCH_GB = 18;                // doubles per staged block: G, 6x3 col-major (9 x 16 B)
 constexpr int SCH_SL = launch::SCHUR_SL;  // off-diagonal slots per task
 constexpr int SCH_PPB = SCH_SL + 1;       // slot-CSR entries per batch
 constexpr int SCH_NI = (SCH_SB + 255) / 256;
-constexpr int SCH_NH = (SCH_SB * 12 + 255) / 256;  // 16-B chunks per batch: 9 of Hpl + 3 of U per block
+constexpr int SCH_NC = (SCH_SB * 9 + 255) / 256;  // 16-B pieces per thread per batch
+static_assert(SCH_SB * 9 % 64 == 0, "a wave's LDS-DMA pieces must tile the batch image");
 }  // namespace
 
 __global__ void __launch_bounds__(256, 2)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
-                 const int* __restrict__ st_obs, const int* __restrict__ st_lm, const int* __restrict__ pairs,
-                 const int* __restrict__ pp, const double* __restrict__ Hpl, const double* __restrict__ Ufac,
-                 const int* __restrict__ s_hpp, const double* __restrict__ Hpp, double* __restrict__ S, int mode) {
-  __shared__ __attribute__((aligned(16))) double Gs[SCH_SB * SCH_GS];
-  __shared__ int so[SCH_SB], sl[SCH_SB];  // staging indices of the next batch to stage
-  __shared__ int sp[2][SCH_SB];           // pair lists, double-buffered by batch parity
+                 const int* __restrict__ st_obs, const int* __restrict__ pairs, const int* __restrict__ pp,
+                 const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,
+                 double* __restrict__ S, int mode) {
+  __shared__ __attribute__((aligned(16))) double Gs[2][SCH_SB * SCH_GB];
+  __shared__ int so[2][SCH_SB];  // staged observation per block
+  __shared__ int sp[2][SCH_SB];  // pair lists (posA | posB << 16), slot-sorted
   __shared__ int spp[2][SCH_PPB];
   const launch::SchurTask t = tasks[blockIdx.x];
   const int nb = t.b1 - t.b0;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6;
   const int ls = tid >> 2, q = tid & 3;
   double acc[18];  // 6 x 3: rows 0..5 of columns h3..h3+2
 #pragma unroll
   for (int k = 0; k < 18; ++k) acc[k] = 0.0;
-  const double2* H2 = reinterpret_cast<const double2*>(Hpl);
-  const double2* U2 = reinterpret_cast<const double2*>(Ufac);
   // records past the task's end read the next task's (or the trailing dummy) record and go unused
   auto rec = [&](int k) { return batches[t.b0 + min(k, nb)]; };
-  int ov[SCH_NI], lv[SCH_NI], pv[SCH_NI], ppv = 0;
+  int ov[SCH_NI], pv[SCH_NI], ppv = 0;
   auto idx_load = [&](const launch::SchurBatch B, int k) {
 #pragma unroll
     for (int u = 0; u < SCH_NI; ++u) {
       const int i = tid + 256 * u;
       ov[u] = ld0(st_obs, B.st0 + i, i < B.nst);
-      lv[u] = ld0(st_lm, B.st0 + i, i < B.nst);
       pv[u] = ld0(pairs, B.pr0 + i, i < B.npr);
     }
     ppv = ld0(pp, (t.b0 + k) * SCH_PPB + tid, tid < SCH_PPB) - B.pr0;
@@ -395,44 +402,21 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
     for (int u = 0; u < SCH_NI; ++u) {
       const int i = tid + 256 * u;
-      if (i < SCH_SB) { so[i] = ov[u]; sl[i] = lv[u]; sp[buf][i] = pv[u]; }
+      if (i < SCH_SB) { so[buf][i] = ov[u]; sp[buf][i] = pv[u]; }
     }
     if (tid < SCH_PPB) spp[buf][tid] = ppv;
   };
-  double2 hv[SCH_NH];
-  auto hpl_load = [&](const launch::SchurBatch B) {  // indices of B sit in so/sl
-    const int n12 = B.nst * 12;
+  auto stage = [&](const launch::SchurBatch B, int buf) {  // so[buf] holds B's observations
+    const int n9 = B.nst * 9;
 #pragma unroll
-    for (int u = 0; u < SCH_NH; ++u) {
-      const int idx = tid + 256 * u;
-      const bool ok = idx < n12;
-      const int item = ok ? idx / 12 : 0, ch = ok ? idx - item * 12 : 0;
-      const bool isH = ch < 9;
-      const int gi = isH ? so[item] * 9 + ch : sl[item] * 3 + (ch - 9);
-      const double2 vh = H2[isH && ok ? gi : 0], vu = U2[!isH && ok ? gi : 0];  // two plain loads, no
-      hv[u] = ok ? (isH ? vh : vu) : double2{0.0, 0.0};                        // pointer select
-    }
-  };
-  auto hpl_store = [&](const launch::SchurBatch B) {
-    const int n12 = B.nst * 12;
-#pragma unroll
-    for (int u = 0; u < SCH_NH; ++u) {
-      const int idx = tid + 256 * u;
-      if (idx < n12) {
-        const int item = idx / 12, ch = idx - item * 12;
-        *reinterpret_cast<double2*>(Gs + item * SCH_GS + 2 * ch) = hv[u];
+    for (int u = 0; u < SCH_NC; ++u) {
+      const int i = tid + 256 * u;
+      if (i < n9) {
+        const int item = i / 9, ch = i - item * 9;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(G + (size_t)so[buf][item] * SCH_GB + 2 * ch),
+            (__attribute__((address_space(3))) void*)(&Gs[buf][(256 * u + 64 * w) * 2]), 16, 0, 0);
       }
-    }
-  };
-  auto transform = [&](const launch::SchurBatch B) {  // G = Hpl U^-T in place, one thread per (block, row)
-    for (int idx = tid; idx < B.nst * 6; idx += 256) {
-      const int item = idx / 6, r = idx - item * 6;
-      double* g = Gs + item * SCH_GS;
-      const double r0 = g[18], r1 = g[19], r2 = g[20], u10 = g[21], u20 = g[22], u21 = g[23];
-      const double g0 = g[r] * r0;
-      const double g1 = (g[6 + r] - u10 * g0) * r1;
-      const double g2 = (g[12 + r] - u20 * g0 - u21 * g1) * r2;
-      g[r] = g0; g[6 + r] = g1; g[12 + r] = g2;
     }
   };
   // thread q of a slot: columns 3h..3h+2 of the block (h = q & 1) over the pairs of parity q >> 1
@@ -442,8 +426,8 @@ __global__ void __launch_bounds__(256, 2)
     const int p1 = spp[buf][ls + 1];
     for (int p = spp[buf][ls] + par; p < p1; p += 2) {
       const int pr = sp[buf][p];
-      const double* ga = Gs + (pr & 0xffff) * SCH_GS;
-      const double* gb = Gs + (pr >> 16) * SCH_GS + h3;
+      const double* ga = &Gs[buf][(pr & 0xffff) * SCH_GB];
+      const double* gb = &Gs[buf][(pr >> 16) * SCH_GB + h3];
 #pragma unroll
       for (int kk = 0; kk < 3; ++kk) {  // one column of G_a and three entries of G_b at a time
         double A[6], Bm[3];
@@ -462,37 +446,30 @@ __global__ void __launch_bounds__(256, 2)
     }
   };
 
-  // Invariant at the top of iteration k: Gs holds G of batch k, so/sl the indices of batch k+1,
-  // sp[k&1] and sp[(k+1)&1] the pair lists of k and k+1.
-  launch::SchurBatch B0 = rec(0), B1 = rec(1), B2 = rec(2);
+  // Invariant at the top of iteration k: Gs[k&1] holds batch k (landed), so/sp/spp[k&1] its indices
+  // and pair list, so/sp/spp[(k+1)&1] those of batch k+1; B1, B2 = records k+1, k+2 (already landed:
+  // every record is loaded one iteration ahead, before a barrier that drains it).
+  launch::SchurBatch B1 = rec(1), B2 = rec(2);
   if (nb > 0) {
-    idx_load(B0, 0);
+    idx_load(rec(0), 0);
     idx_store(0);
-    __syncthreads();
-    hpl_load(B0);
     if (nb > 1) idx_load(B1, 1);
-    __syncthreads();  // every lane has read so/sl of batch 0
-    hpl_store(B0);
+    __syncthreads();  // so[0] visible
+    if (!(mode & 2)) stage(rec(0), 0);
     if (nb > 1) idx_store(1);
-    __syncthreads();
-    transform(B0);
-    __syncthreads();
+    __syncthreads();  // batch 0 landed (the barrier drains the DMA), so[1] visible
   }
   for (int k = 0; k < nb; ++k) {
     const int cur = k & 1;
-    if (k + 1 < nb && !(mode & 2)) hpl_load(B1);
+    if (k + 1 < nb && !(mode & 2)) stage(B1, cur ^ 1);
     if (k + 2 < nb) idx_load(B2, k + 2);
     const launch::SchurBatch B3 = rec(k + 3);
     if (!(mode & 1)) compute(cur);
-    __syncthreads();  // Gs, so/sl and the pair list of batch k are free
-    if (k + 1 < nb) {
-      hpl_store(B1);
-      if (k + 2 < nb) idx_store(cur);
-      __syncthreads();
-      if (!(mode & 4)) transform(B1);
+    __syncthreads();  // batch k+1 landed; Gs, so, sp, spp [cur] free
+    if (k + 2 < nb) {
+      idx_store(cur);
       __syncthreads();
     }
-    B0 = B1;
     B1 = B2;
     B2 = B3;
   }
@@ -802,19 +779,17 @@ void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const 
 }
 void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0, const double* Hpl,
                 const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp, const double* Hpp,
-                const double* b, const double* lam, double* S, double* bschur, hipStream_t s) {
+                const double* b, const double* lam, double* S, double* bschur, double* G, hipStream_t s) {
   if (nrows <= 0) return;
   hipLaunchKernelGGL(k_schur_diag, grid_for(nrows, 4), 256, 0, s, nrows, rptr, robs, obs_lm, lm0, Hpl, Ufac, cl_all,
-                     sdiag, s_hpp, Hpp, b, lam, S, bschur);
+                     sdiag, s_hpp, Hpp, b, lam, S, bschur, G);
   KERNEL_CHECK();
 }
-void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs, const int* st_lm,
-                const int* pairs, const int* pp, const double* Hpl, const double* Ufac, const int* s_hpp,
-                const double* Hpp, double* S, hipStream_t s) {
+void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs, const int* pairs,
+                const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S, hipStream_t s) {
   if (ntasks <= 0) return;
   static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;  // dev A/B only
-  hipLaunchKernelGGL(k_schur_rows, ntasks, 256, 0, s, tasks, batches, st_obs, st_lm, pairs, pp, Hpl, Ufac, s_hpp, Hpp,
-                     S, mode);
+  hipLaunchKernelGGL(k_schur_rows, ntasks, 256, 0, s, tasks, batches, st_obs, pairs, pp, G, s_hpp, Hpp, S, mode);
   KERNEL_CHECK();
 }
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,

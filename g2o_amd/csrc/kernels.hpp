@@ -32,10 +32,10 @@ void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const 
 // diagonal blocks + bschur: one wave per camera row over its observations (CSR rptr/robs)
 void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0, const double* Hpl,
                 const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp, const double* Hpp,
-                const double* b, const double* lam, double* S, double* bschur, hipStream_t s);
+                const double* b, const double* lam, double* S, double* bschur, double* G, hipStream_t s);
 // row-stationary off-diagonal Schur pass (k_schur_rows): task = (camera row, <= SCHUR_SL off-diagonal
 // slots), batch = <= SCHUR_SB staged observation blocks of the row's landmarks
-constexpr int SCHUR_SB = 288, SCHUR_SL = 64;
+constexpr int SCHUR_SB = 256, SCHUR_SL = 64;
 struct SchurTask {
   int row, noff;  // camera row, number of off-diagonal slots of this task
   int b0, b1;     // batches
@@ -43,12 +43,11 @@ struct SchurTask {
   int pad;
 };
 struct SchurBatch {
-  int st0, nst;  // staged blocks (st_obs / st_lm)
+  int st0, nst;  // staged blocks (st_obs)
   int pr0, npr;  // pairs (posA | posB << 16), slot CSR in pp[batch * (SCHUR_SL + 1) ...]
 };
-void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs, const int* st_lm,
-                const int* pairs, const int* pp, const double* Hpl, const double* Ufac, const int* s_hpp,
-                const double* Hpp, double* S, hipStream_t s);
+void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs, const int* pairs,
+                const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S, hipStream_t s);
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
              int size_poses, int lm0, double* x, hipStream_t s);
 void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s);

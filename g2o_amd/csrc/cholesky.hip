@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "device_util.hpp"
@@ -624,7 +625,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
 constexpr int SK = 32;          // K chunk
 constexpr int SPS = SK + 2;     // LDS row stride
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                              double* __restrict__ fronts, const double* __restrict__ lbuf) {
+                                              double* __restrict__ fronts, const double* __restrict__ lbuf, int mode) {
   __shared__ double sh[2 * TT * SPS];
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
@@ -663,9 +664,10 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
       Pb[r * SPS + k] = pb[u];
     }
     __syncthreads();
-    if (kc + SK < ns) fetch(kc + SK);
+    if (kc + SK < ns && !(mode & 2)) fetch(kc + SK);
 #pragma unroll
     for (int kk = 0; kk < SK / 4; ++kk) {
+      if (mode & 1) break;
       const int k = kk * 4 + lk;
       const double a0 = Pa[(wr + lr) * SPS + k], a1 = Pa[(wr + 16 + lr) * SPS + k];
       const double b0 = Pb[(wc + lr) * SPS + k], b1 = Pb[(wc + 16 + lr) * SPS + k];
@@ -800,7 +802,8 @@ void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, 
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
+  static const int mode = getenv("G2OHIP_SYRK_MODE") ? atoi(getenv("G2OHIP_SYRK_MODE")) : 0;  // dev A/B only
+  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf, mode);
   KERNEL_CHECK();
 }
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s) {

@@ -281,10 +281,21 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     std::vector<Task> tk;
     std::vector<launch::StepTask> stk;
     ops.clear();
-    const char* fe = getenv("G2OHIP_CHOL_FUSED");  // dev A/B: 0 = separate k_syrk pass per level
-    const bool fused_contrib = !fe || atoi(fe) != 0;
+    // contribution blocks: fused into the panel steps (each step's rank-32 update also reaches the
+    // contribution block) where the steps are latency-bound on the diagonal chain and the extra tiles
+    // run in its shadow; a separate K = ns k_syrk pass where a level's first step already has more
+    // tiles than one round of the chip (re-reading the contribution block every step costs more)
+    const char* fe = getenv("G2OHIP_CHOL_FUSED_MAX");  // dev A/B: fused-tile threshold per step
+    const long long fused_max = fe ? atoll(fe) : 2LL * 256;
     for (size_t l = 0; l < sym.levels.size(); ++l) {
       const auto& lv = sym.levels[l];
+      long long tiles0 = 0;  // fused tiles of the level's first step
+      for (int sn : lv) {
+        const Supernode& q = sym.sn[sn];
+        const int r0 = std::min(NB, q.ns), T = (q.ns + q.nr - r0 + TT - 1) / TT;
+        tiles0 += (long long)T * (T + 1) / 2;
+      }
+      const bool fused_contrib = tiles0 <= fused_max;
       Op ea{0, (int)tk.size(), 0};
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
@@ -892,7 +903,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         bo[v] = boff0 + v * dim;
       }
       const double avg = vr.nv ? (double)code.size() / vr.nv : 0;
-      vr.lanes = avg >= 128 ? 64 : (avg >= 16 ? 8 : 1);
+      vr.lanes = avg >= 128 ? 64 : (avg >= 16 ? 8 : (avg >= 6 ? 4 : 1));
       vr.ptr.upload(ptr, stream);
       vr.code.upload(code.empty() ? std::vector<int>{0} : code, stream);
       vr.boff.upload(bo, stream);

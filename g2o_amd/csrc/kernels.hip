@@ -9,7 +9,7 @@
 //   k_schur_prep  landmark pass of BlockSolver::solve (:342-360): Dinv = (Hll+lambda I)^-1,
 //                 and the split Hll+lambda I = U U^T, c = U^-1 b_l.
 //   k_schur_diag  Hschur(i,i) = Hpp(i,i) + lambda - sum_l G_il G_il^T, bschur = b - sum G c (:361-400),
-//                 G = Hpl U^-T in registers (and stored once per observation), one wave per camera.
+//                 G = Hpl U^-T in registers (and stored once per observation), one workgroup per camera.
 //   k_schur_rows  Hschur(i,j>i) = Hpp(i,j) - sum_l G_il G_jl^T: one workgroup per camera row (chunk),
 //                 the row's G blocks staged into LDS by LDS-DMA in batches; every output has one
 //                 owner and a fixed summation order (no atomics).
@@ -49,22 +49,52 @@ __global__ void __launch_bounds__(256) k_error(EdgeData d, int ne, double* __res
 }
 
 // ------------------------------------------------------------------------------ linearize
-// slot layouts (AoS per edge): packed upper col-major H (d(d+1)/2) followed by b (d)
+// slot layouts (AoS per edge): packed upper col-major H (d(d+1)/2) followed by b (d).
+// Stores go through a per-wave LDS image: the wave's 64 consecutive edges own one contiguous run of
+// each slot array (and, when their blocks are consecutive, of the off-diagonal blocks), written with
+// coalesced 16-byte stores instead of one 16-byte write request per lane and slot chunk.
+namespace {
+// order one wave's LDS writes before its reads of another lane's words (LDS is in order per wave;
+// this stops compiler motion across the point)
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+// copy n doubles LDS -> global by one wave (dst 8-byte aligned)
+__device__ __forceinline__ void wave_copy_out(double* __restrict__ dst, const double* src, int n, int lane) {
+  int s = 0;
+  if (reinterpret_cast<uintptr_t>(dst) & 15) {  // peel to 16-byte alignment
+    if (lane == 0 && n > 0) dst[0] = src[0];
+    s = 1;
+  }
+  const int n2 = (n - s) >> 1;
+  double2* d2 = reinterpret_cast<double2*>(dst + s);
+  for (int i = lane; i < n2; i += 64) d2[i] = double2{src[s + 2 * i], src[s + 2 * i + 1]};
+  if (lane == 0 && ((n - s) & 1)) dst[n - 1] = src[n - 1];
+}
+}  // namespace
+
 template <class F>
 __global__ void __launch_bounds__(256)
     k_linearize(EdgeData d, int ne, const int* __restrict__ h0, const int* __restrict__ h1, double* __restrict__ slot0,
                 double* __restrict__ slot1, const long long* __restrict__ off_dst, const unsigned char* __restrict__ off_tr,
                 double* __restrict__ off_base) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= ne) return;
   constexpr int D = F::D, DA = F::DA, DB = F::DB;
-  constexpr int SA = DA * (DA + 1) / 2 + DA, SB = DB * (DB + 1) / 2 + DB;
-  const bool nfA = h0[d.v0[e]] >= 0, nfB = h1[d.v1[e]] >= 0;
-  if (!nfA && !nfB) return;
-  double err[D], A[D * DA], B[D * DB];
-  F::linearize(d, e, err, A, B);
-  double Om[D * D];
-  load_info<D>(d.info + (size_t)e * F::INFO, Om);
+  constexpr int SA = DA * (DA + 1) / 2 + DA, SB = DB * (DB + 1) / 2 + DB, SH = DA * DB;
+  constexpr int SM = SA > SB ? (SA > SH ? SA : SH) : (SB > SH ? SB : SH);
+  __shared__ __attribute__((aligned(16))) double stage[4][64 * SM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int e = blockIdx.x * blockDim.x + tid;
+  const int ebase = e - lane, nw = min(64, ne - ebase);  // the wave's edges [ebase, ebase + nw)
+  if (nw <= 0) return;                                  // wave-uniform
+  double* sw = stage[tid >> 6];
+  const bool in = e < ne;
+  const bool nfA = in && h0[d.v0[e]] >= 0, nfB = in && h1[d.v1[e]] >= 0;
+  double err[D], A[D * DA], B[D * DB], Om[D * D];
+  if (nfA || nfB) {
+    F::linearize(d, e, err, A, B);
+    load_info<D>(d.info + (size_t)e * F::INFO, Om);
+  }
   double wr[D];
 #pragma unroll
   for (int r = 0; r < D; ++r) {
@@ -83,8 +113,9 @@ __global__ void __launch_bounds__(256)
       for (int r = 0; r < D; ++r) s += A[r * DA + i] * Om[r * D + c];
       AtO[i * D + c] = s;
     }
+  // side A slot (edges whose side A is fixed leave garbage in their slot: never read)
   if (nfA) {
-    double* o = slot0 + (size_t)e * SA;
+    double* o = sw + lane * SA;
     int k = 0;
 #pragma unroll
     for (int c = 0; c < DA; ++c)
@@ -102,30 +133,44 @@ __global__ void __launch_bounds__(256)
       for (int r = 0; r < D; ++r) s += A[r * DA + i] * wr[r];
       o[k++] = s;
     }
-    if (nfB && off_dst[e] >= 0) {
-      double* H = off_base + off_dst[e];
-      if (off_tr[e]) {  // DB x DA col-major: (j,i)
+  }
+  wave_sync();
+  wave_copy_out(slot0 + (size_t)ebase * SA, sw, nw * SA, lane);
+  wave_sync();
+  // off-diagonal block: staged when the wave's blocks are consecutive with one orientation
+  const long long od = (nfA && nfB) ? off_dst[e] : -1;
+  const bool tr = nfA && nfB && off_tr[e];
+  const long long od0 = __shfl(od, 0, 64);
+  const bool tr0 = __shfl((int)tr, 0, 64) != 0;
+  const bool run = __all(!in || (od >= 0 && od0 >= 0 && od == od0 + (long long)lane * SH && tr == tr0));
+  if (od >= 0) {
+    double* H = run ? sw + lane * SH : off_base + od;
+    if (tr) {  // DB x DA col-major: (j,i)
 #pragma unroll
-        for (int i = 0; i < DA; ++i)
+      for (int i = 0; i < DA; ++i)
 #pragma unroll
-          for (int j = 0; j < DB; ++j) {
-            double s = 0;
+        for (int j = 0; j < DB; ++j) {
+          double s = 0;
 #pragma unroll
-            for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
-            H[i * DB + j] = s;
-          }
-      } else {  // DA x DB col-major: (i,j)
+          for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
+          H[i * DB + j] = s;
+        }
+    } else {  // DA x DB col-major: (i,j)
 #pragma unroll
-        for (int j = 0; j < DB; ++j)
+      for (int j = 0; j < DB; ++j)
 #pragma unroll
-          for (int i = 0; i < DA; ++i) {
-            double s = 0;
+        for (int i = 0; i < DA; ++i) {
+          double s = 0;
 #pragma unroll
-            for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
-            H[j * DA + i] = s;
-          }
-      }
+          for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
+          H[j * DA + i] = s;
+        }
     }
+  }
+  if (run) {
+    wave_sync();
+    wave_copy_out(off_base + od0, sw, nw * SH, lane);
+    wave_sync();
   }
   if (nfB) {
     double BtO[DB * D];
@@ -138,7 +183,7 @@ __global__ void __launch_bounds__(256)
         for (int r = 0; r < D; ++r) s += B[r * DB + j] * Om[r * D + c];
         BtO[j * D + c] = s;
       }
-    double* o = slot1 + (size_t)e * SB;
+    double* o = sw + lane * SB;
     int k = 0;
 #pragma unroll
     for (int c = 0; c < DB; ++c)
@@ -157,6 +202,8 @@ __global__ void __launch_bounds__(256)
       o[k++] = s;
     }
   }
+  wave_sync();
+  wave_copy_out(slot1 + (size_t)ebase * SB, sw, nw * SB, lane);
 }
 
 // ------------------------------------------------------------------------------ vertex reduction
@@ -185,11 +232,29 @@ __global__ void __launch_bounds__(256)
       for (int k = 0; k < S; ++k) acc[k] += s[k];
     }
   }
-  if (LANES > 1) {
+  constexpr int WL = LANES > 64 ? 64 : LANES;  // butterfly width (one wave at most)
+  if (WL > 1) {
 #pragma unroll
-    for (int m = LANES / 2; m >= 1; m >>= 1)
+    for (int m = WL / 2; m >= 1; m >>= 1)
 #pragma unroll
-      for (int k = 0; k < S; ++k) acc[k] += __shfl_xor(acc[k], m, LANES);
+      for (int k = 0; k < S; ++k) acc[k] += __shfl_xor(acc[k], m, WL);
+  }
+  if constexpr (LANES > 64) {  // LANES == blockDim: the waves' sums combined in wave order
+    __shared__ double red[LANES / 64][S];
+    if ((lane & 63) == 0) {
+#pragma unroll
+      for (int k = 0; k < S; ++k) red[lane >> 6][k] = acc[k];
+    }
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        double t = red[0][k];
+#pragma unroll
+        for (int w = 1; w < LANES / 64; ++w) t += red[w][k];
+        acc[k] = t;
+      }
+    }
   }
   if (!active || lane != 0) return;
   double* H = Hdiag + (size_t)v * DIM * DIM;
@@ -278,8 +343,9 @@ __global__ void __launch_bounds__(256)
 
 // Diagonal blocks of the reduced system (block_solver.hpp:361-400, the j == i terms):
 //   S(i,i) = Hpp(i,i) + lambda I - sum_l G_il G_il^T,   bschur_i = b_i - sum_l G_il c_l,
-// one wave per camera row, lanes stride over the row's observations (landmark order), G formed in
-// registers from Hpl, U_l and c_l; fixed butterfly over the lanes (bitwise reproducible).
+// one workgroup per camera row, its 256 lanes striding over the row's observations (landmark
+// order), G formed in registers from Hpl and U_l (and stored, for k_schur_rows); a fixed butterfly
+// per wave and the four wave sums added in wave order (bitwise reproducible).
 __global__ void __launch_bounds__(256)
     k_schur_diag(int nrows, const int* __restrict__ rptr, const int* __restrict__ robs,
                  const int* __restrict__ obs_lm, int lm0, const double* __restrict__ Hpl,
@@ -287,67 +353,77 @@ __global__ void __launch_bounds__(256)
                  const int* __restrict__ s_hpp, const double* __restrict__ Hpp, const double* __restrict__ b,
                  const double* __restrict__ lam, double* __restrict__ S, double* __restrict__ bschur,
                  double* __restrict__ G) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= nrows) return;  // wave-uniform
+  __shared__ double red[4][27];
+  __shared__ __attribute__((aligned(16))) double gst[4][64 * 18];  // per-wave image of 64 G blocks
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   double acc[27];  // packed upper of G G^T (21, col-major) | G c (6)
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
   const int p1 = rptr[row + 1];
-  for (int p = rptr[row] + lane; p < p1; p += 64) {
-    const int a = robs[p], l = obs_lm[a];
-    const double2* h2 = reinterpret_cast<const double2*>(Hpl + (size_t)a * 18);
-    const double2* u2 = reinterpret_cast<const double2*>(Ufac + (size_t)l * 6);
-    double g[18], U[6], c[3];
+  for (int pb = rptr[row] + w * 64; pb < p1; pb += 256) {  // the wave's blocks [pb, pb + nw)
+    const int p = pb + lane, nw = min(64, p1 - pb);
+    if (p < p1) {
+      const int a = robs[p], l = obs_lm[a];
+      const double2* h2 = reinterpret_cast<const double2*>(Hpl + (size_t)a * 18);
+      const double2* u2 = reinterpret_cast<const double2*>(Ufac + (size_t)l * 6);
+      double g[18], U[6], c[3];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) { const double2 v = h2[k]; g[2 * k] = v.x; g[2 * k + 1] = v.y; }
+      for (int k = 0; k < 9; ++k) { const double2 v = h2[k]; g[2 * k] = v.x; g[2 * k + 1] = v.y; }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { const double2 v = u2[k]; U[2 * k] = v.x; U[2 * k + 1] = v.y; }
-    const double* cp = cl_all + (size_t)(lm0 + l) * 3;
-    c[0] = cp[0]; c[1] = cp[1]; c[2] = cp[2];
+      for (int k = 0; k < 3; ++k) { const double2 v = u2[k]; U[2 * k] = v.x; U[2 * k + 1] = v.y; }
+      const double* cp = cl_all + (size_t)(lm0 + l) * 3;
+      c[0] = cp[0]; c[1] = cp[1]; c[2] = cp[2];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {  // row r of G = Hpl U^-T
-      const double g0 = g[r] * U[0];
-      const double g1 = (g[6 + r] - U[3] * g0) * U[1];
-      g[12 + r] = (g[12 + r] - U[4] * g0 - U[5] * g1) * U[2];
-      g[r] = g0;
-      g[6 + r] = g1;
+      for (int r = 0; r < 6; ++r) {  // row r of G = Hpl U^-T
+        const double g0 = g[r] * U[0];
+        const double g1 = (g[6 + r] - U[3] * g0) * U[1];
+        g[12 + r] = (g[12 + r] - U[4] * g0 - U[5] * g1) * U[2];
+        g[r] = g0;
+        g[6 + r] = g1;
+      }
+      {  // every observation lies in exactly one camera row: G is written once, in camera-row order,
+         // for k_schur_rows; the wave's blocks leave as one contiguous coalesced run (below)
+        double2* go = reinterpret_cast<double2*>(gst[w] + lane * 18);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) go[k] = double2{g[2 * k], g[2 * k + 1]};
+      }
+      int k = 0;
+#pragma unroll
+      for (int cc = 0; cc < 6; ++cc)
+#pragma unroll
+        for (int r = 0; r <= cc; ++r) acc[k++] += g[r] * g[cc] + g[6 + r] * g[6 + cc] + g[12 + r] * g[12 + cc];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) acc[21 + r] += g[r] * c[0] + g[6 + r] * c[1] + g[12 + r] * c[2];
     }
-    {  // every observation lies in exactly one camera row: G is written once, in camera-row order
-       // (consecutive lanes, consecutive blocks), for k_schur_rows
-      double2* go = reinterpret_cast<double2*>(G + (size_t)p * 18);
-#pragma unroll
-      for (int k = 0; k < 9; ++k) go[k] = double2{g[2 * k], g[2 * k + 1]};
-    }
-    int k = 0;
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc)
-#pragma unroll
-      for (int r = 0; r <= cc; ++r) acc[k++] += g[r] * g[cc] + g[6 + r] * g[6 + cc] + g[12 + r] * g[12 + cc];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) acc[21 + r] += g[r] * c[0] + g[6 + r] * c[1] + g[12 + r] * c[2];
+    wave_sync();  // converged: the whole wave copies the image out
+    wave_copy_out(G + (size_t)pb * 18, gst[w], nw * 18, lane);
+    wave_sync();
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1)
 #pragma unroll
     for (int k = 0; k < 27; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 27; ++k) red[w][k] = acc[k];
+  }
+  __syncthreads();
+  if (tid >= 27) return;
+  const double v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  if (tid >= 21) {
+    const int r = tid - 21;
+    bschur[(size_t)row * 6 + r] = b[(size_t)row * 6 + r] - v;
+    return;
+  }
   const int sidx = sdiag[row], hp = s_hpp[sidx];
-  const double lambda = *lam;
   const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * 36;
   double* So = S + (size_t)sidx * 36;
-  int k = 0;
-#pragma unroll
-  for (int cc = 0; cc < 6; ++cc)
-#pragma unroll
-    for (int r = 0; r <= cc; ++r, ++k) {  // lane k writes (r, cc) and its mirror
-      if (lane != k) continue;
-      const double h0 = hp >= 0 ? Hh[cc * 6 + r] : 0.0;
-      const double v = (r == cc ? h0 + lambda : h0) - acc[k];
-      So[cc * 6 + r] = v;
-      So[r * 6 + cc] = v;
-    }
-#pragma unroll
-  for (int r = 0; r < 6; ++r)
-    if (lane == 32 + r) bschur[(size_t)row * 6 + r] = b[(size_t)row * 6 + r] - acc[21 + r];
+  int cc = 0, r = tid;  // packed upper index tid -> (r, cc), r <= cc
+  while (r > cc) { r -= cc + 1; ++cc; }
+  const double h0 = hp >= 0 ? Hh[cc * 6 + r] : 0.0;
+  const double o = (r == cc ? h0 + *lam : h0) - v;
+  So[cc * 6 + r] = o;
+  So[r * 6 + cc] = o;
 }
 
 // Off-diagonal blocks, row-stationary (block_solver.hpp:361-391, j > i): one workgroup per (camera
@@ -379,7 +455,11 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ int so[2][SCH_SB];  // staged observation per block
   __shared__ int sp[2][SCH_SB];  // pair lists (posA | posB << 16), slot-sorted
   __shared__ int spp[2][SCH_PPB];
-  const launch::SchurTask t = tasks[blockIdx.x];
+  // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin; give each XCD a contiguous
+  // range of camera rows, so rows that share landmarks run side by side behind the same L2
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int task = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
+  const launch::SchurTask t = tasks[task];
   const int nb = t.b1 - t.b0;
   const int tid = threadIdx.x, w = tid >> 6;
   const int ls = tid >> 2, q = tid & 3;
@@ -492,29 +572,42 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
-// back-substitution: x_l = Dinv_l (b_l - sum_a Hpl_a^T x_pose(a))
-template <int PD>
+// back-substitution: x_l = Dinv_l (b_l - sum_a Hpl_a^T x_pose(a)); LANES lanes per landmark stride over
+// its observations, combined by a fixed butterfly (bitwise reproducible)
+template <int PD, int LANES>
 __global__ void __launch_bounds__(256)
     k_backsub(int nl, const int* __restrict__ lm_ptr, const int* __restrict__ blk_pose, const double* __restrict__ Hpl,
               const double* __restrict__ Dinv, const double* __restrict__ b, int size_poses, int lm0,
               double* __restrict__ x) {
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;  // local landmark; global index lm0 + l
-  if (l >= nl) return;
-  const double* bl = b + size_poses + (size_t)(lm0 + l) * 3;
-  double c0 = bl[0], c1 = bl[1], c2 = bl[2];
-  for (int a = lm_ptr[l]; a < lm_ptr[l + 1]; ++a) {
-    const double* Bm = Hpl + (size_t)a * PD * 3;
-    const double* xp = x + (size_t)blk_pose[a] * PD;
-    double s0 = 0, s1 = 0, s2 = 0;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = gid / LANES, q = gid % LANES;  // local landmark; global index lm0 + l
+  const bool active = l < nl;
+  double c0 = 0, c1 = 0, c2 = 0;
+  if (active) {
+    const int a1 = lm_ptr[l + 1];
+    for (int a = lm_ptr[l] + q; a < a1; a += LANES) {
+      const double* Bm = Hpl + (size_t)a * PD * 3;
+      const double* xp = x + (size_t)blk_pose[a] * PD;
+      double s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
-    for (int r = 0; r < PD; ++r) {
-      const double xr = -xp[r];
-      s0 += Bm[r] * xr;
-      s1 += Bm[PD + r] * xr;
-      s2 += Bm[2 * PD + r] * xr;
+      for (int r = 0; r < PD; ++r) {
+        const double xr = -xp[r];
+        s0 += Bm[r] * xr;
+        s1 += Bm[PD + r] * xr;
+        s2 += Bm[2 * PD + r] * xr;
+      }
+      c0 += s0; c1 += s1; c2 += s2;
     }
-    c0 += s0; c1 += s1; c2 += s2;
   }
+#pragma unroll
+  for (int m = LANES / 2; m >= 1; m >>= 1) {
+    c0 += __shfl_xor(c0, m, LANES);
+    c1 += __shfl_xor(c1, m, LANES);
+    c2 += __shfl_xor(c2, m, LANES);
+  }
+  if (!active || q != 0) return;
+  const double* bl = b + size_poses + (size_t)(lm0 + l) * 3;
+  c0 += bl[0]; c1 += bl[1]; c2 += bl[2];
   const double* D = Dinv + (size_t)l * 9;
   double* xl = x + size_poses + (size_t)(lm0 + l) * 3;
   xl[0] = D[0] * c0 + D[3] * c1 + D[6] * c2;
@@ -750,8 +843,10 @@ static void vreduce_dim(int nv, int lanes, const int* ptr, const int* code, cons
   const unsigned g = grid_for((size_t)nv * lanes, 256);
   switch (lanes) {
     case 1: hipLaunchKernelGGL((k_vertex_reduce<DIM, 1>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+    case 4: hipLaunchKernelGGL((k_vertex_reduce<DIM, 4>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
     case 8: hipLaunchKernelGGL((k_vertex_reduce<DIM, 8>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
-    default: hipLaunchKernelGGL((k_vertex_reduce<DIM, 64>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+    case 64: hipLaunchKernelGGL((k_vertex_reduce<DIM, 64>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+    default: hipLaunchKernelGGL((k_vertex_reduce<DIM, 256>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
   }
   KERNEL_CHECK();
 }
@@ -781,7 +876,7 @@ void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, 
                 const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp, const double* Hpp,
                 const double* b, const double* lam, double* S, double* bschur, double* G, hipStream_t s) {
   if (nrows <= 0) return;
-  hipLaunchKernelGGL(k_schur_diag, grid_for(nrows, 4), 256, 0, s, nrows, rptr, robs, obs_lm, lm0, Hpl, Ufac, cl_all,
+  hipLaunchKernelGGL(k_schur_diag, nrows, 256, 0, s, nrows, rptr, robs, obs_lm, lm0, Hpl, Ufac, cl_all,
                      sdiag, s_hpp, Hpp, b, lam, S, bschur, G);
   KERNEL_CHECK();
 }
@@ -795,7 +890,8 @@ void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, c
 void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
              int size_poses, int lm0, double* x, hipStream_t s) {
   if (nl <= 0) return;
-  hipLaunchKernelGGL(k_backsub<6>, grid_for(nl, 256), 256, 0, s, nl, lm_ptr, blk_pose, Hpl, Dinv, b, size_poses, lm0, x);
+  hipLaunchKernelGGL((k_backsub<6, 4>), grid_for((size_t)nl * 4, 256), 256, 0, s, nl, lm_ptr, blk_pose, Hpl, Dinv, b,
+                     size_poses, lm0, x);
   KERNEL_CHECK();
 }
 

@@ -29,7 +29,7 @@ void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const do
                      const long long* dst, hipStream_t s);
 void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
                 double* Ufac, double* cl_all, int* fail, hipStream_t s);
-// diagonal blocks + bschur: one wave per camera row over its observations (CSR rptr/robs)
+// diagonal blocks + bschur (and G per observation): one workgroup per camera row over its observations (CSR rptr/robs)
 void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0, const double* Hpl,
                 const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp, const double* Hpp,
                 const double* b, const double* lam, double* S, double* bschur, double* G, hipStream_t s);

@@ -174,55 +174,91 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 // Factor the 32x32 diagonal block held row-wise by lanes 0..31 (row[c] = A(lane, c), c <= lane;
 // rows >= kb padded with the identity). On return row[c] = L(lane, c).
 // Returns false if a pivot was not positive (cs_chol's `d <= 0` test).
-// Latency-shaped for one wave, right-looking with a two-column look-ahead: once column j is scaled,
-// columns j+1 and j+2 are updated at once with l_{j+1,j}, l_{j+2,j} broadcast by v_readlane (no LDS
-// on the chain); the rest of column j's rank-1 update goes through LDS and is applied one column
-// later, touching only columns >= j+3, so its reads never stall a pivot. The sequential chain per
-// column is readlane -> rsq + 1 Newton step -> mul -> readlane -> FMA. The forward solve L y = b
-// rides along: y holds b(lane) on entry and y(lane) on return. Entries above a lane's diagonal may
-// collect garbage; they are never read.
-__device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, double* col) {
-  bool ok = true;
+// Latency-shaped for one wave, right-looking. The pivot chain runs on wave-uniform values only:
+// d_{j+1} = A(j+1,j+1) - (A(j+1,j) r_j)^2, both entries read by v_readlane one column early, so the
+// sequential chain per column is rsq -> Newton step -> r_j -> l_{j+1,j} -> d_{j+1}. Off the chain:
+// the scaled column l_j = row[j] r_j, its two-column look-ahead (l_{j+1,j}, l_{j+2,j} are chain
+// values, no broadcast), the rest of column j-1's rank-1 update (through LDS, one column late,
+// columns >= j+2), cut into chunks that sched_barriers pin between the chain's dependent steps.
+// The forward solve L y = b rides along: y holds b(lane) on entry and y(lane) on return. Entries
+// above a lane's diagonal may collect garbage; they are never read. One template instance per
+// column keeps every register index a compile-time constant.
+#define CHOL_SB() __builtin_amdgcn_sched_barrier(0)
+constexpr int C32_NCH = 3;  // chunks of the deferred update per column
+struct C32State {
+  double dn, a1, b1, c2, lp;  // next pivot; A(j+1,j+1), A(j+1,j), A(j+2,j); column j-1's own entry
+  double2 cc[NB / 2];         // column j-1 (entries >= j+2) from LDS
+  bool ok;
+};
+template <int J, int K>
+__device__ __forceinline__ void c32_fill(double (&row)[NB], const C32State& st) {
+  constexpr int c0 = (J + 2) & ~1;
+  constexpr int nf = J >= 1 ? (NB - c0) / 2 : 0;
+  constexpr int qa = nf * K / C32_NCH, qb = nf * (K + 1) / C32_NCH;
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    // deferred part of column j-1 (columns >= j+2), fetched from LDS first (written one iteration ago)
-    double2 cc[NB / 2];
-    const int c0 = (j + 2) & ~1;
-    if (j >= 1) {
-      const double* cb = col + ((j - 1) & 1) * 2 * NB;
-#pragma unroll
-      for (int c = c0; c < NB; c += 2) cc[c >> 1] = *reinterpret_cast<const double2*>(cb + c);
-    }
-    const double djj = rlane(row[j], j);
-    ok &= djj > 0.0;
-    const double d = djj > 0.0 ? djj : 1.0;
-    double r = __builtin_amdgcn_rsq(d);  // ~5e-8 relative; one Newton step -> ~4e-15
-    r = r * (1.5 - 0.5 * d * r * r);
-    // column j of L (or of L^-1 e_c in lanes >= 32); lane j's own row[j] is the pivot d (up to the
-    // non-positive case, which fails the factorisation anyway), so no lane select is needed
-    const double lj = row[j] * r;
-    row[j] = lj;
-    if (j + 1 < NB) {  // look-ahead columns first: they carry the next two pivots
-      row[j + 1] -= lj * rlane(lj, j + 1);
-      if (j + 2 < NB) row[j + 2] -= lj * rlane(lj, j + 2);
-      col[(j & 1) * 2 * NB + lane] = lj;  // every lane writes (lanes >= 32 into the unused half)
-    }
-    const double yj = rlane(y, j) * r;
-    y = lane == j ? yj : (lane > j ? y - lj * yj : y);
-    if (j >= 1) {  // column j-1 onto columns j+2.. (j and j+1 got it at once)
-      const double lp = row[j - 1];
-#pragma unroll
-      for (int c = c0; c < NB; c += 2) {
-        if (c > j + 1) row[c] -= lp * cc[c >> 1].x;
-        row[c + 1] -= lp * cc[c >> 1].y;
-      }
-    }
-    // materialise this iteration's updates: left alone, the scheduler defers the FMAs until each
-    // row[c] is next needed and keeps every fetched column live (register blow-up and spills)
-#pragma unroll
-    for (int c = j + 1; c < NB; ++c) asm volatile("" : "+v"(row[c]));
+  for (int q = qa; q < qb; ++q) {
+    const int c = c0 + 2 * q;
+    if (c > J + 1) row[c] -= st.lp * st.cc[c >> 1].x;
+    row[c + 1] -= st.lp * st.cc[c >> 1].y;
   }
-  return ok;
+}
+template <int J>
+__device__ __forceinline__ void c32_step(double (&row)[NB], double& y, int lane, double* col, C32State& st) {
+  if constexpr (J < NB) {
+    const double d = st.dn;
+    st.ok &= d > 0.0;
+    const double r0 = __builtin_amdgcn_rsq(d);  // ~5e-8 relative; one Newton step -> ~4e-15
+    const double hd = 0.5 * d;
+    CHOL_SB();
+    c32_fill<J, 0>(row, st);
+    CHOL_SB();
+    const double t1 = hd * r0;
+    CHOL_SB();
+    c32_fill<J, 1>(row, st);
+    CHOL_SB();
+    const double t2 = __builtin_fma(-r0, t1, 1.5);
+    CHOL_SB();
+    c32_fill<J, 2>(row, st);
+    CHOL_SB();
+    const double r = r0 * t2;
+    const double l1 = st.b1 * r, l2 = st.c2 * r;  // l_{j+1,j}, l_{j+2,j}
+    if constexpr (J + 1 < NB) st.dn = __builtin_fma(-l1, l1, st.a1);
+    CHOL_SB();
+    // column j of L (or of L^-1 e_c in lanes >= 32); lane j's own row[j] is the pivot d
+    const double lj = row[J] * r;
+    row[J] = lj;
+    if constexpr (J + 1 < NB) {
+      row[J + 1] -= lj * l1;
+      col[(J & 1) * 2 * NB + lane] = lj;  // every lane writes (lanes >= 32 into the unused half)
+    }
+    if constexpr (J + 2 < NB) row[J + 2] -= lj * l2;
+    const double yj = rlane(y, J) * r;
+    y = lane == J ? yj : (lane > J ? y - lj * yj : y);
+    CHOL_SB();
+    if constexpr (J + 1 < NB) {  // column j for the next column's deferred update (entries >= j+3)
+      constexpr int n0 = (J + 3) & ~1;
+      const double* cb = col + (J & 1) * 2 * NB;
+#pragma unroll
+      for (int c = n0; c < NB; c += 2) st.cc[c >> 1] = *reinterpret_cast<const double2*>(cb + c);
+      st.lp = lj;
+    }
+    // pivot inputs of column j+2's step (rows j+1, j+2 hold every update of columns <= j now)
+    if constexpr (J + 2 < NB) { st.a1 = rlane(row[J + 2], J + 2); st.b1 = rlane(row[J + 1], J + 2); }
+    if constexpr (J + 3 < NB) st.c2 = rlane(row[J + 1], J + 3);
+    CHOL_SB();
+    c32_step<J + 1>(row, y, lane, col, st);
+  }
+}
+__device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, double* col) {
+  C32State st;
+  st.ok = true;
+  st.lp = 0.0;
+  st.dn = rlane(row[0], 0);
+  st.a1 = rlane(row[1], 1);
+  st.b1 = rlane(row[0], 1);
+  st.c2 = rlane(row[0], 2);
+  c32_step<0>(row, y, lane, col, st);
+  return st.ok;
 }
 
 // Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid) and

@@ -216,7 +216,9 @@ __global__ void __launch_bounds__(256)
                     double* __restrict__ Hdiag /* [nv][DIM*DIM] */, double* __restrict__ b /* offset per vertex */,
                     const int* __restrict__ boff) {
   constexpr int SP = DIM * (DIM + 1) / 2, S = SP + DIM;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  // vertices with >= 64 lanes: XCD-contiguous vertex ranges (a landmark's edges, neighbours in the
+  // slot arrays, belong to nearby cameras: mostly one L2)
+  const int gid = (LANES >= 64 ? xcd_item(blockIdx.x, gridDim.x) : (int)blockIdx.x) * blockDim.x + threadIdx.x;
   const int v = gid / LANES, lane = gid % LANES;
   const bool active = v < nv;
   double acc[S];
@@ -355,7 +357,9 @@ __global__ void __launch_bounds__(256)
                  double* __restrict__ G) {
   __shared__ double red[4][27];
   __shared__ __attribute__((aligned(16))) double gst[4][64 * 18];  // per-wave image of 64 G blocks
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // XCD-contiguous camera rows: the observations of one landmark (neighbours in Hpl) are read by
+  // rows of nearby cameras, i.e. mostly behind one L2
+  const int row = xcd_item(blockIdx.x, nrows), tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   double acc[27];  // packed upper of G G^T (21, col-major) | G c (6)
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
@@ -455,11 +459,7 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ int so[2][SCH_SB];  // staged observation per block
   __shared__ int sp[2][SCH_SB];  // pair lists (posA | posB << 16), slot-sorted
   __shared__ int spp[2][SCH_PPB];
-  // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin; give each XCD a contiguous
-  // range of camera rows, so rows that share landmarks run side by side behind the same L2
-  const int nwg = gridDim.x, xcd = blockIdx.x & 7, qq = nwg >> 3, rr = nwg & 7;
-  const int task = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
-  const launch::SchurTask t = tasks[task];
+  const launch::SchurTask t = tasks[xcd_item(blockIdx.x, gridDim.x)];  // XCD-contiguous rows
   const int nb = t.b1 - t.b0;
   const int tid = threadIdx.x, w = tid >> 6;
   const int ls = tid >> 2, q = tid & 3;

@@ -12,9 +12,10 @@
 //   k_permute + k_vec_init   rhs -> P rhs -> front vectors (own rows)
 //   k_chol_scatter           input blocks -> fronts (+ lambda on the diagonal)
 //   per level l (all fronts of a level are independent):
-//     k_extend_add     children's update matrices AND update vectors -> parent fronts;
-//                      one workgroup per (front, 4-column slab), children in fixed order
-//     k_potrf0         first 32x32 diagonal block of every front + its forward solve
+//     k_extend_add     children's update matrices AND update vectors -> parent fronts, one
+//                      workgroup per (front, 4-column slab), children in fixed order; beside them
+//                      one workgroup per front assembles, factors and forward-solves its first
+//                      32x32 diagonal block (the first panel step's input)
 //     k_step (x panels) one launch per 32-column panel step: every workgroup owns one 64x64
 //                      tile (I, J) of the panel region, solves the panel rows of I and J
 //                      against L_kk (TRSM), updates the tile on v_mfma_f64_16x16x4f64, and the
@@ -107,57 +108,6 @@ __global__ void __launch_bounds__(256) k_vec_init(const FrontDesc* __restrict__ 
   const int m = me.ns + me.nr;
   double* v = vecs + me.vec_off;
   for (int i = threadIdx.x; i < m; i += 256) v[i] = ld0(rhs_p, me.c0 + i, i < me.ns);
-}
-
-// ---------------------------------------------------------------------------- extend-add
-__global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                                    const int* __restrict__ children, const int* __restrict__ relmap,
-                                                    double* __restrict__ fronts, double* __restrict__ vecs) {
-  const Task t = tasks[blockIdx.x];
-  const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr;
-  double* F = fronts + me.front_off;
-  double* v = vecs + me.vec_off;
-  const int a = t.a, b = t.b;
-  for (int k = me.child_begin; k < me.child_end; ++k) {
-    const FrontDesc cd = fd[children[k]];
-    const int mc = cd.ns + cd.nr, nrc = cd.nr;
-    const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;  // U(i,j) = U[j*mc + i]
-    const double* u = vecs + cd.vec_off + cd.ns;
-    const int* rel = relmap + cd.rows_off;
-    // child columns whose parent column lies in [a, b) (rel is increasing)
-    int lo = 0, hi = nrc;
-    while (lo < hi) { const int mid = (lo + hi) >> 1; if (rel[mid] < a) lo = mid + 1; else hi = mid; }
-    const int j0 = lo;
-    hi = nrc;
-    while (lo < hi) { const int mid = (lo + hi) >> 1; if (rel[mid] < b) lo = mid + 1; else hi = mid; }
-    const int j1 = lo;
-    for (int j = j0 + (int)threadIdx.x; j < j1; j += 256) v[rel[j]] += u[j];
-    // lower triangle of the slab: one wave per column, lanes run down the rows (coalesced U
-    // reads, mostly-contiguous F writes), 4 independent loads in flight per lane
-    const int j = j0 + (int)(threadIdx.x >> 6);
-    if (j < j1) {
-      const double* Uj = U + (size_t)j * mc;
-      double* Fj = F + (size_t)rel[j] * m;
-      for (int i0 = j + (int)(threadIdx.x & 63); i0 < nrc; i0 += 256) {
-        double val[4];
-        int ri[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int i = i0 + q * 64;
-          ri[q] = -1;
-          val[q] = 0.0;
-          const bool ok = i < nrc;
-          val[q] = ld0(Uj, i, ok);
-          ri[q] = ok ? ld0(rel, i, ok) : -1;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (ri[q] >= 0) Fj[ri[q]] += val[q];
-      }
-    }
-    __syncthreads();
-  }
 }
 
 // ---------------------------------------------------------------------------- wave helpers
@@ -307,37 +257,109 @@ __device__ __forceinline__ void publish_block(const double* D, const double* vy,
   if (tid < kb) ysol[r0 + tid] = vy[tid];
 }
 
-// ---------------------------------------------------------------------------- first diagonal block
-// One workgroup per front of the level: A(0:kb, 0:kb) -> L, y(0:kb).
-__global__ void __launch_bounds__(256) k_potrf0(const int* __restrict__ level_list, const FrontDesc* __restrict__ fd,
-                                                const double* __restrict__ fronts, double* __restrict__ lbuf,
-                                                const double* __restrict__ vecs, double* __restrict__ ysol,
-                                                double* __restrict__ linv, double* __restrict__ xinv,
-                                                int* __restrict__ fail) {
-  __shared__ double D[NB * DS];
-  __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
-  __shared__ double vy[NB];
-  PH_BEGIN(1)
-  const FrontDesc me = fd[level_list[blockIdx.x]];
-  const int m = me.ns + me.nr, kb = min(NB, me.ns);
-  const double* F = fronts + me.front_off;
+// ---------------------------------------------------------------------------- extend-add
+// One launch per level (from the second level on) with two kinds of workgroup:
+//  * block-0 tasks (t.c == 1, dispatched first, one per front of the level): the front's first
+//    kb x kb diagonal block and front-vector head are assembled here (scattered values + the
+//    children's update-matrix entries that map into it, children in fixed order), factored and
+//    forward-solved, and L_00, y_0, L_00^-1 published: the first panel step needs no launch of
+//    its own;
+//  * slab tasks (t.c == 0): children's update matrices AND update vectors -> the parent front,
+//    one workgroup per (front, 4-column slab), children in fixed order, every entry outside the
+//    first diagonal block.
+// Every entry is written by exactly one workgroup, in the same child order: bitwise reproducible.
+__global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                                    const int* __restrict__ children, const int* __restrict__ relmap,
+                                                    double* __restrict__ fronts, double* __restrict__ vecs,
+                                                    double* __restrict__ lbuf, double* __restrict__ ysol,
+                                                    double* __restrict__ linv, double* __restrict__ xinv,
+                                                    int* __restrict__ fail) {
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int m = me.ns + me.nr, kb0 = min(NB, me.ns);
+  double* F = fronts + me.front_off;
+  double* v = vecs + me.vec_off;
   const int tid = threadIdx.x;
+  if (t.c == 1) {
+    __shared__ double D[NB * DS];
+    __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
+    __shared__ double vy[NB];
+    PH_BEGIN(1)
 #pragma unroll
-  for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
-    const int e = tid + 256 * u_;
-    const int r = e & (NB - 1), c = e >> 5;
-    const bool ok = r < kb && c < kb && r >= c;
-    const double a = ld0(F, c * m + r, ok);
-    if (ok) D[r * DS + c] = a;
+    for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+      const int e = tid + 256 * u_;
+      const int r = e & (NB - 1), c = e >> 5;
+      const bool ok = r < kb0 && c < kb0 && r >= c;
+      const double a = ld0(F, c * m + r, ok);
+      if (ok) D[r * DS + c] = a;
+    }
+    if (tid < kb0) vy[tid] = v[tid];
+    __syncthreads();
+    for (int k = me.child_begin; k < me.child_end; ++k) {
+      const FrontDesc cd = fd[children[k]];
+      const int mc = cd.ns + cd.nr, nrc = cd.nr;
+      const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;
+      const int* rel = relmap + cd.rows_off;
+      int n0 = 0;  // child rows mapping into the block (rel is increasing)
+      while (n0 < nrc && n0 < NB && rel[n0] < kb0) ++n0;
+#pragma unroll
+      for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+        const int e = tid + 256 * u_;
+        const int i = e & (NB - 1), j = e >> 5;
+        if (i < n0 && j <= i) D[rel[i] * DS + rel[j]] += U[(size_t)j * mc + i];
+      }
+      if (tid < n0) vy[rel[tid]] += vecs[cd.vec_off + cd.ns + tid];
+      __syncthreads();
+    }
+    PH(2)
+    if (tid < 64)
+      factor_block(D, kb0, vy, col, tid, fail, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns, PH_REC);
+    __syncthreads();
+    PH(3)
+    publish_block(D, vy, kb0, lbuf + me.l_off, m, 0, ysol + me.c0, tid);
+    PH(4)
+    return;
   }
-  if (tid < kb) vy[tid] = vecs[me.vec_off + tid];
-  __syncthreads();
-  PH(2)
-  if (tid < 64) factor_block(D, kb, vy, col, tid, fail, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns, PH_REC);
-  __syncthreads();
-  PH(3)
-  publish_block(D, vy, kb, lbuf + me.l_off, m, 0, ysol + me.c0, tid);
-  PH(4)
+  const int a = t.a, b = t.b;
+  for (int k = me.child_begin; k < me.child_end; ++k) {
+    const FrontDesc cd = fd[children[k]];
+    const int mc = cd.ns + cd.nr, nrc = cd.nr;
+    const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;  // U(i,j) = U[j*mc + i]
+    const double* u = vecs + cd.vec_off + cd.ns;
+    const int* rel = relmap + cd.rows_off;
+    // child columns whose parent column lies in [a, b) (rel is increasing)
+    int lo = 0, hi = nrc;
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (rel[mid] < a) lo = mid + 1; else hi = mid; }
+    const int j0 = lo;
+    hi = nrc;
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (rel[mid] < b) lo = mid + 1; else hi = mid; }
+    const int j1 = lo;
+    for (int j = j0 + tid; j < j1; j += 256)
+      if (rel[j] >= kb0) v[rel[j]] += u[j];
+    // lower triangle of the slab: one wave per column, lanes run down the rows (coalesced U
+    // reads, mostly-contiguous F writes), 4 independent loads in flight per lane
+    const int j = j0 + (tid >> 6);
+    if (j < j1) {
+      const double* Uj = U + (size_t)j * mc;
+      double* Fj = F + (size_t)rel[j] * m;
+      const int rlo = rel[j] < kb0 ? kb0 : 0;  // rows of the first diagonal block: block-0 task
+      for (int i0 = j + (tid & 63); i0 < nrc; i0 += 256) {
+        double val[4];
+        int ri[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = i0 + q * 64;
+          const bool ok = i < nrc;
+          val[q] = ld0(Uj, i, ok);
+          ri[q] = ok ? ld0(rel, i, ok) : -1;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (ri[q] >= rlo) Fj[ri[q]] += val[q];
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------- panel step
@@ -819,15 +841,11 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double
   KERNEL_CHECK();
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
-                     double* fronts, double* vecs, hipStream_t s) {
+                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
+                     hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_extend_add, ntasks, 256, 0, s, tasks, fd, children, relmap, fronts, vecs);
-  KERNEL_CHECK();
-}
-void chol_potrf0(int nfronts, const int* level_list, const FrontDesc* fd, const double* fronts, double* lbuf,
-                 const double* vecs, double* ysol, double* linv, double* xinv, int* fail, hipStream_t s) {
-  if (nfronts <= 0) return;
-  hipLaunchKernelGGL(k_potrf0, nfronts, 256, 0, s, level_list, fd, fronts, lbuf, vecs, ysol, linv, xinv, fail);
+  hipLaunchKernelGGL(k_extend_add, ntasks, 256, 0, s, tasks, fd, children, relmap, fronts, vecs, lbuf, ysol, linv, xinv,
+                     fail);
   KERNEL_CHECK();
 }
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,

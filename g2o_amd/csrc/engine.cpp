@@ -272,7 +272,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     ll.insert(ll.end(), lv.begin(), lv.end());
     level_off.push_back((int)ll.size());
   }
-  level_lists.upload(ll, s);
   // work lists per level: extend-add, first diagonal block, one step per 32-wide panel,
   // contribution blocks
   {
@@ -296,7 +295,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         tiles0 += (long long)T * (T + 1) / 2;
       }
       const bool fused_contrib = tiles0 <= fused_max;
+      // k_extend_add: every front's first-diagonal-block task first, then the slabs
       Op ea{0, (int)tk.size(), 0};
+      for (int sn : lv) tk.push_back(Task{sn, 0, 0, 1});
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
         if (sym.children_ptr[sn + 1] == sym.children_ptr[sn]) continue;
@@ -304,8 +305,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         for (int a = 0; a < m; a += EA) tk.push_back(Task{sn, a, std::min(a + EA, m), 0});
       }
       ea.count = (int)tk.size() - ea.off;
-      if (ea.count) ops.push_back(ea);
-      ops.push_back(Op{1, level_off[l], (int)lv.size()});  // k_potrf0 over the level list
+      ops.push_back(ea);
       int maxp = 0;
       for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
       for (int p = 0; p < maxp; ++p) {
@@ -390,9 +390,8 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
   for (const Op& op : ops) {
     const launch::Task* t = tasks.get() + op.off;
     switch (op.kind) {
-      case 0: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), fronts.get(), vecs.get(), s); break;
-      case 1: launch::chol_potrf0(op.count, level_lists.get() + op.off, fd.get(), fronts.get(), lbuf.get(), vecs.get(),
-                                  y_p.get(), linv.get(), xinv.get(), fail, s); break;
+      case 0: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), fronts.get(), vecs.get(),
+                                      lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, s); break;
       case 2: launch::chol_step(op.count, step_tasks.get() + op.off, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),
                                 linv.get(), xinv.get(), fail, s);
         break;

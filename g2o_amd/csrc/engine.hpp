@@ -53,8 +53,8 @@ struct DeviceCholesky {
   DevBuf<long long> dst;
   DevBuf<unsigned char> isdiag;
   DevBuf<launch::FrontDesc> fd;
-  DevBuf<int> level_lists, children, relmap, rows, perm;
-  std::vector<int> level_off;  // host offsets into level_lists
+  DevBuf<int> children, relmap, rows, perm;
+  std::vector<int> level_off;  // host offsets of each level's fronts in the level order
   std::vector<int> bwd_off;    // per level: offset of its backward-gemv tasks in `tasks` (+1 end)
   int max_ns = 0;
   struct Op { int kind, off, count; };  // kind 0 extend-add, 1 first diagonal block, 2 panel step, 3 contribution block

@@ -92,10 +92,11 @@ struct StepTask {  // k_step work item, self-contained so a workgroup needs one 
 void chol_scatter(long long nent, const double* vals, const long long* dst, const unsigned char* is_diag,
                   const double* lam, double* fronts, hipStream_t s);
 void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double* vecs, hipStream_t s);
+// extend-add of a level (slab tasks, t.c == 0) with every front's first diagonal block assembled,
+// factored and forward-solved beside it (t.c == 1)
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
-                     double* fronts, double* vecs, hipStream_t s);
-void chol_potrf0(int nfronts, const int* level_list, const FrontDesc* fd, const double* fronts, double* lbuf,
-                 const double* vecs, double* ysol, double* linv, double* xinv, int* fail, hipStream_t s);
+                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
+                     hipStream_t s);
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
                double* linv, double* xinv, int* fail, hipStream_t s);
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s);

@@ -25,7 +25,7 @@ def main():
     n = L.g2ohip_debug_phases(buf, 4096)
     a = np.frombuffer(buf, dtype=np.uint64, count=8 * n).reshape(n, 8).astype(np.int64)
     print(f"{n} records")
-    for kid, name, labels in ((1, "k_potrf0", ["stage", "factor", "publish"]),
+    for kid, name, labels in ((1, "k_extend_add block-0 task", ["stage+assemble", "factor", "publish"]),
                               (2, "k_step(diag task)", ["stage+trsm+syrk", "factor", "publish"]),
                               (3, "k_step(tile 0,0)", ["stage", "trsm+L21", "update+store"])):
         r = a[a[:, 0] == kid]

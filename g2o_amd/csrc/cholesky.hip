@@ -448,7 +448,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
 #pragma unroll
     for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
       const int e = tid + 256 * u_, r = e & (NB - 1), c = e >> 5;
-      lv[u_] = Lin[e];
+      lv[u_] = ld0(Lin, e, kb > 0);  // kb = 0: first block of a big panel, already fully updated
       pv[u_] = ld0(F, (k0 + c) * m + r0 + r, c < kb);
       cdv[u_] = ld0(F, (r0 + c) * m + r0 + r, r >= c && r < kbn);
     }
@@ -596,7 +596,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     pav[u] = ld0(F, (k0 + q) * m + I0 + r, q < kb && I0 + r < m);
     pbv[u] = ld0(F, (k0 + q) * m + J0 + r, upd && q < kb && J0 + r < m);
   }
-  const int climit = (t.flags & 8) ? m : ns;  // flag 8: the contribution block is updated here too
+  const int climit = t.clim;  // ns; m when the contribution block is fused; the big-panel end when blocked
   if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
 #pragma unroll
   for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
@@ -641,7 +641,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   __syncthreads();
   // rows/columns of the next diagonal block, [r0, r0 + kbn): this step's diagonal task reads their
   // raw values at its start and applies the panel update itself, so tile tasks never write them
-  const int kbn = max(0, min(NB, ns - r0));
+  const int kbn = (t.flags & 32) ? 0 : max(0, min(NB, ns - r0));
   if (writer && tid < 64 && I0 + tid < m && I0 + tid >= r0 + kbn) {  // forward-solve update: v_i -= x_i y_k
     double s2 = 0.0;
 #pragma unroll
@@ -679,7 +679,9 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
 
 // ---------------------------------------------------------------------------- contribution block
 // U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns in 32-wide chunks staged in
-// LDS, the next chunk prefetched into registers. Task: s, b = ti | tj << 16.
+// LDS, the next chunk prefetched into registers. Task: s, b = ti | tj << 16, K = [a, c) (c = 0: [0, ns)).
+// The same kernel is the trailing update of a blocked front after each big panel: rows >= kb, columns
+// [kb, ns), K = the big panel's columns [ka, kb) of the finished factor.
 constexpr int SK = 32;          // K chunk
 constexpr int SPS = SK + 2;     // LDS row stride
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
@@ -691,10 +693,11 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
   double* F = fronts + me.front_off;
   const double* L = lbuf + me.l_off;
   const int ti = t.b & 0xffff, tj = t.b >> 16;
-  const int I0 = ns + ti * TT, J0 = ns + tj * TT;
+  const int ka = t.a, kb = t.c ? t.c : ns, climit = kb == ns ? m : ns;
+  const int I0 = kb + ti * TT, J0 = kb + tj * TT;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   double cv[16];
-  load_ctile(F, m, I0, J0, m, tid, cv);
+  load_ctile(F, m, I0, J0, climit, tid, cv);
   double* Pa = sh;
   double* Pb = sh + TT * SPS;
   double pa[SK / 4], pb[SK / 4];
@@ -702,8 +705,8 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
 #pragma unroll
     for (int u = 0; u < SK / 4; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), k = kc + (e >> 6);
-      pa[u] = ld0(L, k * m + I0 + r, k < ns && I0 + r < m);
-      pb[u] = ld0(L, k * m + J0 + r, k < ns && J0 + r < m);
+      pa[u] = ld0(L, k * m + I0 + r, k < kb && I0 + r < m);
+      pb[u] = ld0(L, k * m + J0 + r, k < kb && J0 + r < m);
     }
   };
   const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
@@ -713,8 +716,8 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) acc[x][y] = dx4{0.0, 0.0, 0.0, 0.0};
-  fetch(0);
-  for (int kc = 0; kc < ns; kc += SK) {
+  fetch(ka);
+  for (int kc = ka; kc < kb; kc += SK) {
 #pragma unroll
     for (int u = 0; u < SK / 4; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), k = e >> 6;
@@ -722,7 +725,7 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
       Pb[r * SPS + k] = pb[u];
     }
     __syncthreads();
-    if (kc + SK < ns && !(mode & 2)) fetch(kc + SK);
+    if (kc + SK < kb && !(mode & 2)) fetch(kc + SK);
 #pragma unroll
     for (int kk = 0; kk < SK / 4; ++kk) {
       if (mode & 1) break;
@@ -748,7 +751,7 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
   for (int u = 0; u < 16; ++u) {
     const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
     const int gi = I0 + r, gj = J0 + c;
-    if (gi < m && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - Ct[r * CS + c];
+    if (gi < m && gj < climit && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - Ct[r * CS + c];
   }
 }
 

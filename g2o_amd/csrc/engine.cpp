@@ -286,6 +286,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     // tiles than one round of the chip (re-reading the contribution block every step costs more)
     const char* fe = getenv("G2OHIP_CHOL_FUSED_MAX");  // dev A/B: fused-tile threshold per step
     const long long fused_max = fe ? atoll(fe) : 2LL * 256;
+    const char* bm = getenv("G2OHIP_CHOL_BLOCK_MIN");  // dev A/B: widest supernode factored unblocked
+    const int block_min = bm ? atoi(bm) : 512;
+    const char* bp = getenv("G2OHIP_CHOL_PB");  // dev A/B: big-panel width (multiple of 64)
+    const int block_pb = bp ? std::max(64, atoi(bp) / 64 * 64) : 256;
+    const bool dev_noinv = getenv("G2OHIP_DEV_NOINV") != nullptr;  // timing experiments only (wrong solve)
     for (size_t l = 0; l < sym.levels.size(); ++l) {
       const auto& lv = sym.levels[l];
       long long tiles0 = 0;  // fused tiles of the level's first step
@@ -308,6 +313,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       ops.push_back(ea);
       int maxp = 0;
       for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
+      // blocked fronts (wide supernodes on levels with a separate contribution pass): the rank-32 tile
+      // updates of the panel steps stop at the end of the current big panel of PB columns; after each big
+      // panel one high-intensity k_syrk launch applies its rank-PB update to the rest of the supernode's
+      // columns, and a next-diagonal task (kb = 0) factors the first block of the next big panel
+      auto blocked = [&](const Supernode& q) { return !fused_contrib && q.ns > block_min; };
       for (int p = 0; p < maxp; ++p) {
         Op st{2, (int)stk.size(), 0};
         // task order inside the launch (= dispatch order): every front's next-diagonal task first (the
@@ -319,21 +329,25 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           const int k0 = p * NB;
           if (k0 >= q.ns) continue;
           const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
+          const bool blk = blocked(q);
+          const int pend = blk ? std::min((k0 / block_pb + 1) * block_pb, q.ns) : q.ns;  // big-panel end
+          const bool bnd = blk && r0 == pend && r0 < q.ns;  // next block starts a big panel: no diag task
           // fused: every panel step also applies its rank-kb update to the contribution block (the
           // step is latency-bound on the diagonal chain, the extra tiles run in its shadow)
-          const int T = (m - r0 + TT - 1) / TT, TJ = fused_contrib ? T : (q.ns - r0 + TT - 1) / TT;
-          const int fl = fused_contrib ? 8 : 0;
+          const int clim = fused_contrib ? m : pend;
+          const int T = (m - r0 + TT - 1) / TT, TJ = (clim - r0 + TT - 1) / TT;
+          const int fl = (fused_contrib ? 8 : 0) | (bnd ? 32 : 0);
           auto mk = [&](int tile, int flags) {
             return launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns, q.c0,
-                                    k0 | (kb << 16), tile, flags};
+                                    k0 | (kb << 16), tile, flags, clim};
           };
-          if (r0 < q.ns) diag_t.push_back(mk(0, 4));
+          if (r0 < q.ns && !bnd) diag_t.push_back(mk(0, 4));
           for (int tj = 0; tj < std::max(TJ, 1); ++tj)
             for (int ti = tj; ti < T; ++ti) tile_t.push_back(mk(ti | (tj << 16), (tj < TJ ? 1 : 0) | fl));
           // inverse tasks: block row p-1's term into every pending block (bp, j), bp >= p, j < p;
           // block row p is final after this step
           const int nblk = (q.ns + NB - 1) / NB;
-          for (int bp = p; bp < nblk && p >= 1; ++bp)
+          for (int bp = p; bp < nblk && p >= 1 && !dev_noinv; ++bp)
             for (int j = 0; j < p; ++j) inv_t.push_back(mk(j | (bp << 16), 16));
         }
         stk.insert(stk.end(), diag_t.begin(), diag_t.end());
@@ -341,6 +355,24 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         stk.insert(stk.end(), inv_t.begin(), inv_t.end());
         st.count = (int)stk.size() - st.off;
         if (st.count) ops.push_back(st);
+        if ((p + 1) * NB % block_pb) continue;
+        // end of a big panel: trailing update of the blocked fronts, then their next first blocks
+        Op gm{3, (int)tk.size(), 0};
+        Op d0{2, (int)stk.size(), 0};
+        for (int sn : lv) {
+          const Supernode& q = sym.sn[sn];
+          const int kb = (p + 1) * NB, ka = kb - block_pb, m = q.ns + q.nr;
+          if (!blocked(q) || kb >= q.ns) continue;
+          const int T = (m - kb + TT - 1) / TT, TJ = (q.ns - kb + TT - 1) / TT;
+          for (int tj = 0; tj < TJ; ++tj)
+            for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, ka, ti | (tj << 16), kb});
+          stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns,
+                                         q.c0, kb, 0, 4, q.ns});
+        }
+        gm.count = (int)tk.size() - gm.off;
+        d0.count = (int)stk.size() - d0.off;
+        if (gm.count) ops.push_back(gm);
+        if (d0.count) ops.push_back(d0);
       }
       Op sy{3, (int)tk.size(), 0};
       for (int sn : lv) {

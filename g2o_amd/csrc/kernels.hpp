@@ -87,7 +87,9 @@ struct StepTask {  // k_step work item, self-contained so a workgroup needs one 
   int m, ns, c0;
   int k0kb;   // k0 | kb << 16
   int tile;   // ti | tj << 16 (inverse task: block column j | block row p << 16)
-  int flags;  // 1 update the tile, 4 next-diagonal task, 8 reaches into the contribution block, 16 inverse
+  int flags;  // 1 update the tile, 4 next-diagonal task, 8 reaches into the contribution block, 16 inverse,
+              // 32 no next-diagonal task this step (blocked front, big-panel boundary): writers update every row
+  int clim;   // tile updates stop at this front column (ns, m when fused, the big-panel end when blocked)
 };
 void chol_scatter(long long nent, const double* vals, const long long* dst, const unsigned char* is_diag,
                   const double* lam, double* fronts, hipStream_t s);
@@ -99,6 +101,8 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
                      hipStream_t s);
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
                double* linv, double* xinv, int* fail, hipStream_t s);
+// C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
+// the contribution block, K = [0, ns)); columns stop at ns unless kb = ns (then m)
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s);
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]
 void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]

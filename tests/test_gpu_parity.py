@@ -117,6 +117,49 @@ def test_linear_solver_ccs(g2o_amd_mod):
     assert not ok2
 
 
+def _dense_spd_ccs(rng, n, density):
+    nb = n // 6
+    mask = np.kron(rng.random((nb, nb)) < density, np.ones((6, 6))) > 0
+    mask = mask | mask.T
+    A = rng.standard_normal((n, n)) * mask
+    A = A @ A.T + n * np.eye(n)
+    Ap, Ai, Ax = [0], [], []
+    for j in range(n):
+        rows = np.nonzero(A[: j + 1, j])[0]
+        Ai += rows.tolist()
+        Ax += A[rows, j].tolist()
+        Ap.append(len(Ai))
+    return A, Ap, Ai, Ax
+
+
+@pytest.mark.parametrize("pb", [64, 128, 256])
+def test_linear_solver_blocked_fronts(g2o_amd_mod, monkeypatch, pb):
+    """Wide supernodes factored in big panels (rank-32 steps inside a panel, one rank-PB trailing update
+    per panel, first block of the next panel on its own): same solution as the unblocked schedule."""
+    rng = np.random.default_rng(11)
+    n = 1800
+    A, Ap, Ai, Ax = _dense_spd_ccs(rng, n, 0.05)
+    b = rng.standard_normal(n)
+    monkeypatch.setenv("G2OHIP_CHOL_FUSED_MAX", "0")
+    monkeypatch.setenv("G2OHIP_CHOL_BLOCK_MIN", "1000000")
+    ok0, x0 = g2o_amd_mod.linear_solve_ccs(n, Ap, Ai, Ax, b, block_dim=6)
+    monkeypatch.setenv("G2OHIP_CHOL_BLOCK_MIN", "32")
+    monkeypatch.setenv("G2OHIP_CHOL_PB", str(pb))
+    ok1, x1 = g2o_amd_mod.linear_solve_ccs(n, Ap, Ai, Ax, b, block_dim=6)
+    assert ok0 and ok1
+    np.testing.assert_allclose(A @ x1, b, rtol=1e-10, atol=1e-10)
+    assert np.linalg.norm(x1 - x0) <= 1e-12 * np.linalg.norm(x0)
+
+
+def test_lm_blocked_fronts_sphere2500(g2o_amd_mod, oracle, monkeypatch):
+    """C1 full size with every supernode wider than 32 columns blocked (PB = 64)."""
+    monkeypatch.setenv("G2OHIP_CHOL_FUSED_MAX", "0")
+    monkeypatch.setenv("G2OHIP_CHOL_BLOCK_MIN", "32")
+    monkeypatch.setenv("G2OHIP_CHOL_PB", "64")
+    prob = synth.by_name("C1")
+    _check(*_run_both(g2o_amd_mod, oracle, prob, 3))
+
+
 def test_g2o_file_roundtrip_parity(g2o_amd_mod, oracle, tmp_path):
     prob = synth.by_name("C4", "small")
     path = str(tmp_path / "ba.g2o")

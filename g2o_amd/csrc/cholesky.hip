@@ -35,6 +35,7 @@
 
 #include "common.hpp"
 #include "device_util.hpp"
+#include "gemm_nt.hpp"
 #include "kernels.hpp"
 
 namespace g2ohip {
@@ -678,81 +679,20 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
 }
 
 // ---------------------------------------------------------------------------- contribution block
-// U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns in 32-wide chunks staged in
-// LDS, the next chunk prefetched into registers. Task: s, b = ti | tj << 16, K = [a, c) (c = 0: [0, ns)).
+// U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns (gemm_nt.hpp: 64x64 tiles, K in
+// double-buffered 16-column LDS chunks). Task: s, b = ti | tj << 16, K = [a, c) (c = 0: [0, ns)).
 // The same kernel is the trailing update of a blocked front after each big panel: rows >= kb, columns
 // [kb, ns), K = the big panel's columns [ka, kb) of the finished factor.
-constexpr int SK = 32;          // K chunk
-constexpr int SPS = SK + 2;     // LDS row stride
+using SyrkTile = GemmNT<TT, TT>;
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                              double* __restrict__ fronts, const double* __restrict__ lbuf, int mode) {
-  __shared__ double sh[2 * TT * SPS];
+                                              double* __restrict__ fronts, const double* __restrict__ lbuf) {
+  __shared__ double sh[SyrkTile::LDS_DOUBLES];
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, ns = me.ns;
-  double* F = fronts + me.front_off;
-  const double* L = lbuf + me.l_off;
   const int ti = t.b & 0xffff, tj = t.b >> 16;
   const int ka = t.a, kb = t.c ? t.c : ns, climit = kb == ns ? m : ns;
-  const int I0 = kb + ti * TT, J0 = kb + tj * TT;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double cv[16];
-  load_ctile(F, m, I0, J0, climit, tid, cv);
-  double* Pa = sh;
-  double* Pb = sh + TT * SPS;
-  double pa[SK / 4], pb[SK / 4];
-  auto fetch = [&](int kc) {
-#pragma unroll
-    for (int u = 0; u < SK / 4; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), k = kc + (e >> 6);
-      pa[u] = ld0(L, k * m + I0 + r, k < kb && I0 + r < m);
-      pb[u] = ld0(L, k * m + J0 + r, k < kb && J0 + r < m);
-    }
-  };
-  const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
-  const int lr = lane & 15, lk = lane >> 4;
-  dx4 acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = dx4{0.0, 0.0, 0.0, 0.0};
-  fetch(ka);
-  for (int kc = ka; kc < kb; kc += SK) {
-#pragma unroll
-    for (int u = 0; u < SK / 4; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), k = e >> 6;
-      Pa[r * SPS + k] = pa[u];
-      Pb[r * SPS + k] = pb[u];
-    }
-    __syncthreads();
-    if (kc + SK < kb && !(mode & 2)) fetch(kc + SK);
-#pragma unroll
-    for (int kk = 0; kk < SK / 4; ++kk) {
-      if (mode & 1) break;
-      const int k = kk * 4 + lk;
-      const double a0 = Pa[(wr + lr) * SPS + k], a1 = Pa[(wr + 16 + lr) * SPS + k];
-      const double b0 = Pb[(wc + lr) * SPS + k], b1 = Pb[(wc + 16 + lr) * SPS + k];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  double* Ct = sh;
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Ct[(wr + x * 16 + lk + 4 * i) * CS + wc + y * 16 + lr] = acc[x][y][i];
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
-    const int gi = I0 + r, gj = J0 + c;
-    if (gi < m && gj < climit && gi >= gj) F[(size_t)gj * m + gi] = cv[u] - Ct[r * CS + c];
-  }
+  SyrkTile::run(lbuf + me.l_off, m, fronts + me.front_off, m, m, climit, kb + ti * TT, kb + tj * TT, ka, kb, sh);
 }
 
 __global__ void k_permute(int n, const int* __restrict__ perm, const double* __restrict__ in, double* __restrict__ out) {
@@ -859,8 +799,7 @@ void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, 
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
   if (ntasks <= 0) return;
-  static const int mode = getenv("G2OHIP_SYRK_MODE") ? atoi(getenv("G2OHIP_SYRK_MODE")) : 0;  // dev A/B only
-  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf, mode);
+  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
   KERNEL_CHECK();
 }
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s) {

@@ -1,0 +1,125 @@
+// Tile update C(I, J) -= A(I, K) A(J, K)^T on v_mfma_f64_16x16x4f64 — the high-intensity half of the
+// supernodal Cholesky (contribution blocks U = A22 - L21 L21^T and the rank-PB trailing updates of
+// blocked fronts). A is a finished factor panel in lbuf (column-major, leading dimension m), C a front
+// (column-major, leading dimension m), lower triangle only.
+//
+// One workgroup of WM x WN waves owns a BM x BN tile; each wave a (BM/WM) x (BN/WN) sub-tile of
+// MI x NJ 16x16 MFMA blocks, so every A fragment read from LDS feeds NJ MFMAs and every B fragment MI. K runs in chunks of KC columns, double-buffered in LDS (k-major images: the global
+// column segments land unchanged, fragment reads are 16 consecutive rows per k), the next chunk's
+// global loads in flight under the current chunk's MFMAs: one barrier per chunk.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device_util.hpp"
+
+namespace g2ohip {
+
+typedef double gdx4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int WM = 2, int WN = 2, int KC_ = 16>
+struct GemmNT {
+  static constexpr int NT = 64 * WM * WN;  // threads
+  static constexpr int KC = KC_;
+  static constexpr int SA = BM + 16;  // k-major LDS strides (doubles), = 16 mod 32: the four k rows of a
+  static constexpr int SB = BN + 16;  // fragment read fall on alternating bank halves
+  static constexpr int LDS_DOUBLES = 2 * KC * (SA + SB);
+  static constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;  // MFMA blocks per wave
+  static constexpr int LA = BM * KC / NT, LB = BN * KC / NT;   // global loads per thread per chunk
+
+  // rows [I0, I0+BM) x columns [J0, J0+BN) of C, K = [ka, kb); entries outside rows < mrows,
+  // columns < climit or above the diagonal are left untouched. lds: LDS_DOUBLES doubles.
+  __device__ static void run(const double* __restrict__ A, int lda, double* __restrict__ C, int ldc, int mrows,
+                             int climit, int I0, int J0, int ka, int kb, double* lds) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w % WM, wc = w / WM;
+    const int lr = lane & 15, lk = lane >> 4;
+    constexpr int BUF = KC * (SA + SB);  // buffer b: A image at lds + b BUF, B image after it
+    // prefetch registers hold the raw loads; the out-of-range mask is applied when they are stashed, so
+    // no wait on the loads precedes the chunk's MFMAs (a second register set for a two-chunk distance
+    // measured slower: the extra VGPRs cost occupancy)
+    double ra[LA], rb[LB];
+    unsigned oka = 0, okb = 0;
+    auto fetch = [&](int kc) {
+      oka = okb = 0;
+#pragma unroll
+      for (int u = 0; u < LA; ++u) {
+        const int e = tid + NT * u, r = e % BM, k = kc + e / BM;
+        const bool ok = k < kb && I0 + r < mrows;
+        ra[u] = A[ok ? k * lda + I0 + r : 0];
+        oka |= (unsigned)ok << u;
+      }
+#pragma unroll
+      for (int u = 0; u < LB; ++u) {
+        const int e = tid + NT * u, r = e % BN, k = kc + e / BN;
+        const bool ok = k < kb && J0 + r < mrows;
+        rb[u] = A[ok ? k * lda + J0 + r : 0];
+        okb |= (unsigned)ok << u;
+      }
+    };
+    auto stash = [&](int b) {
+#pragma unroll
+      for (int u = 0; u < LA; ++u) {
+        const int e = tid + NT * u;
+        lds[b * BUF + (e / BM) * SA + e % BM] = (oka >> u) & 1 ? ra[u] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < LB; ++u) {
+        const int e = tid + NT * u;
+        lds[b * BUF + KC * SA + (e / BN) * SB + e % BN] = (okb >> u) & 1 ? rb[u] : 0.0;
+      }
+    };
+    gdx4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = gdx4{0.0, 0.0, 0.0, 0.0};
+    fetch(ka);
+    stash(0);
+    __syncthreads();
+    const int nch = (kb - ka + KC - 1) / KC;
+    for (int c = 0; c < nch; ++c) {
+      const int b = c & 1;
+      fetch(ka + (c + 1) * KC);  // past kb: fully masked, stashed into the idle buffer
+      const double* pa = lds + b * BUF + wr * (BM / WM) + lr;
+      const double* pb = lds + b * BUF + KC * SA + wc * (BN / WN) + lr;
+#pragma unroll
+      for (int kk = 0; kk < KC / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        double fa[MI], fb[NJ];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) fa[i] = pa[k * SA + 16 * i];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) fb[j] = pb[k * SB + 16 * j];
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+      stash(b ^ 1);
+      __syncthreads();
+    }
+    // epilogue: C -= acc, lane holds D[lk + 4q][lr] of each 16x16 block; one block column at a time
+    // (all loads of the column in flight, then the stores)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int gj = J0 + wc * (BN / WN) + 16 * j + lr;
+      double cv[MI][4];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gi = I0 + wr * (BM / WM) + 16 * i + lk + 4 * q;
+          cv[i][q] = ld0(C, gj * ldc + gi, gi < mrows && gj < climit && gi >= gj);
+        }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gi = I0 + wr * (BM / WM) + 16 * i + lk + 4 * q;
+          if (gi < mrows && gj < climit && gi >= gj) C[(size_t)gj * ldc + gi] = cv[i][q] - acc[i][j][q];
+        }
+    }
+  }
+};
+
+}  // namespace g2ohip

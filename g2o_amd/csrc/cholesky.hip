@@ -10,10 +10,10 @@
 // so no kernel ever reads a column another workgroup of the same launch is rewriting.
 // Each LM trial runs
 //   k_permute + k_vec_init   rhs -> P rhs -> front vectors (own rows)
-//   k_chol_scatter           input blocks -> fronts (+ lambda on the diagonal)
 //   per level l (all fronts of a level are independent):
-//     k_extend_add     children's update matrices AND update vectors -> parent fronts, one
-//                      workgroup per (front, 4-column slab), children in fixed order; beside them
+//     k_extend_add     assembly: input entries (+ lambda) and the children's update matrices AND update
+//                      vectors -> the level's fronts, one workgroup per (front, 16-column slab),
+//                      children in fixed order; beside them
 //                      one workgroup per front assembles, factors and forward-solves its first
 //                      32x32 diagonal block (the first panel step's input)
 //     k_step (x panels) one launch per 32-column panel step: every workgroup owns one 64x64
@@ -89,17 +89,21 @@ __device__ unsigned int g_phase_n;
 #define PH(i)
 #endif
 
+// Small levels (latency-bound, see DeviceCholesky::setup) are zeroed and receive their input entries
+// before the first level, by these two massively parallel passes; their assembly launches then add the
+// children only. Zero tasks: (offset, length) ranges of the front pool.
+__global__ void __launch_bounds__(256) k_zero_ranges(const long long* __restrict__ rng, double* __restrict__ fronts) {
+  const long long off = rng[2 * blockIdx.x], len = rng[2 * blockIdx.x + 1];
+  for (long long i = threadIdx.x; i < len; i += 256) fronts[off + i] = 0.0;
+}
 __global__ void __launch_bounds__(256) k_chol_scatter(long long nent, const double* __restrict__ vals,
-                                                      const long long* __restrict__ dst,
-                                                      const unsigned char* __restrict__ is_diag,
+                                                      const long long* __restrict__ dst, const int* __restrict__ src,
                                                       const double* __restrict__ lam, double* __restrict__ fronts) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nent) return;
-  const long long d = dst[k];
-  if (d < 0) return;
-  double v = vals[k];
-  if (is_diag[k]) v += *lam;
-  fronts[d] = v;
+  const int sr = src[k];
+  const double v = vals[sr & 0x7fffffff];
+  fronts[dst[k]] = sr < 0 ? v + *lam : v;
 }
 
 // front vectors: v_s = [P rhs (own columns); 0]
@@ -258,23 +262,35 @@ __device__ __forceinline__ void publish_block(const double* D, const double* vy,
   if (tid < kb) ysol[r0 + tid] = vy[tid];
 }
 
-// ---------------------------------------------------------------------------- extend-add
-// One launch per level (from the second level on) with two kinds of workgroup:
-//  * block-0 tasks (t.c == 1, dispatched first, one per front of the level): the front's first
-//    kb x kb diagonal block and front-vector head are assembled here (scattered values + the
+// ---------------------------------------------------------------------------- assembly + extend-add
+// One launch per level assembles every front of the level from scratch (no front-pool memset, no
+// separate scatter pass), with two kinds of workgroup:
+//  * block-0 tasks (t.c == 1, dispatched first, one per front): the front's first kb x kb diagonal block
+//    and front-vector head are assembled here (the column's input entries of the reduced system + the
 //    children's update-matrix entries that map into it, children in fixed order), factored and
-//    forward-solved, and L_00, y_0, L_00^-1 published: the first panel step needs no launch of
-//    its own;
-//  * slab tasks (t.c == 0): children's update matrices AND update vectors -> the parent front,
-//    one workgroup per (front, 4-column slab), children in fixed order, every entry outside the
-//    first diagonal block.
-// Every entry is written by exactly one workgroup, in the same child order: bitwise reproducible.
+//    forward-solved, and L_00, y_0, L_00^-1 published: the first panel step needs no launch of its own;
+//  * slab tasks (t.c == 0): columns [a, b) of one front, every entry outside the first diagonal block:
+//    the lower part of each column is written once (zero, or the input entry + lambda on the diagonal;
+//    inputs come from a per-column list, `colptr`/`ent_row`/`ent_src`), then the children's update
+//    matrices AND update vectors are added, children in fixed order. One wave per column, 4 columns per
+//    wave: the column's writes are coalesced runs.
+// Every entry is written by exactly one workgroup, in the same order: bitwise reproducible.
+__device__ __forceinline__ double input_entry(const double* vals, const int* ent_src, const int* ent_row, int e,
+                                              const double* lam, int& row) {
+  const int rr = ent_row[e];
+  row = rr & 0x3fffffff;
+  const double v = vals[ent_src[e]];
+  return (rr >> 30) ? v + *lam : v;
+}
+template <bool ASM>  // ASM: the level's fronts are assembled here; else they were pre-zeroed and scattered
 __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                     const int* __restrict__ children, const int* __restrict__ relmap,
-                                                    double* __restrict__ fronts, double* __restrict__ vecs,
-                                                    double* __restrict__ lbuf, double* __restrict__ ysol,
-                                                    double* __restrict__ linv, double* __restrict__ xinv,
-                                                    int* __restrict__ fail) {
+                                                    const int* __restrict__ colptr, const int* __restrict__ ent_row,
+                                                    const int* __restrict__ ent_src, const double* __restrict__ vals,
+                                                    const double* __restrict__ lam, double* __restrict__ fronts,
+                                                    double* __restrict__ vecs, double* __restrict__ lbuf,
+                                                    double* __restrict__ ysol, double* __restrict__ linv,
+                                                    double* __restrict__ xinv, int* __restrict__ fail) {
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, kb0 = min(NB, me.ns);
@@ -286,15 +302,31 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
     __shared__ double vy[NB];
     PH_BEGIN(1)
+    if constexpr (!ASM) {
 #pragma unroll
-    for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
-      const int e = tid + 256 * u_;
-      const int r = e & (NB - 1), c = e >> 5;
-      const bool ok = r < kb0 && c < kb0 && r >= c;
-      const double a = ld0(F, c * m + r, ok);
-      if (ok) D[r * DS + c] = a;
+      for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+        const int e = tid + 256 * u_;
+        const int r = e & (NB - 1), c = e >> 5;
+        const bool ok = r < kb0 && c < kb0 && r >= c;
+        const double x = ld0(F, c * m + r, ok);
+        if (ok) D[r * DS + c] = x;
+      }
+      if (tid < kb0) vy[tid] = v[tid];
+    } else {
+      __shared__ int cp[NB + 1];
+      for (int i = tid; i < NB * DS; i += 256) D[i] = 0.0;
+      if (tid <= kb0) cp[tid] = colptr[me.c0 + tid];
+      if (tid < kb0) vy[tid] = v[tid];
+      __syncthreads();
+      // input entries of the block's columns (one contiguous range), the whole workgroup striding over it
+      for (int e = cp[0] + tid; e < cp[kb0]; e += 256) {
+        int lo = 0, hi = kb0;  // column of entry e: cp[lo] <= e < cp[lo + 1]
+        while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cp[mid] <= e) lo = mid; else hi = mid; }
+        int r;
+        const double x = input_entry(vals, ent_src, ent_row, e, lam, r);
+        if (r < kb0) D[r * DS + lo] = x;
+      }
     }
-    if (tid < kb0) vy[tid] = v[tid];
     __syncthreads();
     for (int k = me.child_begin; k < me.child_end; ++k) {
       const FrontDesc cd = fd[children[k]];
@@ -322,6 +354,26 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     return;
   }
   const int a = t.a, b = t.b;
+  const int lane = tid & 63, w = tid >> 6;
+  // 1. own columns: zero / input entries, written once (rows of the first diagonal block are block-0's);
+  //    !ASM: the front was zeroed and its inputs scattered before the first level (small levels)
+  for (int j = a + w; j < b && ASM; j += 4) {
+    const int rlo = j < kb0 ? kb0 : j;
+    double* Fj = F + (size_t)j * m;
+    for (int i = rlo + lane; i < m; i += 64) Fj[i] = 0.0;
+  }
+  if constexpr (ASM) __syncthreads();
+  for (int j = a + w; j < b && j < me.ns && ASM; j += 4) {
+    const int rlo = j < kb0 ? kb0 : j;
+    double* Fj = F + (size_t)j * m;
+    for (int e = colptr[me.c0 + j] + lane; e < colptr[me.c0 + j + 1]; e += 64) {
+      int r;
+      const double x = input_entry(vals, ent_src, ent_row, e, lam, r);
+      if (r >= rlo) Fj[r] = x;
+    }
+  }
+  if constexpr (ASM) __syncthreads();
+  // 2. children in fixed order
   for (int k = me.child_begin; k < me.child_end; ++k) {
     const FrontDesc cd = fd[children[k]];
     const int mc = cd.ns + cd.nr, nrc = cd.nr;
@@ -337,14 +389,13 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     const int j1 = lo;
     for (int j = j0 + tid; j < j1; j += 256)
       if (rel[j] >= kb0) v[rel[j]] += u[j];
-    // lower triangle of the slab: one wave per column, lanes run down the rows (coalesced U
-    // reads, mostly-contiguous F writes), 4 independent loads in flight per lane
-    const int j = j0 + (tid >> 6);
-    if (j < j1) {
+    // lower triangle: one wave per child column, lanes run down the rows (coalesced U reads,
+    // mostly-contiguous F writes), 4 independent loads in flight per lane
+    for (int j = j0 + w; j < j1; j += 4) {
       const double* Uj = U + (size_t)j * mc;
       double* Fj = F + (size_t)rel[j] * m;
       const int rlo = rel[j] < kb0 ? kb0 : 0;  // rows of the first diagonal block: block-0 task
-      for (int i0 = j + (tid & 63); i0 < nrc; i0 += 256) {
+      for (int i0 = j + lane; i0 < nrc; i0 += 256) {
         double val[4];
         int ri[4];
 #pragma unroll
@@ -772,11 +823,16 @@ int debug_phases(unsigned long long* out, int maxrec) {
 #endif
 }
 
-void chol_scatter(long long nent, const double* vals, const long long* dst, const unsigned char* is_diag,
-                  const double* lam, double* fronts, hipStream_t s) {
-  if (nent <= 0) return;
-  hipLaunchKernelGGL(k_chol_scatter, grid_for(nent, 256), 256, 0, s, nent, vals, dst, is_diag, lam, fronts);
-  KERNEL_CHECK();
+void chol_prescatter(int nzero, const long long* zr, long long nent, const double* vals, const long long* dst,
+                     const int* src, const double* lam, double* fronts, hipStream_t s) {
+  if (nzero > 0) {
+    hipLaunchKernelGGL(k_zero_ranges, nzero, 256, 0, s, zr, fronts);
+    KERNEL_CHECK();
+  }
+  if (nent > 0) {
+    hipLaunchKernelGGL(k_chol_scatter, grid_for(nent, 256), 256, 0, s, nent, vals, dst, src, lam, fronts);
+    KERNEL_CHECK();
+  }
 }
 void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double* vecs, hipStream_t s) {
   if (nfronts <= 0) return;
@@ -784,11 +840,16 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double
   KERNEL_CHECK();
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
+                     const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
-                     hipStream_t s) {
+                     bool assemble, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_extend_add, ntasks, 256, 0, s, tasks, fd, children, relmap, fronts, vecs, lbuf, ysol, linv, xinv,
-                     fail);
+  if (assemble)
+    hipLaunchKernelGGL(k_extend_add<true>, ntasks, 256, 0, s, tasks, fd, children, relmap, colptr, ent_row, ent_src, vals,
+                       lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
+  else
+    hipLaunchKernelGGL(k_extend_add<false>, ntasks, 256, 0, s, tasks, fd, children, relmap, colptr, ent_row, ent_src, vals,
+                       lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,

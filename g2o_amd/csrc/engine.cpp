@@ -226,10 +226,16 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   sym = analyze(P);
   if ((long long)sym.max_front * sym.max_front >= (1LL << 31))
     throw DeviceError("front too large for 32-bit in-front indexing");
-  // scatter map: input block t (bi, bj) col-major bdim x bdim
+  // input entries per (permuted) scalar column: input block t (bi, bj) col-major bdim x bdim, value index
+  // k = t bdim^2 + c bdim + r; the entry lands at front row rpos of its column (assembled per level by
+  // k_extend_add, lambda added on the diagonal)
   nent = (long long)bi.size() * bdim * bdim;
-  std::vector<long long> hdst(nent, -1);
-  std::vector<unsigned char> hdiag(nent, 0);
+  if (nent >= (1LL << 31)) throw DeviceError("reduced system too large for 32-bit entry indexing");
+  std::vector<int> ecol, erow, esrc, cpv, ent_rowv, ent_srcv;
+  std::vector<long long> edst, edsts;
+  ecol.reserve(nent);
+  erow.reserve(nent);
+  esrc.reserve(nent);
   for (size_t t = 0; t < bi.size(); ++t)
     for (int c = 0; c < bdim; ++c)
       for (int r = 0; r < bdim; ++r) {
@@ -240,7 +246,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         const int row = std::max(a, b), col = std::min(a, b);
         const int sn = sym.block_sn[col / bdim];
         const Supernode& q = sym.sn[sn];
-        const int cpos = col - q.c0;
         int rpos;
         if (row < q.c0 + q.ns) rpos = row - q.c0;
         else {
@@ -249,12 +254,32 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           if (it == rb + q.nr || *it != row) throw std::runtime_error("cholesky setup: entry outside the symbolic pattern");
           rpos = q.ns + (int)(it - rb);
         }
-        const long long m = q.ns + q.nr;
-        hdst[k] = q.front_off + (long long)cpos * m + rpos;
-        hdiag[k] = gi == gj;
+        ecol.push_back(col);
+        erow.push_back(rpos | (gi == gj ? (1 << 30) : 0));
+        esrc.push_back((int)k);
+        edst.push_back(q.front_off + (long long)(col - q.c0) * (q.ns + q.nr) + rpos);
       }
-  dst.upload(hdst, s);
-  isdiag.upload(hdiag, s);
+  {
+    std::vector<int> cp(sym.n + 1, 0);
+    for (int c : ecol) cp[c + 1]++;
+    for (int c = 0; c < sym.n; ++c) cp[c + 1] += cp[c];
+    std::vector<int> fillp(cp.begin(), cp.end() - 1), hr(ecol.size()), hs(ecol.size());
+    for (size_t e = 0; e < ecol.size(); ++e) {
+      const int d = fillp[ecol[e]]++;
+      hr[d] = erow[e];
+      hs[d] = esrc[e];
+    }
+    std::vector<long long> hd(ecol.size());
+    fillp.assign(cp.begin(), cp.end() - 1);
+    for (size_t e = 0; e < ecol.size(); ++e) hd[fillp[ecol[e]]++] = edst[e];
+    colptr.upload(cp, s);
+    ent_row.upload(hr.empty() ? std::vector<int>{0} : hr, s);
+    ent_src.upload(hs.empty() ? std::vector<int>{0} : hs, s);
+    cpv.swap(cp);
+    ent_rowv.swap(hr);
+    ent_srcv.swap(hs);
+    edsts.swap(hd);
+  }
   std::vector<launch::FrontDesc> hfd(sym.sn.size());
   long long loff = 0, xoff = 0;
   for (size_t k = 0; k < sym.sn.size(); ++k) {
@@ -291,6 +316,10 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const char* bp = getenv("G2OHIP_CHOL_PB");  // dev A/B: big-panel width (multiple of 64)
     const int block_pb = bp ? std::max(64, atoi(bp) / 64 * 64) : 256;
     const bool dev_noinv = getenv("G2OHIP_DEV_NOINV") != nullptr;  // timing experiments only (wrong solve)
+    const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
+    const long long pre_max = pm ? atoll(pm) : (256LL << 20);
+    std::vector<long long> zr, pdst;
+    std::vector<int> psrc;
     for (size_t l = 0; l < sym.levels.size(); ++l) {
       const auto& lv = sym.levels[l];
       long long tiles0 = 0;  // fused tiles of the level's first step
@@ -301,13 +330,34 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       }
       const bool fused_contrib = tiles0 <= fused_max;
       // k_extend_add: every front's first-diagonal-block task first, then the slabs
-      Op ea{0, (int)tk.size(), 0};
+      // small levels (all fronts <= pre_max bytes together) are zeroed + scattered before the first level
+      // (two massively parallel passes off the critical chain); large ones are assembled in place
+      long long lbytes = 0;
+      for (int sn : lv) lbytes += 8LL * (sym.sn[sn].ns + sym.sn[sn].nr) * (sym.sn[sn].ns + sym.sn[sn].nr);
+      const bool pre = lbytes <= pre_max;
+      if (pre)
+        for (int sn : lv) {
+          const Supernode& q = sym.sn[sn];
+          const long long len = (long long)(q.ns + q.nr) * (q.ns + q.nr);
+          for (long long o = 0; o < len; o += 65536) { zr.push_back(q.front_off + o); zr.push_back(std::min(65536LL, len - o)); }
+          for (int c = q.c0; c < q.c0 + q.ns; ++c)
+            for (int e = cpv[c]; e < cpv[c + 1]; ++e) {
+              pdst.push_back(edsts[e]);
+              psrc.push_back(ent_srcv[e] | ((ent_rowv[e] >> 30) ? (int)0x80000000 : 0));
+            }
+        }
+      Op ea{pre ? 0 : 4, (int)tk.size(), 0};
       for (int sn : lv) tk.push_back(Task{sn, 0, 0, 1});
+      // every front is assembled here (input entries, zeros, children); slabs of EA columns where the level
+      // has enough of them to fill the chip several times over, else 4 (latency-bound upper levels)
+      long long lcols = 0;
+      for (int sn : lv) lcols += sym.sn[sn].ns + sym.sn[sn].nr;
+      const int slab = lcols >= 16LL * EA * 256 ? EA : 4;
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
-        if (sym.children_ptr[sn + 1] == sym.children_ptr[sn]) continue;
         const int m = q.ns + q.nr;
-        for (int a = 0; a < m; a += EA) tk.push_back(Task{sn, a, std::min(a + EA, m), 0});
+        if (pre && sym.children_ptr[sn + 1] == sym.children_ptr[sn]) continue;  // nothing left to assemble
+        for (int a = 0; a < m; a += slab) tk.push_back(Task{sn, a, std::min(a + slab, m), 0});
       }
       ea.count = (int)tk.size() - ea.off;
       ops.push_back(ea);
@@ -385,6 +435,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       sy.count = (int)tk.size() - sy.off;
       if (sy.count) ops.push_back(sy);
     }
+    nzero = (int)(zr.size() / 2);
+    npre = (long long)pdst.size();
+    zero_rng.upload(zr.empty() ? std::vector<long long>{0, 0} : zr, s);
+    pre_dst.upload(pdst.empty() ? std::vector<long long>{0} : pdst, s);
+    pre_src.upload(psrc.empty() ? std::vector<int>{0} : psrc, s);
     // backward-solve gemv tasks per level: (front, 4 columns)
     bwd_off.assign(1, (int)tk.size());
     max_ns = 1;
@@ -417,13 +472,14 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
 void DeviceCholesky::factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s) {
   launch::chol_permute(sym.n, perm.get(), rhs, rhs_p.get(), s);
   launch::chol_vec_init((int)sym.sn.size(), fd.get(), rhs_p.get(), vecs.get(), s);
-  HIP_CHECK(hipMemsetAsync(fronts.get(), 0, fronts.bytes(), s));
-  launch::chol_scatter(nent, vals, dst.get(), isdiag.get(), lam, fronts.get(), s);
+  launch::chol_prescatter(nzero, zero_rng.get(), npre, vals, pre_dst.get(), pre_src.get(), lam, fronts.get(), s);
   for (const Op& op : ops) {
     const launch::Task* t = tasks.get() + op.off;
     switch (op.kind) {
-      case 0: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), fronts.get(), vecs.get(),
-                                      lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, s); break;
+      case 0:
+      case 4: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), colptr.get(), ent_row.get(),
+                                      ent_src.get(), vals, lam, fronts.get(), vecs.get(),
+                                      lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 4, s); break;
       case 2: launch::chol_step(op.count, step_tasks.get() + op.off, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),
                                 linv.get(), xinv.get(), fail, s);
         break;

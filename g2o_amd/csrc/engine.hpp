@@ -50,14 +50,17 @@ struct DeviceCholesky {
   Symbolic sym;
   int pd = 0;
   long long nent = 0;
-  DevBuf<long long> dst;
-  DevBuf<unsigned char> isdiag;
+  DevBuf<int> colptr, ent_row, ent_src;  // input entries per permuted scalar column (k_extend_add)
+  long long npre = 0;                     // entries of pre-scattered (small-level) fronts
+  DevBuf<long long> pre_dst, zero_rng;
+  DevBuf<int> pre_src;
+  int nzero = 0;
   DevBuf<launch::FrontDesc> fd;
   DevBuf<int> children, relmap, rows, perm;
   std::vector<int> level_off;  // host offsets of each level's fronts in the level order
   std::vector<int> bwd_off;    // per level: offset of its backward-gemv tasks in `tasks` (+1 end)
   int max_ns = 0;
-  struct Op { int kind, off, count; };  // kind 0 extend-add, 1 first diagonal block, 2 panel step, 3 contribution block
+  struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add, 2 panel step, 3 syrk
   std::vector<Op> ops;
   DevBuf<launch::Task> tasks;
   DevBuf<launch::StepTask> step_tasks;

@@ -91,14 +91,18 @@ struct StepTask {  // k_step work item, self-contained so a workgroup needs one 
               // 32 no next-diagonal task this step (blocked front, big-panel boundary): writers update every row
   int clim;   // tile updates stop at this front column (ns, m when fused, the big-panel end when blocked)
 };
-void chol_scatter(long long nent, const double* vals, const long long* dst, const unsigned char* is_diag,
-                  const double* lam, double* fronts, hipStream_t s);
+// zero ranges (offset, length pairs) of the front pool, then scatter input entries: fronts[dst[k]] =
+// vals[src[k] & 0x7fffffff] (+ lambda when src[k] < 0)
+void chol_prescatter(int nzero, const long long* zr, long long nent, const double* vals, const long long* dst,
+                     const int* src, const double* lam, double* fronts, hipStream_t s);
 void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double* vecs, hipStream_t s);
-// extend-add of a level (slab tasks, t.c == 0) with every front's first diagonal block assembled,
-// factored and forward-solved beside it (t.c == 1)
+// assembly + extend-add of a level (slab tasks, t.c == 0: columns [a, b)) with every front's first
+// diagonal block assembled, factored and forward-solved beside it (t.c == 1). Input entries of scalar
+// column c (permuted): ent_row/ent_src[colptr[c] .. colptr[c+1]) = row in the front | diag << 30, index in vals
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
+                     const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
-                     hipStream_t s);
+                     bool assemble, hipStream_t s);
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
                double* linv, double* xinv, int* fail, hipStream_t s);
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
@@ -111,6 +115,6 @@ void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int
 void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,
                 hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only
-constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 4, CHOL_BW = 4;
+constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 16, CHOL_BW = 4;
 }  // namespace launch
 }  // namespace g2ohip

@@ -132,14 +132,15 @@ def _dense_spd_ccs(rng, n, density):
     return A, Ap, Ai, Ax
 
 
-@pytest.mark.parametrize("pb", [64, 128, 256])
-def test_linear_solver_blocked_fronts(g2o_amd_mod, monkeypatch, pb):
+@pytest.mark.parametrize("pb,pre_max", [(64, "0"), (128, "1000000000000"), (256, "0")])
+def test_linear_solver_blocked_fronts(g2o_amd_mod, monkeypatch, pb, pre_max):
     """Wide supernodes factored in big panels (rank-32 steps inside a panel, one rank-PB trailing update
     per panel, first block of the next panel on its own): same solution as the unblocked schedule."""
     rng = np.random.default_rng(11)
     n = 1800
     A, Ap, Ai, Ax = _dense_spd_ccs(rng, n, 0.05)
     b = rng.standard_normal(n)
+    monkeypatch.setenv("G2OHIP_CHOL_PRE_MAX", pre_max)
     monkeypatch.setenv("G2OHIP_CHOL_FUSED_MAX", "0")
     monkeypatch.setenv("G2OHIP_CHOL_BLOCK_MIN", "1000000")
     ok0, x0 = g2o_amd_mod.linear_solve_ccs(n, Ap, Ai, Ax, b, block_dim=6)
@@ -151,8 +152,11 @@ def test_linear_solver_blocked_fronts(g2o_amd_mod, monkeypatch, pb):
     assert np.linalg.norm(x1 - x0) <= 1e-12 * np.linalg.norm(x0)
 
 
-def test_lm_blocked_fronts_sphere2500(g2o_amd_mod, oracle, monkeypatch):
-    """C1 full size with every supernode wider than 32 columns blocked (PB = 64)."""
+@pytest.mark.parametrize("pre_max", ["0", "1000000000000"])
+def test_lm_blocked_fronts_sphere2500(g2o_amd_mod, oracle, monkeypatch, pre_max):
+    """C1 full size with every supernode wider than 32 columns blocked (PB = 64); fronts assembled in
+    place by the level launches (pre_max 0) or zeroed + scattered before the first level (all levels)."""
+    monkeypatch.setenv("G2OHIP_CHOL_PRE_MAX", pre_max)
     monkeypatch.setenv("G2OHIP_CHOL_FUSED_MAX", "0")
     monkeypatch.setenv("G2OHIP_CHOL_BLOCK_MIN", "32")
     monkeypatch.setenv("G2OHIP_CHOL_PB", "64")

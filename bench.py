@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=2, help="timed oracle LM iterations (after iteration 0)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="OpenMP threads for the CPU baseline (0 = all)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-posegraph", action="store_true", help="skip the C3 (100k-pose SE3) secondary leg")
     return ap.parse_args()
 
 
@@ -105,6 +106,52 @@ def cpu_baseline(prob, iters, threads):
         "sample": f"{len(timed)} LM iterations (after iteration 0) of the same {prob.name} problem: oracle C++ "
                   f"restatement of BlockSolver/Schur/LM (OpenMP {nthreads} threads for assembly+Schur) with "
                   f"the reference's vendored CSparse 3.1.0 cs_amd(block)+LL^T ({'loaded' if oracle_py.ref_available() else 'restated'}), single-threaded factorization as in the reference",
+    }
+
+
+def solver_name(prob):
+    if prob.landmark_dim:
+        return f"BlockSolver_{prob.pose_dim}_{prob.landmark_dim} + Schur"
+    return f"BlockSolver_{prob.pose_dim}_{prob.pose_dim} (no Schur)"
+
+
+def posegraph_leg(local, steps=5, warmup=1):
+    """The metric's second workload (BASELINE config C3: 100k-pose SE3 pose graph, 500k edges,
+    BlockSolver_6_6, no Schur), measured the same way on the same GPU: LM it/s, ms/linear-solve and the
+    supernodal factorization's MFMA throughput against the FP64 peak."""
+    import g2o_amd
+    prob = make_problem("C3")
+    opt = g2o_amd.SparseOptimizer(local).add_problem(prob)
+    opt.set_algorithm("lm_hip_fix6_6")
+    it = 0
+    for _ in range(max(warmup, 1)):
+        opt.optimize_step(it)
+        it += 1
+    opt.set_stats_level(1)
+    t0 = time.perf_counter()
+    timed = []
+    for _ in range(steps):
+        timed.append(opt.optimize_step(it)[1])
+        it += 1
+    dt = time.perf_counter() - t0  # optimize_step returns after the trial's scalar readback: device idle
+    opt.enable_kernel_timing(True, only="chol_factor")
+    opt.set_stats_level(2)
+    for _ in range(2):
+        opt.optimize_step(it)
+        it += 1
+    fms = opt.kernel_ms("chol_factor")
+    flops = opt.kernel_flops("chol_factor")
+    tf = flops / (fms * 1e-3) / 1e12 if fms > 0 else 0.0
+    lin = [1e3 * s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
+    return {
+        "workload": f"C3: {prob.name} ({prob.num_vertices} poses, {prob.num_edges} edges), {solver_name(prob)}",
+        "value": steps / dt,
+        "unit": "LM it/s",
+        "ms_per_linear_solve": float(np.median(lin)),
+        "steps": steps,
+        "final_chi2": timed[-1].chi2,
+        "factor": {"bound": "mfma", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                   "frac": tf / PEAK_FP64_TFLOPS, "flops_per_launch": flops, "avg_launch_ms": fms},
     }
 
 
@@ -199,7 +246,7 @@ def main():
         "data": "synthetic (numpy Philox seed 20261015, BAL-style recipe of ba_demo.cpp; SURVEY.md 8d)",
         "config": {
             "workload": f"{args.config}: {prob.name} ({prob.num_vertices} vertices, {prob.num_edges} edges), "
-                        f"BlockSolver_6_3 + Schur, landmarks sharded over {world} GPU(s)",
+                        f"{solver_name(prob)}" + (f", landmarks sharded over {world} GPU(s)" if prob.landmark_dim else ""),
             "levenberg_trials": trials,
             "final_chi2": timed[-1].chi2 if timed else None,
             "parallelism": f"landmark-shard{world}" if world > 1 else "single",
@@ -219,6 +266,11 @@ def main():
         },
         "setup_s": {"generate": gen_s, "warmup_incl_structure": warm_s},
     }
+    if rank == 0 and world == 1 and not args.no_posegraph and args.config == "C4":
+        try:
+            out["pose_graph"] = posegraph_leg(local)
+        except Exception as ex:  # reported, not fatal
+            out["pose_graph"] = {"error": repr(ex)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(prob, args.cpu_iters, args.cpu_threads)

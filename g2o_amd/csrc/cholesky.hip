@@ -217,13 +217,13 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, d
 }
 
 // Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid) and
-// forward-solve vy (LDS, kb values) in place. On return D holds L (lower, with diagonal).
-// Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid) and
-// forward-solve vy (LDS, kb values) in place. On return D holds L (lower, with diagonal).
+// forward-solve vy (LDS, kb values); L goes to L (leading dimension ldl, the block's first entry) and y to
+// ysol straight from the registers.
 // Lanes 32..63 run the same instruction stream on the identity: lane 32 + c ends holding column c
 // of L^-1 (right-looking substitution on the broadcast columns of L), written row-major to linv.
 __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, double* col, int lane, int* fail,
-                                             double* linv, double* X, int ldx, unsigned long long* ph = nullptr) {
+                                             double* linv, double* X, int ldx, double* L, int ldl, double* ysol,
+                                             unsigned long long* ph = nullptr) {
   double row[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
@@ -235,10 +235,11 @@ __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, doub
   const bool ok = chol32(row, y, lane, col);
   if (ph) { asm volatile("" : "+v"(row[NB - 1])); ph[6] = __builtin_amdgcn_s_memtime(); }
   if (lane == 0 && !ok) *fail = 1;
-  if (lane < kb) {  // whole row (the upper part is never read back)
+  if (lane < kb) {  // publish L (column c: lanes c..kb-1 store consecutive rows) and y straight from registers
 #pragma unroll
-    for (int c = 0; c < NB; ++c) D[lane * DS + c] = row[c];
-    vy[lane] = y;
+    for (int c = 0; c < NB; ++c)
+      if (c <= lane) L[(size_t)c * ldl + lane] = row[c];
+    ysol[lane] = y;
   }
   if (lane >= NB) {
 #pragma unroll
@@ -251,17 +252,6 @@ __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, doub
     }
   }
 }
-__device__ __forceinline__ void publish_block(const double* D, const double* vy, int kb, double* L, int m, int r0,
-                                              double* ysol, int tid) {
-#pragma unroll
-  for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
-    const int e = tid + 256 * u_;
-    const int r = e & (NB - 1), c = e >> 5;
-    if (r < kb && c < kb && r >= c) L[(size_t)(r0 + c) * m + r0 + r] = D[r * DS + c];
-  }
-  if (tid < kb) ysol[r0 + tid] = vy[tid];
-}
-
 // ---------------------------------------------------------------------------- assembly + extend-add
 // One launch per level assembles every front of the level from scratch (no front-pool memset, no
 // separate scatter pass), with two kinds of workgroup:
@@ -346,10 +336,9 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     }
     PH(2)
     if (tid < 64)
-      factor_block(D, kb0, vy, col, tid, fail, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns, PH_REC);
-    __syncthreads();
+      factor_block(D, kb0, vy, col, tid, fail, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns,
+                   lbuf + me.l_off, m, ysol + me.c0, PH_REC);
     PH(3)
-    publish_block(D, vy, kb0, lbuf + me.l_off, m, 0, ysol + me.c0, tid);
     PH(4)
     return;
   }
@@ -560,10 +549,8 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     PH(2)
     if (tid < 64)
       factor_block(Dn, kbn, vn, col, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB),
-                   xinv + t.x_off + (size_t)r0 * ns + r0, ns, PH_REC);
-    __syncthreads();
+                   xinv + t.x_off + (size_t)r0 * ns + r0, ns, L + (size_t)r0 * m + r0, m, ysol + t.c0 + r0, PH_REC);
     PH(3)
-    publish_block(Dn, vn, kbn, L, m, r0, ysol + t.c0, tid);
     PH(4)
     return;
   }

@@ -316,6 +316,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const char* bp = getenv("G2OHIP_CHOL_PB");  // dev A/B: big-panel width (multiple of 64)
     const int block_pb = bp ? std::max(64, atoi(bp) / 64 * 64) : 256;
     const bool dev_noinv = getenv("G2OHIP_DEV_NOINV") != nullptr;  // timing experiments only (wrong solve)
+    const bool dev_diagonly = getenv("G2OHIP_DEV_DIAGONLY") != nullptr;  // timing experiments only (wrong factor)
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
     const long long pre_max = pm ? atoll(pm) : (256LL << 20);
     std::vector<long long> zr, pdst;
@@ -401,8 +402,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
             for (int j = 0; j < p; ++j) inv_t.push_back(mk(j | (bp << 16), 16));
         }
         stk.insert(stk.end(), diag_t.begin(), diag_t.end());
-        stk.insert(stk.end(), tile_t.begin(), tile_t.end());
-        stk.insert(stk.end(), inv_t.begin(), inv_t.end());
+        if (!dev_diagonly) stk.insert(stk.end(), tile_t.begin(), tile_t.end());
+        if (!dev_diagonly) stk.insert(stk.end(), inv_t.begin(), inv_t.end());
         st.count = (int)stk.size() - st.off;
         if (st.count) ops.push_back(st);
         if ((p + 1) * NB % block_pb) continue;

@@ -25,6 +25,7 @@ def main():
     n = L.g2ohip_debug_phases(buf, 4096)
     a = np.frombuffer(buf, dtype=np.uint64, count=8 * n).reshape(n, 8).astype(np.int64)
     print(f"{n} records")
+    periods(a)
     for kid, name, labels in ((1, "k_extend_add block-0 task", ["stage+assemble", "factor", "publish"]),
                               (2, "k_step(diag task)", ["stage+trsm+syrk", "factor", "publish"]),
                               (3, "k_step(tile 0,0)", ["stage", "trsm+L21", "update+store"])):
@@ -44,6 +45,20 @@ def main():
             ok = (t[:, i + 1] > 0) & (t[:, i] > 0)
             if ok.any():
                 print(f"   {lab:16s} median {np.median(d[ok]) / CLK:7.2f} us  mean {np.mean(d[ok]) / CLK:7.2f} us  (n={ok.sum()})")
+
+
+def periods(a):
+    """Diag-task chain: start-to-start period of consecutive k_step diag records vs the task's own span."""
+    r = a[a[:, 0] == 2]
+    if len(r) < 3:
+        return
+    st = r[:, 1]
+    en = r[:, 4]
+    per = np.diff(st) / CLK
+    own = (en - st) / CLK
+    ok = (per > 0) & (per < 100)
+    print(f"diag chain: period median {np.median(per[ok]):.2f} us, task span median {np.median(own):.2f} us, "
+          f"gap (period - span) median {np.median(per[ok] - own[:-1][ok]):.2f} us")
 
 
 if __name__ == "__main__":

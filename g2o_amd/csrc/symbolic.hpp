@@ -55,11 +55,15 @@ struct Symbolic {
 };
 
 // Nested-dissection ordering of the block graph. leaf_size: subgraphs at most this
-// large are ordered by minimum degree.
-std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size = 48);
+// large are ordered by minimum degree; refine: greedy separator refinement after each bisection.
+std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size = 48, bool refine = false);
+
+// Modelled GPU factor time of a symbolic analysis (seconds): flops at the MFMA rate plus the
+// level-synchronous panel-step chain.
+double gpu_cost(const Symbolic& S);
 
 // Full symbolic analysis with a given block ordering (bperm: new->old). If bperm is
-// empty, nested dissection is used.
+// empty, nested dissection is used (with or without separator refinement, whichever models faster).
 Symbolic analyze(const BlockPattern& P, std::vector<int> bperm = {}, double relax = 0.25, int relax_max_blocks = 64);
 
 }  // namespace g2ohip

@@ -275,7 +275,7 @@ __device__ __forceinline__ double input_entry(const double* vals, const int* ent
 template <bool ASM>  // ASM: the level's fronts are assembled here; else they were pre-zeroed and scattered
 __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                     const int* __restrict__ children, const int* __restrict__ relmap,
-                                                    const int* __restrict__ colptr, const int* __restrict__ ent_row,
+                                                    const int* __restrict__ jtab, const int* __restrict__ colptr, const int* __restrict__ ent_row,
                                                     const int* __restrict__ ent_src, const double* __restrict__ vals,
                                                     const double* __restrict__ lam, double* __restrict__ fronts,
                                                     double* __restrict__ vecs, double* __restrict__ lbuf,
@@ -323,8 +323,7 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
       const int mc = cd.ns + cd.nr, nrc = cd.nr;
       const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;
       const int* rel = relmap + cd.rows_off;
-      int n0 = 0;  // child rows mapping into the block (rel is increasing)
-      while (n0 < nrc && n0 < NB && rel[n0] < kb0) ++n0;
+      const int n0 = jtab[cd.jt_off];  // child rows mapping into the block (rel is increasing)
 #pragma unroll
       for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
         const int e = tid + 256 * u_;
@@ -369,13 +368,8 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;  // U(i,j) = U[j*mc + i]
     const double* u = vecs + cd.vec_off + cd.ns;
     const int* rel = relmap + cd.rows_off;
-    // child columns whose parent column lies in [a, b) (rel is increasing)
-    int lo = 0, hi = nrc;
-    while (lo < hi) { const int mid = (lo + hi) >> 1; if (rel[mid] < a) lo = mid + 1; else hi = mid; }
-    const int j0 = lo;
-    hi = nrc;
-    while (lo < hi) { const int mid = (lo + hi) >> 1; if (rel[mid] < b) lo = mid + 1; else hi = mid; }
-    const int j1 = lo;
+    // child columns whose parent column lies in [a, b) (rel is increasing; precomputed per slab)
+    const int j0 = jtab[cd.jt_off + t.c - 1], j1 = jtab[cd.jt_off + t.c];
     for (int j = j0 + tid; j < j1; j += 256)
       if (rel[j] >= kb0) v[rel[j]] += u[j];
     // lower triangle: one wave per child column, lanes run down the rows (coalesced U reads,
@@ -827,15 +821,15 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double
   KERNEL_CHECK();
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
-                     const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
+                     const int* jtab, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
                      bool assemble, hipStream_t s) {
   if (ntasks <= 0) return;
   if (assemble)
-    hipLaunchKernelGGL(k_extend_add<true>, ntasks, 256, 0, s, tasks, fd, children, relmap, colptr, ent_row, ent_src, vals,
+    hipLaunchKernelGGL(k_extend_add<true>, ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, colptr, ent_row, ent_src, vals,
                        lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
   else
-    hipLaunchKernelGGL(k_extend_add<false>, ntasks, 256, 0, s, tasks, fd, children, relmap, colptr, ent_row, ent_src, vals,
+    hipLaunchKernelGGL(k_extend_add<false>, ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, colptr, ent_row, ent_src, vals,
                        lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }

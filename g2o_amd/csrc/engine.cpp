@@ -280,17 +280,38 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     ent_srcv.swap(hs);
     edsts.swap(hd);
   }
+  // extend-add slab width per level: EA columns where the level has enough of them to fill the chip
+  // several times over, else 4 (latency-bound upper levels)
+  std::vector<int> level_slab(sym.levels.size(), 4), sn_level(sym.sn.size(), 0);
+  for (size_t l = 0; l < sym.levels.size(); ++l) {
+    long long lcols = 0;
+    for (int sn : sym.levels[l]) { lcols += sym.sn[sn].ns + sym.sn[sn].nr; sn_level[sn] = (int)l; }
+    level_slab[l] = lcols >= 16LL * launch::CHOL_EA * 256 ? launch::CHOL_EA : 4;
+  }
+  // per child: [#rows mapping into the parent's first diagonal block | first child row of every parent
+  // slab] (rel is increasing), so the extend-add tasks need no search on the chain
+  std::vector<int> hjt;
   std::vector<launch::FrontDesc> hfd(sym.sn.size());
   long long loff = 0, xoff = 0;
   for (size_t k = 0; k < sym.sn.size(); ++k) {
     const Supernode& q = sym.sn[k];
+    int jt = 0;
+    if (q.parent >= 0) {
+      const Supernode& pq = sym.sn[q.parent];
+      const int mp = pq.ns + pq.nr, slab = level_slab[sn_level[q.parent]], kb0 = std::min(launch::CHOL_NB, pq.ns);
+      const int* rel = sym.relmap.data() + q.rows_off;
+      jt = (int)hjt.size();
+      hjt.push_back((int)(std::lower_bound(rel, rel + q.nr, kb0) - rel));
+      for (int a = 0; a < mp + slab; a += slab) hjt.push_back((int)(std::lower_bound(rel, rel + q.nr, std::min(a, mp)) - rel));
+    }
     hfd[k] = launch::FrontDesc{q.front_off, q.vec_off, loff, q.rows_off, xoff, q.c0, q.ns, q.nr, q.parent,
-                               sym.children_ptr[k], sym.children_ptr[k + 1]};
+                               sym.children_ptr[k], sym.children_ptr[k + 1], jt};
     loff += (long long)(q.ns + q.nr) * q.ns;
     xoff += (long long)q.ns * q.ns;  // X = L11^-1, column-major
   }
   lpool = loff;
   fd.upload(hfd, s);
+  jtab.upload(hjt.empty() ? std::vector<int>{0} : hjt, s);
   std::vector<int> ll;
   level_off.assign(1, 0);
   for (auto& lv : sym.levels) {
@@ -351,14 +372,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       for (int sn : lv) tk.push_back(Task{sn, 0, 0, 1});
       // every front is assembled here (input entries, zeros, children); slabs of EA columns where the level
       // has enough of them to fill the chip several times over, else 4 (latency-bound upper levels)
-      long long lcols = 0;
-      for (int sn : lv) lcols += sym.sn[sn].ns + sym.sn[sn].nr;
-      const int slab = lcols >= 16LL * EA * 256 ? EA : 4;
+      const int slab = level_slab[l];
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
         const int m = q.ns + q.nr;
         if (pre && sym.children_ptr[sn + 1] == sym.children_ptr[sn]) continue;  // nothing left to assemble
-        for (int a = 0; a < m; a += slab) tk.push_back(Task{sn, a, std::min(a + slab, m), 0});
+        for (int a = 0; a < m; a += slab) tk.push_back(Task{sn, a, std::min(a + slab, m), 2 + a / slab});
       }
       ea.count = (int)tk.size() - ea.off;
       ops.push_back(ea);
@@ -478,7 +497,8 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
     const launch::Task* t = tasks.get() + op.off;
     switch (op.kind) {
       case 0:
-      case 4: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), colptr.get(), ent_row.get(),
+      case 4: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), colptr.get(),
+                                      ent_row.get(),
                                       ent_src.get(), vals, lam, fronts.get(), vecs.get(),
                                       lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 4, s); break;
       case 2: launch::chol_step(op.count, step_tasks.get() + op.off, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),

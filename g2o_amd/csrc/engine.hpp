@@ -51,6 +51,7 @@ struct DeviceCholesky {
   int pd = 0;
   long long nent = 0;
   DevBuf<int> colptr, ent_row, ent_src;  // input entries per permuted scalar column (k_extend_add)
+  DevBuf<int> jtab;                       // per child: row ranges per parent slab (FrontDesc::jt_off)
   long long npre = 0;                     // entries of pre-scattered (small-level) fronts
   DevBuf<long long> pre_dst, zero_rng;
   DevBuf<int> pre_src;

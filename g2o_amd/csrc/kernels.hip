@@ -450,7 +450,7 @@ constexpr int SCH_NC = (SCH_SB * 9 + 255) / 256;  // 16-B pieces per thread per 
 static_assert(SCH_SB * 9 % 64 == 0, "a wave's LDS-DMA pieces must tile the batch image");
 }  // namespace
 
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
                  const int* __restrict__ st_obs, const int* __restrict__ pairs, const int* __restrict__ pp,
                  const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,

@@ -35,7 +35,7 @@ void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, 
                 const double* b, const double* lam, double* S, double* bschur, double* G, hipStream_t s);
 // row-stationary off-diagonal Schur pass (k_schur_rows): task = (camera row, <= SCHUR_SL off-diagonal
 // slots), batch = <= SCHUR_SB staged observation blocks of the row's landmarks
-constexpr int SCHUR_SB = 256, SCHUR_SL = 64;
+constexpr int SCHUR_SB = 128, SCHUR_SL = 64;  // 128: 4 workgroups per CU (LDS), 150 vs 172 us at C4
 struct SchurTask {
   int row, noff;  // camera row, number of off-diagonal slots of this task
   int b0, b1;     // batches

@@ -46,6 +46,22 @@ int main() {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     printf("chain of launches, %-16s %6.2f us per launch\n", c.name, ms * 1e3 / N);
   }
+  // the same chains captured into a hipGraph and replayed
+  for (auto& c : cfg) {
+    hipStream_t st; CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipGraph_t g; hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+    for (int i = 0; i < N; ++i) hipLaunchKernelGGL(k_tiny, c.grid, 256, 0, st, p, c.nwrite);
+    CK(hipStreamEndCapture(st, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, st)); CK(hipStreamSynchronize(st));
+    CK(hipEventRecord(e0, st));
+    CK(hipGraphLaunch(ge, st));
+    CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("graph of launches, %-16s %6.2f us per launch\n", c.name, ms * 1e3 / N);
+    CK(hipGraphExecDestroy(ge)); CK(hipGraphDestroy(g)); CK(hipStreamDestroy(st));
+  }
   const int iters = 2000;
   for (int sc = 0; sc < 2; ++sc)
     for (int pair = 0; pair < 2; ++pair) {

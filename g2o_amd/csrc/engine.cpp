@@ -336,6 +336,10 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const int block_min = bm ? atoi(bm) : 512;
     const char* bp = getenv("G2OHIP_CHOL_PB");  // dev A/B: big-panel width (multiple of 64)
     const int block_pb = bp ? std::max(64, atoi(bp) / 64 * 64) : 256;
+    const char* wf = getenv("G2OHIP_CHOL_WIDE_FRONTS");  // dev A/B: fronts per level that make it "wide"
+    const int wide_fronts = wf ? atoi(wf) : 64;
+    const char* wp = getenv("G2OHIP_CHOL_WIDE_PB");
+    const int wide_pb = wp ? std::max(64, atoi(wp) / 64 * 64) : 128;
     const bool dev_noinv = getenv("G2OHIP_DEV_NOINV") != nullptr;  // timing experiments only (wrong solve)
     const bool dev_diagonly = getenv("G2OHIP_DEV_DIAGONLY") != nullptr;  // timing experiments only (wrong factor)
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
@@ -387,7 +391,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       // updates of the panel steps stop at the end of the current big panel of PB columns; after each big
       // panel one high-intensity k_syrk launch applies its rank-PB update to the rest of the supernode's
       // columns, and a next-diagonal task (kb = 0) factors the first block of the next big panel
-      auto blocked = [&](const Supernode& q) { return !fused_contrib && q.ns > block_min; };
+      // throughput-bound levels (many fronts: the panel steps' rank-32 tile traffic, not the diagonal
+      // chain, sets their time) block every front wider than one small big panel
+      const bool wide = (int)lv.size() >= wide_fronts;
+      const int lpb = wide ? wide_pb : block_pb, lmin = wide ? wide_pb : block_min;
+      auto blocked = [&](const Supernode& q) { return !fused_contrib && q.ns > lmin; };
       for (int p = 0; p < maxp; ++p) {
         Op st{2, (int)stk.size(), 0};
         // task order inside the launch (= dispatch order): every front's next-diagonal task first (the
@@ -400,7 +408,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           if (k0 >= q.ns) continue;
           const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
           const bool blk = blocked(q);
-          const int pend = blk ? std::min((k0 / block_pb + 1) * block_pb, q.ns) : q.ns;  // big-panel end
+          const int pend = blk ? std::min((k0 / lpb + 1) * lpb, q.ns) : q.ns;  // big-panel end
           const bool bnd = blk && r0 == pend && r0 < q.ns;  // next block starts a big panel: no diag task
           // fused: every panel step also applies its rank-kb update to the contribution block (the
           // step is latency-bound on the diagonal chain, the extra tiles run in its shadow)
@@ -425,13 +433,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         if (!dev_diagonly) stk.insert(stk.end(), inv_t.begin(), inv_t.end());
         st.count = (int)stk.size() - st.off;
         if (st.count) ops.push_back(st);
-        if ((p + 1) * NB % block_pb) continue;
+        if ((p + 1) * NB % lpb) continue;
         // end of a big panel: trailing update of the blocked fronts, then their next first blocks
         Op gm{3, (int)tk.size(), 0};
         Op d0{2, (int)stk.size(), 0};
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
-          const int kb = (p + 1) * NB, ka = kb - block_pb, m = q.ns + q.nr;
+          const int kb = (p + 1) * NB, ka = kb - lpb, m = q.ns + q.nr;
           if (!blocked(q) || kb >= q.ns) continue;
           const int T = (m - kb + TT - 1) / TT, TJ = (q.ns - kb + TT - 1) / TT;
           for (int tj = 0; tj < TJ; ++tj)

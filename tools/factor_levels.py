@@ -12,7 +12,7 @@ b = next(i for i in range(a, len(rows)) if 'k_bwd_gemv' in rows[i]['Kernel_Name'
 seg = rows[a + 1:b]
 levels, cur = [], None
 for r in seg:
-    name = r['Kernel_Name'].split('(')[0].replace('g2ohip::', '')
+    name = r['Kernel_Name'].split('(')[0].replace('g2ohip::', '').replace('void ', '').split('<')[0]
     if cur is None or (name == 'k_extend_add' and cur['has_ea']):
         cur = {'k': collections.defaultdict(float), 'n': collections.Counter(), 't0': int(r['Start_Timestamp']), 'has_ea': False}
         levels.append(cur)

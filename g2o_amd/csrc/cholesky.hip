@@ -769,20 +769,40 @@ __global__ void __launch_bounds__(256) k_bwd_x(const Task* __restrict__ tasks, c
   const FrontDesc me = fd[t.s];
   const int ns = me.ns;
   const int lane = threadIdx.x & 63, j = t.a + (int)(threadIdx.x >> 6);
-  if (j >= ns) return;
+  if (j >= (t.b ? t.b : ns)) return;
   const double* xc = xinv + me.x_off + (size_t)j * ns;  // column j of X (rows >= j are nonzero)
   const double* tt = tsol + me.c0;
+  const int ie = t.c;  // X(j.., j) up to row ie: ns, or the end of a blocked front's big panel (X_bb)
   double a4[4] = {0.0, 0.0, 0.0, 0.0};
   int i = j + lane;
-  for (; i + 192 < ns; i += 256) {
+  for (; i + 192 < ie; i += 256) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) a4[u] += xc[i + 64 * u] * tt[i + 64 * u];
   }
-  for (; i < ns; i += 64) a4[0] += xc[i] * tt[i];
+  for (; i < ie; i += 64) a4[0] += xc[i] * tt[i];
   double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if (lane == 0) xsol[me.c0 + j] = acc;
+}
+
+// blocked fronts: t_j -= sum_{i in [t.b, ns)} L(i, j) x_i for the columns j of one big panel (the later big
+// panels of the supernode are solved already); one wave per column
+__global__ void __launch_bounds__(256) k_bwd_inner(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                                   const double* __restrict__ lbuf, const double* __restrict__ xsol,
+                                                   double* __restrict__ tsol) {
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int m = me.ns + me.nr, ns = me.ns;
+  const int lane = threadIdx.x & 63, j = t.a + (int)(threadIdx.x >> 6);
+  if (j >= t.b) return;
+  const double* col = lbuf + me.l_off + (size_t)j * m;
+  const double* xx = xsol + me.c0;
+  double acc = 0.0;
+  for (int i = t.b + lane; i < ns; i += 64) acc += col[i] * xx[i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) tsol[me.c0 + j] -= acc;
 }
 
 namespace launch {
@@ -858,6 +878,12 @@ void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int
                    const double* ysol, const double* xsol, double* tsol, hipStream_t s) {
   if (ntasks <= 0) return;
   hipLaunchKernelGGL(k_bwd_gemv, ntasks, 256, 0, s, tasks, fd, rows, lbuf, ysol, xsol, tsol);
+  KERNEL_CHECK();
+}
+void chol_bwd_inner(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* xsol, double* tsol,
+                    hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_bwd_inner, ntasks, 256, 0, s, tasks, fd, lbuf, xsol, tsol);
   KERNEL_CHECK();
 }
 void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,

@@ -325,6 +325,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const int NB = launch::CHOL_NB, TT = launch::CHOL_TT, EA = launch::CHOL_EA;
     std::vector<Task> tk;
     std::vector<launch::StepTask> stk;
+    std::vector<int> sn_pb(sym.sn.size(), 0);  // big-panel width of blocked fronts (0: unblocked)
     ops.clear();
     // contribution blocks: fused into the panel steps (each step's rank-32 update also reaches the
     // contribution block) where the steps are latency-bound on the diagonal chain and the extra tiles
@@ -423,10 +424,15 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           for (int tj = 0; tj < std::max(TJ, 1); ++tj)
             for (int ti = tj; ti < T; ++ti) tile_t.push_back(mk(ti | (tj << 16), (tj < TJ ? 1 : 0) | fl));
           // inverse tasks: block row p-1's term into every pending block (bp, j), bp >= p, j < p;
-          // block row p is final after this step
+          // block row p is final after this step. Blocked fronts build only the diagonal big-panel
+          // blocks of X (their backward solve substitutes big panel by big panel)
           const int nblk = (q.ns + NB - 1) / NB;
-          for (int bp = p; bp < nblk && p >= 1 && !dev_noinv; ++bp)
-            for (int j = 0; j < p; ++j) inv_t.push_back(mk(j | (bp << 16), 16));
+          const bool bsolve = blk && q.ns > block_min;  // narrower blocked fronts keep the full X
+          const int ib0 = bsolve ? (k0 / lpb) * (lpb / NB) : 0;
+          const int ib1 = bsolve ? std::min(nblk, ib0 + lpb / NB) : nblk;
+          if (bsolve) sn_pb[sn] = lpb;
+          for (int bp = p; bp < ib1 && p - 1 >= ib0 && !dev_noinv; ++bp)
+            for (int j = ib0; j < p; ++j) inv_t.push_back(mk(j | (bp << 16), 16));
         }
         stk.insert(stk.end(), diag_t.begin(), diag_t.end());
         if (!dev_diagonly) stk.insert(stk.end(), tile_t.begin(), tile_t.end());
@@ -468,15 +474,54 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     zero_rng.upload(zr.empty() ? std::vector<long long>{0, 0} : zr, s);
     pre_dst.upload(pdst.empty() ? std::vector<long long>{0} : pdst, s);
     pre_src.upload(psrc.empty() ? std::vector<int>{0} : psrc, s);
-    // backward-solve gemv tasks per level: (front, 4 columns)
+    // backward solve per level: gemv tasks (front, 4 columns) for every front, then x = X^T t for the
+    // unblocked fronts (one launch) and, for blocked fronts, rounds over their big panels from the last:
+    // t_b -= L(later rows of the supernode, b)^T x, x_b = X_bb^T t_b
     bwd_off.assign(1, (int)tk.size());
+    bwd_ops.clear();
     max_ns = 1;
-    for (auto& lv : sym.levels) {
+    for (size_t l = 0; l < sym.levels.size(); ++l) {
+      const auto& lv = sym.levels[l];
+      BwdLevel bl;
+      bl.gemv = {(int)tk.size(), 0};
       for (int sn : lv) {
         const int ns = sym.sn[sn].ns;
         max_ns = std::max(max_ns, ns);
         for (int a = 0; a < ns; a += launch::CHOL_BW) tk.push_back(Task{sn, a, 0, 0});
       }
+      bl.gemv.second = (int)tk.size() - bl.gemv.first;
+      bl.xall = {(int)tk.size(), 0};
+      int rounds = 0;
+      for (int sn : lv) {
+        const int ns = sym.sn[sn].ns;
+        if (sn_pb[sn]) { rounds = std::max(rounds, (ns + sn_pb[sn] - 1) / sn_pb[sn]); continue; }
+        for (int a = 0; a < ns; a += launch::CHOL_BW) tk.push_back(Task{sn, a, 0, ns});
+      }
+      bl.xall.second = (int)tk.size() - bl.xall.first;
+      for (int r = 0; r < rounds; ++r) {
+        std::pair<int, int> g{(int)tk.size(), 0}, x{0, 0};
+        for (int sn : lv) {  // inner gemv: t_b -= L([be, ns), b)^T x([be, ns))
+          const int ns = sym.sn[sn].ns, pb = sn_pb[sn];
+          if (!pb) continue;
+          const int nbp = (ns + pb - 1) / pb, b = nbp - 1 - r;
+          if (b < 0 || r == 0) continue;
+          const int bs = b * pb, be = std::min(ns, bs + pb);
+          for (int a = bs; a < be; a += launch::CHOL_BW) tk.push_back(Task{sn, a, be, 0});
+        }
+        g.second = (int)tk.size() - g.first;
+        x.first = (int)tk.size();
+        for (int sn : lv) {  // x_b = X_bb^T t_b
+          const int ns = sym.sn[sn].ns, pb = sn_pb[sn];
+          if (!pb) continue;
+          const int nbp = (ns + pb - 1) / pb, b = nbp - 1 - r;
+          if (b < 0) continue;
+          const int bs = b * pb, be = std::min(ns, bs + pb);
+          for (int a = bs; a < be; a += launch::CHOL_BW) tk.push_back(Task{sn, a, be, be});
+        }
+        x.second = (int)tk.size() - x.first;
+        bl.rounds.push_back({g, x});
+      }
+      bwd_ops.push_back(bl);
       bwd_off.push_back((int)tk.size());
     }
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
@@ -519,10 +564,14 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
 
 void DeviceCholesky::solve(double* x, hipStream_t s) {
   for (size_t l = level_off.size() - 1; l-- > 0;) {  // root level first
-    const int nt = bwd_off[l + 1] - bwd_off[l];
-    launch::chol_bwd_gemv(nt, tasks.get() + bwd_off[l], fd.get(), rows.get(), lbuf.get(), y_p.get(), x_p.get(), t_p.get(),
-                          s);
-    launch::chol_bwd_x(nt, tasks.get() + bwd_off[l], fd.get(), xinv.get(), t_p.get(), x_p.get(), s);
+    const BwdLevel& bl = bwd_ops[l];
+    launch::chol_bwd_gemv(bl.gemv.second, tasks.get() + bl.gemv.first, fd.get(), rows.get(), lbuf.get(), y_p.get(),
+                          x_p.get(), t_p.get(), s);
+    launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), t_p.get(), x_p.get(), s);
+    for (const auto& rd : bl.rounds) {
+      launch::chol_bwd_inner(rd.first.second, tasks.get() + rd.first.first, fd.get(), lbuf.get(), x_p.get(), t_p.get(), s);
+      launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), t_p.get(), x_p.get(), s);
+    }
   }
   launch::chol_ipermute(sym.n, perm.get(), x_p.get(), x, s);
 }

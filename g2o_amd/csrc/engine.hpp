@@ -60,6 +60,11 @@ struct DeviceCholesky {
   DevBuf<int> children, relmap, rows, perm;
   std::vector<int> level_off;  // host offsets of each level's fronts in the level order
   std::vector<int> bwd_off;    // per level: offset of its backward-gemv tasks in `tasks` (+1 end)
+  struct BwdLevel {            // backward solve of one level: (offset, count) task ranges in `tasks`
+    std::pair<int, int> gemv, xall;
+    std::vector<std::pair<std::pair<int, int>, std::pair<int, int>>> rounds;  // blocked fronts: (inner, x)
+  };
+  std::vector<BwdLevel> bwd_ops;
   int max_ns = 0;
   struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add, 2 panel step, 3 syrk
   std::vector<Op> ops;

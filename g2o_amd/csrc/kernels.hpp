@@ -113,6 +113,8 @@ void chol_permute(int n, const int* perm, const double* in, double* out, hipStre
 void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]
 void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int* rows, const double* lbuf,
                    const double* ysol, const double* xsol, double* tsol, hipStream_t s);
+void chol_bwd_inner(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* xsol, double* tsol,
+                    hipStream_t s);
 void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,
                 hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only

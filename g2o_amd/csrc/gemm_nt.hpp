@@ -123,3 +123,4 @@ struct GemmNT {
 };
 
 }  // namespace g2ohip
+

@@ -29,8 +29,8 @@ PEAK_FP64_TFLOPS = 78.6    # MI355X FP64 vector == FP64 matrix (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C4", help="C4 (default, BASELINE metric) or C5/C3/C2/C1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=2, help="timed oracle LM iterations (after iteration 0)")

@@ -318,20 +318,43 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
       }
     }
     __syncthreads();
-    for (int k = me.child_begin; k < me.child_end; ++k) {
-      const FrontDesc cd = fd[children[k]];
-      const int mc = cd.ns + cd.nr, nrc = cd.nr;
-      const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;
-      const int* rel = relmap + cd.rows_off;
-      const int n0 = jtab[cd.jt_off];  // child rows mapping into the block (rel is increasing)
+    // children in groups of B0C: every load of a group (descriptors, n0, rel, update entries) is issued
+    // before the first add, so a group costs three dependent round trips instead of three per child;
+    // the adds then run child by child in the fixed order (bitwise reproducible)
+    constexpr int B0C = 4;
+    for (int kc = me.child_begin; kc < me.child_end; kc += B0C) {
+      double val[B0C][NB * NB / 256], vv[B0C];
+      int dst[B0C][NB * NB / 256], vdst[B0C];
 #pragma unroll
-      for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
-        const int e = tid + 256 * u_;
-        const int i = e & (NB - 1), j = e >> 5;
-        if (i < n0 && j <= i) D[rel[i] * DS + rel[j]] += U[(size_t)j * mc + i];
+      for (int c = 0; c < B0C; ++c) {
+        const bool has = kc + c < me.child_end;
+        const FrontDesc cd = fd[children[has ? kc + c : kc]];
+        const int mc = cd.ns + cd.nr, nrc = cd.nr;
+        const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;
+        const int* rel = relmap + cd.rows_off;
+        const int n0 = has ? jtab[cd.jt_off] : 0;  // child rows mapping into the block (rel is increasing)
+#pragma unroll
+        for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+          const int e = tid + 256 * u_;
+          const int i = e & (NB - 1), j = e >> 5;
+          const bool in = i < nrc && j <= i;  // independent of n0: issued together with it
+          val[c][u_] = ld0(U, j * mc + i, in);
+          const int ri = ld0(rel, i, in), rj = ld0(rel, j, in);
+          dst[c][u_] = (in && i < n0) ? ri * DS + rj : -1;
+        }
+        vv[c] = ld0(vecs + cd.vec_off + cd.ns, tid, tid < nrc && tid < NB);
+        const int rt = ld0(rel, tid, tid < nrc && tid < NB);
+        vdst[c] = tid < n0 ? rt : -1;
       }
-      if (tid < n0) vy[rel[tid]] += vecs[cd.vec_off + cd.ns + tid];
-      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < B0C; ++c) {
+        if (kc + c >= me.child_end) break;
+#pragma unroll
+        for (int u_ = 0; u_ < NB * NB / 256; ++u_)
+          if (dst[c][u_] >= 0) D[dst[c][u_]] += val[c][u_];
+        if (vdst[c] >= 0) vy[vdst[c]] += vv[c];
+        __syncthreads();
+      }
     }
     PH(2)
     if (tid < 64)

@@ -275,7 +275,8 @@ __device__ __forceinline__ double input_entry(const double* vals, const int* ent
 template <bool ASM>  // ASM: the level's fronts are assembled here; else they were pre-zeroed and scattered
 __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                     const int* __restrict__ children, const int* __restrict__ relmap,
-                                                    const int* __restrict__ jtab, const int* __restrict__ colptr, const int* __restrict__ ent_row,
+                                                    const int* __restrict__ jtab, const int* __restrict__ cmptr,
+                                                    const int2* __restrict__ cment, const int* __restrict__ colptr, const int* __restrict__ ent_row,
                                                     const int* __restrict__ ent_src, const double* __restrict__ vals,
                                                     const double* __restrict__ lam, double* __restrict__ fronts,
                                                     double* __restrict__ vecs, double* __restrict__ lbuf,
@@ -366,24 +367,61 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
   }
   const int a = t.a, b = t.b;
   const int lane = tid & 63, w = tid >> 6;
-  // 1. own columns: zero / input entries, written once (rows of the first diagonal block are block-0's);
-  //    !ASM: the front was zeroed and its inputs scattered before the first level (small levels)
-  for (int j = a + w; j < b && ASM; j += 4) {
-    const int rlo = j < kb0 ? kb0 : j;
-    double* Fj = F + (size_t)j * m;
-    for (int i = rlo + lane; i < m; i += 64) Fj[i] = 0.0;
-  }
-  if constexpr (ASM) __syncthreads();
-  for (int j = a + w; j < b && j < me.ns && ASM; j += 4) {
-    const int rlo = j < kb0 ? kb0 : j;
-    double* Fj = F + (size_t)j * m;
-    for (int e = colptr[me.c0 + j] + lane; e < colptr[me.c0 + j + 1]; e += 64) {
-      int r;
-      const double x = input_entry(vals, ent_src, ent_row, e, lam, r);
-      if (r >= rlo) Fj[r] = x;
+  if constexpr (ASM) {
+    // In-place assembly: each wave builds its columns in an LDS column buffer (zero, the column's input
+    // entries, then every (child, child column) pair mapping to it in child order) and writes each entry
+    // of the front once; rows in chunks of EAC. The children's update vectors follow below.
+    constexpr int EAC = 2048;
+    __shared__ double cbuf[4][EAC];
+    for (int j = a + w; j < b; j += 4) {
+      const int rlo = j < kb0 ? kb0 : j;  // rows of the first diagonal block: block-0 task
+      double* Fj = F + (size_t)j * m;
+      const int q0 = cmptr[me.cm_off + j], q1 = cmptr[me.cm_off + j + 1];
+      for (int rc = rlo; rc < m; rc += EAC) {
+        const int rce = min(m, rc + EAC);
+        double* cb = cbuf[w] - rc;
+        for (int i = rc + lane; i < rce; i += 64) cb[i] = 0.0;
+        if (j < me.ns)
+          for (int e = colptr[me.c0 + j] + lane; e < colptr[me.c0 + j + 1]; e += 64) {
+            int r;
+            const double x = input_entry(vals, ent_src, ent_row, e, lam, r);
+            if (r >= rc && r < rce) cb[r] = x;
+          }
+        for (int q = q0; q < q1; ++q) {
+          const int2 ce = cment[q];
+          const FrontDesc cd = fd[ce.x];
+          const int mc = cd.ns + cd.nr, nrc = cd.nr;
+          const double* Uj = fronts + cd.front_off + (size_t)(cd.ns + ce.y) * mc + cd.ns;
+          const int* rel = relmap + cd.rows_off;
+          for (int i0 = ce.y + lane; i0 < nrc; i0 += 256) {
+            double val[4];
+            int ri[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int i = i0 + u * 64;
+              const bool ok = i < nrc;
+              val[u] = ld0(Uj, i, ok);
+              ri[u] = ok ? ld0(rel, i, ok) : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (ri[u] >= rc && ri[u] < rce) cb[ri[u]] += val[u];
+          }
+        }
+        for (int i = rc + lane; i < rce; i += 64) Fj[i] = cb[i];
+      }
     }
+    for (int k = me.child_begin; k < me.child_end; ++k) {  // update vectors, children in fixed order
+      const FrontDesc cd = fd[children[k]];
+      const double* u = vecs + cd.vec_off + cd.ns;
+      const int* rel = relmap + cd.rows_off;
+      const int j0 = jtab[cd.jt_off + t.c - 1], j1 = jtab[cd.jt_off + t.c];
+      for (int j = j0 + tid; j < j1; j += 256)
+        if (rel[j] >= kb0) v[rel[j]] += u[j];
+      __syncthreads();
+    }
+    return;
   }
-  if constexpr (ASM) __syncthreads();
   // 2. children in fixed order
   for (int k = me.child_begin; k < me.child_end; ++k) {
     const FrontDesc cd = fd[children[k]];
@@ -864,15 +902,15 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double
   KERNEL_CHECK();
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
-                     const int* jtab, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
+                     const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
                      bool assemble, hipStream_t s) {
   if (ntasks <= 0) return;
   if (assemble)
-    hipLaunchKernelGGL(k_extend_add<true>, ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, colptr, ent_row, ent_src, vals,
+    hipLaunchKernelGGL(k_extend_add<true>, ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, colptr, ent_row, ent_src, vals,
                        lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
   else
-    hipLaunchKernelGGL(k_extend_add<false>, ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, colptr, ent_row, ent_src, vals,
+    hipLaunchKernelGGL(k_extend_add<false>, ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, colptr, ent_row, ent_src, vals,
                        lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }

@@ -290,7 +290,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   }
   // per child: [#rows mapping into the parent's first diagonal block | first child row of every parent
   // slab] (rel is increasing), so the extend-add tasks need no search on the chain
-  std::vector<int> hjt;
+  std::vector<int> hjt, hcmp;
+  std::vector<int2> hcme;
   std::vector<launch::FrontDesc> hfd(sym.sn.size());
   long long loff = 0, xoff = 0;
   for (size_t k = 0; k < sym.sn.size(); ++k) {
@@ -304,14 +305,35 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       hjt.push_back((int)(std::lower_bound(rel, rel + q.nr, kb0) - rel));
       for (int a = 0; a < mp + slab; a += slab) hjt.push_back((int)(std::lower_bound(rel, rel + q.nr, std::min(a, mp)) - rel));
     }
+    // (child, child column) pairs of every column of this front, children in fixed order
+    const int m = q.ns + q.nr, cm = (int)hcmp.size();
+    {
+      std::vector<int> cnt(m + 1, 0);
+      for (int ci = sym.children_ptr[k]; ci < sym.children_ptr[k + 1]; ++ci) {
+        const Supernode& cq = sym.sn[sym.children[ci]];
+        for (int jc = 0; jc < cq.nr; ++jc) cnt[sym.relmap[cq.rows_off + jc] + 1]++;
+      }
+      for (int j = 0; j < m; ++j) cnt[j + 1] += cnt[j];
+      const int base = (int)hcme.size();
+      hcme.resize(base + cnt[m]);
+      std::vector<int> fillc(cnt.begin(), cnt.end() - 1);
+      for (int ci = sym.children_ptr[k]; ci < sym.children_ptr[k + 1]; ++ci) {
+        const int c = sym.children[ci];
+        const Supernode& cq = sym.sn[c];
+        for (int jc = 0; jc < cq.nr; ++jc) hcme[base + fillc[sym.relmap[cq.rows_off + jc]]++] = int2{c, jc};
+      }
+      for (int j = 0; j <= m; ++j) hcmp.push_back(base + cnt[j]);
+    }
     hfd[k] = launch::FrontDesc{q.front_off, q.vec_off, loff, q.rows_off, xoff, q.c0, q.ns, q.nr, q.parent,
-                               sym.children_ptr[k], sym.children_ptr[k + 1], jt};
+                               sym.children_ptr[k], sym.children_ptr[k + 1], jt, cm};
     loff += (long long)(q.ns + q.nr) * q.ns;
     xoff += (long long)q.ns * q.ns;  // X = L11^-1, column-major
   }
   lpool = loff;
   fd.upload(hfd, s);
   jtab.upload(hjt.empty() ? std::vector<int>{0} : hjt, s);
+  cmptr.upload(hcmp.empty() ? std::vector<int>{0} : hcmp, s);
+  cment.upload(hcme.empty() ? std::vector<int2>{int2{0, 0}} : hcme, s);
   std::vector<int> ll;
   level_off.assign(1, 0);
   for (auto& lv : sym.levels) {
@@ -550,7 +572,8 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
     const launch::Task* t = tasks.get() + op.off;
     switch (op.kind) {
       case 0:
-      case 4: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), colptr.get(),
+      case 4: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), cmptr.get(),
+                                      cment.get(), colptr.get(),
                                       ent_row.get(),
                                       ent_src.get(), vals, lam, fronts.get(), vecs.get(),
                                       lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 4, s); break;

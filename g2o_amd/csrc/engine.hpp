@@ -52,6 +52,8 @@ struct DeviceCholesky {
   long long nent = 0;
   DevBuf<int> colptr, ent_row, ent_src;  // input entries per permuted scalar column (k_extend_add)
   DevBuf<int> jtab;                       // per child: row ranges per parent slab (FrontDesc::jt_off)
+  DevBuf<int> cmptr;                      // per front column: range of (child, child column) pairs
+  DevBuf<int2> cment;
   long long npre = 0;                     // entries of pre-scattered (small-level) fronts
   DevBuf<long long> pre_dst, zero_rng;
   DevBuf<int> pre_src;

@@ -79,6 +79,7 @@ struct FrontDesc {  // device view of one supernode (see symbolic.hpp)
   int c0, ns, nr, parent;
   int child_begin, child_end;  // into the children array
   int jt_off;  // into jtab: [rows into the parent's first diagonal block | first row of every parent slab]
+  int cm_off;  // into cmptr: per column of this front, the range of (child, child column) pairs mapping to it
 };
 struct Task {  // one workgroup's work item (meaning per kernel, see cholesky.hip)
   int s, a, b, c;
@@ -101,7 +102,7 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double
 // diagonal block assembled, factored and forward-solved beside it (t.c == 1). Input entries of scalar
 // column c (permuted): ent_row/ent_src[colptr[c] .. colptr[c+1]) = row in the front | diag << 30, index in vals
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
-                     const int* jtab, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
+                     const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
                      bool assemble, hipStream_t s);
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,

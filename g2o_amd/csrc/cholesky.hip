@@ -272,7 +272,9 @@ __device__ __forceinline__ double input_entry(const double* vals, const int* ent
   const double v = vals[ent_src[e]];
   return (rr >> 30) ? v + *lam : v;
 }
-template <bool ASM>  // ASM: the level's fronts are assembled here; else they were pre-zeroed and scattered
+// ASM: the level's fronts are assembled here (EAC: rows per LDS column chunk); else they were pre-zeroed and
+// scattered
+template <bool ASM, int EAC>
 __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                     const int* __restrict__ children, const int* __restrict__ relmap,
                                                     const int* __restrict__ jtab, const int* __restrict__ cmptr,
@@ -371,7 +373,6 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     // In-place assembly: each wave builds its columns in an LDS column buffer (zero, the column's input
     // entries, then every (child, child column) pair mapping to it in child order) and writes each entry
     // of the front once; rows in chunks of EAC. The children's update vectors follow below.
-    constexpr int EAC = 2048;
     __shared__ double cbuf[4][EAC];
     for (int j = a + w; j < b; j += 4) {
       const int rlo = j < kb0 ? kb0 : j;  // rows of the first diagonal block: block-0 task
@@ -904,13 +905,16 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
-                     bool assemble, hipStream_t s) {
+                     int assemble, hipStream_t s) {
   if (ntasks <= 0) return;
-  if (assemble)
-    hipLaunchKernelGGL(k_extend_add<true>, ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, colptr, ent_row, ent_src, vals,
+  if (assemble == 2)  // fronts up to 512 rows: a small column buffer keeps more workgroups per CU
+    hipLaunchKernelGGL((k_extend_add<true, 512>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment,
+                       colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
+  else if (assemble)
+    hipLaunchKernelGGL((k_extend_add<true, 2048>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, colptr, ent_row, ent_src, vals,
                        lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
   else
-    hipLaunchKernelGGL(k_extend_add<false>, ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, colptr, ent_row, ent_src, vals,
+    hipLaunchKernelGGL((k_extend_add<false, 1>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, colptr, ent_row, ent_src, vals,
                        lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }

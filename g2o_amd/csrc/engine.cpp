@@ -395,7 +395,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
               psrc.push_back(ent_srcv[e] | ((ent_rowv[e] >> 30) ? (int)0x80000000 : 0));
             }
         }
-      Op ea{pre ? 0 : 4, (int)tk.size(), 0};
+      int lmaxm = 0;
+      for (int sn : lv) lmaxm = std::max(lmaxm, sym.sn[sn].ns + sym.sn[sn].nr);
+      Op ea{pre ? 0 : (lmaxm <= 512 ? 5 : 4), (int)tk.size(), 0};
       for (int sn : lv) tk.push_back(Task{sn, 0, 0, 1});
       // every front is assembled here (input entries, zeros, children); slabs of EA columns where the level
       // has enough of them to fill the chip several times over, else 4 (latency-bound upper levels)
@@ -572,11 +574,12 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
     const launch::Task* t = tasks.get() + op.off;
     switch (op.kind) {
       case 0:
-      case 4: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), cmptr.get(),
+      case 4:
+      case 5: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), cmptr.get(),
                                       cment.get(), colptr.get(),
                                       ent_row.get(),
                                       ent_src.get(), vals, lam, fronts.get(), vecs.get(),
-                                      lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 4, s); break;
+                                      lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 0 ? 0 : (op.kind == 5 ? 2 : 1), s); break;
       case 2: launch::chol_step(op.count, step_tasks.get() + op.off, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),
                                 linv.get(), xinv.get(), fail, s);
         break;

@@ -104,7 +104,7 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
-                     bool assemble, hipStream_t s);
+                     int assemble, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place, 2 in place (m <= 512)
 void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
                double* linv, double* xinv, int* fail, hipStream_t s);
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is

@@ -221,3 +221,42 @@ def test_full_size_properties_c4(g2o_amd_mod):
     assert all(b <= a for a, b in zip(chis, chis[1:]))
     dof = 2 * prob.num_edges - (6 * 998 + 3 * 100_000)
     assert abs(chis[-1] / dof - 1.0) < 0.05
+
+
+def _ragged_ba(seed=11, dup=40):
+    """BA with ragged observation counts (1..12 per point, not the recipe's fixed k), duplicate
+    observations of a point by the same camera (two Hpl contributions into one block: the duplicate
+    off-diagonal path: block_solver.hpp:181-205 maps both edges onto the one block `block(i, j, true)` returns), and the edges in a
+    random order (the reference takes edges in any order)."""
+    base = synth.ba(num_cameras=40, num_points=1500, obs_per_point=12, window=16, seed=seed)
+    e = base.edges[0]
+    rng = np.random.default_rng(seed)
+    npts = len(base.vertices[1].ids)
+    keep = np.zeros(len(e.v0), bool)
+    kper = rng.integers(1, 13, size=npts)
+    for p in range(npts):  # edges of point p are rows 12p .. 12p+11
+        keep[12 * p + rng.permutation(12)[: kper[p]]] = True
+    idx = np.nonzero(keep)[0]
+    idx = np.concatenate([idx, rng.choice(idx, size=dup, replace=False)])  # duplicate observations
+    idx = idx[rng.permutation(len(idx))]
+    meas = e.meas[idx] + rng.standard_normal((len(idx), 2)) * 0.5
+    edges = synth.EdgeSet(e.etype, e.v0[idx], e.v1[idx], meas, e.info[idx], e.params[idx])
+    return synth.Problem(base.name + "_ragged", base.vertices, [edges], 6, 3)
+
+
+def test_lm_ragged_ba_duplicates_shuffled(g2o_amd_mod, oracle):
+    prob = _ragged_ba()
+    _check(*_run_both(g2o_amd_mod, oracle, prob, 6))
+
+
+def test_lm_pose_graph_shuffled_edges(g2o_amd_mod, oracle):
+    """SE3 and SE2 pose graphs with their edges in random order and some edges reversed in the
+    file sense (i > j: the Hessian block lands transposed, block_solver.hpp:181-184)."""
+    for name in ("C1", "C2"):
+        base = synth.by_name(name, "small")
+        e = base.edges[0]
+        rng = np.random.default_rng(5)
+        perm = rng.permutation(len(e.v0))
+        edges = synth.EdgeSet(e.etype, e.v0[perm], e.v1[perm], e.meas[perm], e.info[perm], None)
+        prob = synth.Problem(base.name + "_shuffled", base.vertices, [edges], base.pose_dim, base.landmark_dim)
+        _check(*_run_both(g2o_amd_mod, oracle, prob, 5))

@@ -21,5 +21,8 @@ cat $O/bench_$TAG.json
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest_gpu.log; exit 1; }
 echo PYTEST_OK
 tail -3 $O/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $O/smoke.log; exit 1; }
+echo SMOKE_OK
+cat $O/smoke.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/profc3 -o run -- python bench.py --config C3 --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_c3prof.json 2> $O/bench_c3prof.err || { echo PROF_C3_FAIL; tail -20 $O/bench_c3prof.err; exit 1; }
 echo PROF_C3_OK

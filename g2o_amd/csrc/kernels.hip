@@ -286,6 +286,56 @@ __global__ void __launch_bounds__(256) k_offblock_reduce(int nb, int bsz, const 
   out[dst[blk] + k] = s;
 }
 
+// High-degree vertices (BA cameras, ~1000 incident edges): one workgroup per vertex, 8 slot streams
+// (two per wave, one per half-wave); lane k of a half-wave reads entry k of its slot, so every load
+// instruction reads two slots' contiguous S-double runs (a few cache lines, not 64 scattered ones), U slots
+// per stream in flight. Each lane sums its entry over its stream in slot order; the 8 stream sums are
+// added in stream order: a fixed order, bitwise reproducible.
+template <int DIM>
+__global__ void __launch_bounds__(256)
+    k_vertex_reduce_wide(int nv, const int* __restrict__ inc_ptr, const int* __restrict__ inc_code,
+                         const double* __restrict__ slot0, const double* __restrict__ slot1, int stride0, int stride1,
+                         double* __restrict__ Hdiag, double* __restrict__ b, const int* __restrict__ boff) {
+  constexpr int SP = DIM * (DIM + 1) / 2, S = SP + DIM, U = 8, NS = 8;  // U = 16: no change
+  static_assert(S <= 32, "one half-wave per slot");
+  __shared__ double red[NS][32];
+  const int v = xcd_item(blockIdx.x, gridDim.x);
+  if (v >= nv) return;  // workgroup-uniform
+  const int tid = threadIdx.x, k = tid & 31, q = tid >> 5;  // entry, stream
+  const int p0 = inc_ptr[v], p1 = inc_ptr[v + 1];
+  double acc = 0.0;
+  for (int p = p0 + q; p < p1; p += NS * U) {
+    int c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) c[u] = p + NS * u < p1 ? inc_code[p + NS * u] : -1;
+    double d[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = c[u] >> 1;
+      const double* sl = (c[u] & 1) ? slot1 + (size_t)e * stride1 : slot0 + (size_t)e * stride0;
+      d[u] = (c[u] >= 0 && k < S) ? sl[k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += d[u];
+  }
+  red[q][k] = acc;
+  __syncthreads();
+  if (tid >= S) return;
+  double t = red[0][tid];
+#pragma unroll
+  for (int j = 1; j < NS; ++j) t += red[j][tid];
+  if (tid < SP) {  // packed upper column-major index -> (r, c)
+    int c = 0, base = 0;
+    while (tid >= base + c + 1) base += ++c;
+    const int r = tid - base;
+    double* H = Hdiag + (size_t)v * DIM * DIM;
+    H[c * DIM + r] = t;
+    H[r * DIM + c] = t;
+  } else {
+    b[boff[v] + tid - SP] = t;
+  }
+}
+
 // ------------------------------------------------------------------------------ Schur
 // Landmark pass (block_solver.hpp:341-360): Dinv = (Hll + lambda I)^-1 (cofactor inverse, as
 // Eigen's 3x3 inverse; kept for the back-substitution) and the symmetric split
@@ -837,6 +887,10 @@ void linearize(int family, const EdgeArgs& a, int ne, const int* h0, const int* 
   KERNEL_CHECK();
 }
 
+static bool vr_wide() {
+  static const bool w = !getenv("G2OHIP_VR_WIDE") || atoi(getenv("G2OHIP_VR_WIDE")) != 0;  // dev A/B
+  return w;
+}
 template <int DIM>
 static void vreduce_dim(int nv, int lanes, const int* ptr, const int* code, const double* s0, const double* s1, int st0,
                         int st1, double* H, double* b, const int* boff, hipStream_t s) {
@@ -845,7 +899,12 @@ static void vreduce_dim(int nv, int lanes, const int* ptr, const int* code, cons
     case 1: hipLaunchKernelGGL((k_vertex_reduce<DIM, 1>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
     case 4: hipLaunchKernelGGL((k_vertex_reduce<DIM, 4>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
     case 8: hipLaunchKernelGGL((k_vertex_reduce<DIM, 8>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
-    case 64: hipLaunchKernelGGL((k_vertex_reduce<DIM, 64>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+    case 64:
+      if (vr_wide())
+        hipLaunchKernelGGL((k_vertex_reduce_wide<DIM>), nv, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff);
+      else
+        hipLaunchKernelGGL((k_vertex_reduce<DIM, 64>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff);
+      break;
     default: hipLaunchKernelGGL((k_vertex_reduce<DIM, 256>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
   }
   KERNEL_CHECK();

@@ -29,10 +29,12 @@ int guarded(F&& f) {
 }
 bool algorithm_known(const std::string& n) {
   // {gn,lm}_hip_{var,fix6_3,fix3_3,fix6_6} (cf. solver_csparse.cpp:51-84 name parsing)
-  if (n.size() < 7) return false;
+  if (n.size() < 6) return false;
   const std::string m = n.substr(0, 3), rest = n.substr(3);
   if (m != "lm_" && m != "gn_") return false;
-  return rest == "hip_var" || rest == "hip_fix6_3" || rest == "hip_fix3_3" || rest == "hip_fix6_6";
+  // {gn,lm}_pcg{,6_3,3_3,6_6}: block-Jacobi PCG instead of the Cholesky (solver_pcg.cpp name table)
+  return rest == "hip_var" || rest == "hip_fix6_3" || rest == "hip_fix3_3" || rest == "hip_fix6_6" || rest == "pcg" ||
+         rest == "pcg6_3" || rest == "pcg3_3" || rest == "pcg6_6";
 }
 }  // namespace
 

@@ -1269,7 +1269,10 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     dG.resize(std::max<long long>((long long)nHpl * 18, 1));  // G = Hpl U^-T per observation (6x3)
     dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
-    chol.setup(num_poses, pd, s_bi, s_bj, stream);
+    if (use_pcg()) pcg.setup(num_poses, pd, s_bi, s_bj, stream);
+    else chol.setup(num_poses, pd, s_bi, s_bj, stream);
+  } else if (use_pcg()) {
+    pcg.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
   } else {
     chol.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
   }
@@ -1364,6 +1367,14 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   ev_valid_ = sev;
   if (!do_schur) {
     if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
+    if (use_pcg()) {
+      timer.begin("pcg", stream);
+      pcg.solve(dH.get(), dscal.get(), db.get(), dx.get(), stream);
+      timer.end(stream);
+      if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
+      if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
+      return;
+    }
     timer.begin("chol_factor", stream);
     chol.factor(dH.get(), dscal.get(), db.get(), failp(), stream);
     timer.end(stream);
@@ -1393,13 +1404,20 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   timer.end(stream);
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
   if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
-  timer.begin("chol_factor", stream);
-  chol.factor(S, dscal.get() + 5, bschur, failp(), stream);
-  timer.end(stream);
-  if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
-  timer.begin("chol_solve", stream);
-  chol.solve(dx.get(), stream);
-  timer.end(stream);
+  if (use_pcg()) {
+    timer.begin("pcg", stream);
+    pcg.solve(S, dscal.get() + 5, bschur, dx.get(), stream);
+    timer.end(stream);
+    if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
+  } else {
+    timer.begin("chol_factor", stream);
+    chol.factor(S, dscal.get() + 5, bschur, failp(), stream);
+    timer.end(stream);
+    if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
+    timer.begin("chol_solve", stream);
+    chol.solve(dx.get(), stream);
+    timer.end(stream);
+  }
   if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
   timer.begin("backsub", stream);
   launch::backsub(nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get(), size_poses, lm_begin, dx.get(),

@@ -12,6 +12,7 @@
 #include "comm.hpp"
 #include "common.hpp"
 #include "kernels.hpp"
+#include "pcg.hpp"
 #include "symbolic.hpp"
 
 namespace g2ohip {
@@ -211,6 +212,8 @@ class Engine {
   DevBuf<int> sch_rptr, sch_robs, sch_obs_lm, sch_sdiag;
   std::vector<int> s_bi, s_bj, hpp_bi, hpp_bj;
   DeviceCholesky chol;
+  DevicePCG pcg;  // {lm,gn}_pcg* algorithms (linear_solver_pcg.hpp)
+  bool use_pcg() const { return algorithm.find("_pcg") != std::string::npos; }
   // scalars: [0] lambda, [1] chi2, [2] scale, [3] maxdiag
   DevBuf<double> dscal;
   DevBuf<double> dpartial;

@@ -25,12 +25,20 @@ struct DevicePCG {
   void solve(const double* vals, const double* lam, const double* b, double* x, hipStream_t s);
   // LinearSolverPCG::init (linear_solver_pcg.h:63-68): forget the carried residual
   void reset(hipStream_t s);
+  DevicePCG() = default;
+  DevicePCG(const DevicePCG&) = delete;
+  DevicePCG& operator=(const DevicePCG&) = delete;
+  ~DevicePCG() {
+    if (chunk_exec) (void)hipGraphExecDestroy(chunk_exec);
+  }
 
  private:
   int nb = 0, pd = 0, n = 0, npa = 0, npb = 0;
   DevBuf<int> rptr, diag;
   DevBuf<int2> ent;  // (block index, other block row | 0x80000000 when the block is used transposed)
   DevBuf<double> J, r, sv, q, dbuf, part, sc;
+  hipGraphExec_t chunk_exec = nullptr;  // CHUNK iterations captured once per (vals, λ, x, maxIter)
+  const void* chunk_key[4] = {};
 };
 
 }  // namespace g2ohip

@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C4", help="C4 (default, BASELINE metric) or C5/C3/C2/C1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=2, help="timed oracle LM iterations (after iteration 0)")
+    ap.add_argument("--cpu-iters", type=int, default=6, help="timed oracle LM iterations (after iteration 0)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="OpenMP threads for the CPU baseline (0 = all)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-posegraph", action="store_true", help="skip the C3 (100k-pose SE3) secondary leg")
@@ -81,31 +81,65 @@ def bcast_bytes(b, world):
     return obj[0]
 
 
-def cpu_baseline(prob, iters, threads):
-    """The oracle (C++ restatement of BlockSolver + LM) with the reference's own CSparse
-    (oracle/_ref, cs_amd block ordering + LL^T) timed on this host."""
+def cpu_model():
+    """lscpu model name + logical CPU count of this host (BASELINE.md asks for both)."""
+    model = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    if model is None and os.path.exists("/proc/cpuinfo"):
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    return {"model": model, "nproc": os.cpu_count()}
+
+
+def _oracle_run(prob, iters, nthreads):
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle_py
-    nthreads = threads or os.cpu_count() or 1
-    nthreads = min(nthreads, 16)  # the GPU box grants a 16-CPU share
     g = oracle_py.OracleGraph(prob)
     cfg = oracle_py.make_config(threads=nthreads, use_ref=True, block_ordering=True)
     n, st = g.optimize(iters + 1, cfg)
     timed = st[1:n]
     if not timed:
-        return None
+        return None, oracle_py
     t = sum(s.timeIteration for s in timed)
     lin = [s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
+    return {"value": len(timed) / t, "iterations": len(timed), "ms_per_linear_solve": 1e3 * float(np.median(lin)),
+            "chi2": timed[-1].chi2}, oracle_py
+
+
+def cpu_baseline(prob, iters, threads, iters_1t=2):
+    """The oracle (C++ restatement of BlockSolver + LM) with the reference's own CSparse (oracle/_ref,
+    cs_amd block ordering + up-looking LL^T) timed on this host: OpenMP assembly/Schur on all granted
+    cores (the reference forces OpenMP, CMakeLists.txt:146) and a 1-thread run; the factorization is
+    single-threaded in both, as CSparse is."""
+    nthreads = threads or os.cpu_count() or 1
+    nthreads = min(nthreads, 16)  # the GPU box grants a 16-CPU share
+    multi, oracle_py = _oracle_run(prob, iters, nthreads)
+    if multi is None:
+        return None
+    one, _ = _oracle_run(prob, iters_1t, 1)
     return {
-        "value": len(timed) / t,
+        "value": multi["value"],
         "unit": "LM it/s",
         "cores": nthreads,
         "kind": "port",
-        "ms_per_linear_solve": 1e3 * float(np.median(lin)),
+        "ms_per_linear_solve": multi["ms_per_linear_solve"],
+        "one_thread": one,
+        "host": cpu_model(),
         "ref_csparse": bool(oracle_py.ref_available()),
-        "sample": f"{len(timed)} LM iterations (after iteration 0) of the same {prob.name} problem: oracle C++ "
-                  f"restatement of BlockSolver/Schur/LM (OpenMP {nthreads} threads for assembly+Schur) with "
-                  f"the reference's vendored CSparse 3.1.0 cs_amd(block)+LL^T ({'loaded' if oracle_py.ref_available() else 'restated'}), single-threaded factorization as in the reference",
+        "sample": f"{multi['iterations']} LM iterations ({nthreads} threads) and {one['iterations'] if one else 0} "
+                  f"(1 thread), each after iteration 0, of the same {prob.name} problem: oracle C++ restatement of "
+                  f"BlockSolver/Schur/LM with the reference's vendored CSparse 3.1.0 cs_amd(block)+LL^T "
+                  f"({'loaded' if oracle_py.ref_available() else 'restated'}), single-threaded factorization as in "
+                  f"the reference",
     }
 
 
@@ -140,7 +174,9 @@ def posegraph_leg(local, steps=5, warmup=1):
         opt.optimize_step(it)
         it += 1
     fms = opt.kernel_ms("chol_factor")
-    flops = opt.kernel_flops("chol_factor")
+    own = opt.kernel_flops("chol_factor")
+    ref = load_json("chol_flops.json").get("C3", {}).get("ref_cs_amd", {}).get("flops")
+    flops = ref or own
     tf = flops / (fms * 1e-3) / 1e12 if fms > 0 else 0.0
     lin = [1e3 * s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
     return {
@@ -151,8 +187,32 @@ def posegraph_leg(local, steps=5, warmup=1):
         "steps": steps,
         "final_chi2": timed[-1].chi2,
         "factor": {"bound": "mfma", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                   "frac": tf / PEAK_FP64_TFLOPS, "flops_per_launch": flops, "avg_launch_ms": fms},
+                   "frac": tf / PEAK_FP64_TFLOPS, "flops_per_launch": flops,
+                   "flops_convention": "reference cs_amd sum c_k^2" if ref else "backend ordering",
+                   "backend_ordering_flops": own, "avg_launch_ms": fms},
     }
+
+
+def load_json(name):
+    path = os.path.join(HERE, "profiles", name)
+    try:
+        return json.load(open(path)) if os.path.exists(path) else {}
+    except Exception:
+        return {}
+
+
+def stage_bytes(prob):
+    """SURVEY.md §8d algorithmic bytes per launch of the assembly and Schur stages (BA configs):
+    assembly: per edge 80 B read (meas, Omega, intrinsics, 2 ids) + 144 B Hpl written, per point 24 B
+    read + 96 B (Hll, b_l) written, per camera 56 B read + 336 B (Hpp block, b_p) written;
+    Schur: per point k*144 + 96 B read, 288 B per upper Hschur block written once."""
+    if not prob.landmark_dim:
+        return None
+    cams, pts = prob.vertices
+    ne = prob.edges[0].v0.size
+    nc, npt = int((cams.fixed == 0).sum()), pts.ids.size
+    asm = ne * (80 + 144) + npt * (24 + 96) + nc * (56 + 336)
+    return {"assembly": asm, "schur_read": ne * 144 + npt * 96}
 
 
 def main():
@@ -177,16 +237,15 @@ def main():
 
     # warmup: iteration 0 builds the structure (symbolic analysis) and lambda0
     t0 = time.time()
-    stats = []
     it = 0
     for _ in range(max(args.warmup, 1)):
-        r, st = opt.optimize_step(it)
-        stats.append(st)
+        opt.optimize_step(it)
         it += 1
     warm_s = time.time() - t0
-    # roofline kernel: the dominant HBM-bound dispatch, timed with HIP events inside the timed region
-    # (only it: every timed kernel class adds two event records per launch to the stream)
-    dom = "schur_rows" if prob.landmark_dim else "linearize"
+    # roofline kernel: the dominant dispatch chain, the supernodal factorization of the reduced system
+    # (60 % of the C4 step), timed with HIP events on the engine's stream inside the timed region (only it:
+    # every timed class adds two event records per launch to the stream)
+    dom = "chol_factor"
     if not args.no_kernel_timing:
         opt.enable_kernel_timing(True, only=dom)
     opt.set_stats_level(1)  # G2OBatchStatistics: timeLinearSolution per trial (ms/linear-solve) only
@@ -205,9 +264,9 @@ def main():
     value = args.steps / dt
     lin_ms = [1e3 * s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
     trials = sum(s.levenbergIterations for s in timed)
-
     avg_ms = opt.kernel_ms(dom)
     launches = opt.kernel_count(dom)
+
     # stage breakdown: two more (untimed) iterations with every kernel class and stage timer on
     names = ["linearize", "vreduce", "schur_dinv", "schur_diag", "schur_rows", "chol_factor", "chol_solve", "backsub",
              "error", "oplus"]
@@ -218,18 +277,72 @@ def main():
         opt.optimize_step(it)
         it += 1
     kt = {k: {"avg_ms": opt.kernel_ms(k), "count": opt.kernel_count(k)} for k in names}
-    algo_bytes = opt.kernel_bytes(dom)
-    achieved = algo_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    # HBM traffic per launch from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs of
-    # this same command, gpu_session.sh; parsed and gfx950-corrected by tools/pmc_traffic.py)
-    traffic = None
-    tf = os.environ.get("G2OHIP_TRAFFIC_JSON") or os.path.join(HERE, "profiles", "traffic.json")
-    if os.path.exists(tf):
-        try:
-            rec = json.load(open(tf)).get(dom)
-            traffic = rec["bytes_per_launch"] if isinstance(rec, dict) else rec
-        except Exception:
-            traffic = None
+    finfo = opt.factor_info()
+
+    # algorithmic flops of the factorization: sum_k c_k^2 under the REFERENCE ordering (cs_amd on the block
+    # pattern), from tools/chol_flops.py (oracle/_ref, committed JSON); the backend's own
+    # nested-dissection ordering count beside it
+    cf = load_json("chol_flops.json").get(args.config, {})
+    ref_flops = cf.get("ref_cs_amd", {}).get("flops")
+    own_flops = finfo["flops"]
+    traffic_all = load_json("traffic.json")
+    tf = os.environ.get("G2OHIP_TRAFFIC_JSON")
+    if tf and os.path.exists(tf):
+        traffic_all = json.load(open(tf))
+
+    def traffic(k):
+        rec = traffic_all.get(k)
+        return rec.get("bytes_per_launch") if isinstance(rec, dict) else rec
+
+    flops = ref_flops if ref_flops else own_flops
+    achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    roofline = {
+        "kernel": dom,
+        "bound": "mfma",
+        "achieved": achieved,
+        "peak": PEAK_FP64_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": achieved / PEAK_FP64_TFLOPS,
+        "traffic": traffic(dom),
+        "algorithmic_flops_per_launch": flops,
+        "flops_convention": ("sum_k c_k^2 of the reference cs_amd block ordering (tools/chol_flops.py)" if ref_flops
+                             else "backend ordering (reference count missing for this config)"),
+        "backend_ordering_flops": own_flops,
+        "backend_ordering_frac": own_flops / (avg_ms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if avg_ms > 0 else 0.0,
+        "avg_launch_ms": avg_ms,
+        "launches_timed": launches,
+    }
+    secondary = []
+    if prob.landmark_dim:
+        sb = stage_bytes(prob)
+        rows_bytes = opt.kernel_bytes("schur_rows")
+        ms_rows = kt["schur_rows"]["avg_ms"]
+        if ms_rows > 0:
+            a = rows_bytes / (ms_rows * 1e-3) / 1e9
+            secondary.append({"kernel": "schur_rows", "bound": "hbm", "achieved": a, "peak": PEAK_HBM_GBS,
+                              "unit": "GB/s", "frac": a / PEAK_HBM_GBS, "traffic": traffic("schur_rows"),
+                              "algorithmic_bytes_per_launch": rows_bytes, "avg_launch_ms": ms_rows})
+        ms_asm = kt["linearize"]["avg_ms"] + kt["vreduce"]["avg_ms"]
+        if ms_asm > 0:
+            a = sb["assembly"] / (ms_asm * 1e-3) / 1e9
+            tr = [traffic(k) for k in ("linearize", "vreduce")]
+            secondary.append({"kernel": "assembly (linearize + vertex reductions)", "bound": "hbm", "achieved": a,
+                              "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": a / PEAK_HBM_GBS,
+                              "traffic": sum(tr) if all(t is not None for t in tr) else None,
+                              "algorithmic_bytes_per_launch": sb["assembly"], "avg_launch_ms": ms_asm})
+        ms_sch = kt["schur_dinv"]["avg_ms"] + kt["schur_diag"]["avg_ms"] + kt["schur_rows"]["avg_ms"]
+        nsblk = cf.get("blocks_upper")
+        if ms_sch > 0 and nsblk:
+            by = sb["schur_read"] + 288 * nsblk
+            a = by / (ms_sch * 1e-3) / 1e9
+            tr = [traffic(k) for k in ("schur_dinv", "schur_diag", "schur_rows")]
+            secondary.append({"kernel": "schur stage (dinv + diag + rows)", "bound": "hbm", "achieved": a,
+                              "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": a / PEAK_HBM_GBS,
+                              "traffic": sum(tr) if all(t is not None for t in tr) else None,
+                              "algorithmic_bytes_per_launch": by, "avg_launch_ms": ms_sch})
+    fixed = ""
+    if prob.landmark_dim:
+        fixed = f", {int(prob.vertices[0].fixed.sum())} fixed cameras (gauge + monocular scale; ba_demo.cpp fixes 1)"
     out = {
         "metric": "LM iterations/sec + ms/linear-solve, synthetic BA 1k×100k at 1/2/4/8 GPUs",
         "value": value,
@@ -246,24 +359,15 @@ def main():
         "data": "synthetic (numpy Philox seed 20261015, BAL-style recipe of ba_demo.cpp; SURVEY.md 8d)",
         "config": {
             "workload": f"{args.config}: {prob.name} ({prob.num_vertices} vertices, {prob.num_edges} edges), "
-                        f"{solver_name(prob)}" + (f", landmarks sharded over {world} GPU(s)" if prob.landmark_dim else ""),
+                        f"{solver_name(prob)}{fixed}" + (f", landmarks sharded over {world} GPU(s)" if prob.landmark_dim else ""),
             "levenberg_trials": trials,
             "final_chi2": timed[-1].chi2 if timed else None,
             "parallelism": f"landmark-shard{world}" if world > 1 else "single",
         },
         "stages_ms_avg": {k: v["avg_ms"] for k, v in kt.items()},  # 2 extra untimed iterations
-        "roofline": {
-            "kernel": dom,
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": PEAK_HBM_GBS,
-            "unit": "GB/s",
-            "frac": achieved / PEAK_HBM_GBS,
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": algo_bytes,
-            "avg_launch_ms": avg_ms,
-            "launches_timed": launches,
-        },
+        "roofline": roofline,
+        "roofline_secondary": secondary,
+        "factor": finfo,
         "setup_s": {"generate": gen_s, "warmup_incl_structure": warm_s},
     }
     if rank == 0 and world == 1 and not args.no_posegraph and args.config == "C4":

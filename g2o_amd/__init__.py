@@ -46,7 +46,8 @@ EXPORTS = [
     "g2ohip_initialize", "g2ohip_chi2", "g2ohip_optimize", "g2ohip_optimize_step",
     "g2ohip_solver_build_structure", "g2ohip_solver_build_system", "g2ohip_solver_set_lambda",
     "g2ohip_solver_restore_diagonal", "g2ohip_solver_solve", "g2ohip_solver_vector_size",
-    "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
+    "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_solver_multiply_hessian",
+    "g2ohip_solver_linear_residual", "g2ohip_solver_factor_info", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
     "g2ohip_discard_top", "g2ohip_stage", "g2ohip_linear_solve_ccs", "g2ohip_comm_unique_id",
     "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
     "g2ohip_kernel_timing_only", "g2ohip_set_stats_level", "g2ohip_kernel_ms",
@@ -96,6 +97,9 @@ def lib() -> C.CDLL:
         "g2ohip_solver_vector_size": ([P], LL),
         "g2ohip_solver_get_x": ([P, P], I),
         "g2ohip_solver_get_b": ([P, P], I),
+        "g2ohip_solver_multiply_hessian": ([P, P, P], I),
+        "g2ohip_solver_linear_residual": ([P, P], I),
+        "g2ohip_solver_factor_info": ([P, P, I], I),
         "g2ohip_update": ([P, P], I),
         "g2ohip_push": ([P], I),
         "g2ohip_pop": ([P], I),
@@ -278,6 +282,27 @@ class SparseOptimizer:
         out = np.zeros(self.vector_size())
         _check(lib().g2ohip_solver_get_b(self.h, _p(out)), "b")
         return out
+
+    def multiply_hessian(self, src) -> np.ndarray:
+        """BlockSolverBase::multiplyHessian (block_solver.h:146): Hpp @ src (pose part)."""
+        src = np.ascontiguousarray(src, np.float64)
+        out = np.zeros_like(src)
+        _check(lib().g2ohip_solver_multiply_hessian(self.h, _p(out), _p(src)), "multiplyHessian")
+        return out
+
+    def linear_residual(self) -> float:
+        """||(A + lambda I) x - b|| / ||b|| of the last solve, computed on the device."""
+        r = np.zeros(1)
+        _check(lib().g2ohip_solver_linear_residual(self.h, _p(r)), "linear_residual")
+        return float(r[0])
+
+    FACTOR_INFO_KEYS = ("n", "nnzL", "flops", "supernodes", "levels", "max_front", "blocked_fronts",
+                        "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds")
+
+    def factor_info(self) -> dict:
+        out = np.zeros(len(self.FACTOR_INFO_KEYS))
+        _check(lib().g2ohip_solver_factor_info(self.h, _p(out), len(out)), "factor_info")
+        return dict(zip(self.FACTOR_INFO_KEYS, out.tolist()))
 
     def stage(self, lam: float):
         dims = np.zeros(3, np.int64)

@@ -27,14 +27,38 @@ int guarded(F&& f) {
     return G2OHIP_ERR_DEVICE;
   }
 }
-bool algorithm_known(const std::string& n) {
+// 1 known, 0 unknown, -1 a reference name this backend does not build (with g_err set)
+int algorithm_known(const std::string& n) {
   // {gn,lm}_hip_{var,fix6_3,fix3_3,fix6_6} (cf. solver_csparse.cpp:51-84 name parsing)
-  if (n.size() < 6) return false;
+  if (n.size() < 6) return 0;
   const std::string m = n.substr(0, 3), rest = n.substr(3);
-  if (m != "lm_" && m != "gn_") return false;
-  // {gn,lm}_pcg{,6_3,3_3,6_6}: block-Jacobi PCG instead of the Cholesky (solver_pcg.cpp name table)
-  return rest == "hip_var" || rest == "hip_fix6_3" || rest == "hip_fix3_3" || rest == "hip_fix6_6" || rest == "pcg" ||
-         rest == "pcg6_3" || rest == "pcg3_3" || rest == "pcg6_6";
+  if (m != "lm_" && m != "gn_") return 0;
+  if (rest == "hip_var" || rest == "hip_fix6_3" || rest == "hip_fix3_3" || rest == "hip_fix6_6") return 1;
+  // g2o/solvers/pcg registry (solver_pcg.cpp:91-98): pcg (variable block size), pcg3_2, pcg6_3, pcg7_3.
+  // Block-Jacobi PCG on the device replaces the Cholesky; pose blocks of 3 or 6 only.
+  if (rest == "pcg" || rest == "pcg6_3") return 1;
+  if (rest == "pcg3_2" || rest == "pcg7_3") {
+    g_err = n + ": fixed block sizes 3_2 / 7_3 are not supported by the device PCG (pose blocks of 3 or 6 only; "
+                "use " + m + "pcg)";
+    return -1;
+  }
+  return 0;
+}
+// the kernels are built for gfx950 only (MFMA f64 16x16x4, 160 KB LDS, 8 XCDs): refuse anything else
+bool gfx950_device(int device) {
+  int n = 0;
+  if (device < 0 || hipGetDeviceCount(&n) != hipSuccess || n <= device) {
+    g_err = "no HIP device " + std::to_string(device) + " (libg2o_hip requires a gfx950 GPU)";
+    return false;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    g_err = "HIP device " + std::to_string(device) + " is not gfx950 (" +
+            std::string(hipGetDeviceProperties(&prop, device) == hipSuccess ? prop.gcnArchName : "unknown") +
+            "): libg2o_hip requires a MI355X";
+    return false;
+  }
+  return true;
 }
 }  // namespace
 
@@ -43,10 +67,7 @@ extern "C" {
 g2ohip_graph* g2ohip_graph_create(int device) {
   try {
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= device) {
-      g_err = "no HIP device " + std::to_string(device) + " (libg2o_hip requires a gfx950 GPU)";
-      return nullptr;
-    }
+    if (!gfx950_device(device)) return nullptr;
     return new g2ohip_graph{new g2ohip::Engine(device)};
   } catch (const std::exception& ex) {
     g_err = ex.what();
@@ -65,7 +86,7 @@ int g2ohip_add_vertices(g2ohip_graph* g, int type, int n, const int* ids, const 
 }
 int g2ohip_add_edges(g2ohip_graph* g, int type, int n, const int* v0, const int* v1, const double* meas,
                      const double* info, const double* params) {
-  if (!g || (n > 0 && (!v0 || !v1 || !meas || !info))) return G2OHIP_ERR_ARG;
+  if (!g || (n > 0 && (!v0 || !v1 || !info))) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->add_edges(type, n, v0, v1, meas, info, params); });
 }
 int g2ohip_load_g2o(g2ohip_graph* g, const char* path, int marginalize_xyz) {
@@ -77,7 +98,23 @@ int g2ohip_save_g2o(g2ohip_graph* g, const char* path) {
   return guarded([&] { return g->e->save(path); });
 }
 int g2ohip_num_vertices(g2ohip_graph* g) { return g ? (int)g->e->hg.verts.size() : G2OHIP_ERR_ARG; }
-int g2ohip_num_edges(g2ohip_graph* g) { return g ? (int)g->e->hg.ev0.size() : G2OHIP_ERR_ARG; }
+int g2ohip_num_edges(g2ohip_graph* g) { return g ? (int)g->e->hg.num_edges() : G2OHIP_ERR_ARG; }
+int g2ohip_set_robust_kernel(g2ohip_graph* g, int edge_type, int kind, double delta) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->set_robust_kernel(edge_type, kind, delta); });
+}
+int g2ohip_set_host_jacobians(g2ohip_graph* g, int edge_type, const double* payload) {
+  if (!g || !payload) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->set_host_payload(edge_type, payload); });
+}
+int g2ohip_set_host_edge_callback(g2ohip_graph* g, g2ohip_host_edge_fn fn, void* user) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return g->e->set_host_callback(fn, user);
+}
+int g2ohip_solver_diag_absmax(g2ohip_graph* g, double* out) {
+  if (!g || !out) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->diag_absmax(out); });
+}
 int g2ohip_get_estimates(g2ohip_graph* g, int type, double* out, int* ids_out) {
   if (!g) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->get_estimates(type, out, ids_out); });
@@ -91,7 +128,13 @@ int g2ohip_minimal_state(g2ohip_graph* g, double* out) {
   return guarded([&] { return g->e->minimal_state(out); });
 }
 int g2ohip_set_algorithm(g2ohip_graph* g, const char* name) {
-  if (!g || !name || !algorithm_known(name)) return G2OHIP_ERR_ARG;
+  if (!g || !name) return G2OHIP_ERR_ARG;
+  const int k = algorithm_known(name);
+  if (k < 0) return G2OHIP_ERR_UNSUPPORTED;
+  if (k == 0) {
+    g_err = std::string("unknown optimization algorithm ") + name;
+    return G2OHIP_ERR_ARG;
+  }
   g->e->algorithm = name;
   g->e->levenberg = std::string(name).rfind("lm_", 0) == 0;
   return G2OHIP_OK;
@@ -146,6 +189,18 @@ int g2ohip_solver_get_b(g2ohip_graph* g, double* b) {
   if (!g || !b) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->get_b(b); });
 }
+int g2ohip_solver_multiply_hessian(g2ohip_graph* g, double* dest, const double* src) {
+  if (!g || !dest || !src) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->multiply_hessian(dest, src); });
+}
+int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel) {
+  if (!g || !rel) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->linear_residual(rel); });
+}
+int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n) {
+  if (!g || !out || n < 0) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->factor_info(out, n); });
+}
 int g2ohip_update(g2ohip_graph* g, const double* x_host) {
   if (!g) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->update_from(x_host); });
@@ -161,6 +216,7 @@ int g2ohip_stage(g2ohip_graph* g, double lambda, double* b, double* x, double* H
 int g2ohip_linear_solve_ccs(int device, int n, const int* Ap, const int* Ai, const double* Ax, const double* b,
                             double* x, int nblocks, const int* block_ends) {
   if (n <= 0 || !Ap || !Ai || !Ax || !b || !x) return G2OHIP_ERR_ARG;
+  if (!gfx950_device(device)) return G2OHIP_ERR_DEVICE;
   return guarded([&]() -> int {
     // Uniform block partition required (BlockSolver<p,l> pose blocks); default 1x1 blocks.
     int bd = 1;

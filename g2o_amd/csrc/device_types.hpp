@@ -233,12 +233,83 @@ DI double normalize_theta(double theta) {  // stuff/misc.h:114-127
 struct EdgeData {
   const int* v0;            // local index of vertex 0 (in its type's state array)
   const int* v1;
-  const double* meas;       // per-edge measurement payload (family-specific stride)
+  const double* meas;       // per-edge measurement payload (family-specific stride; host-J: e | Ji | Jj)
   const double* info;       // packed upper information (family-specific stride)
   const double* params;     // BA intrinsics [4] or nullptr
   const double* s0;         // state array of vertex-0 type
   const double* s1;         // state array of vertex-1 type
+  int rk;                   // robust kernel of the edge set (G2OHIP_RK_*), 0 none
+  double rk_delta;          // RobustKernel::delta
 };
+
+// RobustKernel*::robustify (robust_kernel_impl.cpp:65-200): rho[0] = rho(e2), rho[1] = rho'(e2) (rho'' is not
+// used on this path: base_edge.h:117-123 builds the weighted information from rho' only)
+DI void robustify(int kind, double delta, double e2, double& r0, double& r1) {
+  switch (kind) {
+    case 1: {  // Huber
+      const double dsqr = delta * delta;
+      if (e2 <= dsqr) { r0 = e2; r1 = 1.0; }
+      else { const double sq = sqrt(e2); r0 = 2 * sq * delta - dsqr; r1 = delta / sq; }
+      break;
+    }
+    case 2: {  // PseudoHuber
+      const double dsqr = delta * delta, aux1 = (1. / dsqr) * e2 + 1.0, aux2 = sqrt(aux1);
+      r0 = 2 * dsqr * (aux2 - 1);
+      r1 = 1. / aux2;
+      break;
+    }
+    case 3: {  // Cauchy
+      const double dsqr = delta * delta, aux = (1. / dsqr) * e2 + 1.0;
+      r0 = dsqr * log(aux);
+      r1 = 1. / aux;
+      break;
+    }
+    case 4: {  // GemanMcClure
+      const double aux = delta / (delta + e2);
+      r0 = e2 * aux;
+      r1 = aux * aux;
+      break;
+    }
+    case 5: {  // Welsch
+      const double dsqr = delta * delta, aux2 = exp(-(e2 / dsqr));
+      r0 = dsqr * (1. - aux2);
+      r1 = aux2;
+      break;
+    }
+    case 6: {  // Fair
+      const double aux = sqrt(e2) / delta;
+      r0 = 2. * delta * delta * (aux - log(1. + aux));
+      r1 = 1. / (1. + aux);
+      break;
+    }
+    case 7: {  // Tukey
+      const double e = sqrt(e2), delta2 = delta * delta;
+      if (e <= delta) {
+        const double aux = 1. - e2 / delta2;
+        r0 = delta2 * (1. - aux * aux * aux) / 3.;
+        r1 = aux * aux;
+      } else {
+        r0 = delta2 / 3.;
+        r1 = 0;
+      }
+      break;
+    }
+    case 8: {  // Saturated
+      const double dsqr = delta * delta;
+      if (e2 <= dsqr) { r0 = e2; r1 = 1.; }
+      else { r0 = dsqr; r1 = 0.; }
+      break;
+    }
+    case 9: {  // DCS (delta = phi)
+      double scale = (2.0 * delta) / (delta + e2);
+      if (scale >= 1.0) scale = 1.0;
+      r0 = scale * e2 * scale;
+      r1 = scale * scale;
+      break;
+    }
+    default: r0 = e2; r1 = 1.0; break;
+  }
+}
 
 DI int up_idx(int r, int c) { return c * (c + 1) / 2 + r; }  // packed upper, r <= c
 
@@ -455,6 +526,28 @@ struct FamilySE2 {
     const double Z[9] = {rc, -rs, 0, rs, rc, 0, 0, 0, 1};
     mat3mul(Z, A, Ji);
     mat3mul(Z, B, Jj);
+  }
+};
+
+// ---- host-Jacobian edges (an edge type the device does not know): the host's linearizeOplus
+// (base_binary_edge.hpp:198-266 numeric, or the type's own analytic one) supplies, per edge, the error and
+// both Jacobians row-major in the meas payload: [e (D) | Ji (D x DA) | Jj (D x DB)] ----
+template <int D_, int DA_, int DB_>
+struct FamilyHostJ {
+  static constexpr int D = D_, DA = DA_, DB = DB_, INFO = D * (D + 1) / 2, P = D + D * DA + D * DB;
+  DI static void error(const EdgeData& d, int e, double* err) {
+    const double* p = d.meas + (size_t)e * P;
+#pragma unroll
+    for (int i = 0; i < D; ++i) err[i] = p[i];
+  }
+  DI static void linearize(const EdgeData& d, int e, double* err, double* A, double* B) {
+    const double* p = d.meas + (size_t)e * P;
+#pragma unroll
+    for (int i = 0; i < D; ++i) err[i] = p[i];
+#pragma unroll
+    for (int i = 0; i < D * DA; ++i) A[i] = p[D + i];
+#pragma unroll
+    for (int i = 0; i < D * DB; ++i) B[i] = p[D + D * DA + i];
   }
 };
 

@@ -21,6 +21,7 @@
 #include <limits>
 #include <numeric>
 #include <sstream>
+#include <thread>
 
 namespace g2ohip {
 
@@ -39,8 +40,15 @@ int vertex_state_stride(int t) {
   }
   return 0;
 }
-int edge_dim(int e) { return e == G2OHIP_E_SE3_PROJECT_XYZ ? 2 : (e == G2OHIP_E_SE3_QUAT ? 6 : (e == G2OHIP_E_SE2 ? 3 : -1)); }
-int edge_meas_dim(int e) { return e == G2OHIP_E_SE3_PROJECT_XYZ ? 2 : (e == G2OHIP_E_SE3_QUAT ? 7 : 3); }
+static bool is_hostj(int e) { return e > G2OHIP_E_HOSTJ(0) && e <= G2OHIP_E_HOSTJ(6); }
+int edge_dim(int e) {
+  if (is_hostj(e)) return e - G2OHIP_E_HOSTJ(0);
+  return e == G2OHIP_E_SE3_PROJECT_XYZ ? 2 : (e == G2OHIP_E_SE3_QUAT ? 6 : (e == G2OHIP_E_SE2 ? 3 : -1));
+}
+int edge_meas_dim(int e) {
+  if (is_hostj(e)) return 0;
+  return e == G2OHIP_E_SE3_PROJECT_XYZ ? 2 : (e == G2OHIP_E_SE3_QUAT ? 7 : 3);
+}
 
 // ------------------------------------------------------------------ host-side math for I/O
 namespace {
@@ -372,6 +380,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     for (size_t l = 0; l < sym.levels.size(); ++l) {
       const auto& lv = sym.levels[l];
       long long tiles0 = 0;  // fused tiles of the level's first step
+      if (l == 0) n_blocked = n_inplace_levels = n_pre_levels = n_syrk_ops = n_bwd_rounds = 0;
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
         const int r0 = std::min(NB, q.ns), T = (q.ns + q.nr - r0 + TT - 1) / TT;
@@ -384,6 +393,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       long long lbytes = 0;
       for (int sn : lv) lbytes += 8LL * (sym.sn[sn].ns + sym.sn[sn].nr) * (sym.sn[sn].ns + sym.sn[sn].nr);
       const bool pre = lbytes <= pre_max;
+      (pre ? n_pre_levels : n_inplace_levels)++;
       if (pre)
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
@@ -479,7 +489,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         }
         gm.count = (int)tk.size() - gm.off;
         d0.count = (int)stk.size() - d0.off;
-        if (gm.count) ops.push_back(gm);
+        if (gm.count) { ops.push_back(gm); ++n_syrk_ops; }
         if (d0.count) ops.push_back(d0);
       }
       Op sy{3, (int)tk.size(), 0};
@@ -491,7 +501,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, 0, ti | (tj << 16), 0});
       }
       sy.count = (int)tk.size() - sy.off;
-      if (sy.count) ops.push_back(sy);
+      if (sy.count) { ops.push_back(sy); ++n_syrk_ops; }
+      for (int sn : lv) n_blocked += blocked(sym.sn[sn]) ? 1 : 0;
     }
     nzero = (int)(zr.size() / 2);
     npre = (long long)pdst.size();
@@ -544,6 +555,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         }
         x.second = (int)tk.size() - x.first;
         bl.rounds.push_back({g, x});
+        if (g.second) ++n_bwd_rounds;
       }
       bwd_ops.push_back(bl);
       bwd_off.push_back((int)tk.size());
@@ -642,83 +654,257 @@ int Engine::add_edges(int type, int n, const int* v0, const int* v1, const doubl
                       const double* params) {
   const int D = edge_dim(type);
   if (D < 0 || n < 0) return G2OHIP_ERR_ARG;
-  if (hg.etype && hg.etype != type) return G2OHIP_ERR_UNSUPPORTED;  // one edge family per graph
   if (type == G2OHIP_E_SE3_PROJECT_XYZ && !params) return G2OHIP_ERR_ARG;
-  hg.etype = type;
   const int nm = edge_meas_dim(type);
-  for (int k = 0; k < n; ++k) {
-    auto a = hg.idmap.find(v0[k]), b = hg.idmap.find(v1[k]);
-    if (a == hg.idmap.end() || b == hg.idmap.end()) return G2OHIP_ERR_ARG;
-    hg.ev0.push_back(a->second);
-    hg.ev1.push_back(b->second);
+  if (nm > 0 && !meas && n > 0) return G2OHIP_ERR_ARG;
+  for (int k = 0; k < n; ++k)
+    if (!hg.idmap.count(v0[k]) || !hg.idmap.count(v1[k])) return G2OHIP_ERR_ARG;
+  HEdgeSet* es = hg.set_of(type);
+  if (!es) {
+    hg.esets.emplace_back();
+    es = &hg.esets.back();
+    es->type = type;
+    es->D = D;
+    es->nm = nm;
   }
-  hg.emeas.insert(hg.emeas.end(), meas, meas + (size_t)n * nm);
-  hg.einfo.insert(hg.einfo.end(), info, info + (size_t)n * D * D);
-  if (type == G2OHIP_E_SE3_PROJECT_XYZ) hg.eparams.insert(hg.eparams.end(), params, params + (size_t)n * 4);
+  for (int k = 0; k < n; ++k) {
+    es->ev0.push_back(hg.idmap[v0[k]]);
+    es->ev1.push_back(hg.idmap[v1[k]]);
+  }
+  if (nm > 0) es->meas.insert(es->meas.end(), meas, meas + (size_t)n * nm);
+  es->info.insert(es->info.end(), info, info + (size_t)n * D * D);
+  if (type == G2OHIP_E_SE3_PROJECT_XYZ) es->params.insert(es->params.end(), params, params + (size_t)n * 4);
+  es->payload.clear();
   initialized = false;
   return G2OHIP_OK;
 }
 
-// optimizable_graph.cpp:397-661 for the tags on this path
-int Engine::load(const char* path, int marginalize_xyz) {
-  std::ifstream in(path);
-  if (!in) return G2OHIP_ERR_ARG;
-  std::string line, tag;
+int Engine::set_robust_kernel(int type, int kind, double delta) {
+  HEdgeSet* es = hg.set_of(type);
+  if (!es || kind < G2OHIP_RK_NONE || kind > G2OHIP_RK_DCS || !(delta > 0)) return G2OHIP_ERR_ARG;
+  es->rk = kind;
+  es->rk_delta = delta;
+  ++state_ver;  // the robust chi2 of the same state changes
+  return G2OHIP_OK;
+}
+
+int Engine::set_host_payload(int type, const double* payload) {
+  HEdgeSet* es = hg.set_of(type);
+  if (!es || !is_hostj(type) || !payload) return G2OHIP_ERR_ARG;
+  std::vector<int> dims(es->ev0.size() * 2);
+  size_t len = 0;
+  for (size_t k = 0; k < es->ev0.size(); ++k)
+    len += (size_t)es->D * (1 + hg.verts[es->ev0[k]].dim + hg.verts[es->ev1[k]].dim);
+  es->payload.assign(payload, payload + len);
+  es->payload_ver = 0;  // caller-provided: used as is
+  if (initialized && edges_ready) {
+    for (auto& g : groups)
+      if (g.set == (int)(es - hg.esets.data())) {
+        // gather the group's edges (the host payload has per-edge strides of the edge's own dims; a group has
+        // one (DA, DB), so offsets come from a prefix over the set)
+        std::vector<size_t> off(es->ev0.size() + 1, 0);
+        for (size_t k = 0; k < es->ev0.size(); ++k)
+          off[k + 1] = off[k] + (size_t)es->D * (1 + hg.verts[es->ev0[k]].dim + hg.verts[es->ev1[k]].dim);
+        const int P = g.payload_stride();
+        std::vector<double> buf((size_t)std::max(g.ne, 1) * P);
+        for (int k = 0; k < g.ne; ++k)
+          std::memcpy(buf.data() + (size_t)k * P, es->payload.data() + off[g.edges[k]], sizeof(double) * P);
+        g.meas.upload(buf, stream);
+      }
+    ++state_ver;  // errors (chi2) of the host-J edges changed
+  }
+  return G2OHIP_OK;
+}
+
+int Engine::set_host_callback(g2ohip_host_edge_fn fn, void* user) {
+  host_fn = fn;
+  host_user = user;
+  return G2OHIP_OK;
+}
+
+// OptimizableGraph::load (optimizable_graph.cpp:397-661) for the tags on this path, parsed in parallel: the file
+// is read once, cut into line-aligned chunks, each chunk parsed by its own thread (strtod/strtol, no streams)
+// into typed records, and the records added in file order with batched add_vertices / add_edges. Unknown tags
+// are skipped with one warning per tag (:455-460); FIX lines fix vertices after loading (:409-417).
+namespace {
+struct ParsedVertex { int type, id; double est[7]; };
+struct ParsedEdge { int type, a, b; double m[7], info[36], p[4]; };
+struct ParsedChunk {
+  std::vector<ParsedVertex> verts;
+  std::vector<ParsedEdge> edges;
   std::vector<int> fix;
-  while (std::getline(in, line)) {
-    std::istringstream ss(line);
-    if (!(ss >> tag) || tag[0] == '#') continue;
-    int r = 0;
-    if (tag == "VERTEX_SE3:EXPMAP") {  // file holds cam2world (types_six_dof_expmap.cpp:93-101)
-      int id; double v[7], w[7];
-      ss >> id; for (double& d : v) ss >> d;
-      double q[4] = {v[3], v[4], v[5], v[6]};
-      double tq[7] = {v[0], v[1], v[2], q[0], q[1], q[2], q[3]};
-      se3quat_inverse(tq, w);
-      int z = 0;
-      r = add_vertices(G2OHIP_V_SE3_EXPMAP, 1, &id, w, &z, &z);
-    } else if (tag == "VERTEX_XYZ") {
-      int id; double v[3];
-      ss >> id >> v[0] >> v[1] >> v[2];
-      int z = 0, m = marginalize_xyz ? 1 : 0;
-      r = add_vertices(G2OHIP_V_XYZ, 1, &id, v, &z, &m);
-    } else if (tag == "VERTEX_SE3:QUAT") {
-      int id; double v[7];
-      ss >> id; for (double& d : v) ss >> d;
-      int z = 0;
-      r = add_vertices(G2OHIP_V_SE3_QUAT, 1, &id, v, &z, &z);
-    } else if (tag == "VERTEX_SE2") {
-      int id; double v[3];
-      ss >> id >> v[0] >> v[1] >> v[2];
-      int z = 0;
-      r = add_vertices(G2OHIP_V_SE2, 1, &id, v, &z, &z);
+  std::vector<std::string> unknown;
+  bool bad = false;
+};
+struct Cursor {
+  const char* p;
+  const char* e;
+  bool ok = true;
+  void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) ++p; }
+  double d() {
+    ws();
+    char* end = nullptr;
+    const double v = std::strtod(p, &end);
+    if (end == p || end > e) { ok = false; return 0; }
+    p = end;
+    return v;
+  }
+  int i() {
+    ws();
+    char* end = nullptr;
+    const long v = std::strtol(p, &end, 10);
+    if (end == p || end > e) { ok = false; return 0; }
+    p = end;
+    return (int)v;
+  }
+  bool more() { ws(); return p < e; }
+};
+void parse_chunk(const char* b, const char* e, ParsedChunk& out) {
+  while (b < e) {
+    const char* nl = static_cast<const char*>(std::memchr(b, '\n', (size_t)(e - b)));
+    const char* le = nl ? nl : e;
+    Cursor c{b, le};
+    c.ws();
+    const char* t0 = c.p;
+    while (c.p < le && *c.p != ' ' && *c.p != '\t' && *c.p != '\r') ++c.p;
+    const std::string tag(t0, c.p);
+    b = nl ? nl + 1 : e;
+    if (tag.empty() || tag[0] == '#') continue;
+    if (tag == "VERTEX_SE3:EXPMAP" || tag == "VERTEX_SE3:QUAT") {
+      ParsedVertex v{tag == "VERTEX_SE3:EXPMAP" ? G2OHIP_V_SE3_EXPMAP : G2OHIP_V_SE3_QUAT, c.i(), {}};
+      for (double& x : v.est) x = c.d();
+      if (v.type == G2OHIP_V_SE3_EXPMAP) {  // the file holds cam2world (types_six_dof_expmap.cpp:93-101)
+        double w[7];
+        se3quat_inverse(v.est, w);
+        std::memcpy(v.est, w, sizeof w);
+      }
+      out.verts.push_back(v);
+    } else if (tag == "VERTEX_XYZ" || tag == "VERTEX_SE2") {
+      ParsedVertex v{tag == "VERTEX_XYZ" ? G2OHIP_V_XYZ : G2OHIP_V_SE2, c.i(), {}};
+      for (int k = 0; k < 3; ++k) v.est[k] = c.d();
+      out.verts.push_back(v);
     } else if (tag == "FIX") {
-      int id;
-      while (ss >> id) fix.push_back(id);
-    } else if (tag == "EDGE_SE3_PROJECT_XYZ:EXPMAP") {
-      int a, b; double m[2], o[3], p[4];
-      ss >> a >> b >> m[0] >> m[1] >> o[0] >> o[1] >> o[2] >> p[0] >> p[1] >> p[2] >> p[3];
-      double info[4] = {o[0], o[1], o[1], o[2]};
-      r = add_edges(G2OHIP_E_SE3_PROJECT_XYZ, 1, &a, &b, m, info, p);
-    } else if (tag == "EDGE_SE3:QUAT") {
-      int a, b; double m[7], info[36];
-      ss >> a >> b; for (double& d : m) ss >> d;
-      for (int i = 0; i < 6; ++i) for (int j = i; j < 6; ++j) { ss >> info[i * 6 + j]; info[j * 6 + i] = info[i * 6 + j]; }
-      r = add_edges(G2OHIP_E_SE3_QUAT, 1, &a, &b, m, info, nullptr);
-    } else if (tag == "EDGE_SE2") {
-      int a, b; double m[3], info[9];
-      ss >> a >> b >> m[0] >> m[1] >> m[2];
-      for (int i = 0; i < 3; ++i) for (int j = i; j < 3; ++j) { ss >> info[i * 3 + j]; info[j * 3 + i] = info[i * 3 + j]; }
-      r = add_edges(G2OHIP_E_SE2, 1, &a, &b, m, info, nullptr);
+      while (c.more()) {
+        const int id = c.i();
+        if (!c.ok) break;
+        out.fix.push_back(id);
+      }
+      c.ok = true;
+    } else if (tag == "EDGE_SE3_PROJECT_XYZ:EXPMAP") {  // types_six_dof_expmap.cpp:363-378
+      ParsedEdge ed{G2OHIP_E_SE3_PROJECT_XYZ, c.i(), c.i(), {}, {}, {}};
+      ed.m[0] = c.d(); ed.m[1] = c.d();
+      const double o0 = c.d(), o1 = c.d(), o2 = c.d();
+      ed.info[0] = o0; ed.info[1] = o1; ed.info[2] = o1; ed.info[3] = o2;
+      for (double& x : ed.p) x = c.d();
+      out.edges.push_back(ed);
+    } else if (tag == "EDGE_SE3:QUAT" || tag == "EDGE_SE2") {  // edge_se3.cpp:42-65, edge_se2.cpp:41-53
+      const bool se3 = tag == "EDGE_SE3:QUAT";
+      const int D = se3 ? 6 : 3, nm = se3 ? 7 : 3;
+      ParsedEdge ed{se3 ? G2OHIP_E_SE3_QUAT : G2OHIP_E_SE2, c.i(), c.i(), {}, {}, {}};
+      for (int k = 0; k < nm; ++k) ed.m[k] = c.d();
+      for (int r = 0; r < D; ++r)
+        for (int q = r; q < D; ++q) ed.info[r * D + q] = ed.info[q * D + r] = c.d();
+      out.edges.push_back(ed);
     } else {
-      return G2OHIP_ERR_UNSUPPORTED;
+      if (std::find(out.unknown.begin(), out.unknown.end(), tag) == out.unknown.end()) out.unknown.push_back(tag);
+      continue;
     }
-    if (r) return r;
+    if (!c.ok) { out.bad = true; return; }
   }
-  for (int id : fix) {
-    auto it = hg.idmap.find(id);
-    if (it != hg.idmap.end()) hg.verts[it->second].fixed = true;
+}
+}  // namespace
+
+int Engine::load(const char* path, int marginalize_xyz) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return G2OHIP_ERR_ARG;
+  std::vector<char> buf;
+  {
+    std::fseek(f, 0, SEEK_END);
+    const long sz = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    buf.resize(sz > 0 ? (size_t)sz : 0);
+    const size_t got = sz > 0 ? std::fread(buf.data(), 1, (size_t)sz, f) : 0;
+    fclose(f);
+    if (got != buf.size()) return G2OHIP_ERR_ARG;
   }
+  const char* base = buf.data();
+  const size_t n = buf.size();
+  const int nthreads = (int)std::max<size_t>(1, std::min<size_t>(16, n / (1 << 20)));
+  std::vector<size_t> cut(nthreads + 1, n);
+  cut[0] = 0;
+  for (int t = 1; t < nthreads; ++t) {
+    size_t c = std::max(cut[t - 1], n * t / nthreads);
+    while (c < n && base[c - 1] != '\n') ++c;
+    cut[t] = c;
+  }
+  std::vector<ParsedChunk> chunks(nthreads);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+      th.emplace_back([&, t] { parse_chunk(base + cut[t], base + cut[t + 1], chunks[t]); });
+    for (auto& x : th) x.join();
+  }
+  std::vector<std::string> warned;
+  for (auto& c : chunks) {
+    if (c.bad) return G2OHIP_ERR_ARG;
+    for (auto& u : c.unknown)
+      if (std::find(warned.begin(), warned.end(), u) == warned.end()) {
+        warned.push_back(u);
+        fprintf(stderr, "g2o_hip load: unknown type %s (lines skipped)\n", u.c_str());
+      }
+  }
+  // vertices in file order, batched per run of one type
+  std::vector<int> ids, fx, mg;
+  std::vector<double> est;
+  auto flush_v = [&](int type) -> int {
+    if (ids.empty()) return G2OHIP_OK;
+    const int r = add_vertices(type, (int)ids.size(), ids.data(), est.data(), fx.data(), mg.data());
+    ids.clear(); est.clear(); fx.clear(); mg.clear();
+    return r;
+  };
+  int cur = 0;
+  for (auto& c : chunks)
+    for (auto& v : c.verts) {
+      if (v.type != cur) {
+        if (int r = flush_v(cur)) return r;
+        cur = v.type;
+      }
+      ids.push_back(v.id);
+      est.insert(est.end(), v.est, v.est + vertex_est_dim(v.type));
+      fx.push_back(0);
+      mg.push_back(v.type == G2OHIP_V_XYZ && marginalize_xyz ? 1 : 0);
+    }
+  if (int r = flush_v(cur)) return r;
+  // edges in file order, batched per run of one type
+  std::vector<int> ea, eb;
+  std::vector<double> em, ei, ep;
+  auto flush_e = [&](int type) -> int {
+    if (ea.empty()) return G2OHIP_OK;
+    const int r = add_edges(type, (int)ea.size(), ea.data(), eb.data(), em.data(), ei.data(),
+                            type == G2OHIP_E_SE3_PROJECT_XYZ ? ep.data() : nullptr);
+    ea.clear(); eb.clear(); em.clear(); ei.clear(); ep.clear();
+    return r;
+  };
+  cur = 0;
+  for (auto& c : chunks)
+    for (auto& ed : c.edges) {
+      if (ed.type != cur) {
+        if (int r = flush_e(cur)) return r;
+        cur = ed.type;
+      }
+      const int D = edge_dim(ed.type), nm = edge_meas_dim(ed.type);
+      ea.push_back(ed.a);
+      eb.push_back(ed.b);
+      em.insert(em.end(), ed.m, ed.m + nm);
+      ei.insert(ei.end(), ed.info, ed.info + D * D);
+      if (ed.type == G2OHIP_E_SE3_PROJECT_XYZ) ep.insert(ep.end(), ed.p, ed.p + 4);
+    }
+  if (int r = flush_e(cur)) return r;
+  for (auto& c : chunks)
+    for (int id : c.fix) {
+      auto it = hg.idmap.find(id);
+      if (it != hg.idmap.end()) hg.verts[it->second].fixed = true;
+    }
   return G2OHIP_OK;
 }
 
@@ -745,20 +931,26 @@ int Engine::save(const char* path) {
     }
     if (v.fixed) fprintf(f, "FIX %d\n", v.id);
   }
-  const int D = edge_dim(hg.etype), nm = edge_meas_dim(hg.etype);
-  for (size_t k = 0; k < hg.ev0.size(); ++k) {
-    const int a = hg.verts[hg.ev0[k]].id, b = hg.verts[hg.ev1[k]].id;
-    const double* m = hg.emeas.data() + k * nm;
-    const double* I = hg.einfo.data() + k * D * D;
-    if (hg.etype == G2OHIP_E_SE3_PROJECT_XYZ) {
-      const double* p = hg.eparams.data() + k * 4;
-      fprintf(f, "EDGE_SE3_PROJECT_XYZ:EXPMAP %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", a, b, m[0], m[1],
-              I[0], I[1], I[3], p[0], p[1], p[2], p[3]);
-    } else {
-      fprintf(f, "%s %d %d", hg.etype == G2OHIP_E_SE3_QUAT ? "EDGE_SE3:QUAT" : "EDGE_SE2", a, b);
-      for (int i = 0; i < nm; ++i) fprintf(f, " %.17g", m[i]);
-      for (int i = 0; i < D; ++i) for (int j = i; j < D; ++j) fprintf(f, " %.17g", I[i * D + j]);
-      fprintf(f, "\n");
+  for (const HEdgeSet& es : hg.esets) {
+    if (is_hostj(es.type)) {  // the device does not know the host type's tag: the host saves those edges
+      fprintf(stderr, "g2o_hip save: %zu host-Jacobian edges (type %d) not written\n", es.ev0.size(), es.type);
+      continue;
+    }
+    const int D = es.D, nm = es.nm;
+    for (size_t k = 0; k < es.ev0.size(); ++k) {
+      const int a = hg.verts[es.ev0[k]].id, b = hg.verts[es.ev1[k]].id;
+      const double* m = es.meas.data() + k * nm;
+      const double* I = es.info.data() + k * D * D;
+      if (es.type == G2OHIP_E_SE3_PROJECT_XYZ) {
+        const double* p = es.params.data() + k * 4;
+        fprintf(f, "EDGE_SE3_PROJECT_XYZ:EXPMAP %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", a, b, m[0],
+                m[1], I[0], I[1], I[3], p[0], p[1], p[2], p[3]);
+      } else {
+        fprintf(f, "%s %d %d", es.type == G2OHIP_E_SE3_QUAT ? "EDGE_SE3:QUAT" : "EDGE_SE2", a, b);
+        for (int i = 0; i < nm; ++i) fprintf(f, " %.17g", m[i]);
+        for (int i = 0; i < D; ++i) for (int j = i; j < D; ++j) fprintf(f, " %.17g", I[i * D + j]);
+        fprintf(f, "\n");
+      }
     }
   }
   fclose(f);
@@ -820,18 +1012,32 @@ int Engine::minimal_state(double* out) {
 }
 
 // ------------------------------------------------------------------ Engine: structure
-int Engine::initialize() {  // sparse_optimizer.cpp:201-279 + buildIndexMapping :168-192
-  if (hg.ev0.empty()) return G2OHIP_ERR_STATE;
-  switch (hg.etype) {
-    case G2OHIP_E_SE3_PROJECT_XYZ: family = FAM_BA; vt0 = G2OHIP_V_XYZ; vt1 = G2OHIP_V_SE3_EXPMAP; break;
-    case G2OHIP_E_SE3_QUAT: family = FAM_SE3; vt0 = vt1 = G2OHIP_V_SE3_QUAT; break;
-    case G2OHIP_E_SE2: family = FAM_SE2; vt0 = vt1 = G2OHIP_V_SE2; break;
-    default: return G2OHIP_ERR_UNSUPPORTED;
+// device family of an edge type (host-J types: any endpoint vertex types)
+static int family_of(int etype, int& vtA, int& vtB) {
+  switch (etype) {
+    case G2OHIP_E_SE3_PROJECT_XYZ: vtA = G2OHIP_V_XYZ; vtB = G2OHIP_V_SE3_EXPMAP; return FAM_BA;
+    case G2OHIP_E_SE3_QUAT: vtA = vtB = G2OHIP_V_SE3_QUAT; return FAM_SE3;
+    case G2OHIP_E_SE2: vtA = vtB = G2OHIP_V_SE2; return FAM_SE2;
   }
-  for (size_t k = 0; k < hg.ev0.size(); ++k)
-    if (hg.verts[hg.ev0[k]].type != vt0 || hg.verts[hg.ev1[k]].type != vt1) return G2OHIP_ERR_UNSUPPORTED;
+  vtA = vtB = 0;
+  return is_hostj(etype) ? FAM_HOSTJ : FAM_NONE;
+}
+
+int Engine::initialize() {  // sparse_optimizer.cpp:201-279 + buildIndexMapping :168-192
+  if (hg.num_edges() == 0) return G2OHIP_ERR_STATE;
+  has_hostj = false;
   std::vector<char> has(hg.verts.size(), 0);
-  for (size_t k = 0; k < hg.ev0.size(); ++k) has[hg.ev0[k]] = has[hg.ev1[k]] = 1;
+  for (const HEdgeSet& es : hg.esets) {
+    int vtA, vtB;
+    const int fam = family_of(es.type, vtA, vtB);
+    if (fam == FAM_NONE) return G2OHIP_ERR_UNSUPPORTED;
+    has_hostj |= fam == FAM_HOSTJ;
+    for (size_t k = 0; k < es.ev0.size(); ++k) {
+      const HVertex &a = hg.verts[es.ev0[k]], &b = hg.verts[es.ev1[k]];
+      if (fam != FAM_HOSTJ && (a.type != vtA || b.type != vtB)) return G2OHIP_ERR_UNSUPPORTED;
+      has[es.ev0[k]] = has[es.ev1[k]] = 1;
+    }
+  }
   active.clear();
   for (size_t k = 0; k < hg.verts.size(); ++k)
     if (has[k]) active.push_back((int)k);
@@ -851,7 +1057,7 @@ int Engine::initialize() {  // sparse_optimizer.cpp:201-279 + buildIndexMapping 
   for (int vi : ivmap) {
     const HVertex& v = hg.verts[vi];
     if (!v.marg) {
-      if (pd && pd != v.dim) return G2OHIP_ERR_UNSUPPORTED;
+      if (pd && pd != v.dim) return G2OHIP_ERR_UNSUPPORTED;  // BlockSolver<p, l>: one pose block size
       pd = v.dim;
       ++num_poses;
     } else {
@@ -864,16 +1070,71 @@ int Engine::initialize() {  // sparse_optimizer.cpp:201-279 + buildIndexMapping 
   size_poses = num_poses * pd;
   size_landmarks = num_landmarks * ld;
   do_schur = num_landmarks > 0;  // optimization_algorithm_with_hessian.cpp:48-73
-  if (do_schur && (family != FAM_BA || pd != 6)) return G2OHIP_ERR_UNSUPPORTED;
+  if (do_schur && pd != 6) return G2OHIP_ERR_UNSUPPORTED;  // the Schur kernels are BlockSolver_6_3
+  // landmark-landmark edges have no place in BlockSolver's Schur layout here
+  for (const HEdgeSet& es : hg.esets)
+    for (size_t k = 0; k < es.ev0.size(); ++k) {
+      const int a = hidx[es.ev0[k]], b = hidx[es.ev1[k]];
+      if (a >= num_poses && b >= num_poses) return G2OHIP_ERR_UNSUPPORTED;
+    }
   initialized = true;
   structure_built = false;
   edges_ready = false;
   return G2OHIP_OK;
 }
 
+EdgeArgs Engine::group_args(const EGroup& g) const {
+  EdgeArgs a{g.v0.get(), g.v1.get(), g.meas.get(), g.info.get(), g.params.get(),
+             g.vtA ? dstate[g.vtA].get() : nullptr, g.vtB ? dstate[g.vtB].get() : nullptr};
+  a.rk = hg.esets[g.set].rk;
+  a.rk_delta = hg.esets[g.set].rk_delta;
+  a.D = g.D;
+  a.DA = g.DA;
+  a.DB = g.DB;
+  return a;
+}
+
+// upload the host-J payload of one group (its local edges, gathered from the set's insertion-order payload)
+static void upload_group_payload(const HostGraph& hg, EGroup& g, hipStream_t s) {
+  const HEdgeSet& es = hg.esets[g.set];
+  const int P = g.payload_stride();
+  std::vector<double> buf((size_t)std::max(g.ne, 1) * P, 0.0);
+  if (!es.payload.empty()) {
+    std::vector<size_t> off(es.ev0.size() + 1, 0);
+    for (size_t k = 0; k < es.ev0.size(); ++k)
+      off[k + 1] = off[k] + (size_t)es.D * (1 + hg.verts[es.ev0[k]].dim + hg.verts[es.ev1[k]].dim);
+    if (off.back() != es.payload.size()) throw std::runtime_error("host-J payload size does not match the edges");
+    for (int k = 0; k < g.ne; ++k)
+      std::memcpy(buf.data() + (size_t)k * P, es.payload.data() + off[g.edges[k]], sizeof(double) * P);
+  }
+  g.meas.upload(buf, s);
+}
+
+void Engine::refresh_host_payload(bool jacobians) {
+  if (!has_hostj) return;
+  for (size_t si = 0; si < hg.esets.size(); ++si) {
+    HEdgeSet& es = hg.esets[si];
+    if (!is_hostj(es.type)) continue;
+    if (host_fn) {
+      if (!jacobians && es.payload_ver == state_ver) continue;  // errors of this state already there
+      sync_host_state();  // the callback reads the estimates the device holds
+      size_t len = 0;
+      for (size_t k = 0; k < es.ev0.size(); ++k)
+        len += (size_t)es.D * (1 + hg.verts[es.ev0[k]].dim + hg.verts[es.ev1[k]].dim);
+      es.payload.assign(len, 0.0);
+      if (host_fn(host_user, es.type, jacobians ? 1 : 0, es.payload.data()) != 0)
+        throw std::runtime_error("host edge callback failed for edge type " + std::to_string(es.type));
+      es.payload_ver = state_ver;
+    } else if (es.payload.empty()) {
+      throw std::runtime_error("host-Jacobian edges (type " + std::to_string(es.type) +
+                               ") need g2ohip_set_host_jacobians or a host edge callback");
+    }
+    for (auto& g : groups)
+      if (g.set == (int)si) upload_group_payload(hg, g, stream);
+  }
+}
+
 void Engine::setup_edges_device() {
-  const int nall = (int)hg.ev0.size();
-  local_edges.clear();
   int lm_begin = 0, lm_end = num_landmarks;
   if (do_schur && nranks > 1) {
     lm_begin = (int)((long long)num_landmarks * rank / nranks);
@@ -881,63 +1142,98 @@ void Engine::setup_edges_device() {
   }
   local_lm.clear();
   for (int l = lm_begin; l < lm_end; ++l) local_lm.push_back(l);
-  for (int k = 0; k < nall; ++k) {
-    int owner = 0;
-    if (do_schur && nranks > 1) {
-      const int h = hidx[hg.ev0[k]];  // BA: vertex 0 is the point
-      if (h >= num_poses) {
-        const int l = h - num_poses;
-        for (int r = 0; r < nranks; ++r)
-          if (l >= (int)((long long)num_landmarks * r / nranks) && l < (int)((long long)num_landmarks * (r + 1) / nranks))
-            owner = r;
+  // landmark shards: an edge belongs to the rank owning its landmark endpoint; edges without a (free) landmark
+  // are assembled by rank 0 once. Pose graphs run replicas: every rank assembles every edge.
+  std::vector<int> bnd(nranks + 1);
+  for (int r = 0; r <= nranks; ++r) bnd[r] = (int)((long long)num_landmarks * r / nranks);
+  auto owner_of = [&](int va, int vb) {
+    if (!(do_schur && nranks > 1)) return rank;
+    const int h = hidx[va] >= num_poses ? hidx[va] : (hidx[vb] >= num_poses ? hidx[vb] : -1);
+    if (h < 0) return 0;
+    return (int)(std::upper_bound(bnd.begin(), bnd.end(), h - num_poses) - bnd.begin()) - 1;
+  };
+  groups.clear();
+  ne = 0;
+  for (size_t si = 0; si < hg.esets.size(); ++si) {
+    const HEdgeSet& es = hg.esets[si];
+    int vtA, vtB;
+    const int fam = family_of(es.type, vtA, vtB);
+    // groups: one per (endpoint vertex type pair) in first-seen order; device families have exactly one
+    std::vector<std::pair<int, int>> keys;
+    std::vector<std::vector<int>> lists;
+    for (size_t k = 0; k < es.ev0.size(); ++k) {
+      const int va = es.ev0[k], vb = es.ev1[k];
+      if (owner_of(va, vb) != rank) continue;
+      const std::pair<int, int> key{hg.verts[va].type, hg.verts[vb].type};
+      size_t gi = std::find(keys.begin(), keys.end(), key) - keys.begin();
+      if (gi == keys.size()) { keys.push_back(key); lists.emplace_back(); }
+      lists[gi].push_back((int)k);
+    }
+    for (size_t gi = 0; gi < keys.size(); ++gi) {
+      groups.emplace_back();
+      EGroup& g = groups.back();
+      g.set = (int)si;
+      g.family = fam;
+      g.vtA = keys[gi].first;
+      g.vtB = keys[gi].second;
+      g.D = es.D;
+      g.DA = vertex_dim(g.vtA);
+      g.DB = vertex_dim(g.vtB);
+      g.edges = std::move(lists[gi]);
+      g.ne = (int)g.edges.size();
+      ne += g.ne;
+    }
+  }
+  for (EGroup& g : groups) {
+    const HEdgeSet& es = hg.esets[g.set];
+    const int D = g.D, nm = es.nm, gne = g.ne;
+    std::vector<int> v0(std::max(gne, 1), 0), v1(std::max(gne, 1), 0);
+    const int minfo = D * (D + 1) / 2;
+    const int mmeas = g.family == FAM_BA ? 2 : (g.family == FAM_SE3 ? 12 : (g.family == FAM_SE2 ? 3 : 0));
+    std::vector<double> meas((size_t)std::max(gne, 1) * std::max(mmeas, 1)), info((size_t)std::max(gne, 1) * minfo),
+        params(g.family == FAM_BA ? (size_t)gne * 4 : 1);
+    for (int k = 0; k < gne; ++k) {
+      const int e = g.edges[k];
+      v0[k] = hg.verts[es.ev0[e]].local;
+      v1[k] = hg.verts[es.ev1[e]].local;
+      const double* m = es.meas.data() + (size_t)e * nm;
+      double* mo = meas.data() + (size_t)k * mmeas;
+      if (g.family == FAM_BA) {
+        mo[0] = m[0]; mo[1] = m[1];
+        for (int j = 0; j < 4; ++j) params[(size_t)k * 4 + j] = es.params[(size_t)e * 4 + j];
+      } else if (g.family == FAM_SE3) {  // edge_se3.cpp:42-50: normalise q, Z = fromVectorQT, store Z^-1
+        double q[4] = {m[3], m[4], m[5], m[6]};
+        const double n = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        for (double& x : q) x /= n;
+        double Z[9];
+        q2R(q[0], q[1], q[2], q[3], Z);
+        double Rt[9] = {Z[0], Z[3], Z[6], Z[1], Z[4], Z[7], Z[2], Z[5], Z[8]};
+        for (int j = 0; j < 9; ++j) mo[j] = Rt[j];
+        for (int i = 0; i < 3; ++i) mo[9 + i] = -(Rt[i * 3] * m[0] + Rt[i * 3 + 1] * m[1] + Rt[i * 3 + 2] * m[2]);
+      } else if (g.family == FAM_SE2) {  // edge_se2.cpp:41-47: inverse measurement
+        const double th = norm_theta(-m[2]);
+        const double c = std::cos(th), s = std::sin(th);
+        mo[0] = c * (-m[0]) - s * (-m[1]);
+        mo[1] = s * (-m[0]) + c * (-m[1]);
+        mo[2] = th;
       }
-    } else if (nranks > 1) {
-      owner = rank;  // pose graphs: replicas
+      const double* I = es.info.data() + (size_t)e * D * D;
+      double* io = info.data() + (size_t)k * minfo;
+      int q = 0;
+      for (int c = 0; c < D; ++c)
+        for (int r = 0; r <= c; ++r) io[q++] = I[r * D + c];
     }
-    if (owner == rank) local_edges.push_back(k);
+    g.v0.upload(v0, stream);
+    g.v1.upload(v1, stream);
+    g.info.upload(info, stream);
+    g.params.upload(params, stream);
+    if (g.family == FAM_HOSTJ) upload_group_payload(hg, g, stream);
+    else g.meas.upload(meas, stream);
   }
-  ne = (int)local_edges.size();
-  const int D = edge_dim(hg.etype), nm = edge_meas_dim(hg.etype);
-  std::vector<int> v0(ne), v1(ne);
-  int minfo = D * (D + 1) / 2, mmeas = family == FAM_BA ? 2 : (family == FAM_SE3 ? 12 : 3);
-  std::vector<double> meas((size_t)ne * mmeas), info((size_t)ne * minfo), params(family == FAM_BA ? (size_t)ne * 4 : 1);
-  for (int k = 0; k < ne; ++k) {
-    const int e = local_edges[k];
-    v0[k] = hg.verts[hg.ev0[e]].local;
-    v1[k] = hg.verts[hg.ev1[e]].local;
-    const double* m = hg.emeas.data() + (size_t)e * nm;
-    double* mo = meas.data() + (size_t)k * mmeas;
-    if (family == FAM_BA) {
-      mo[0] = m[0]; mo[1] = m[1];
-      for (int j = 0; j < 4; ++j) params[(size_t)k * 4 + j] = hg.eparams[(size_t)e * 4 + j];
-    } else if (family == FAM_SE3) {  // edge_se3.cpp:42-50: normalise q, Z = fromVectorQT, store Z^-1
-      double q[4] = {m[3], m[4], m[5], m[6]};
-      const double n = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-      for (double& x : q) x /= n;
-      double Z[9];
-      q2R(q[0], q[1], q[2], q[3], Z);
-      double Rt[9] = {Z[0], Z[3], Z[6], Z[1], Z[4], Z[7], Z[2], Z[5], Z[8]};
-      for (int j = 0; j < 9; ++j) mo[j] = Rt[j];
-      for (int i = 0; i < 3; ++i) mo[9 + i] = -(Rt[i * 3] * m[0] + Rt[i * 3 + 1] * m[1] + Rt[i * 3 + 2] * m[2]);
-    } else {  // edge_se2.cpp:41-47: inverse measurement
-      const double th = norm_theta(-m[2]);
-      const double c = std::cos(th), s = std::sin(th);
-      mo[0] = c * (-m[0]) - s * (-m[1]);
-      mo[1] = s * (-m[0]) + c * (-m[1]);
-      mo[2] = th;
-    }
-    const double* I = hg.einfo.data() + (size_t)e * D * D;
-    double* io = info.data() + (size_t)k * minfo;
-    int q = 0;
-    for (int c = 0; c < D; ++c)
-      for (int r = 0; r <= c; ++r) io[q++] = I[r * D + c];
-  }
-  dv0.upload(v0, stream);
-  dv1.upload(v1, stream);
-  dmeas.upload(meas, stream);
-  dinfo.upload(info, stream);
-  dparams.upload(params, stream);
-  dpartial.resize(std::max<size_t>(launch::sum_partials(std::max<long long>(std::max<long long>(ne, vector_size()), 1)) + 64, 128));
+  long long maxp = std::max<long long>(vector_size(), 1);
+  long long ptot = 0;
+  for (auto& g : groups) ptot += (long long)launch::sum_partials(std::max(g.ne, 1));
+  dpartial.resize(std::max<size_t>(std::max<size_t>(launch::sum_partials(maxp), (size_t)ptot) + 64, 128));
   edges_ready = true;
   ++state_ver;  // the edge set (and so chi2) changed
 }
@@ -965,97 +1261,128 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     d_hidx[t].upload(hx, stream);
     d_xoff[t].upload(xo, stream);
   }
-  // off-diagonal blocks (mapHessianMemory)
-  const int DA = vertex_dim(vt0), DB = vertex_dim(vt1);
+  // off-diagonal blocks (mapHessianMemory, block_solver.hpp:142-210) over every local edge of every group
+  std::vector<long long> gfirst(groups.size() + 1, 0);  // flat local edge index of each group's first edge
+  for (size_t gi = 0; gi < groups.size(); ++gi) gfirst[gi + 1] = gfirst[gi] + groups[gi].ne;
+  auto verts_of = [&](size_t gi, int k, int& va, int& vb) {
+    const HEdgeSet& es = hg.esets[groups[gi].set];
+    const int e = groups[gi].edges[k];
+    va = es.ev0[e];
+    vb = es.ev1[e];
+  };
   std::map<std::pair<int, int>, int> hppmap;  // (i<j) -> block id
   hpp_bi.assign(num_poses, 0);
   hpp_bj.assign(num_poses, 0);
   for (int i = 0; i < num_poses; ++i) hpp_bi[i] = hpp_bj[i] = i;
   struct OffRef { int kind; int a, b; bool tr; };
-  std::vector<OffRef> offref(ne, OffRef{0, 0, 0, false});
+  std::vector<OffRef> offref(std::max(ne, 1), OffRef{0, 0, 0, false});
   std::vector<std::pair<int, int>> plpairs;  // (lm, pose)
-  for (int k = 0; k < ne; ++k) {
-    const int e = local_edges[k];
-    int i1 = hidx[hg.ev0[e]], i2 = hidx[hg.ev1[e]];
-    if (i1 < 0 || i2 < 0) continue;
-    const bool m1 = i1 >= num_poses, m2 = i2 >= num_poses;
-    if (!m1 && !m2) {
-      bool tr = i1 > i2;
-      if (tr) std::swap(i1, i2);
-      auto it = hppmap.find({i1, i2});
-      if (it == hppmap.end()) {
-        it = hppmap.emplace(std::make_pair(i1, i2), (int)hpp_bi.size()).first;
-        hpp_bi.push_back(i1);
-        hpp_bj.push_back(i2);
+  for (size_t gi = 0; gi < groups.size(); ++gi)
+    for (int k = 0; k < groups[gi].ne; ++k) {
+      int va, vb;
+      verts_of(gi, k, va, vb);
+      const long long f = gfirst[gi] + k;
+      int i1 = hidx[va], i2 = hidx[vb];
+      if (i1 < 0 || i2 < 0) continue;
+      const bool m1 = i1 >= num_poses, m2 = i2 >= num_poses;
+      if (!m1 && !m2) {
+        bool tr = i1 > i2;
+        if (tr) std::swap(i1, i2);
+        auto it = hppmap.find({i1, i2});
+        if (it == hppmap.end()) {
+          it = hppmap.emplace(std::make_pair(i1, i2), (int)hpp_bi.size()).first;
+          hpp_bi.push_back(i1);
+          hpp_bj.push_back(i2);
+        }
+        offref[f] = OffRef{1, it->second, 0, tr};
+      } else if (m1 && !m2) {
+        offref[f] = OffRef{2, i2, i1 - num_poses, true};
+        plpairs.push_back({i1 - num_poses, i2});
+      } else if (!m1 && m2) {
+        offref[f] = OffRef{2, i1, i2 - num_poses, false};
+        plpairs.push_back({i2 - num_poses, i1});
+      } else {
+        return G2OHIP_ERR_UNSUPPORTED;  // landmark-landmark edges
       }
-      offref[k] = OffRef{1, it->second, 0, tr};
-    } else if (m1 && !m2) {
-      offref[k] = OffRef{2, i2, i1 - num_poses, true};
-      plpairs.push_back({i1 - num_poses, i2});
-    } else if (!m1 && m2) {
-      offref[k] = OffRef{2, i1, i2 - num_poses, false};
-      plpairs.push_back({i2 - num_poses, i1});
-    } else {
-      return G2OHIP_ERR_UNSUPPORTED;  // landmark-landmark edges
     }
-  }
   nHpp = (int)hpp_bi.size();
   std::sort(plpairs.begin(), plpairs.end());
   plpairs.erase(std::unique(plpairs.begin(), plpairs.end()), plpairs.end());
   nHpl = (int)plpairs.size();
   const long long hpl_base = (long long)nHpp * pd * pd;
-  std::vector<long long> offdst(std::max(ne, 1), -1);
-  std::vector<unsigned char> offtr(std::max(ne, 1), 0);
-  std::vector<long long> blkdst;  // per distinct off block id (global index over hpp offdiag + hpl)
-  std::vector<int> blk_count;
   auto blk_key = [&](const OffRef& r) -> long long {
     if (r.kind == 1) return r.a;  // hpp block id
     auto it = std::lower_bound(plpairs.begin(), plpairs.end(), std::make_pair(r.b, r.a));
     return nHpp + (long long)(it - plpairs.begin());
   };
-  blk_count.assign(nHpp + nHpl, 0);
-  std::vector<long long> ekey(ne, -1);
-  for (int k = 0; k < ne; ++k) {
-    if (!offref[k].kind) continue;
-    ekey[k] = blk_key(offref[k]);
-    blk_count[ekey[k]]++;
-    offtr[k] = offref[k].tr ? 1 : 0;
-    offdst[k] = ekey[k] < nHpp ? ekey[k] * pd * pd : hpl_base + (ekey[k] - nHpp) * pd * ld;
+  auto blk_off = [&](long long key) { return key < nHpp ? key * pd * pd : hpl_base + (key - nHpp) * pd * ld; };
+  std::vector<int> blk_count(nHpp + nHpl, 0);
+  std::vector<long long> ekey(std::max(ne, 1), -1);
+  for (int f = 0; f < ne; ++f) {
+    if (!offref[f].kind) continue;
+    ekey[f] = blk_key(offref[f]);
+    blk_count[ekey[f]]++;
   }
-  off_dup = false;
-  for (int c : blk_count) if (c > 1) off_dup = true;
-  off_bsz = DA * DB;
-  if (off_dup) {  // per-edge slots + ordered reduction into the blocks
-    std::vector<int> ptr(nHpp + nHpl + 1, 0), edges;
-    for (int k = 0; k < ne; ++k) if (ekey[k] >= 0) ptr[ekey[k] + 1]++;
-    for (size_t b = 0; b + 1 < ptr.size(); ++b) ptr[b + 1] += ptr[b];
-    edges.assign(ptr.back(), 0);
-    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
-    for (int k = 0; k < ne; ++k) if (ekey[k] >= 0) edges[fill[ekey[k]]++] = k;
-    std::vector<long long> dstb(nHpp + nHpl, -1);
-    for (int b = 0; b < nHpp + nHpl; ++b) dstb[b] = b < nHpp ? (long long)b * pd * pd : hpl_base + (long long)(b - nHpp) * pd * ld;
-    // blocks without off-diagonal contributions (pose diagonal blocks) keep an empty list
-    for (int k = 0; k < ne; ++k) if (ekey[k] >= 0) offdst[k] = (long long)k * off_bsz;
-    noffb = nHpp + nHpl;
-    doffb_ptr.upload(ptr, stream);
-    doffb_edges.upload(edges.empty() ? std::vector<int>{0} : edges, stream);
-    std::vector<long long> dstb2;
-    std::vector<int> ptr2{0}, edges2;
-    // only keep blocks with >= 1 contribution (diagonal Hpp blocks are reduced elsewhere)
-    for (int b = 0; b < nHpp + nHpl; ++b) {
-      if (ptr[b + 1] == ptr[b]) continue;
-      for (int p = ptr[b]; p < ptr[b + 1]; ++p) edges2.push_back(edges[p]);
-      ptr2.push_back((int)edges2.size());
-      dstb2.push_back(dstb[b]);
+  // a block written by one local edge is stored directly by it; a block several edges share (two edges between
+  // the same vertex pair, e.g. duplicate observations or an odometry edge beside another type) gets one slot per
+  // edge, summed in edge order afterwards (deterministic; the reference's unlocked += races here, §2.3)
+  constexpr long long SLOT_BIT = 1LL << 62;
+  std::vector<long long> offdst(std::max(ne, 1), -1), slotoff(std::max(ne, 1), -1);
+  long long nslotd = 0;
+  for (int f = 0; f < ne; ++f) {
+    if (ekey[f] < 0) continue;
+    const long long bsz = ekey[f] < nHpp ? (long long)pd * pd : (long long)pd * ld;
+    if (blk_count[ekey[f]] == 1) {
+      offdst[f] = blk_off(ekey[f]);
+    } else {
+      slotoff[f] = nslotd;
+      offdst[f] = SLOT_BIT | nslotd;
+      nslotd += bsz;
     }
-    noffb = (int)dstb2.size();
-    doffb_ptr.upload(ptr2, stream);
-    doffb_edges.upload(edges2.empty() ? std::vector<int>{0} : edges2, stream);
-    doffb_dst.upload(dstb2.empty() ? std::vector<long long>{0} : dstb2, stream);
-    doffslot.resize((size_t)std::max(ne, 1) * off_bsz);
   }
-  doff_dst.upload(offdst, stream);
-  doff_tr.upload(offtr, stream);
+  for (int c = 0; c < 2; ++c) {
+    OffRed& R = offred[c];
+    std::vector<int> ptr{0};
+    std::vector<long long> so, dst;
+    std::vector<std::vector<long long>> lists;
+    std::map<long long, int> bl;  // block key -> list (ascending block key: a fixed launch order)
+    for (int f = 0; f < ne; ++f)
+      if (slotoff[f] >= 0 && ((ekey[f] < nHpp) == (c == 0))) {
+        auto it = bl.find(ekey[f]);
+        if (it == bl.end()) { it = bl.emplace(ekey[f], (int)lists.size()).first; lists.emplace_back(); }
+        lists[it->second].push_back(slotoff[f]);
+      }
+    for (auto& kv : bl) {
+      so.insert(so.end(), lists[kv.second].begin(), lists[kv.second].end());
+      ptr.push_back((int)so.size());
+      dst.push_back(blk_off(kv.first));
+    }
+    R.nb = (int)dst.size();
+    R.bsz = c == 0 ? pd * pd : pd * ld;
+    R.ptr.upload(ptr, stream);
+    R.soff.upload(so.empty() ? std::vector<long long>{0} : so, stream);
+    R.dst.upload(dst.empty() ? std::vector<long long>{0} : dst, stream);
+  }
+  doffslot.resize((size_t)std::max<long long>(nslotd, 1));
+  // per-vertex-side slots: arena by vertex dimension, each group's sides contiguous
+  nslot3 = nslot6 = 0;
+  for (EGroup& g : groups) {
+    long long& ca = g.DA == 3 ? nslot3 : nslot6;
+    g.slotA = ca;
+    ca += g.ne;
+    long long& cb = g.DB == 3 ? nslot3 : nslot6;
+    g.slotB = cb;
+    cb += g.ne;
+  }
+  for (size_t gi = 0; gi < groups.size(); ++gi) {
+    EGroup& g = groups[gi];
+    std::vector<long long> od(offdst.begin() + gfirst[gi], offdst.begin() + gfirst[gi + 1]);
+    std::vector<unsigned char> tr(g.ne);
+    for (int k = 0; k < g.ne; ++k) tr[k] = offref[gfirst[gi] + k].tr ? 1 : 0;
+    if (od.empty()) { od.push_back(-1); tr.push_back(0); }
+    g.off_dst.upload(od, stream);
+    g.off_tr.upload(tr, stream);
+  }
   // storage
   dH.resize(std::max<long long>((long long)nHpp * pd * pd + (long long)nHpl * pd * ld, 1));
   dH.zero(stream);
@@ -1067,21 +1394,26 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
   db.zero(stream);
   dx.resize(std::max<long long>(n, 1));
   dx.zero(stream);
-  slot_stride0 = DA * (DA + 1) / 2 + DA;
-  slot_stride1 = DB * (DB + 1) / 2 + DB;
-  dslot0.resize((size_t)std::max(ne, 1) * slot_stride0);
-  dslot1.resize((size_t)std::max(ne, 1) * slot_stride1);
-  // vertex incidence lists (hessian order), slot code = local_edge * 2 + side
+  dslot3.resize((size_t)std::max<long long>(nslot3, 1) * 9);
+  dslot6.resize((size_t)std::max<long long>(nslot6, 1) * 27);
+  // vertex incidence lists (hessian order): code = slot index in the arena of the vertex's dimension, in
+  // group / edge order (a fixed summation order)
   {
     std::vector<std::vector<int>> incp(num_poses), incl(nLloc);
-    for (int k = 0; k < ne; ++k) {
-      const int e = local_edges[k];
-      const int hs[2] = {hidx[hg.ev0[e]], hidx[hg.ev1[e]]};
-      for (int s = 0; s < 2; ++s) {
-        const int h = hs[s];
-        if (h < 0) continue;
-        if (h < num_poses) incp[h].push_back(k * 2 + s);
-        else incl[h - num_poses - lm_begin].push_back(k * 2 + s);
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+      const EGroup& g = groups[gi];
+      for (int k = 0; k < g.ne; ++k) {
+        int va, vb;
+        verts_of(gi, k, va, vb);
+        const int hs[2] = {hidx[va], hidx[vb]};
+        const long long code[2] = {g.slotA + k, g.slotB + k};
+        for (int sd = 0; sd < 2; ++sd) {
+          const int h = hs[sd];
+          if (h < 0) continue;
+          if (code[sd] >= (1LL << 31)) throw DeviceError("too many edge slots for 32-bit slot codes");
+          if (h < num_poses) incp[h].push_back((int)code[sd]);
+          else incl[h - num_poses - lm_begin].push_back((int)code[sd]);
+        }
       }
     }
     auto build = [&](VRed& vr, std::vector<std::vector<int>>& inc, int dim, int boff0) {
@@ -1123,20 +1455,18 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     d_blk_lm.upload(blk_lm, stream);
     // global Schur pattern from ALL edges (identical on every rank)
     std::vector<std::vector<int>> lmposes(num_landmarks);
-    for (size_t e = 0; e < hg.ev0.size(); ++e) {
-      const int hp = hidx[hg.ev1[e]], hl = hidx[hg.ev0[e]];
-      if (hp < 0 || hl < num_poses) continue;
-      lmposes[hl - num_poses].push_back(hp);
-    }
     std::vector<std::vector<int>> rowcols(num_poses);
     for (int i = 0; i < num_poses; ++i) rowcols[i].push_back(i);
     for (int b = num_poses; b < nHpp; ++b) rowcols[hpp_bi[b]].push_back(hpp_bj[b]);
-    // pose-pose edges owned by other ranks must also be in the global pattern
-    for (size_t e = 0; e < hg.ev0.size(); ++e) {
-      int i1 = hidx[hg.ev0[e]], i2 = hidx[hg.ev1[e]];
-      if (i1 < 0 || i2 < 0 || i1 >= num_poses || i2 >= num_poses) continue;
-      rowcols[std::min(i1, i2)].push_back(std::max(i1, i2));
-    }
+    for (const HEdgeSet& es : hg.esets)
+      for (size_t e = 0; e < es.ev0.size(); ++e) {
+        const int i1 = hidx[es.ev0[e]], i2 = hidx[es.ev1[e]];
+        if (i1 < 0 || i2 < 0) continue;
+        if (i1 >= num_poses && i2 < num_poses) lmposes[i1 - num_poses].push_back(i2);
+        else if (i2 >= num_poses && i1 < num_poses) lmposes[i2 - num_poses].push_back(i1);
+        // pose-pose edges owned by other ranks must also be in the global pattern
+        else if (i1 < num_poses && i2 < num_poses) rowcols[std::min(i1, i2)].push_back(std::max(i1, i2));
+      }
     for (auto& ps : lmposes) {
       std::sort(ps.begin(), ps.end());
       ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
@@ -1282,21 +1612,18 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
 }
 
 // ------------------------------------------------------------------ Engine: numeric steps
-static EdgeArgs edge_args(const DevBuf<int>& v0, const DevBuf<int>& v1, const DevBuf<double>& meas,
-                          const DevBuf<double>& info, const DevBuf<double>& params, const double* s0, const double* s1) {
-  return EdgeArgs{v0.get(), v1.get(), meas.get(), info.get(), params.get(), s0, s1};
-}
-
 void Engine::allreduce_sum(double* p, size_t n) {
   if (nranks <= 1 || !comm) return;
   comm->allreduce_sum(p, n, stream);
 }
 
-void Engine::compute_errors_async() {
+void Engine::compute_errors_async() {  // computeActiveErrors + activeRobustChi2 (sparse_optimizer.cpp:63-116)
   ensure_device_state();
-  EdgeArgs a = edge_args(dv0, dv1, dmeas, dinfo, dparams, dstate[vt0].get(), dstate[vt1].get());
+  refresh_host_payload(false);
   timer.begin("error", stream);
-  launch::error_sum(family, a, ne, dpartial.get(), dscal.get() + 1, stream);
+  int np = 0;  // every group's partials back to back, summed in one fixed tree
+  for (const EGroup& g : groups) np += launch::error_partials(g.family, group_args(g), g.ne, dpartial.get() + np, stream);
+  launch::sum_final(dpartial.get(), np, dscal.get() + 1, stream);
   timer.end(stream);
   if (do_schur) allreduce_sum(dscal.get() + 1, 1);
 }
@@ -1327,19 +1654,22 @@ int Engine::build_system() {  // block_solver.hpp:462-521
     if (r) return r;
   }
   ensure_device_state();
-  EdgeArgs a = edge_args(dv0, dv1, dmeas, dinfo, dparams, dstate[vt0].get(), dstate[vt1].get());
+  refresh_host_payload(true);
   timer.begin("linearize", stream);
-  launch::linearize(family, a, ne, d_hidx[vt0].get(), d_hidx[vt1].get(), dslot0.get(), dslot1.get(), doff_dst.get(),
-                    doff_tr.get(), off_dup ? doffslot.get() : dH.get(), stream);
+  for (const EGroup& g : groups)
+    launch::linearize(g.family, group_args(g), g.ne, d_hidx[g.vtA].get(), d_hidx[g.vtB].get(),
+                      slot_arena(g.DA) + g.slotA * (g.DA * (g.DA + 1) / 2 + g.DA),
+                      slot_arena(g.DB) + g.slotB * (g.DB * (g.DB + 1) / 2 + g.DB), g.off_dst.get(), g.off_tr.get(),
+                      dH.get(), doffslot.get(), stream);
   timer.end(stream);
-  if (off_dup) launch::offblock_reduce(noffb, off_bsz, doffb_ptr.get(), doffb_edges.get(), doffslot.get(), dH.get(),
-                                       doffb_dst.get(), stream);
+  for (const OffRed& R : offred)
+    launch::offblock_reduce(R.nb, R.bsz, R.ptr.get(), R.soff.get(), doffslot.get(), dH.get(), R.dst.get(), stream);
   timer.begin("vreduce", stream);
-  launch::vertex_reduce(pd, vr_pose.nv, vr_pose.lanes, vr_pose.ptr.get(), vr_pose.code.get(), dslot0.get(), dslot1.get(),
-                        slot_stride0, slot_stride1, vr_pose.H, db.get(), vr_pose.boff.get(), stream);
+  launch::vertex_reduce(pd, vr_pose.nv, vr_pose.lanes, vr_pose.ptr.get(), vr_pose.code.get(), slot_arena(pd), vr_pose.H,
+                        db.get(), vr_pose.boff.get(), stream);
   if (do_schur)
-    launch::vertex_reduce(ld, vr_lm.nv, vr_lm.lanes, vr_lm.ptr.get(), vr_lm.code.get(), dslot0.get(), dslot1.get(),
-                          slot_stride0, slot_stride1, vr_lm.H, db.get(), vr_lm.boff.get(), stream);
+    launch::vertex_reduce(ld, vr_lm.nv, vr_lm.lanes, vr_lm.ptr.get(), vr_lm.code.get(), slot_arena(ld), vr_lm.H, db.get(),
+                          vr_lm.boff.get(), stream);
   timer.end(stream);
   return G2OHIP_OK;
 }
@@ -1506,7 +1836,15 @@ int Engine::discard_top() {
   return G2OHIP_OK;
 }
 
-double Engine::lambda_init() {  // optimization_algorithm_levenberg.cpp:152-175
+int Engine::diag_absmax(double* out) {  // the vertex Hessian diagonal computeLambdaInit reads (:152-175)
+  if (!structure_built) return G2OHIP_ERR_STATE;
+  *out = max_diagonal();
+  return G2OHIP_OK;
+}
+
+double Engine::lambda_init() { return 1e-5 * max_diagonal(); }  // optimization_algorithm_levenberg.cpp:152-175
+
+double Engine::max_diagonal() {
   // Hpp diagonal blocks are partial per rank when sharded: reduce them first (copy)
   const double* Hp = dH.get();
   DevBuf<double> tmp;
@@ -1524,7 +1862,7 @@ double Engine::lambda_init() {  // optimization_algorithm_levenberg.cpp:152-175
   double m = 0;
   HIP_CHECK(hipMemcpyAsync(&m, dscal.get() + 3, sizeof(double), hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
-  return 1e-5 * m;
+  return m;
 }
 
 // OptimizationAlgorithmLevenberg::solve (optimization_algorithm_levenberg.cpp:58-150)
@@ -1639,6 +1977,44 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   return 0;                                                                       // OK
 }
 
+// OptimizationAlgorithmGaussNewton::solve (optimization_algorithm_gauss_newton.cpp:50-92): errors, buildStructure on
+// iteration 0, buildSystem, solve (no damping: lambda 0), update with whatever x the solve left, Fail on not-PD
+int Engine::gn_solve(int iteration, g2ohip_batch_stats* st) {
+  double t = wall();
+  chi2_sync();  // computeActiveErrors (:56)
+  if (st) st->timeResiduals = wall() - t;
+  if (iteration == 0 && !structure_built) {
+    if (build_structure()) return 2;
+  }
+  t = wall();
+  if (built_ver != state_ver || iteration == 0) build_system();
+  built_ver = 0;
+  if (st && stats_level >= 2) {
+    HIP_CHECK(hipStreamSynchronize(stream));
+    st->timeQuadraticForm = wall() - t;
+  }
+  set_lambda_device(0.0, true);  // also clears the not-PD flags
+  const bool ev1 = st && stats_level >= 1;
+  if (ev1) HIP_CHECK(hipEventRecord(lm_ev_[0], stream));
+  solve_async(false);
+  if (ev1) HIP_CHECK(hipEventRecord(lm_ev_[1], stream));
+  update_async();
+  if (ev1) HIP_CHECK(hipEventRecord(lm_ev_[2], stream));
+  int f[2] = {0, 0};
+  HIP_CHECK(hipMemcpyAsync(f, failp(), sizeof f, hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  timer.collect();
+  if (ev1) {
+    float a = 0, b = 0;
+    HIP_CHECK(hipEventElapsedTime(&a, lm_ev_[0], lm_ev_[1]));
+    HIP_CHECK(hipEventElapsedTime(&b, lm_ev_[1], lm_ev_[2]));
+    st->timeLinearSolution = a * 1e-3;
+    st->timeUpdate = b * 1e-3;
+  }
+  levenberg_iterations = 0;
+  return f[0] == 0 ? 0 : 2;
+}
+
 int Engine::optimize_step(const g2ohip_config* cfgp, int i, g2ohip_batch_stats* st) {
   g2ohip_config cfg{10, 0.0, 0};
   if (cfgp) cfg = *cfgp;
@@ -1651,16 +2027,16 @@ int Engine::optimize_step(const g2ohip_config* cfgp, int i, g2ohip_batch_stats* 
   if (st) {
     std::memset(st, 0, sizeof *st);
     st->iteration = i;
-    st->numEdges = (int)hg.ev0.size();
+    st->numEdges = (int)hg.num_edges();
     st->numVertices = (int)active.size();
   }
   const double ts = wall();
-  const int result = lm_solve(i, cfg, st);
+  const int result = levenberg ? lm_solve(i, cfg, st) : gn_solve(i, st);
   if (st || cfg.verbose) {
     const double c = chi2_sync();
     if (st) {
       st->chi2 = c;
-      st->lambda = current_lambda;
+      st->lambda = levenberg ? current_lambda : 0.0;
       st->timeIteration = wall() - ts;
       st->hessianPoseDimension = size_poses;
       st->hessianLandmarkDimension = size_landmarks;
@@ -1669,7 +2045,7 @@ int Engine::optimize_step(const g2ohip_config* cfgp, int i, g2ohip_batch_stats* 
     }
     if (cfg.verbose && rank == 0)
       fprintf(stderr, "iteration= %d\t chi2= %.6f\t time= %g\t edges= %zu\t lambda= %.6f\t levenbergIter= %d\n", i, c,
-              wall() - ts, hg.ev0.size(), current_lambda, levenberg_iterations);
+              wall() - ts, (size_t)hg.num_edges(), current_lambda, levenberg_iterations);
   }
   return result;
 }
@@ -1764,6 +2140,86 @@ int Engine::set_comm_local(const std::string& key, int r, int nr) {
   return G2OHIP_OK;
 }
 
+void BlockSymv::setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s) {
+  nb = nblocks;
+  pd = bdim;
+  std::vector<int> dg(nb, -1), cnt(nb + 1, 0);
+  for (size_t t = 0; t < bi.size(); ++t) {
+    if (bi[t] == bj[t]) dg[bi[t]] = (int)t;
+    else { ++cnt[bi[t] + 1]; ++cnt[bj[t] + 1]; }
+  }
+  for (int i = 0; i < nb; ++i) {
+    if (dg[i] < 0) throw std::runtime_error("BlockSymv: missing diagonal block " + std::to_string(i));
+    cnt[i + 1] += cnt[i];
+  }
+  std::vector<int2> e(std::max(cnt[nb], 1), make_int2(0, 0));
+  std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+  for (size_t t = 0; t < bi.size(); ++t) {  // stored order: a fixed summation order per row
+    if (bi[t] == bj[t]) continue;
+    e[fill[bi[t]]++] = make_int2((int)t, bj[t]);
+    e[fill[bj[t]]++] = make_int2((int)t, (int)((unsigned)bi[t] | 0x80000000u));
+  }
+  rptr.upload(cnt, s);
+  diag.upload(dg, s);
+  ent.upload(e, s);
+}
+
+int Engine::multiply_hessian(double* dest, const double* src) {  // block_solver.h:146
+  if (!structure_built) return G2OHIP_ERR_STATE;
+  if (nranks > 1) return G2OHIP_ERR_UNSUPPORTED;  // Hpp diagonal blocks are partial per landmark shard
+  if (symv_hpp.key != (const void*)&hpp_bi) {
+    symv_hpp.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
+    symv_hpp.key = &hpp_bi;
+  }
+  const int n = size_poses;
+  dtmp.resize(2 * (size_t)std::max(n, 1));
+  HIP_CHECK(hipMemcpyAsync(dtmp.get(), src, sizeof(double) * n, hipMemcpyHostToDevice, stream));
+  launch::block_symv(pd, n, symv_hpp.rptr.get(), symv_hpp.ent.get(), symv_hpp.diag.get(), dH.get(),
+                     lambda_set ? dscal.get() : nullptr, dtmp.get(), dtmp.get() + n, nullptr, nullptr, nullptr, stream);
+  HIP_CHECK(hipMemcpyAsync(dest, dtmp.get() + n, sizeof(double) * n, hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  return G2OHIP_OK;
+}
+
+int Engine::linear_residual(double* out) {
+  if (!structure_built || !out) return G2OHIP_ERR_STATE;
+  if (use_pcg()) return G2OHIP_ERR_UNSUPPORTED;
+  const std::vector<int>& bi = do_schur ? s_bi : hpp_bi;
+  const std::vector<int>& bj = do_schur ? s_bj : hpp_bj;
+  BlockSymv& M = do_schur ? symv_s : symv_hpp;
+  if (M.key != (const void*)&bi) {
+    M.setup(num_poses, pd, bi, bj, stream);
+    M.key = &bi;
+  }
+  const int n = size_poses;
+  // S already holds lambda on its diagonal (k_schur_diag); Hpp gets the virtual lambda like the factor
+  const double* vals = do_schur ? dS.get() : dH.get();
+  const double* lam = do_schur ? nullptr : dscal.get();
+  const double* rhs = do_schur ? dS.get() + (size_t)nS * pd * pd : db.get();
+  dtmp.resize(2 * (size_t)std::max(n, 1) + 2);
+  launch::block_symv(pd, n, M.rptr.get(), M.ent.get(), M.diag.get(), vals, lam, dx.get(), nullptr, rhs, dtmp.get(),
+                     dtmp.get() + n, stream);
+  double* res = dtmp.get() + 2 * (size_t)n;
+  launch::sum(dtmp.get(), n, dpartial.get(), res, stream);
+  launch::sum(dtmp.get() + n, n, dpartial.get(), res + 1, stream);
+  double h[2];
+  HIP_CHECK(hipMemcpyAsync(h, res, sizeof h, hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  *out = h[1] > 0 ? std::sqrt(h[0] / h[1]) : std::sqrt(h[0]);
+  return G2OHIP_OK;
+}
+
+int Engine::factor_info(double* out, int n) {
+  if (!structure_built) return G2OHIP_ERR_STATE;
+  const Symbolic& S = chol.sym;
+  const double v[] = {(double)S.n, (double)S.nnzL, S.flops, (double)S.sn.size(), (double)S.num_levels,
+                      (double)S.max_front, (double)chol.n_blocked, (double)chol.n_inplace_levels,
+                      (double)chol.n_pre_levels, (double)chol.n_syrk_ops, (double)chol.n_bwd_rounds};
+  const int m = (int)(sizeof v / sizeof v[0]);
+  for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
+  return m;
+}
+
 double Engine::kernel_bytes(const std::string& name) const {
   // algorithmic bytes per launch (SURVEY.md §8d formulas)
   const double npl = nHpl, pb = (double)pd * ld * 8;
@@ -1775,7 +2231,12 @@ double Engine::kernel_bytes(const std::string& name) const {
   if (name == "schur_diag") return 2 * npl * pb + local_lm.size() * 9 * 8.0 + (double)num_poses * pd * pd * 8 * 2 +
                                    size_poses * 16.0;
   if (name == "schur_dinv") return local_lm.size() * ((9 + 3) * 8.0 + (9 + 6 + 3) * 8.0);
-  if (name == "linearize") return ne * (family == FAM_BA ? (2 + 3 + 4) * 8.0 + 8 + (double)(slot_stride0 + slot_stride1 + pd * ld) * 8 : 0.0);
+  if (name == "linearize") {  // BA groups: edge data read, both slots + the Hpl block written
+    double by = 0;
+    for (const EGroup& g : groups)
+      if (g.family == FAM_BA) by += g.ne * ((2 + 3 + 4) * 8.0 + 8 + (9.0 + 27.0 + pd * ld) * 8);
+    return by;
+  }
   if (name == "backsub") return local_lm.size() * (3 * 8.0 * 2 + 72) + npl * (pb + 4) + size_poses * 8.0;
   if (name == "chol_factor") return (double)chol.sym.front_pool * 8 * 2;
   return 0;

@@ -31,15 +31,47 @@ struct HVertex {
   int local;  // index within its type's state array
 };
 
+// one edge type of the graph (edges kept in insertion order)
+struct HEdgeSet {
+  int type = 0, D = 0, nm = 0;          // G2OHIP_E_*, error dimension, measurement doubles per edge
+  std::vector<int> ev0, ev1;            // vertex indices
+  std::vector<double> meas, info, params;  // raw: meas (as given), info D*D row-major, params 4
+  int rk = 0;                           // robust kernel (G2OHIP_RK_*), delta
+  double rk_delta = 1.0;
+  std::vector<double> payload;          // host-J edges: latest [e | Ji | Jj] per edge from the host
+  unsigned long long payload_ver = 0;   // device-state version the payload was computed at (0: set by the caller)
+};
+
 struct HostGraph {
   std::vector<HVertex> verts;
   std::unordered_map<int, int> idmap;
   std::vector<double> st[5];            // per type, device layout
   std::vector<std::vector<int>> by_type = std::vector<std::vector<int>>(5);  // local -> vertex
   std::vector<int> nopl;                // VertexSE3 oplus counters (per local SE3QUAT vertex)
-  int etype = 0;
-  std::vector<int> ev0, ev1;            // vertex indices
-  std::vector<double> emeas, einfo, eparams;  // raw: meas (as given), info D*D, params 4
+  std::vector<HEdgeSet> esets;          // in first-seen type order
+  long long num_edges() const {
+    long long n = 0;
+    for (auto& e : esets) n += (long long)e.ev0.size();
+    return n;
+  }
+  HEdgeSet* set_of(int type) {
+    for (auto& e : esets) if (e.type == type) return &e;
+    return nullptr;
+  }
+};
+
+// A device edge group: the local-shard edges of one edge set with one pair of endpoint vertex types,
+// linearized by one kernel instantiation (family, D, DA, DB)
+struct EGroup {
+  int set = 0, family = 0, vtA = 0, vtB = 0, D = 0, DA = 0, DB = 0;
+  std::vector<int> edges;               // indices into the edge set
+  int ne = 0;
+  DevBuf<int> v0, v1;                   // local vertex indices (per type)
+  DevBuf<double> meas, info, params;    // meas: family payload (host-J: [e | Ji | Jj] per edge)
+  long long slotA = 0, slotB = 0;       // first slot of the group's A / B sides in the arenas of dims DA / DB
+  DevBuf<long long> off_dst;            // per edge: offset of its off-diagonal block (bit 62: a shared-block slot)
+  DevBuf<unsigned char> off_tr;
+  int payload_stride() const { return D + D * DA + D * DB; }
 };
 
 void set_state_from_est(int vtype, const double* est, double* st);
@@ -69,6 +101,9 @@ struct DeviceCholesky {
   };
   std::vector<BwdLevel> bwd_ops;
   int max_ns = 0;
+  // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
+  // trailing-update (k_syrk) launches, big-panel backward rounds
+  int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
   struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add, 2 panel step, 3 syrk
   std::vector<Op> ops;
   DevBuf<launch::Task> tasks;
@@ -80,6 +115,15 @@ struct DeviceCholesky {
   void factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s);
   // backward solve x = P^T L^-T y
   void solve(double* x, hipStream_t s);
+};
+
+// y = (A + lam I) x for a symmetric block matrix held as upper blocks (multiplyHessian, residual checks)
+struct BlockSymv {
+  int nb = 0, pd = 0;
+  const void* key = nullptr;  // the block list it was built for
+  DevBuf<int> rptr, diag;
+  DevBuf<int2> ent;
+  void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
 };
 
 struct KernelTimer {
@@ -115,6 +159,14 @@ class Engine {
   int add_vertices(int type, int n, const int* ids, const double* est, const int* fixed, const int* marg);
   int add_edges(int type, int n, const int* v0, const int* v1, const double* meas, const double* info,
                 const double* params);
+  // RobustKernel per edge type (base_edge.h setRobustKernel; uniform kind and delta over the type)
+  int set_robust_kernel(int type, int kind, double delta);
+  // host-J edges: error + Jacobians of every edge of the type (insertion order), [e | Ji | Jj] row-major
+  int set_host_payload(int type, const double* payload);
+  // host callback that recomputes a host-J type's payload at the current estimates (device LM loop, chi2)
+  int set_host_callback(g2ohip_host_edge_fn fn, void* user);
+  // computeLambdaInit (optimization_algorithm_levenberg.cpp:152-175): max |diagonal| of Hpp and Hll
+  int diag_absmax(double* out);
   int load(const char* path, int marginalize_xyz);
   int save(const char* path);
   int get_estimates(int type, double* out, int* ids);
@@ -141,6 +193,14 @@ class Engine {
   int pop();
   int discard_top();
   int stage(double lambda, double* b, double* x, double* Hs, double* bs, long long* dims);
+  // BlockSolverBase::multiplyHessian (block_solver.h:94,146): dest = Hpp src (upper blocks mirrored, + lambda
+  // while setLambda is active), host arrays of size_poses
+  int multiply_hessian(double* dest, const double* src);
+  // ||(A + lambda I) x - b|| / ||b|| of the last linear solve (A = Schur complement S or Hpp), on the device
+  int linear_residual(double* out);
+  // [n, nnz(L), flops, supernodes, levels, max front, blocked fronts, in-place levels, pre-scattered levels,
+  //  k_syrk launches, backward big-panel rounds]
+  int factor_info(double* out, int n);
 
   // comm
   int set_comm(const unsigned char* uid, int rank, int nranks);
@@ -152,19 +212,20 @@ class Engine {
  private:
   // structure
   bool initialized = false, structure_built = false, device_state_dirty = true, host_state_stale = false;
-  int family = FAM_NONE;
   int pd = 0, ld = 0;
   int num_poses = 0, num_landmarks = 0, size_poses = 0, size_landmarks = 0;
   std::vector<int> active;       // active vertex indices sorted by id
   std::vector<int> ivmap;        // hessian order
   std::vector<int> hidx;         // per vertex: hessian index or -1
   bool do_schur = false;
-  int vt0 = 0, vt1 = 0;          // vertex types of edge endpoints
-  int ne = 0;
+  int ne = 0;                    // local edges over all groups
+  std::vector<EGroup> groups;
+  bool has_hostj = false;
+  g2ohip_host_edge_fn host_fn = nullptr;
+  void* host_user = nullptr;
   // sharding
   int rank = 0, nranks = 1;
   std::unique_ptr<Comm> comm;
-  std::vector<int> local_edges;  // edge indices this rank assembles (all when nranks == 1)
   std::vector<int> local_lm;     // landmark (hessian - num_poses) this rank owns
 
   // device state
@@ -177,18 +238,14 @@ class Engine {
   bool ev_valid_ = false;
   DevBuf<int> d_xoff[5];         // per type local -> x offset or -1
   DevBuf<int> d_hidx[5];         // per type local -> hessian index (-1 fixed)
-  // device edges (local shard, in active-edge order)
-  DevBuf<int> dv0, dv1;
-  DevBuf<double> dmeas, dinfo, dparams;
-  DevBuf<double> dslot0, dslot1;
-  int slot_stride0 = 0, slot_stride1 = 0;
-  DevBuf<long long> doff_dst;
-  DevBuf<unsigned char> doff_tr;
-  bool off_dup = false;
+  // per-vertex-side slot arenas by vertex dimension (3, 6): packed upper H + b, one slot per (edge, side)
+  DevBuf<double> dslot3, dslot6;
+  long long nslot3 = 0, nslot6 = 0;
+  double* slot_arena(int dim) { return dim == 3 ? dslot3.get() : dslot6.get(); }
+  // off-diagonal blocks several local edges share: per-edge slots reduced in edge order, one launch per block size
   DevBuf<double> doffslot;
-  DevBuf<int> doffb_ptr, doffb_edges;
-  DevBuf<long long> doffb_dst;
-  int noffb = 0, off_bsz = 0;
+  struct OffRed { int nb = 0, bsz = 0; DevBuf<int> ptr; DevBuf<long long> soff, dst; };
+  OffRed offred[2];  // [Hpp off-diagonal blocks (pd x pd), Hpl blocks (pd x ld)]
   // hessian storage
   int nHpp = 0, nHpl = 0;
   DevBuf<double> dH;             // [Hpp blocks | Hpl blocks]
@@ -212,6 +269,8 @@ class Engine {
   DevBuf<int> sch_rptr, sch_robs, sch_obs_lm, sch_sdiag;
   std::vector<int> s_bi, s_bj, hpp_bi, hpp_bj;
   DeviceCholesky chol;
+  BlockSymv symv_hpp, symv_s;
+  DevBuf<double> dtmp;
   DevicePCG pcg;  // {lm,gn}_pcg* algorithms (linear_solver_pcg.hpp)
   bool use_pcg() const { return algorithm.find("_pcg") != std::string::npos; }
   // scalars: [0] lambda, [1] chi2, [2] scale, [3] maxdiag
@@ -230,20 +289,23 @@ class Engine {
   double chi_cache = 0.0;
   hipEvent_t lm_ev_[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int levenberg_iterations = 0;
-  g2ohip_batch_stats* cur_stats = nullptr;
 
   void ensure_device_state();
   void sync_host_state();
   void setup_edges_device();
   void compute_errors_async();
+  void refresh_host_payload(bool jacobians);  // host-J groups: payload at the current state (callback), upload
+  EdgeArgs group_args(const EGroup& g) const;
   double chi2_sync();
   double lambda_init();
+  double max_diagonal();
   void solve_async(bool reset_fail);
   int* failp() const { return reinterpret_cast<int*>(dscal.get() + 8); }
   void update_async();
   void set_lambda_device(double l, bool reset_fail = false);
   void allreduce_sum(double* dptr, size_t n);
   int lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats* st);
+  int gn_solve(int iteration, g2ohip_batch_stats* st);
 };
 
 }  // namespace g2ohip

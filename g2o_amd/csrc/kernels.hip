@@ -45,6 +45,11 @@ __global__ void __launch_bounds__(256) k_error(EdgeData d, int ne, double* __res
     for (int j = 0; j < F::D; ++j) r += Om[i * F::D + j] * err[j];
     s += err[i] * r;
   }
+  if (d.rk) {  // activeRobustChi2 (sparse_optimizer.cpp:102-116): rho[0]
+    double r0, r1;
+    robustify(d.rk, d.rk_delta, s, r0, r1);
+    s = r0;
+  }
   chi[e] = s;
 }
 
@@ -78,7 +83,7 @@ template <class F>
 __global__ void __launch_bounds__(256)
     k_linearize(EdgeData d, int ne, const int* __restrict__ h0, const int* __restrict__ h1, double* __restrict__ slot0,
                 double* __restrict__ slot1, const long long* __restrict__ off_dst, const unsigned char* __restrict__ off_tr,
-                double* __restrict__ off_base) {
+                double* __restrict__ off_base, double* __restrict__ off_slot) {
   constexpr int D = F::D, DA = F::DA, DB = F::DB;
   constexpr int SA = DA * (DA + 1) / 2 + DA, SB = DB * (DB + 1) / 2 + DB, SH = DA * DB;
   constexpr int SM = SA > SB ? (SA > SH ? SA : SH) : (SB > SH ? SB : SH);
@@ -94,6 +99,20 @@ __global__ void __launch_bounds__(256)
   if (nfA || nfB) {
     F::linearize(d, e, err, A, B);
     load_info<D>(d.info + (size_t)e * F::INFO, Om);
+    if (d.rk) {  // robust branch of constructQuadraticForm (base_binary_edge.hpp:104-135): Omega, omega_r scaled by rho'
+      double chi = 0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        double r = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) r += Om[i * D + j] * err[j];
+        chi += err[i] * r;
+      }
+      double r0, r1;
+      robustify(d.rk, d.rk_delta, chi, r0, r1);
+#pragma unroll
+      for (int i = 0; i < D * D; ++i) Om[i] *= r1;
+    }
   }
   double wr[D];
 #pragma unroll
@@ -137,14 +156,20 @@ __global__ void __launch_bounds__(256)
   wave_sync();
   wave_copy_out(slot0 + (size_t)ebase * SA, sw, nw * SA, lane);
   wave_sync();
-  // off-diagonal block: staged when the wave's blocks are consecutive with one orientation
-  const long long od = (nfA && nfB) ? off_dst[e] : -1;
+  // off-diagonal block: staged when the wave's blocks are consecutive with one orientation. Destinations with
+  // bit 62 set are per-edge slots of a block several edges share (summed in order by k_offblock_reduce)
+  constexpr long long SLOT_BIT = 1LL << 62;
+  const long long od_raw = (nfA && nfB) ? off_dst[e] : -1;
+  const bool in_slot = od_raw >= 0 && (od_raw & SLOT_BIT);
+  const long long od = od_raw >= 0 ? (od_raw & ~SLOT_BIT) : -1;
   const bool tr = nfA && nfB && off_tr[e];
   const long long od0 = __shfl(od, 0, 64);
   const bool tr0 = __shfl((int)tr, 0, 64) != 0;
-  const bool run = __all(!in || (od >= 0 && od0 >= 0 && od == od0 + (long long)lane * SH && tr == tr0));
+  const bool slot0f = __shfl((int)in_slot, 0, 64) != 0;
+  const bool run = __all(!in || (od >= 0 && od0 >= 0 && od == od0 + (long long)lane * SH && tr == tr0 && in_slot == slot0f));
+  double* const obase = in_slot ? off_slot : off_base;
   if (od >= 0) {
-    double* H = run ? sw + lane * SH : off_base + od;
+    double* H = run ? sw + lane * SH : obase + od;
     if (tr) {  // DB x DA col-major: (j,i)
 #pragma unroll
       for (int i = 0; i < DA; ++i)
@@ -169,7 +194,7 @@ __global__ void __launch_bounds__(256)
   }
   if (run) {
     wave_sync();
-    wave_copy_out(off_base + od0, sw, nw * SH, lane);
+    wave_copy_out((slot0f ? off_slot : off_base) + od0, sw, nw * SH, lane);
     wave_sync();
   }
   if (nfB) {
@@ -212,9 +237,8 @@ __global__ void __launch_bounds__(256)
 template <int DIM, int LANES>
 __global__ void __launch_bounds__(256)
     k_vertex_reduce(int nv, const int* __restrict__ inc_ptr, const int* __restrict__ inc_code,
-                    const double* __restrict__ slot0, const double* __restrict__ slot1, int stride0, int stride1,
-                    double* __restrict__ Hdiag /* [nv][DIM*DIM] */, double* __restrict__ b /* offset per vertex */,
-                    const int* __restrict__ boff) {
+                    const double* __restrict__ slots, double* __restrict__ Hdiag /* [nv][DIM*DIM] */,
+                    double* __restrict__ b /* offset per vertex */, const int* __restrict__ boff) {
   constexpr int SP = DIM * (DIM + 1) / 2, S = SP + DIM;
   // vertices with >= 64 lanes: XCD-contiguous vertex ranges (a landmark's edges, neighbours in the
   // slot arrays, belong to nearby cameras: mostly one L2)
@@ -227,9 +251,7 @@ __global__ void __launch_bounds__(256)
   if (active) {
     const int p0 = inc_ptr[v], p1 = inc_ptr[v + 1];
     for (int p = p0 + lane; p < p1; p += LANES) {
-      const int code = inc_code[p];
-      const int e = code >> 1;
-      const double* s = (code & 1) ? slot1 + (size_t)e * stride1 : slot0 + (size_t)e * stride0;
+      const double* s = slots + (size_t)inc_code[p] * S;
 #pragma unroll
       for (int k = 0; k < S; ++k) acc[k] += s[k];
     }
@@ -274,15 +296,16 @@ __global__ void __launch_bounds__(256)
   for (int i = 0; i < DIM; ++i) bb[i] = acc[SP + i];
 }
 
-// duplicate off-diagonal blocks: sum per-edge slots in edge order
+// off-diagonal blocks shared by several edges: sum their per-edge slots (offsets into `slots`) in edge order
 __global__ void __launch_bounds__(256) k_offblock_reduce(int nb, int bsz, const int* __restrict__ ptr,
-                                                          const int* __restrict__ edges, const double* __restrict__ slots,
-                                                          double* __restrict__ out, const long long* __restrict__ dst) {
+                                                          const long long* __restrict__ soff,
+                                                          const double* __restrict__ slots, double* __restrict__ out,
+                                                          const long long* __restrict__ dst) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int blk = gid / bsz, k = gid % bsz;
   if (blk >= nb) return;
   double s = 0;
-  for (int p = ptr[blk]; p < ptr[blk + 1]; ++p) s += slots[(size_t)edges[p] * bsz + k];
+  for (int p = ptr[blk]; p < ptr[blk + 1]; ++p) s += slots[soff[p] + k];
   out[dst[blk] + k] = s;
 }
 
@@ -294,8 +317,8 @@ __global__ void __launch_bounds__(256) k_offblock_reduce(int nb, int bsz, const 
 template <int DIM>
 __global__ void __launch_bounds__(256)
     k_vertex_reduce_wide(int nv, const int* __restrict__ inc_ptr, const int* __restrict__ inc_code,
-                         const double* __restrict__ slot0, const double* __restrict__ slot1, int stride0, int stride1,
-                         double* __restrict__ Hdiag, double* __restrict__ b, const int* __restrict__ boff) {
+                         const double* __restrict__ slots, double* __restrict__ Hdiag, double* __restrict__ b,
+                         const int* __restrict__ boff) {
   constexpr int SP = DIM * (DIM + 1) / 2, S = SP + DIM, U = 8, NS = 8;  // U = 16: no change
   static_assert(S <= 32, "one half-wave per slot");
   __shared__ double red[NS][32];
@@ -311,8 +334,7 @@ __global__ void __launch_bounds__(256)
     double d[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int e = c[u] >> 1;
-      const double* sl = (c[u] & 1) ? slot1 + (size_t)e * stride1 : slot0 + (size_t)e * stride0;
+      const double* sl = slots + (size_t)(c[u] >= 0 ? c[u] : 0) * S;
       d[u] = (c[u] >= 0 && k < S) ? sl[k] : 0.0;
     }
 #pragma unroll
@@ -809,6 +831,11 @@ __global__ void __launch_bounds__(RED_BLOCK) k_error_partial(EdgeData d, int ne,
         for (int j = 0; j < F::D; ++j) r += Om[i * F::D + j] * err[j];
         c += err[i] * r;
       }
+      if (d.rk) {  // activeRobustChi2: rho[0] (sparse_optimizer.cpp:102-116)
+        double r0, r1;
+        robustify(d.rk, d.rk_delta, c, r0, r1);
+        c = r0;
+      }
       s += c;
     }
   }
@@ -847,43 +874,105 @@ __global__ void __launch_bounds__(RED_BLOCK) k_scale_partial(long long n, long l
   if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
 }
 
+// ------------------------------------------------------------------------------ symmetric block SpMV
+// y = (A + lam I) x for A symmetric, stored as its upper blocks (pd x pd col-major): thread per scalar row,
+// its block row's entries in a fixed order (rptr/ent: block index, other block row | 0x80000000 when the
+// stored block is used transposed), as SparseBlockMatrix::multiplySymmetricUpperTriangle
+// (sparse_block_matrix.hpp:289-314). With b: also (y - b)^2 and b^2 per row for the residual norm.
+template <int PD>
+__global__ void __launch_bounds__(256)
+    k_block_symv(int n, const int* __restrict__ rptr, const int2* __restrict__ ent, const int* __restrict__ diag,
+                 const double* __restrict__ vals, const double* __restrict__ lam, const double* __restrict__ x,
+                 double* __restrict__ y, const double* __restrict__ b, double* __restrict__ r2,
+                 double* __restrict__ b2) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= n) return;
+  const int i = row / PD, rr = row - i * PD;
+  const double* D = vals + (size_t)diag[i] * PD * PD;
+  double acc = (lam ? *lam : 0.0) * x[row];
+#pragma unroll
+  for (int c = 0; c < PD; ++c) acc += D[c * PD + rr] * x[(size_t)i * PD + c];
+  for (int e = rptr[i]; e < rptr[i + 1]; ++e) {
+    const int2 t = ent[e];
+    const int j = t.y & 0x7fffffff;
+    const double* B = vals + (size_t)t.x * PD * PD;
+    const double* xj = x + (size_t)j * PD;
+    if (t.y < 0) {
+#pragma unroll
+      for (int c = 0; c < PD; ++c) acc += B[rr * PD + c] * xj[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < PD; ++c) acc += B[c * PD + rr] * xj[c];
+    }
+  }
+  if (y) y[row] = acc;
+  if (b) {
+    const double d = acc - b[row];
+    r2[row] = d * d;
+    b2[row] = b[row] * b[row];
+  }
+}
+
 // ------------------------------------------------------------------------------ launchers
 namespace launch {
 
-template <class F>
 static EdgeData mk(const EdgeArgs& a) {
-  return EdgeData{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1};
+  return EdgeData{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
+}
+
+// host-Jacobian families: runtime (D, DA, DB) -> FamilyHostJ<D, DA, DB> (vertex dims 3 or 6, D = 1..6)
+template <int D, int DA, class Fn>
+static void hj_b(int DB, Fn& fn) {
+  if (DB == 3) fn(FamilyHostJ<D, DA, 3>{});
+  else if (DB == 6) fn(FamilyHostJ<D, DA, 6>{});
+  else throw std::runtime_error("host-Jacobian edge: vertex dimension must be 3 or 6");
+}
+template <int D, class Fn>
+static void hj_a(int DA, int DB, Fn& fn) {
+  if (DA == 3) hj_b<D, 3>(DB, fn);
+  else if (DA == 6) hj_b<D, 6>(DB, fn);
+  else throw std::runtime_error("host-Jacobian edge: vertex dimension must be 3 or 6");
+}
+template <class Fn>
+static void family_dispatch(int family, const EdgeArgs& a, Fn&& fn) {
+  switch (family) {
+    case FAM_BA: fn(FamilyBA{}); break;
+    case FAM_SE3: fn(FamilySE3{}); break;
+    case FAM_SE2: fn(FamilySE2{}); break;
+    case FAM_HOSTJ:
+      switch (a.D) {
+        case 1: hj_a<1>(a.DA, a.DB, fn); break;
+        case 2: hj_a<2>(a.DA, a.DB, fn); break;
+        case 3: hj_a<3>(a.DA, a.DB, fn); break;
+        case 4: hj_a<4>(a.DA, a.DB, fn); break;
+        case 5: hj_a<5>(a.DA, a.DB, fn); break;
+        case 6: hj_a<6>(a.DA, a.DB, fn); break;
+        default: throw std::runtime_error("host-Jacobian edge: error dimension must be 1..6");
+      }
+      break;
+    default: throw std::runtime_error("unknown edge family");
+  }
 }
 
 void error(int family, const EdgeArgs& a, int ne, double* chi, hipStream_t s) {
   if (ne <= 0) return;
   const unsigned g = grid_for(ne, 256);
-  switch (family) {
-    case FAM_BA: hipLaunchKernelGGL(k_error<FamilyBA>, g, 256, 0, s, mk<FamilyBA>(a), ne, chi); break;
-    case FAM_SE3: hipLaunchKernelGGL(k_error<FamilySE3>, g, 256, 0, s, mk<FamilySE3>(a), ne, chi); break;
-    case FAM_SE2: hipLaunchKernelGGL(k_error<FamilySE2>, g, 256, 0, s, mk<FamilySE2>(a), ne, chi); break;
-  }
+  family_dispatch(family, a, [&](auto fam) {
+    using F = decltype(fam);
+    hipLaunchKernelGGL(k_error<F>, g, 256, 0, s, mk(a), ne, chi);
+  });
   KERNEL_CHECK();
 }
 
 void linearize(int family, const EdgeArgs& a, int ne, const int* h0, const int* h1, double* slot0, double* slot1,
-               const long long* off_dst, const unsigned char* off_tr, double* off_base, hipStream_t s) {
+               const long long* off_dst, const unsigned char* off_tr, double* off_base, double* off_slot, hipStream_t s) {
   if (ne <= 0) return;
   const unsigned g = grid_for(ne, 256);
-  switch (family) {
-    case FAM_BA:
-      hipLaunchKernelGGL(k_linearize<FamilyBA>, g, 256, 0, s, mk<FamilyBA>(a), ne, h0, h1, slot0, slot1, off_dst, off_tr,
-                         off_base);
-      break;
-    case FAM_SE3:
-      hipLaunchKernelGGL(k_linearize<FamilySE3>, g, 256, 0, s, mk<FamilySE3>(a), ne, h0, h1, slot0, slot1, off_dst,
-                         off_tr, off_base);
-      break;
-    case FAM_SE2:
-      hipLaunchKernelGGL(k_linearize<FamilySE2>, g, 256, 0, s, mk<FamilySE2>(a), ne, h0, h1, slot0, slot1, off_dst,
-                         off_tr, off_base);
-      break;
-  }
+  family_dispatch(family, a, [&](auto fam) {
+    using F = decltype(fam);
+    hipLaunchKernelGGL(k_linearize<F>, g, 256, 0, s, mk(a), ne, h0, h1, slot0, slot1, off_dst, off_tr, off_base,
+                       off_slot);
+  });
   KERNEL_CHECK();
 }
 
@@ -892,36 +981,36 @@ static bool vr_wide() {
   return w;
 }
 template <int DIM>
-static void vreduce_dim(int nv, int lanes, const int* ptr, const int* code, const double* s0, const double* s1, int st0,
-                        int st1, double* H, double* b, const int* boff, hipStream_t s) {
+static void vreduce_dim(int nv, int lanes, const int* ptr, const int* code, const double* slots, double* H, double* b,
+                        const int* boff, hipStream_t s) {
   const unsigned g = grid_for((size_t)nv * lanes, 256);
   switch (lanes) {
-    case 1: hipLaunchKernelGGL((k_vertex_reduce<DIM, 1>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
-    case 4: hipLaunchKernelGGL((k_vertex_reduce<DIM, 4>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
-    case 8: hipLaunchKernelGGL((k_vertex_reduce<DIM, 8>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+    case 1: hipLaunchKernelGGL((k_vertex_reduce<DIM, 1>), g, 256, 0, s, nv, ptr, code, slots, H, b, boff); break;
+    case 4: hipLaunchKernelGGL((k_vertex_reduce<DIM, 4>), g, 256, 0, s, nv, ptr, code, slots, H, b, boff); break;
+    case 8: hipLaunchKernelGGL((k_vertex_reduce<DIM, 8>), g, 256, 0, s, nv, ptr, code, slots, H, b, boff); break;
     case 64:
       if (vr_wide())
-        hipLaunchKernelGGL((k_vertex_reduce_wide<DIM>), nv, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff);
+        hipLaunchKernelGGL((k_vertex_reduce_wide<DIM>), nv, 256, 0, s, nv, ptr, code, slots, H, b, boff);
       else
-        hipLaunchKernelGGL((k_vertex_reduce<DIM, 64>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff);
+        hipLaunchKernelGGL((k_vertex_reduce<DIM, 64>), g, 256, 0, s, nv, ptr, code, slots, H, b, boff);
       break;
-    default: hipLaunchKernelGGL((k_vertex_reduce<DIM, 256>), g, 256, 0, s, nv, ptr, code, s0, s1, st0, st1, H, b, boff); break;
+    default: hipLaunchKernelGGL((k_vertex_reduce<DIM, 256>), g, 256, 0, s, nv, ptr, code, slots, H, b, boff); break;
   }
   KERNEL_CHECK();
 }
 
-void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, const double* s0, const double* s1,
-                   int st0, int st1, double* H, double* b, const int* boff, hipStream_t s) {
+void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, const double* slots, double* H,
+                   double* b, const int* boff, hipStream_t s) {
   if (nv <= 0) return;
-  if (dim == 3) vreduce_dim<3>(nv, lanes, ptr, code, s0, s1, st0, st1, H, b, boff, s);
-  else if (dim == 6) vreduce_dim<6>(nv, lanes, ptr, code, s0, s1, st0, st1, H, b, boff, s);
+  if (dim == 3) vreduce_dim<3>(nv, lanes, ptr, code, slots, H, b, boff, s);
+  else if (dim == 6) vreduce_dim<6>(nv, lanes, ptr, code, slots, H, b, boff, s);
   else throw std::runtime_error("vertex_reduce: unsupported dim");
 }
 
-void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const double* slots, double* out,
+void offblock_reduce(int nb, int bsz, const int* ptr, const long long* soff, const double* slots, double* out,
                      const long long* dst, hipStream_t s) {
   if (nb <= 0) return;
-  hipLaunchKernelGGL(k_offblock_reduce, grid_for((size_t)nb * bsz, 256), 256, 0, s, nb, bsz, ptr, edges, slots, out, dst);
+  hipLaunchKernelGGL(k_offblock_reduce, grid_for((size_t)nb * bsz, 256), 256, 0, s, nb, bsz, ptr, soff, slots, out, dst);
   KERNEL_CHECK();
 }
 
@@ -975,15 +1064,17 @@ void sum(const double* v, long long n, double* partial, double* out, hipStream_t
   KERNEL_CHECK();
 }
 
-void error_sum(int family, const EdgeArgs& a, int ne, double* partial, double* out, hipStream_t s) {
+int error_partials(int family, const EdgeArgs& a, int ne, double* partial, hipStream_t s) {
   const int np = (int)sum_partials(ne);
-  if (np > 0) {
-    switch (family) {
-      case FAM_BA: hipLaunchKernelGGL(k_error_partial<FamilyBA>, np, RED_BLOCK, 0, s, mk<FamilyBA>(a), ne, partial); break;
-      case FAM_SE3: hipLaunchKernelGGL(k_error_partial<FamilySE3>, np, RED_BLOCK, 0, s, mk<FamilySE3>(a), ne, partial); break;
-      case FAM_SE2: hipLaunchKernelGGL(k_error_partial<FamilySE2>, np, RED_BLOCK, 0, s, mk<FamilySE2>(a), ne, partial); break;
-    }
-  }
+  if (np <= 0) return 0;
+  family_dispatch(family, a, [&](auto fam) {
+    using F = decltype(fam);
+    hipLaunchKernelGGL(k_error_partial<F>, np, RED_BLOCK, 0, s, mk(a), ne, partial);
+  });
+  KERNEL_CHECK();
+  return np;
+}
+void sum_final(const double* partial, int np, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_sum_final, 1, RED_BLOCK, 0, s, partial, np, out);
   KERNEL_CHECK();
 }
@@ -992,6 +1083,15 @@ void scale_sum(long long n, long long npose, const double* x, const double* b, c
   const int np = (int)sum_partials(n);
   if (np > 0) hipLaunchKernelGGL(k_scale_partial, np, RED_BLOCK, 0, s, n, npose, x, b, lam, partial);
   hipLaunchKernelGGL(k_sum_final, 1, RED_BLOCK, 0, s, partial, np, out);
+  KERNEL_CHECK();
+}
+void block_symv(int pd, int n, const int* rptr, const int2* ent, const int* diag, const double* vals, const double* lam,
+                const double* x, double* y, const double* b, double* r2, double* b2, hipStream_t s) {
+  if (n <= 0) return;
+  const unsigned g = grid_for(n, 256);
+  if (pd == 6) hipLaunchKernelGGL(k_block_symv<6>, g, 256, 0, s, n, rptr, ent, diag, vals, lam, x, y, b, r2, b2);
+  else if (pd == 3) hipLaunchKernelGGL(k_block_symv<3>, g, 256, 0, s, n, rptr, ent, diag, vals, lam, x, y, b, r2, b2);
+  else throw std::runtime_error("block_symv: block dimension must be 3 or 6");
   KERNEL_CHECK();
 }
 void scale_terms(long long n, const double* x, const double* b, const double* lam, double* out, hipStream_t s) {

@@ -7,25 +7,31 @@
 
 namespace g2ohip {
 
-enum Family { FAM_NONE = 0, FAM_BA = 1, FAM_SE3 = 2, FAM_SE2 = 3 };
+enum Family { FAM_NONE = 0, FAM_BA = 1, FAM_SE3 = 2, FAM_SE2 = 3, FAM_HOSTJ = 4 };
 
 struct EdgeArgs {
   const int* v0;
   const int* v1;
-  const double* meas;
+  const double* meas;  // host-J family: per edge [e | Ji | Jj]
   const double* info;
   const double* params;
   const double* s0;
   const double* s1;
+  int rk = 0;          // robust kernel (G2OHIP_RK_*), uniform over the edge group
+  double rk_delta = 1.0;
+  int D = 0, DA = 0, DB = 0;  // host-J family dimensions
 };
 
 namespace launch {
 void error(int family, const EdgeArgs& a, int ne, double* chi, hipStream_t s);
+// off_dst: destination of each edge's off-diagonal block, an offset into off_base (the Hessian) or, with bit 62
+// set, into off_slot (per-edge slots of blocks several edges share)
 void linearize(int family, const EdgeArgs& a, int ne, const int* h0, const int* h1, double* slot0, double* slot1,
-               const long long* off_dst, const unsigned char* off_tr, double* off_base, hipStream_t s);
-void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, const double* s0, const double* s1,
-                   int st0, int st1, double* H, double* b, const int* boff, hipStream_t s);
-void offblock_reduce(int nb, int bsz, const int* ptr, const int* edges, const double* slots, double* out,
+               const long long* off_dst, const unsigned char* off_tr, double* off_base, double* off_slot, hipStream_t s);
+// code[p] = slot index in `slots` (stride dim(dim+1)/2 + dim)
+void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, const double* slots, double* H,
+                   double* b, const int* boff, hipStream_t s);
+void offblock_reduce(int nb, int bsz, const int* ptr, const long long* soff, const double* slots, double* out,
                      const long long* dst, hipStream_t s);
 void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
                 double* Ufac, double* cl_all, int* fail, hipStream_t s);
@@ -54,11 +60,18 @@ void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* 
 size_t sum_partials(long long n);
 void sum(const double* v, long long n, double* partial, double* out, hipStream_t s);
 void scale_terms(long long n, const double* x, const double* b, const double* lam, double* out, hipStream_t s);
-// fused computeActiveErrors + chi2 sum, computeScale + sum (same chunking/tree as sum(): deterministic)
-void error_sum(int family, const EdgeArgs& a, int ne, double* partial, double* out, hipStream_t s);
+// computeActiveErrors + activeRobustChi2 of one edge group fused with the first pass of the deterministic sum:
+// writes the group's partials at partial[0..np) and returns np; sum_final adds all groups' partials in order
+int error_partials(int family, const EdgeArgs& a, int ne, double* partial, hipStream_t s);
+void sum_final(const double* partial, int np, double* out, hipStream_t s);
+// computeScale + sum (same chunking/tree as sum(): deterministic)
 void scale_sum(long long n, long long npose, const double* x, const double* b, const double* lam, double* partial,
                double* out, hipStream_t s);
 void set_scalars(double* p, double lam, double lam_rank, hipStream_t s, bool reset_fail = false);
+// y = (A + lam I) x, A symmetric as upper blocks (block CSR with transposed entries); lam may be null; with b also
+// per-row (y - b)^2 -> r2 and b^2 -> b2 (y may be null)
+void block_symv(int pd, int n, const int* rptr, const int2* ent, const int* diag, const double* vals, const double* lam,
+                const double* x, double* y, const double* b, double* r2, double* b2, hipStream_t s);
 struct CopyList {  // up to 4 device-to-device copies of doubles in one launch (vertex push/pop)
   const double* src[4];
   double* dst[4];

@@ -19,7 +19,7 @@ namespace {
 
 constexpr int PB = 256;
 constexpr int CHUNK = 16;
-enum { SC_DN = 0, SC_D0, SC_A, SC_BA, SC_ITER, SC_DONE, SC_RESID, SC_N };
+enum { SC_DN = 0, SC_D0, SC_A, SC_BA, SC_ITER, SC_DONE, SC_RESID, SC_NAN, SC_N };
 
 __device__ inline double block_sum(double v, double* sh) {
   __syncthreads();  // sh may still be read from a previous call
@@ -37,8 +37,9 @@ __device__ inline double sum_partials(const double* p, int np, double* sh) {
   return block_sum(v, sh);
 }
 
-// J_i = (D_i + λ I)^-1 by Cholesky (diagonal blocks are symmetric; the reference inverts with Eigen's
-// LU, linear_solver_pcg.hpp:95 — equal up to rounding)
+// J_i = (D_i + λ I)^-1 (linear_solver_pcg.hpp:92-96: Eigen's inverse() of the diagonal block, i.e. an LU with
+// partial pivoting). Gauss-Jordan with row pivoting, pivot rows exchanged by selects so the register arrays
+// keep compile-time indices. Indefinite blocks invert like the reference's (no Cholesky NaN).
 template <int PD>
 __global__ void __launch_bounds__(PB) k_pcg_jacobi(int nb, const int* __restrict__ diag, const double* __restrict__ vals,
                                                    const double* __restrict__ lam, double* __restrict__ J) {
@@ -46,43 +47,47 @@ __global__ void __launch_bounds__(PB) k_pcg_jacobi(int nb, const int* __restrict
   if (i >= nb) return;
   const double* D = vals + (size_t)diag[i] * PD * PD;
   const double l = *lam;
-  double L[PD][PD], Li[PD][PD];
+  double M[PD][PD], V[PD][PD];
 #pragma unroll
-  for (int j = 0; j < PD; ++j) {
-    double s = D[j * PD + j] + l;
+  for (int r = 0; r < PD; ++r)
 #pragma unroll
-    for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
-    L[j][j] = sqrt(s);
-    const double inv = 1.0 / L[j][j];
-#pragma unroll
-    for (int r = j + 1; r < PD; ++r) {
-      double t = D[j * PD + r];
-#pragma unroll
-      for (int k = 0; k < j; ++k) t -= L[r][k] * L[j][k];
-      L[r][j] = t * inv;
+    for (int c = 0; c < PD; ++c) {
+      M[r][c] = D[c * PD + r] + (r == c ? l : 0.0);
+      V[r][c] = r == c ? 1.0 : 0.0;
     }
-  }
 #pragma unroll
-  for (int j = 0; j < PD; ++j) {
-    Li[j][j] = 1.0 / L[j][j];
+  for (int c = 0; c < PD; ++c) {
+    int p = c;
+    double best = fabs(M[c][c]);
 #pragma unroll
-    for (int r = j + 1; r < PD; ++r) {
-      double t = 0.0;
+    for (int r = c + 1; r < PD; ++r)
+      if (fabs(M[r][c]) > best) { best = fabs(M[r][c]); p = r; }
 #pragma unroll
-      for (int k = j; k < r; ++k) t += L[r][k] * Li[k][j];
-      Li[r][j] = -t / L[r][r];
+    for (int r = c + 1; r < PD; ++r) {
+      const bool sw = r == p;
+#pragma unroll
+      for (int k = 0; k < PD; ++k) {
+        const double m0 = M[c][k], m1 = M[r][k], v0 = V[c][k], v1 = V[r][k];
+        M[c][k] = sw ? m1 : m0; M[r][k] = sw ? m0 : m1;
+        V[c][k] = sw ? v1 : v0; V[r][k] = sw ? v0 : v1;
+      }
+    }
+    const double inv = 1.0 / M[c][c];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) { M[c][k] *= inv; V[c][k] *= inv; }
+#pragma unroll
+    for (int r = 0; r < PD; ++r) {
+      if (r == c) continue;
+      const double f = M[r][c];
+#pragma unroll
+      for (int k = 0; k < PD; ++k) { M[r][k] -= f * M[c][k]; V[r][k] -= f * V[c][k]; }
     }
   }
   double* Jo = J + (size_t)i * PD * PD;
 #pragma unroll
   for (int c = 0; c < PD; ++c)
 #pragma unroll
-    for (int r = 0; r < PD; ++r) {
-      double t = 0.0;
-#pragma unroll
-      for (int k = (r > c ? r : c); k < PD; ++k) t += Li[k][r] * Li[k][c];
-      Jo[c * PD + r] = t;
-    }
+    for (int r = 0; r < PD; ++r) Jo[c * PD + r] = V[r][c];
 }
 
 // x = 0, r = b, s = J r (= the first direction), d_prev = 0, partial of r·s (linear_solver_pcg.hpp:118-123)
@@ -130,7 +135,11 @@ __global__ void __launch_bounds__(PB) k_pcg_start(const double* __restrict__ par
     sc[SC_D0] = d0;
     sc[SC_BA] = 0.0;
     sc[SC_ITER] = 0.0;
-    sc[SC_DONE] = (dn <= d0 || maxit <= 0 || !isfinite(dn)) ? 1.0 : 0.0;
+    // a NaN residual never satisfies dn <= d0: the reference keeps iterating to maxIter and returns a NaN
+    // x (every later x += a d is NaN); stop here and poison x instead (k_pcg_finish), same result
+    const bool nan = dn != dn;
+    sc[SC_NAN] = nan ? 1.0 : 0.0;
+    sc[SC_DONE] = (dn <= d0 || maxit <= 0 || nan) ? 1.0 : 0.0;
   }
 }
 
@@ -227,11 +236,36 @@ __global__ void __launch_bounds__(PB) k_pcg_beta(const double* __restrict__ part
     sc[SC_BA] = dn / sc[SC_DN];
     sc[SC_DN] = dn;
     sc[SC_ITER] = it;
-    sc[SC_DONE] = (dn <= sc[SC_D0] || it >= (double)maxit || !isfinite(dn)) ? 1.0 : 0.0;
+    const bool nan = dn != dn;
+    if (nan) sc[SC_NAN] = 1.0;
+    sc[SC_DONE] = (dn <= sc[SC_D0] || it >= (double)maxit || nan) ? 1.0 : 0.0;
   }
 }
 
-__global__ void k_pcg_finish(double* __restrict__ sc) { sc[SC_RESID] = 0.5 * sc[SC_DN]; }  // :153
+// _residual = 0.5 dn (:153); a NaN recurrence leaves x NaN, as the reference's maxIter NaN iterations would
+__global__ void __launch_bounds__(PB) k_pcg_finish(int n, double* __restrict__ x, double* __restrict__ sc) {
+  const bool nan = sc[SC_NAN] != 0.0;
+  if (nan)
+    for (int k = blockIdx.x * PB + threadIdx.x; k < n; k += gridDim.x * PB) x[k] = __builtin_nan("");
+  if (blockIdx.x == 0 && threadIdx.x == 0) sc[SC_RESID] = 0.5 * sc[SC_DN];
+}
+
+// stream capture that always ends (and frees its graph) even when a capture call throws
+struct CaptureGuard {
+  hipStream_t st;
+  hipGraph_t g = nullptr;
+  bool open = true;
+  explicit CaptureGuard(hipStream_t s) : st(s) { HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal)); }
+  hipGraph_t end() {
+    open = false;
+    HIP_CHECK(hipStreamEndCapture(st, &g));
+    return g;
+  }
+  ~CaptureGuard() {
+    if (open) (void)hipStreamEndCapture(st, &g);
+    if (g) (void)hipGraphDestroy(g);
+  }
+};
 
 template <int PD>
 void run(int nb, int n, int npa, int npb, int maxit, double tol, int abs_tol, const int* rptr, const int2* ent,
@@ -266,12 +300,15 @@ void run(int nb, int n, int npa, int npb, int maxit, double tol, int abs_tol, co
       if (!exec || key[0] != want[0] || key[1] != want[1] || key[2] != want[2] || key[3] != want[3]) {
         if (exec) HIP_CHECK(hipGraphExecDestroy(exec));
         exec = nullptr;
-        hipGraph_t g;
-        HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        enqueue(0, CHUNK);
-        HIP_CHECK(hipStreamEndCapture(st, &g));
-        HIP_CHECK(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
-        HIP_CHECK(hipGraphDestroy(g));
+        for (auto& k : key) k = nullptr;  // set only once a graph is instantiated
+        {
+          CaptureGuard cap(st);
+          enqueue(0, CHUNK);
+          hipGraph_t g = cap.end();
+          hipGraphExec_t ex = nullptr;
+          HIP_CHECK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+          exec = ex;
+        }
         for (int u = 0; u < 4; ++u) key[u] = want[u];
       }
       HIP_CHECK(hipGraphLaunch(exec, st));
@@ -284,7 +321,7 @@ void run(int nb, int n, int npa, int npb, int maxit, double tol, int abs_tol, co
     HIP_CHECK(hipStreamSynchronize(st));
     if (h[SC_DONE] != 0.0) break;
   }
-  hipLaunchKernelGGL(k_pcg_finish, 1, 1, 0, st, sc);
+  hipLaunchKernelGGL(k_pcg_finish, grid_for(n, PB) < 1024 ? grid_for(n, PB) : 1024, PB, 0, st, n, x, sc);
   KERNEL_CHECK();
   HIP_CHECK(hipMemcpyAsync(h, sc, sizeof h, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
@@ -332,7 +369,7 @@ void DevicePCG::setup(int nblocks, int bdim, const std::vector<int>& bi, const s
 }
 
 void DevicePCG::reset(hipStream_t s) {
-  const double init[SC_N] = {0, 0, 0, 0, 0, 0, -1.0};  // _residual = -1 (linear_solver_pcg.h:56,66)
+  const double init[SC_N] = {0, 0, 0, 0, 0, 0, -1.0, 0};  // _residual = -1 (linear_solver_pcg.h:56,66)
   HIP_CHECK(hipMemcpyAsync(sc.get(), init, sizeof init, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipStreamSynchronize(s));
 }

@@ -36,6 +36,24 @@ extern "C" {
                                       meas u v; info 2x2; params fx fy cx cy */
 #define G2OHIP_E_SE3_QUAT 2        /* EdgeSE3, edge_se3.h: meas x y z qx qy qz qw; info 6x6 */
 #define G2OHIP_E_SE2 3             /* EdgeSE2, edge_se2.h:46-52: meas x y theta; info 3x3 */
+/* An edge type the device does not know (any BaseBinaryEdge<D, E, Vi, Vj> between registered vertices of
+ * dimension 3 or 6): the host's own linearizeOplus (the type's analytic one, or BaseBinaryEdge's numeric
+ * central differences, base_binary_edge.hpp:198-266) supplies the error and both Jacobians, see
+ * g2ohip_set_host_jacobians; the device assembles, marginalises and solves. meas unused (may be NULL);
+ * info D*D. Several host-J types (different D) may coexist with the device types in one graph. */
+#define G2OHIP_E_HOSTJ(D) (32 + (D)) /* D = error dimension, 1..6 */
+
+/* robust kernels (robust_kernel_impl.cpp; RobustKernelFactory names) */
+#define G2OHIP_RK_NONE 0
+#define G2OHIP_RK_HUBER 1
+#define G2OHIP_RK_PSEUDO_HUBER 2
+#define G2OHIP_RK_CAUCHY 3
+#define G2OHIP_RK_GEMAN_MCCLURE 4
+#define G2OHIP_RK_WELSCH 5
+#define G2OHIP_RK_FAIR 6
+#define G2OHIP_RK_TUKEY 7
+#define G2OHIP_RK_SATURATED 8
+#define G2OHIP_RK_DCS 9
 
 /* status codes */
 #define G2OHIP_OK 0
@@ -94,6 +112,20 @@ int g2ohip_set_estimates(g2ohip_graph* g, int type, const double* est);
 /* minimal state vector concatenated in vertex-id order (parity checks) */
 int g2ohip_minimal_state(g2ohip_graph* g, double* out);
 
+/* OptimizableGraph::Edge::setRobustKernel (optimizable_graph.h; base_binary_edge.hpp:104-135 weighted
+ * quadratic form, sparse_optimizer.cpp:102-116 robust chi2) for every edge of a type: kind G2OHIP_RK_*,
+ * delta = RobustKernel::setDelta. G2OHIP_RK_NONE removes it. */
+int g2ohip_set_robust_kernel(g2ohip_graph* g, int edge_type, int kind, double delta);
+/* Host-computed linearization of the G2OHIP_E_HOSTJ(D) edges of one type, in insertion order: per edge
+ * [e (D) | Ji (D x dim(v0)) | Jj (D x dim(v1))], row-major, at the estimates the device holds (call after
+ * g2ohip_set_estimates, before g2ohip_solver_build_system). The J_host_fallback of SURVEY.md 8b. */
+int g2ohip_set_host_jacobians(g2ohip_graph* g, int edge_type, const double* payload);
+/* Callback for the device-resident loops (g2ohip_optimize / g2ohip_chi2) when host-J edges exist: fill the
+ * payload of every edge of `edge_type` at the current estimates (read them with g2ohip_get_estimates);
+ * with_jacobians = 0 only needs the errors. Return 0 on success. */
+typedef int (*g2ohip_host_edge_fn)(void* user, int edge_type, int with_jacobians, double* payload);
+int g2ohip_set_host_edge_callback(g2ohip_graph* g, g2ohip_host_edge_fn fn, void* user);
+
 /* OptimizationAlgorithmFactory::construct by name; default "lm_hip_var" */
 int g2ohip_set_algorithm(g2ohip_graph* g, const char* name);
 /* SparseOptimizer::initializeOptimization(0): active edges/vertices, index mapping */
@@ -116,6 +148,21 @@ int g2ohip_solver_solve(g2ohip_graph* g);                       /* Solver::solve
 long long g2ohip_solver_vector_size(g2ohip_graph* g);           /* Solver::vectorSize */
 int g2ohip_solver_get_x(g2ohip_graph* g, double* x);            /* Solver::x() (host copy) */
 int g2ohip_solver_get_b(g2ohip_graph* g, double* b);            /* Solver::b() (host copy) */
+/* BlockSolverBase::multiplyHessian (core/block_solver.h:94,146; used by OptimizationAlgorithmDogleg
+ * optimization_algorithm_dogleg.cpp:100,179): dest = Hpp src with the upper blocks mirrored (+ lambda on the
+ * diagonal while a setLambda is active), host arrays of hessianPoseDimension. Single rank only. */
+int g2ohip_solver_multiply_hessian(g2ohip_graph* g, double* dest, const double* src);
+/* max |diagonal entry| of the vertex Hessian blocks (Hpp, Hll) after buildSystem: the quantity
+ * OptimizationAlgorithmLevenberg::computeLambdaInit reads through the vertices' mapped Hessians
+ * (optimization_algorithm_levenberg.cpp:152-175) in the host-authoritative Solver mode. */
+int g2ohip_solver_diag_absmax(g2ohip_graph* g, double* out);
+/* ||(A + lambda I) x - b|| / ||b|| of the last Solver::solve, evaluated on the device (A = the Schur complement
+ * with Schur, else Hpp): a size-independent check of the factorization at any problem size. */
+int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel);
+/* Symbolic / schedule summary of the device factorization: out[0..10] = n, nnz(L), flops (this ordering),
+ * supernodes, tree levels, largest front, blocked fronts, levels assembled in place, pre-scattered levels,
+ * trailing-update launches, big-panel backward rounds. Returns the number of entries available. */
+int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n);
 /* SparseOptimizer::update(x) + push/pop/discardTop on the device-resident state */
 int g2ohip_update(g2ohip_graph* g, const double* x_host /* NULL: use device x */);
 int g2ohip_push(g2ohip_graph* g);

@@ -360,6 +360,7 @@ struct Config {
   int threads = 1;
   bool useRef = true;
   bool blockOrdering = true;
+  bool gaussNewton = false;
 };
 
 struct Stats {
@@ -1208,6 +1209,29 @@ struct LM {  // optimization_algorithm_levenberg.cpp
   }
 };
 
+// optimization_algorithm_gauss_newton.cpp:50-92
+LM::Result gaussNewtonSolve(Graph& G, const Config& cfg, int iteration, oracle_batch_stats* st) {
+  BlockSolver& S = G.solver;
+  double t = now();
+  computeActiveErrors(G, cfg.threads);
+  if (st) st->timeResiduals = now() - t;
+  if (iteration == 0) {
+    if (!S.buildStructure(G)) return LM::Fail;
+    G.structureBuilt = true;
+    S.lin.blockOrdering = cfg.blockOrdering;
+    S.lin.useRef = cfg.useRef;
+    S.lin.reset();
+  }
+  t = now();
+  S.buildSystem(G, cfg.threads);
+  if (st) { st->timeQuadraticForm = now() - t; t = now(); }
+  const bool ok = S.solve(cfg.threads, st);
+  if (st) { st->timeLinearSolution = now() - t; t = now(); }
+  update(G, S.x.data());
+  if (st) st->timeUpdate = now() - t;
+  return ok ? LM::OK : LM::Fail;
+}
+
 Config toConfig(const oracle_config* c) {
   Config cfg;
   if (c) {
@@ -1216,6 +1240,7 @@ Config toConfig(const oracle_config* c) {
     cfg.threads = c->threads > 0 ? c->threads : 1;
     cfg.useRef = c->use_ref_csparse != 0;
     cfg.blockOrdering = c->block_ordering != 0;
+    cfg.gaussNewton = c->gauss_newton != 0;
   }
   return cfg;
 }
@@ -1499,12 +1524,12 @@ int oracle_optimize(OracleGraph* og, const oracle_config* c, int iterations, ora
       st->numVertices = (int)G.activeVertices.size();
     }
     double ts = now();
-    result = og->lm.solve(G, cfg, i, st);
+    result = cfg.gaussNewton ? gaussNewtonSolve(G, cfg, i, st) : og->lm.solve(G, cfg, i, st);
     ok = result == LM::OK;
     if (st) {
       computeActiveErrors(G, cfg.threads);
       st->chi2 = activeRobustChi2(G);
-      st->lambda = og->lm.currentLambda;
+      st->lambda = cfg.gaussNewton ? 0.0 : og->lm.currentLambda;
       st->timeIteration = now() - ts;
     }
     ++cj;
@@ -1643,6 +1668,72 @@ int oracle_ccs_cholsol(int n, const int* Ap, const int* Ai, const double* Ax, do
   if (!chol_numeric(C, parent, cp, Li, Lx)) return 0;
   chol_solve(n, pinv, cp, Li, Lx, b, xw);
   return 1;
+}
+
+// Symbolic statistics of LinearSolverCSparse::computeSymbolicDecomposition (linear_solver_csparse.h:246-308) for
+// a block pattern (upper blocks bi <= bj of uniform size bdim): cs_amd on the block pattern (reference CSparse
+// when use_ref and loaded, else natural order) expanded to scalars, symperm, etree, column counts.
+// out[0] = nnz(L) = sum c_k, out[1] = sum c_k^2 (the factorization flop count of SURVEY.md 8d, cs_demo's "fl").
+int oracle_block_symbolic(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int use_ref, double* out) {
+  if (nblocks <= 0 || bdim <= 0 || nblk < 0 || !out) return -1;
+  std::vector<std::vector<int>> colrows(nblocks);
+  for (int k = 0; k < nblk; ++k) {
+    const int r = std::min(bi[k], bj[k]), c = std::max(bi[k], bj[k]);
+    if (r < 0 || c >= nblocks) return -1;
+    colrows[c].push_back(r);
+  }
+  for (int c = 0; c < nblocks; ++c) {
+    colrows[c].push_back(c);
+    std::sort(colrows[c].begin(), colrows[c].end());
+    colrows[c].erase(std::unique(colrows[c].begin(), colrows[c].end()), colrows[c].end());
+  }
+  std::vector<int> bp(nblocks + 1, 0), bix;
+  for (int c = 0; c < nblocks; ++c) {
+    bp[c] = (int)bix.size();
+    bix.insert(bix.end(), colrows[c].begin(), colrows[c].end());
+  }
+  bp[nblocks] = (int)bix.size();
+  std::vector<int> bperm(nblocks);
+  if (use_ref && refcs().ok()) {
+    cs_ref aux{(int)bix.size(), nblocks, nblocks, bp.data(), bix.data(), nullptr, -1};
+    int* pp = refcs().cs_amd(1, &aux);
+    if (!pp) return -1;
+    for (int k = 0; k < nblocks; ++k) bperm[k] = pp[k];
+    refcs().cs_free(pp);
+  } else {
+    for (int k = 0; k < nblocks; ++k) bperm[k] = k;
+  }
+  const int n = nblocks * bdim;
+  std::vector<int> P;
+  P.reserve(n);
+  for (int k = 0; k < nblocks; ++k)
+    for (int j = 0; j < bdim; ++j) P.push_back(bperm[k] * bdim + j);
+  CCS A;  // scalar upper pattern (fillCCS(upper=true), sparse_block_matrix.hpp:496-549)
+  A.n = n;
+  A.p.assign(n + 1, 0);
+  for (int bc = 0; bc < nblocks; ++bc)
+    for (int c = 0; c < bdim; ++c) {
+      A.p[bc * bdim + c] = (int)A.i.size();
+      for (int br : colrows[bc]) {
+        const int elems = br == bc ? c + 1 : bdim;
+        for (int r = 0; r < elems; ++r) A.i.push_back(br * bdim + r);
+      }
+    }
+  A.p[n] = (int)A.i.size();
+  A.x.assign(A.i.size(), 1.0);
+  CCS C;
+  std::vector<int> map;
+  symperm_upper(A, make_pinv(P), C, map);
+  const std::vector<int> parent = etree(C);
+  const std::vector<int> cnt = colcounts(C, parent);
+  double lnz = 0, fl = 0;
+  for (int k = 0; k < n; ++k) {
+    lnz += cnt[k];
+    fl += (double)cnt[k] * cnt[k];
+  }
+  out[0] = lnz;
+  out[1] = fl;
+  return 0;
 }
 
 int oracle_ref_available(void) { return refcs().ok() ? 1 : 0; }

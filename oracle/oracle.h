@@ -47,6 +47,7 @@ typedef struct {
   int threads;                  /* OpenMP threads for assembly / Schur (1 = deterministic) */
   int use_ref_csparse;          /* 1: cs_amd + cs_chol from oracle/_ref (if loaded); 0: restated */
   int block_ordering;           /* 1: AMD on block pattern (lm_fixP_L), 0: scalar (lm_var) */
+  int gauss_newton;             /* 1: OptimizationAlgorithmGaussNewton instead of Levenberg */
 } oracle_config;
 
 typedef struct OracleGraph OracleGraph;
@@ -89,6 +90,9 @@ int oracle_edge_jacobians(OracleGraph* g, int edge_index, double* err, double* J
  * up-looking LL^T with natural ordering, 1 = restated with cs_amd ordering (needs _ref),
  * 2 = reference CSparse cs_cholsol (needs _ref).  Returns 1 on success, 0 not PD, -1 unavailable. */
 int oracle_ccs_cholsol(int n, const int* Ap, const int* Ai, const double* Ax, double* b, int mode);
+/* Symbolic stats of the CSparse block ordering (cs_amd on the block pattern when use_ref, else natural):
+ * out[0] = nnz(L), out[1] = sum of squared column counts (factorization flops). */
+int oracle_block_symbolic(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int use_ref, double* out);
 int oracle_ref_available(void);
 const char* oracle_ref_path(void);
 

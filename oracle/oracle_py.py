@@ -32,7 +32,8 @@ class BatchStats(C.Structure):
 
 class Config(C.Structure):
     _fields_ = [("max_trials_after_failure", C.c_int), ("user_lambda_init", C.c_double),
-                ("threads", C.c_int), ("use_ref_csparse", C.c_int), ("block_ordering", C.c_int)]
+                ("threads", C.c_int), ("use_ref_csparse", C.c_int), ("block_ordering", C.c_int),
+                ("gauss_newton", C.c_int)]
 
 
 def build():
@@ -67,6 +68,7 @@ def lib():
         L.oracle_hessian_dense.argtypes = [P, P, P, P]
         L.oracle_edge_jacobians.argtypes = [P, I, P, P, P, P, P]
         L.oracle_ccs_cholsol.argtypes = [I, P, P, P, P, I]
+        L.oracle_block_symbolic.argtypes = [I, I, I, P, P, I, P]
         L.oracle_ref_available.restype = I
         L.oracle_ref_path.restype = C.c_char_p
         _lib = L
@@ -81,8 +83,10 @@ def ref_available() -> bool:
     return bool(lib().oracle_ref_available())
 
 
-def make_config(threads=1, use_ref=True, block_ordering=True, max_trials=10, lambda_init=0.0) -> Config:
-    return Config(max_trials, lambda_init, threads, 1 if use_ref else 0, 1 if block_ordering else 0)
+def make_config(threads=1, use_ref=True, block_ordering=True, max_trials=10, lambda_init=0.0,
+                gauss_newton=False) -> Config:
+    return Config(max_trials, lambda_init, threads, 1 if use_ref else 0, 1 if block_ordering else 0,
+                  1 if gauss_newton else 0)
 
 
 class OracleGraph:
@@ -180,3 +184,13 @@ def ccs_cholsol(n, Ap, Ai, Ax, b, mode):
     x = np.array(b, dtype=np.float64, copy=True)
     r = lib().oracle_ccs_cholsol(n, _p(Ap), _p(Ai), _p(Ax), _p(x), mode)
     return r, x
+
+
+def block_symbolic(nblocks, bdim, bi, bj, use_ref=True):
+    """(nnz(L), sum c_k^2) of LinearSolverCSparse's block-AMD symbolic analysis for an upper block pattern."""
+    bi = np.ascontiguousarray(bi, np.int32)
+    bj = np.ascontiguousarray(bj, np.int32)
+    out = np.zeros(2)
+    r = lib().oracle_block_symbolic(nblocks, bdim, len(bi), _p(bi), _p(bj), 1 if use_ref else 0, _p(out))
+    assert r == 0, r
+    return float(out[0]), float(out[1])

@@ -1,0 +1,164 @@
+"""BASELINE configs C2, C3 and C5 at their full sizes on the GPU.
+
+Trajectories are compared with committed fixtures of the oracle run with the reference's own CSparse
+(cs_amd block ordering + cs_chol), generated in the development container by
+tests/golden/make_fullsize.py: per-iteration chi2 and LM trial counts, and the final minimal state
+(C5: the cameras, every 97th point and per-4096-point sums of all point coordinates). Tolerance is the
+north_star bar: 1e-6 relative on chi2 and on the state vector.
+
+Size-independent properties on top (any size): the relative residual of the device factorization
+||(A + lambda I) x - b|| / ||b|| of a staged linear solve, monotone chi2, and - for C5 - the landmark-
+sharded path (8 ranks over the in-process transport, the same call sequence as RCCL) against the
+single-GPU run.
+"""
+import os
+import threading
+import uuid
+
+import numpy as np
+import pytest
+
+from g2o_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+RTOL = 1e-6
+ALG = {"C2": "lm_hip_fix3_3", "C3": "lm_hip_fix6_6", "C4": "lm_hip_fix6_3", "C5": "lm_hip_fix6_3"}
+
+
+def _fixture(name):
+    path = os.path.join(HERE, "golden", f"{name.lower()}_full.npz")
+    assert os.path.exists(path), f"missing fixture {path}: run tests/golden/make_fullsize.py {name}"
+    return np.load(path)
+
+
+def _check_trajectory(fx, st, n):
+    assert n == int(fx["iterations"])
+    for k, s in enumerate(st):
+        assert s.levenbergIterations == int(fx["trials"][k]), (k, s.levenbergIterations, fx["trials"][k])
+        assert abs(s.chi2 - fx["chi2"][k]) <= RTOL * abs(fx["chi2"][k]), (k, s.chi2, fx["chi2"][k])
+
+
+def _staged_residual(g2o_amd_mod, prob, algo, lam):
+    """Solver-plugin sequence (core/solver.h): buildStructure, buildSystem, setLambda, solve, then the
+    device residual of the factorization."""
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm(algo)
+    opt.initialize_optimization()
+    opt.build_structure()
+    opt.build_system()
+    opt.set_lambda(lam, True)
+    assert opt.solve()
+    rel = opt.linear_residual()
+    info = opt.factor_info()
+    opt.restore_diagonal()
+    return rel, info, opt
+
+
+def test_c2_full_trajectory(g2o_amd_mod):
+    """C2: SE2 pose graph, 100k poses / ~400k edges, BlockSolver_3_3 (no Schur)."""
+    fx = _fixture("C2")
+    prob = synth.by_name("C2")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm(ALG["C2"])
+    assert abs(opt.chi2() - float(fx["chi2_0"])) <= 1e-9 * float(fx["chi2_0"])
+    n, st = opt.optimize(int(fx["iterations"]))
+    _check_trajectory(fx, st, n)
+    x, xr = opt.minimal_state(), fx["state"]
+    assert np.linalg.norm(x - xr) <= RTOL * np.linalg.norm(xr)
+
+
+def test_c3_full_trajectory(g2o_amd_mod):
+    """C3: SE3 pose graph, 100k poses / ~500k edges, BlockSolver_6_6: the blocked-front, in-place assembly
+    and big-panel backward-solve paths of the factorization are all active at this size."""
+    fx = _fixture("C3")
+    prob = synth.by_name("C3")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm(ALG["C3"])
+    assert abs(opt.chi2() - float(fx["chi2_0"])) <= 1e-9 * float(fx["chi2_0"])
+    n, st = opt.optimize(int(fx["iterations"]))
+    _check_trajectory(fx, st, n)
+    x, xr = opt.minimal_state(), fx["state"]
+    assert np.linalg.norm(x - xr) <= RTOL * np.linalg.norm(xr)
+    info = opt.factor_info()
+    assert info["blocked_fronts"] > 0 and info["inplace_levels"] > 0 and info["bwd_rounds"] > 0, info
+    assert info["syrk_launches"] > 0, info
+
+
+@pytest.mark.parametrize("name,lam", [("C2", 1e-3), ("C3", 1e-3), ("C4", 1e-2), ("C5", 1e-2)])
+def test_full_size_linear_residual(g2o_amd_mod, name, lam):
+    """||(A + lambda I) x - b|| / ||b|| <= 1e-10 for the reduced system of every config at full size."""
+    rel, info, _ = _staged_residual(g2o_amd_mod, synth.by_name(name), ALG[name], lam)
+    assert rel <= 1e-10, (name, rel, info)
+
+
+def _check_c5_state(prob, x, fx):
+    ncam = prob.vertices[0].ids.size
+    cams, pts = x[:6 * ncam], x[6 * ncam:].reshape(-1, 3)
+    assert x.size == int(fx["state_len"])
+    assert np.linalg.norm(cams - fx["cams"]) <= RTOL * np.linalg.norm(fx["cams"])
+    ps = pts[::int(fx["stride"])]
+    assert np.linalg.norm(ps - fx["pts_strided"]) <= RTOL * np.linalg.norm(fx["pts_strided"])
+    ch = int(fx["chunk"])
+    sums = np.array([pts[c * ch:(c + 1) * ch].sum(axis=0) for c in range((pts.shape[0] + ch - 1) // ch)])
+    assert np.linalg.norm(sums - fx["pts_chunk_sums"]) <= RTOL * np.linalg.norm(fx["pts_chunk_sums"])
+    assert abs(np.linalg.norm(x) - float(fx["state_norm"])) <= RTOL * float(fx["state_norm"])
+
+
+def test_c5_full_single_gpu(g2o_amd_mod):
+    """C5: BA 4000 cameras x 1M points x 10M observations on one GPU against the oracle fixture."""
+    fx = _fixture("C5")
+    prob = synth.by_name("C5")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm(ALG["C5"])
+    assert abs(opt.chi2() - float(fx["chi2_0"])) <= 1e-9 * float(fx["chi2_0"])
+    n, st = opt.optimize(int(fx["iterations"]))
+    _check_trajectory(fx, st, n)
+    _check_c5_state(prob, opt.minimal_state(), fx)
+
+
+def test_c5_full_sharded_8_ranks(g2o_amd_mod):
+    """C5 landmark-sharded over 8 ranks (each holds 1/8 of the points; the reduced camera system is
+    summed across ranks where RCCL would all-reduce it) against the single-GPU run and the fixture."""
+    fx = _fixture("C5")
+    prob = synth.by_name("C5")
+    iters = int(fx["iterations"])
+    nranks = 8
+    key = uuid.uuid4().hex
+    opts = [g2o_amd_mod.SparseOptimizer(0).add_problem(prob) for _ in range(nranks)]
+    for r, o in enumerate(opts):
+        o.set_algorithm(ALG["C5"])
+        o.set_comm_local(key, r, nranks)
+    res, errs = [None] * nranks, []
+
+    def body(r):
+        try:
+            res[r] = opts[r].optimize(iters)
+        except Exception as ex:  # surfaced below
+            errs.append(ex)
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=900)
+    assert not errs, errs
+    for r in range(nranks):
+        n, st = res[r]
+        _check_trajectory(fx, st, n)
+    C, P = prob.vertices[0].ids.size, prob.vertices[1].ids.size
+    states = [o.minimal_state() for o in opts]
+    x = states[0].copy()
+    for r in range(nranks):
+        a, b = P * r // nranks, P * (r + 1) // nranks
+        x[6 * C + 3 * a: 6 * C + 3 * b] = states[r][6 * C + 3 * a: 6 * C + 3 * b]
+    for s in states[1:]:
+        assert np.array_equal(s[:6 * C], states[0][:6 * C])  # every rank factors the same reduced system
+    _check_c5_state(prob, x, fx)
+    del opts, states
+    single = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    single.set_algorithm(ALG["C5"])
+    single.optimize(iters)
+    xs = single.minimal_state()
+    assert np.linalg.norm(x - xs) <= 1e-9 * np.linalg.norm(xs)

@@ -260,3 +260,58 @@ def test_lm_pose_graph_shuffled_edges(g2o_amd_mod, oracle):
         edges = synth.EdgeSet(e.etype, e.v0[perm], e.v1[perm], e.meas[perm], e.info[perm], None)
         prob = synth.Problem(base.name + "_shuffled", base.vertices, [edges], base.pose_dim, base.landmark_dim)
         _check(*_run_both(g2o_amd_mod, oracle, prob, 5))
+
+
+@pytest.mark.parametrize("name", ["C1", "C4"])
+def test_gauss_newton_trajectory(g2o_amd_mod, oracle, name):
+    """gn_hip_*: OptimizationAlgorithmGaussNewton (optimization_algorithm_gauss_newton.cpp:50-92) — no damping,
+    no trial loop — against the oracle's GN, and a different trajectory from LM on the same problem."""
+    prob = synth.by_name(name, "small")
+    algo = "gn_hip_fix6_3" if prob.landmark_dim else "gn_hip_fix6_6"
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm(algo)
+    n, st = opt.optimize(4)
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.optimize(4, oracle.make_config(threads=4, gauss_newton=True))
+    assert n == nr == 4
+    for a, b in zip(st, sr):
+        assert a.levenbergIterations == 0
+        assert abs(a.chi2 - b.chi2) <= CHI2_RTOL * abs(b.chi2), (a.chi2, b.chi2)
+    xg, xr = opt.minimal_state(), ref.minimal_state()
+    assert np.linalg.norm(xg - xr) <= STATE_RTOL * np.linalg.norm(xr)
+    lm = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    lm.optimize(4)
+    assert np.linalg.norm(lm.minimal_state() - xg) > 1e-9 * np.linalg.norm(xg)
+
+
+@pytest.mark.parametrize("name", ["C1", "C4"])
+def test_multiply_hessian(g2o_amd_mod, oracle, name):
+    """BlockSolverBase::multiplyHessian (block_solver.h:146): Hpp (upper blocks mirrored) times a vector,
+    against the oracle's dense Hpp; with setLambda active the damped diagonal is used."""
+    prob = synth.by_name(name, "small")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.initialize_optimization()
+    opt.build_structure()
+    opt.build_system()
+    ref = oracle.OracleGraph(prob)
+    r = ref.stage(0.0)
+    Hpp, _, _ = ref.hessian_dense(r["np"], r["nl"])
+    v = np.random.default_rng(1).standard_normal(r["np"])
+    y = opt.multiply_hessian(v)
+    assert np.linalg.norm(y - Hpp @ v) <= 1e-12 * np.linalg.norm(Hpp @ v)
+    opt.set_lambda(0.5, True)
+    y2 = opt.multiply_hessian(v)
+    assert np.linalg.norm(y2 - (Hpp @ v + 0.5 * v)) <= 1e-12 * np.linalg.norm(Hpp @ v)
+    opt.restore_diagonal()
+
+
+def test_linear_residual_small(g2o_amd_mod):
+    for name, lam in (("C1", 1e-3), ("C4", 1e-2)):
+        opt = g2o_amd_mod.SparseOptimizer(0).add_problem(synth.by_name(name, "small"))
+        opt.initialize_optimization()
+        opt.build_structure()
+        opt.build_system()
+        opt.set_lambda(lam, True)
+        assert opt.solve()
+        assert opt.linear_residual() <= 1e-12
+        opt.restore_diagonal()

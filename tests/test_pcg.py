@@ -43,7 +43,7 @@ def test_pcg_restatement_absolute_residual_carry():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,algo,pd", [("C4", "lm_pcg6_3", 6), ("C1", "lm_pcg", 6), ("C2", "lm_pcg3_3", 3)])
+@pytest.mark.parametrize("name,algo,pd", [("C4", "lm_pcg6_3", 6), ("C1", "lm_pcg", 6), ("C2", "lm_pcg", 3)])
 def test_gpu_pcg_matches_restatement(g2o_amd_mod, name, algo, pd):
     prob = synth.by_name(name, "small")
     opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)

@@ -1,5 +1,5 @@
 import sys, time, os
-sys.path.insert(0,'/root/repo'); sys.path.insert(0,'/root/repo/oracle')
+R = __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))); sys.path.insert(0, R); sys.path.insert(0, R + '/oracle')
 import numpy as np
 import g2o_amd, oracle_py
 from g2o_amd import synth

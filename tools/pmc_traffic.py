@@ -7,7 +7,9 @@ Usage: python tools/pmc_traffic.py OUT.json FETCH_DIR WRITE_DIR
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KB; on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so it is doubled. Traffic
 per launch = mean over the kernel's dispatches of (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes.
-Kernel names are mapped to the bench.py stage names below.
+Kernel names are mapped to the bench.py stage names below. The factorization ("chol_factor") is a
+chain of launches (scatter, extend-add, panel steps, trailing updates): its traffic is the sum over
+all of its dispatches divided by the number of factorizations (k_vec_init runs once per factorization).
 """
 import csv
 import glob
@@ -26,8 +28,12 @@ STAGES = {  # substring of the kernel name -> stage name used by bench.py
 }
 
 
+FACTOR = ("k_zero_ranges", "k_chol_scatter", "k_vec_init", "k_extend_add", "k_step", "k_syrk", "k_permute")
+
+
 def read_counter(d, counter):
     per = defaultdict(list)
+    fsum, nfac = 0.0, 0
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
@@ -36,6 +42,11 @@ def read_counter(d, counter):
             for sub, stage in STAGES.items():
                 if sub in name:
                     per[stage].append(float(r["Counter_Value"]))
+            if any("::" + k + "(" in name or "::" + k + "<" in name for k in FACTOR):
+                fsum += float(r["Counter_Value"])
+                nfac += "::k_vec_init(" in name
+    if nfac:
+        per["chol_factor"] = [fsum / nfac] * nfac
     return per
 
 
@@ -56,6 +67,8 @@ def main():
             "launches": len(fetch[stage]),
             "correction": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)",
         }
+        if stage == "chol_factor":
+            res[stage]["launches"] = "factorizations (sum over the factor's kernel chain)"
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))

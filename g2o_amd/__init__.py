@@ -39,9 +39,22 @@ class Config(C.Structure):
     _fields_ = [("max_trials_after_failure", C.c_int), ("user_lambda_init", C.c_double), ("verbose", C.c_int)]
 
 
+# edge types the device does not know: host-supplied error + Jacobians (include/g2o_hip.h G2OHIP_E_HOSTJ)
+def E_HOSTJ(D: int) -> int:
+    return 32 + D
+
+
+# robust kernels (G2OHIP_RK_*, robust_kernel_impl.cpp)
+RK = {"none": 0, "Huber": 1, "PseudoHuber": 2, "Cauchy": 3, "GemanMcClure": 4, "Welsch": 5, "Fair": 6, "Tukey": 7,
+      "Saturated": 8, "DCS": 9}
+
+HOST_EDGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double))
+
 EXPORTS = [
     "g2ohip_graph_create", "g2ohip_graph_destroy", "g2ohip_add_vertices", "g2ohip_add_edges",
     "g2ohip_load_g2o", "g2ohip_save_g2o", "g2ohip_num_vertices", "g2ohip_num_edges",
+    "g2ohip_set_robust_kernel", "g2ohip_set_host_jacobians", "g2ohip_set_host_edge_callback",
+    "g2ohip_solver_diag_absmax",
     "g2ohip_get_estimates", "g2ohip_set_estimates", "g2ohip_minimal_state", "g2ohip_set_algorithm",
     "g2ohip_initialize", "g2ohip_chi2", "g2ohip_optimize", "g2ohip_optimize_step",
     "g2ohip_solver_build_structure", "g2ohip_solver_build_system", "g2ohip_solver_set_lambda",
@@ -81,6 +94,10 @@ def lib() -> C.CDLL:
         "g2ohip_save_g2o": ([P, C.c_char_p], I),
         "g2ohip_num_vertices": ([P], I),
         "g2ohip_num_edges": ([P], I),
+        "g2ohip_set_robust_kernel": ([P, I, I, D], I),
+        "g2ohip_set_host_jacobians": ([P, I, P], I),
+        "g2ohip_set_host_edge_callback": ([P, HOST_EDGE_FN, P], I),
+        "g2ohip_solver_diag_absmax": ([P, P], I),
         "g2ohip_get_estimates": ([P, I, P, P], I),
         "g2ohip_set_estimates": ([P, I, P], I),
         "g2ohip_minimal_state": ([P, P], I),
@@ -201,7 +218,7 @@ class SparseOptimizer:
     def add_edges(self, es):
         v0 = np.ascontiguousarray(es.v0, np.int32)
         v1 = np.ascontiguousarray(es.v1, np.int32)
-        meas = np.ascontiguousarray(es.meas, np.float64)
+        meas = None if es.meas is None else np.ascontiguousarray(es.meas, np.float64)
         info = np.ascontiguousarray(es.info, np.float64)
         par = None if es.params is None else np.ascontiguousarray(es.params, np.float64)
         _check(lib().g2ohip_add_edges(self.h, es.etype, len(v0), _p(v0), _p(v1), _p(meas), _p(info), _p(par)),
@@ -213,6 +230,41 @@ class SparseOptimizer:
         for es in prob.edges:
             self.add_edges(es)
         return self
+
+    def set_robust_kernel(self, etype: int, kind, delta: float):
+        """Edge::setRobustKernel for every edge of a type; kind = RK name or G2OHIP_RK_* number."""
+        k = RK[kind] if isinstance(kind, str) else int(kind)
+        _check(lib().g2ohip_set_robust_kernel(self.h, etype, k, float(delta)), "set_robust_kernel")
+
+    def set_host_jacobians(self, etype: int, payload):
+        """[e | Ji | Jj] row-major per edge of a host-J type (insertion order), at the device's estimates."""
+        payload = np.ascontiguousarray(payload, np.float64)
+        _check(lib().g2ohip_set_host_jacobians(self.h, etype, _p(payload)), "set_host_jacobians")
+
+    def set_host_edge_callback(self, fn):
+        """fn(edge_type, with_jacobians) -> payload ndarray, called by the device-resident loops for host-J edges."""
+        if fn is None:
+            self._host_cb = None
+            _check(lib().g2ohip_set_host_edge_callback(self.h, HOST_EDGE_FN(), None), "set_host_edge_callback")
+            return
+
+        def tramp(user, etype, with_jac, out):
+            try:
+                pay = np.ascontiguousarray(fn(etype, bool(with_jac)), np.float64)
+                C.memmove(out, pay.ctypes.data, pay.nbytes)
+                return 0
+            except Exception:  # reported as a failed callback by the engine
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._host_cb = HOST_EDGE_FN(tramp)  # keep alive
+        _check(lib().g2ohip_set_host_edge_callback(self.h, self._host_cb, None), "set_host_edge_callback")
+
+    def set_estimates(self, vtype: int, est):
+        """Overwrite the estimates of one vertex type (insertion order): host-authoritative Solver mode."""
+        est = np.ascontiguousarray(est, np.float64)
+        _check(lib().g2ohip_set_estimates(self.h, vtype, _p(est)), "set_estimates")
 
     def load(self, path: str, marginalize_xyz: bool = True):
         _check(lib().g2ohip_load_g2o(self.h, path.encode(), int(marginalize_xyz)), "load")
@@ -289,6 +341,12 @@ class SparseOptimizer:
         out = np.zeros_like(src)
         _check(lib().g2ohip_solver_multiply_hessian(self.h, _p(out), _p(src)), "multiplyHessian")
         return out
+
+    def diag_absmax(self) -> float:
+        """max |diag| of the vertex Hessians (computeLambdaInit's input) after buildSystem."""
+        r = np.zeros(1)
+        _check(lib().g2ohip_solver_diag_absmax(self.h, _p(r)), "diag_absmax")
+        return float(r[0])
 
     def linear_residual(self) -> float:
         """||(A + lambda I) x - b|| / ||b|| of the last solve, computed on the device."""

@@ -250,6 +250,7 @@ int edim(int type) {
     case ORACLE_E_SE3_PROJECT_XYZ: return 2;
     case ORACLE_E_SE3_QUAT: return 6;
     case ORACLE_E_SE2: return 3;
+    case ORACLE_E_SE3_EXPMAP: return 6;
   }
   return -1;
 }
@@ -287,7 +288,79 @@ struct Edge {
   int offKind = 0;  // 0 none, 1 Hpp block, 2 Hpl block, 3 Hll block
   size_t offOff = 0;
   bool rowMajor = false;
+  int rk = 0;              // robust kernel (ORACLE_RK_* = G2OHIP_RK_*), 0 none
+  double rkDelta = 1.0;
+  bool numeric = false;    // linearizeOplus by BaseBinaryEdge's numeric differences (a type without analytic J)
 };
+
+// RobustKernel*::robustify (robust_kernel_impl.cpp:60-200): rho[0], rho[1]
+void robustify(int kind, double delta, double e2, double& r0, double& r1) {
+  switch (kind) {
+    case 1: {  // Huber :65-78
+      const double dsqr = delta * delta;
+      if (e2 <= dsqr) { r0 = e2; r1 = 1.; }
+      else { const double sqrte = std::sqrt(e2); r0 = 2 * sqrte * delta - dsqr; r1 = delta / sqrte; }
+      return;
+    }
+    case 2: {  // PseudoHuber
+      const double dsqr = delta * delta, dsqrReci = 1. / dsqr, aux1 = dsqrReci * e2 + 1.0, aux2 = std::sqrt(aux1);
+      r0 = 2 * dsqr * (aux2 - 1);
+      r1 = 1. / aux2;
+      return;
+    }
+    case 3: {  // Cauchy
+      const double dsqr = delta * delta, dsqrReci = 1. / dsqr, aux = dsqrReci * e2 + 1.0;
+      r0 = dsqr * std::log(aux);
+      r1 = 1. / aux;
+      return;
+    }
+    case 4: {  // GemanMcClure
+      const double aux = delta / (delta + e2);
+      r0 = e2 * aux;
+      r1 = aux * aux;
+      return;
+    }
+    case 5: {  // Welsch
+      const double dsqr = delta * delta, aux = e2 / dsqr, aux2 = std::exp(-aux);
+      r0 = dsqr * (1. - aux2);
+      r1 = aux2;
+      return;
+    }
+    case 6: {  // Fair
+      const double sqrte = std::sqrt(e2), aux = sqrte / delta;
+      r0 = 2. * delta * delta * (aux - std::log(1. + aux));
+      r1 = 1. / (1. + aux);
+      return;
+    }
+    case 7: {  // Tukey
+      const double e = std::sqrt(e2), delta2 = delta * delta;
+      if (e <= delta) {
+        const double aux = e2 / delta2;
+        r0 = delta2 * (1. - std::pow((1. - aux), 3)) / 3.;
+        r1 = std::pow((1. - aux), 2);
+      } else {
+        r0 = delta2 / 3.;
+        r1 = 0;
+      }
+      return;
+    }
+    case 8: {  // Saturated
+      const double dsqr = delta * delta;
+      if (e2 <= dsqr) { r0 = e2; r1 = 1.; }
+      else { r0 = dsqr; r1 = 0.; }
+      return;
+    }
+    case 9: {  // DCS
+      double scale = (2.0 * delta) / (delta + e2);
+      if (scale >= 1.0) scale = 1.0;
+      r0 = scale * e2 * scale;
+      r1 = scale * scale;
+      return;
+    }
+  }
+  r0 = e2;
+  r1 = 1.;
+}
 
 struct SBM {  // core/sparse_block_matrix.h:62-231
   std::vector<int> rowBlockIndices, colBlockIndices;  // cumulative END offsets
@@ -540,6 +613,13 @@ void computeError(const Graph& G, Edge& e) {
       toVectorMQT(delta, e.err);
       break;
     }
+    case ORACLE_E_SE3_EXPMAP: {  // types_six_dof_expmap.h:117-124: (v2^-1 * C * v1).log()
+      SE3Quat C;
+      C.t = {e.meas[0], e.meas[1], e.meas[2]};
+      C.r = Quat{e.meas[6], e.meas[3], e.meas[4], e.meas[5]};
+      se3log(se3mul(se3mul(se3inv(b.est.q), C), a.est.q), e.err);
+      break;
+    }
     case ORACLE_E_SE2: {  // edge_se2.h:46-52
       SE2 delta = se2mul(e.m2inv, se2mul(se2inv(a.est.se2), b.est.se2));
       e.err[0] = delta.x;
@@ -740,9 +820,17 @@ void computeActiveErrors(Graph& G, int threads) {  // sparse_optimizer.cpp:63-90
 #pragma omp parallel for num_threads(threads) if (ne > 50)
   for (int k = 0; k < ne; ++k) computeError(G, G.edges[k]);
 }
-double activeRobustChi2(const Graph& G) {  // :102-116 (no robust kernels)
+double activeRobustChi2(const Graph& G) {  // :102-116
   double chi = 0;
-  for (const Edge& e : G.edges) chi += edgeChi2(e);
+  for (const Edge& e : G.edges) {
+    if (e.rk) {
+      double r0, r1;
+      robustify(e.rk, e.rkDelta, edgeChi2(e), r0, r1);
+      chi += r0;
+    } else {
+      chi += edgeChi2(e);
+    }
+  }
   return chi;
 }
 void update(Graph& G, const double* upd) {  // :441-454
@@ -879,6 +967,16 @@ void BlockSolver::buildSystem(Graph& G, int threads) {  // block_solver.hpp:462-
     for (auto& l : vlocks) omp_init_lock(&l);
   }
   const int ne = (int)G.edges.size();
+  // numeric Jacobians perturb vertex estimates (push / oplus / pop, base_binary_edge.hpp:198-266, which the
+  // reference guards with the vertex's QuadraticFormLock): computed serially up front, before the parallel loop
+  std::vector<int> numIdx(ne, -1);
+  std::vector<double> numJ;
+  for (int k = 0; k < ne; ++k)
+    if (G.edges[k].numeric) {
+      numIdx[k] = (int)(numJ.size() / 72);
+      numJ.resize(numJ.size() + 72);
+      linearizeNumeric(G, G.edges[k], numJ.data() + (size_t)numIdx[k] * 72, numJ.data() + (size_t)numIdx[k] * 72 + 36);
+    }
 #pragma omp parallel for num_threads(threads) schedule(static) if (ne > 100)
   for (int k = 0; k < ne; ++k) {
     Edge& e = G.edges[k];
@@ -887,20 +985,33 @@ void BlockSolver::buildSystem(Graph& G, int threads) {  // block_solver.hpp:462-
     const bool fromNotFixed = !from.fixed, toNotFixed = !to.fixed;
     if (!fromNotFixed && !toNotFixed) continue;
     double A[36], B[36];
-    linearizeOplus(G, e, A, B);
+    if (e.numeric) {
+      std::memcpy(A, numJ.data() + (size_t)numIdx[k] * 72, sizeof A);
+      std::memcpy(B, numJ.data() + (size_t)numIdx[k] * 72 + 36, sizeof B);
+    } else {
+      linearizeOplus(G, e, A, B);
+    }
     const int D = e.D, di = from.dim, dj = to.dim;
-    // base_binary_edge.hpp:61-100 (no robust kernel)
+    // base_binary_edge.hpp:61-137: omega_r = -Omega e; robust: weightedOmega = rho' Omega, omega_r *= rho'
+    double Om[36];
+    for (int k = 0; k < D * D; ++k) Om[k] = e.info[k];
+    double w = 1.0;
+    if (e.rk) {
+      double r0;
+      robustify(e.rk, e.rkDelta, edgeChi2(e), r0, w);
+      for (int k = 0; k < D * D; ++k) Om[k] = w * e.info[k];
+    }
     double omega_r[6];
     for (int r = 0; r < D; ++r) {
       double s = 0;
       for (int c = 0; c < D; ++c) s += e.info[r * D + c] * e.err[c];
-      omega_r[r] = -s;
+      omega_r[r] = -s * w;
     }
     double AtO[6 * 6];  // di x D
     for (int i = 0; i < di; ++i)
       for (int c = 0; c < D; ++c) {
         double s = 0;
-        for (int r = 0; r < D; ++r) s += A[r * di + i] * e.info[r * D + c];
+        for (int r = 0; r < D; ++r) s += A[r * di + i] * Om[r * D + c];
         AtO[i * D + c] = s;
       }
     if (fromNotFixed) {
@@ -950,7 +1061,7 @@ void BlockSolver::buildSystem(Graph& G, int threads) {  // block_solver.hpp:462-
       for (int j = 0; j < dj; ++j)
         for (int c = 0; c < D; ++c) {
           double s = 0;
-          for (int r = 0; r < D; ++r) s += B[r * dj + j] * e.info[r * D + c];
+          for (int r = 0; r < D; ++r) s += B[r * dj + j] * Om[r * D + c];
           BtO[j * D + c] = s;
         }
       for (int cc = 0; cc < dj; ++cc)
@@ -1267,8 +1378,9 @@ int addEdgeRaw(Graph& G, int type, int id0, int id1, const double* meas, const d
   e.D = edim(type);
   e.v[0] = a->second;
   e.v[1] = b->second;
-  const int nm = type == ORACLE_E_SE3_PROJECT_XYZ ? 2 : (type == ORACLE_E_SE3_QUAT ? 7 : 3);
+  const int nm = type == ORACLE_E_SE3_PROJECT_XYZ ? 2 : (type == ORACLE_E_SE3_QUAT || type == ORACLE_E_SE3_EXPMAP ? 7 : 3);
   std::memcpy(e.meas, meas, sizeof(double) * nm);
+  e.numeric = type == ORACLE_E_SE3_EXPMAP;  // no analytic Jacobian restated: base_binary_edge.hpp:198-266
   std::memcpy(e.info, info, sizeof(double) * e.D * e.D);
   if (params && type == ORACLE_E_SE3_PROJECT_XYZ) std::memcpy(e.params, params, sizeof(double) * 4);
   setEdgeDerived(e);
@@ -1353,7 +1465,7 @@ int oracle_add_edges(OracleGraph* og, int type, int n, const int* v0, const int*
   Graph& G = og->g;
   const int D = edim(type);
   if (D < 0) return -1;
-  const int nm = type == ORACLE_E_SE3_PROJECT_XYZ ? 2 : (type == ORACLE_E_SE3_QUAT ? 7 : 3);
+  const int nm = type == ORACLE_E_SE3_PROJECT_XYZ ? 2 : (type == ORACLE_E_SE3_QUAT || type == ORACLE_E_SE3_EXPMAP ? 7 : 3);
   G.edges.reserve(G.edges.size() + n);
   for (int k = 0; k < n; ++k) {
     int r = addEdgeRaw(G, type, v0[k], v1[k], meas + (size_t)k * nm, info + (size_t)k * D * D,
@@ -1735,6 +1847,52 @@ int oracle_block_symbolic(int nblocks, int bdim, int nblk, const int* bi, const 
   out[1] = fl;
   return 0;
 }
+
+int oracle_set_robust_kernel(OracleGraph* og, int etype, int kind, double delta) {
+  for (Edge& e : og->g.edges)
+    if (e.type == etype) { e.rk = kind; e.rkDelta = delta; }
+  return 0;
+}
+int oracle_set_edge_numeric(OracleGraph* og, int n, const int* idx) {
+  for (int k = 0; k < n; ++k) {
+    if (idx[k] < 0 || idx[k] >= (int)og->g.edges.size()) return -1;
+    og->g.edges[idx[k]].numeric = true;
+  }
+  return 0;
+}
+// [e | Ji | Jj] row-major per listed edge at the current estimates (the host side of a host-Jacobian edge)
+int oracle_edge_payload(OracleGraph* og, int n, const int* idx, int numeric, double* out) {
+  Graph& G = og->g;
+  size_t o = 0;
+  for (int k = 0; k < n; ++k) {
+    if (idx[k] < 0 || idx[k] >= (int)G.edges.size()) return -1;
+    Edge& e = G.edges[idx[k]];
+    computeError(G, e);
+    double A[36], B[36];
+    if (numeric) linearizeNumeric(G, e, A, B);
+    else linearizeOplus(G, e, A, B);
+    const int di = G.verts[e.v[0]].dim, dj = G.verts[e.v[1]].dim;
+    for (int i = 0; i < e.D; ++i) out[o++] = e.err[i];
+    for (int i = 0; i < e.D * di; ++i) out[o++] = A[i];
+    for (int i = 0; i < e.D * dj; ++i) out[o++] = B[i];
+  }
+  return (int)o;
+}
+int oracle_update(OracleGraph* og, const double* x) {
+  if (!og->g.initialized) initializeOptimization(og->g);
+  update(og->g, x);
+  return 0;
+}
+int oracle_set_estimates(OracleGraph* og, int type, const double* est) {
+  const int ed = estDim(type);
+  int n = 0;
+  for (auto& v : og->g.verts)
+    if (v.type == type) setVertexEstimate(v, est + (size_t)(n++) * ed);
+  return n;
+}
+int oracle_push(OracleGraph* og) { push(og->g); return 0; }
+int oracle_pop(OracleGraph* og) { pop(og->g); return 0; }
+int oracle_discard_top(OracleGraph* og) { discardTop(og->g); return 0; }
 
 int oracle_ref_available(void) { return refcs().ok() ? 1 : 0; }
 const char* oracle_ref_path(void) { return refcs().path.c_str(); }

@@ -18,6 +18,8 @@ extern "C" {
 #define ORACLE_E_SE3_PROJECT_XYZ 1 /* v0 = point, v1 = camera; meas u v; info 2x2; params fx fy cx cy */
 #define ORACLE_E_SE3_QUAT 2        /* meas x y z qx qy qz qw; info 6x6 */
 #define ORACLE_E_SE2 3             /* meas x y theta; info 3x3 */
+#define ORACLE_E_SE3_EXPMAP 4      /* EdgeSE3Expmap (types_six_dof_expmap.h:108-127) between two VertexSE3Expmap:
+                                      meas tx ty tz qx qy qz qw; info 6x6; Jacobians always numeric here */
 
 typedef struct {
   int iteration;
@@ -93,6 +95,17 @@ int oracle_ccs_cholsol(int n, const int* Ap, const int* Ai, const double* Ax, do
 /* Symbolic stats of the CSparse block ordering (cs_amd on the block pattern when use_ref, else natural):
  * out[0] = nnz(L), out[1] = sum of squared column counts (factorization flops). */
 int oracle_block_symbolic(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int use_ref, double* out);
+/* robust kernel (G2OHIP_RK_* numbering) for every edge of a type; numeric-Jacobian flag for listed edges */
+int oracle_set_robust_kernel(OracleGraph* g, int etype, int kind, double delta);
+int oracle_set_edge_numeric(OracleGraph* g, int n, const int* idx);
+/* [e | Ji | Jj] row-major per listed edge at the current estimates; returns doubles written */
+int oracle_edge_payload(OracleGraph* g, int n, const int* idx, int numeric, double* out);
+/* SparseOptimizer::update / push / pop / discardTop (host-authoritative Solver-mode tests) */
+int oracle_update(OracleGraph* g, const double* x);
+int oracle_set_estimates(OracleGraph* g, int type, const double* est); /* insertion order of the type */
+int oracle_push(OracleGraph* g);
+int oracle_pop(OracleGraph* g);
+int oracle_discard_top(OracleGraph* g);
 int oracle_ref_available(void);
 const char* oracle_ref_path(void);
 

@@ -168,6 +168,28 @@ inline SE3Quat se3exp(const double* u) {
   return res;
 }
 
+// se3quat.h:173-209 log (se3_ops.hpp:27-47 skew / deltaR): [omega; upsilon]
+inline void se3log(const SE3Quat& a, double* res) {
+  const M3 R = qToR(a.r);
+  const double d = 0.5 * (R.m[0][0] + R.m[1][1] + R.m[2][2] - 1);
+  const V3 dR{R.m[2][1] - R.m[1][2], R.m[0][2] - R.m[2][0], R.m[1][0] - R.m[0][1]};
+  V3 omega;
+  M3 Vinv;
+  if (d > 0.99999) {
+    omega = scale(dR, 0.5);
+    const M3 Om = skew(omega);
+    Vinv = madd(madd(meye(), Om, -0.5), mmul(Om, Om), 1. / 12.);
+  } else {
+    const double theta = std::acos(d);
+    omega = scale(dR, theta / (2 * std::sqrt(1 - d * d)));
+    const M3 Om = skew(omega);
+    Vinv = madd(madd(meye(), Om, -0.5), mmul(Om, Om), (1 - theta / (2 * std::tan(theta / 2))) / (theta * theta));
+  }
+  const V3 ups = mv(Vinv, a.t);
+  res[0] = omega.x; res[1] = omega.y; res[2] = omega.z;
+  res[3] = ups.x; res[4] = ups.y; res[5] = ups.z;
+}
+
 // ---- Isometry3 (Eigen::Isometry3d as used by types/slam3d) ----
 struct Iso3 {
   M3 R = meye();

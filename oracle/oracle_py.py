@@ -69,6 +69,14 @@ def lib():
         L.oracle_edge_jacobians.argtypes = [P, I, P, P, P, P, P]
         L.oracle_ccs_cholsol.argtypes = [I, P, P, P, P, I]
         L.oracle_block_symbolic.argtypes = [I, I, I, P, P, I, P]
+        L.oracle_set_robust_kernel.argtypes = [P, I, I, D]
+        L.oracle_set_edge_numeric.argtypes = [P, I, P]
+        L.oracle_edge_payload.argtypes = [P, I, P, I, P]
+        L.oracle_update.argtypes = [P, P]
+        L.oracle_set_estimates.argtypes = [P, I, P]
+        L.oracle_push.argtypes = [P]
+        L.oracle_pop.argtypes = [P]
+        L.oracle_discard_top.argtypes = [P]
         L.oracle_ref_available.restype = I
         L.oracle_ref_path.restype = C.c_char_p
         _lib = L
@@ -149,6 +157,38 @@ class OracleGraph:
         out = np.zeros((n, EST_DIM[vtype]))
         lib().oracle_get_estimates(self.h, vtype, _p(out), None)
         return out
+
+    def set_robust_kernel(self, etype, kind, delta):
+        assert lib().oracle_set_robust_kernel(self.h, etype, kind, delta) == 0
+
+    def set_numeric(self, idx):
+        idx = np.ascontiguousarray(idx, np.int32)
+        assert lib().oracle_set_edge_numeric(self.h, len(idx), _p(idx)) == 0
+
+    def edge_payload(self, idx, size, numeric=True):
+        """[e | Ji | Jj] per listed edge (row-major) at the current estimates; `size` = total doubles."""
+        idx = np.ascontiguousarray(idx, np.int32)
+        out = np.zeros(size)
+        n = lib().oracle_edge_payload(self.h, len(idx), _p(idx), 1 if numeric else 0, _p(out))
+        assert n == size, (n, size)
+        return out
+
+    def update(self, x):
+        x = np.ascontiguousarray(x, np.float64)
+        lib().oracle_update(self.h, _p(x))
+
+    def set_estimates(self, vtype, est):
+        est = np.ascontiguousarray(est, np.float64)
+        lib().oracle_set_estimates(self.h, vtype, _p(est))
+
+    def push(self):
+        lib().oracle_push(self.h)
+
+    def pop(self):
+        lib().oracle_pop(self.h)
+
+    def discard_top(self):
+        lib().oracle_discard_top(self.h)
 
     def stage(self, lam: float, cfg: Config | None = None):
         """buildStructure/buildSystem/setLambda/solve at the current state; dense outputs."""

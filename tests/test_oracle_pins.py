@@ -177,3 +177,30 @@ def test_oracle_deterministic_single_thread(oracle):
     a.optimize(3)
     b.optimize(3)
     assert np.array_equal(a.minimal_state(), b.minimal_state())
+
+
+def test_oracle_gauss_newton_clear_and_redo(oracle):
+    """unit_test/general/clear_and_redo.cpp:38-107 through the oracle's Gauss-Newton: optimize() > 0 and chi2
+    decreasing on the 3-pose loop."""
+    import test_gpu_generic as T
+    g = oracle.OracleGraph(T._clear_and_redo_graph())
+    c0 = g.chi2()
+    n, st = g.optimize(10, oracle.make_config(threads=1, gauss_newton=True, block_ordering=False))
+    assert n > 0 and st[-1].chi2 < c0
+
+
+def test_oracle_block_symbolic_natural_order(oracle):
+    """sum c_k^2 / nnz(L) of the CSparse symbolic path against a dense boolean elimination (natural order)."""
+    rng = np.random.default_rng(4)
+    nb, bd = 30, 3
+    M = rng.random((nb, nb)) < 0.12
+    bi, bj = np.nonzero(np.triu(M | M.T, 1))
+    lnz, fl = oracle.block_symbolic(nb, bd, bi, bj, use_ref=False)
+    n = nb * bd
+    P = np.kron(np.eye(nb, dtype=bool) | M | M.T, np.ones((bd, bd), bool))
+    L = np.tril(P).copy()
+    for k in range(n):  # symbolic elimination: column k's pattern fills below
+        rows = np.nonzero(L[k + 1:, k])[0] + k + 1
+        L[np.ix_(rows, rows)] |= np.tril(np.ones((len(rows), len(rows)), bool))
+    cnt = L.sum(axis=0)
+    assert lnz == cnt.sum() and fl == float((cnt.astype(np.float64) ** 2).sum())

@@ -154,7 +154,10 @@ def _oracle_mixed(oracle, ora, hostj):
 def test_solver_mode_mixed_host_jacobian_edges(g2o_amd_mod, oracle, odometry):
     gp, ora, hostj = _mixed_ba(odometry=odometry)
     gpu = g2o_amd_mod.SparseOptimizer(0).add_problem(gp)
+    # the oracle robustifies every projection edge, host-J ones included: so does the device (robust weighting
+    # of the host-supplied error and Jacobians)
     gpu.set_robust_kernel(synth.E_SE3_PROJECT_XYZ, "Huber", 2.447)
+    gpu.set_robust_kernel(g2o_amd_mod.E_HOSTJ(2), "Huber", 2.447)
     host = _oracle_mixed(oracle, ora, hostj)
     host.set_robust_kernel(synth.E_SE3_PROJECT_XYZ, RK["Huber"], 2.447)
     st = solver_mode.solver_mode_lm(gpu, host, 5, [synth.V_SE3_EXPMAP, synth.V_XYZ], hostj)

@@ -1,0 +1,329 @@
+// Fused bundle-adjustment assembly (graphs whose only edge type is EdgeSE3ProjectXYZ, BlockSolver_6_3 + Schur):
+// BlockSolver::buildSystem (block_solver.hpp:462-521) + BaseBinaryEdge::constructQuadraticForm
+// (base_binary_edge.hpp:61-137) without the per-edge slot round trip of the generic path.
+//
+//   k_linearize_fused  edges sorted landmark-major and cut into wave chunks of whole landmarks (<= 64 edges):
+//                      one lane per edge computes J, the Hpl block A^T Omega B (stored, as in the generic path)
+//                      and its landmark-side terms A^T Omega A, A^T omega_r; the wave sums each landmark's
+//                      terms in edge order (segment heads walk their segment in LDS) and writes Hll and b_l
+//                      directly. Landmarks with more than 64 observations span several chunks: each chunk
+//                      leaves a partial that k_lm_fixup adds in chunk order.
+//   k_cam_assemble     one workgroup per camera over a camera-major copy of its observations: recomputes the
+//                      camera Jacobian (cheap) instead of reading per-edge slots, accumulates B^T Omega B and
+//                      B^T omega_r per thread in edge order and reduces them in a fixed tree: Hpp(i,i), b_i.
+// Every output has one owner and a fixed summation order: bitwise reproducible run to run (no atomics).
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "device_types.hpp"
+#include "device_util.hpp"
+#include "kernels.hpp"
+
+namespace g2ohip {
+using namespace dev;
+
+namespace {
+__device__ __forceinline__ void wsync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void copy_out(double* __restrict__ dst, const double* src, int n, int lane) {
+  int s = 0;
+  if (reinterpret_cast<uintptr_t>(dst) & 15) {
+    if (lane == 0 && n > 0) dst[0] = src[0];
+    s = 1;
+  }
+  const int n2 = (n - s) >> 1;
+  double2* d2 = reinterpret_cast<double2*>(dst + s);
+  for (int i = lane; i < n2; i += 64) d2[i] = double2{src[s + 2 * i], src[s + 2 * i + 1]};
+  if (lane == 0 && ((n - s) & 1)) dst[n - 1] = src[n - 1];
+}
+
+// error, Jacobians and the (robust-weighted) information of one edge (base_binary_edge.hpp:104-135)
+template <class F>
+__device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err, double* A, double* B, double* Om) {
+  constexpr int D = F::D;
+  F::linearize(d, e, err, A, B);
+  load_info<D>(d.info + (size_t)e * F::INFO, Om);
+  if (d.rk) {
+    double chi = 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double r = 0;
+#pragma unroll
+      for (int j = 0; j < D; ++j) r += Om[i * D + j] * err[j];
+      chi += err[i] * r;
+    }
+    double r0, r1;
+    robustify(d.rk, d.rk_delta, chi, r0, r1);
+#pragma unroll
+    for (int i = 0; i < D * D; ++i) Om[i] *= r1;
+  }
+}
+}  // namespace
+
+template <class F>
+__global__ void __launch_bounds__(256)
+    k_linearize_fused(EdgeData d, const int4* __restrict__ chunks, int nchunks, const int* __restrict__ h0,
+                      const int* __restrict__ h1, const long long* __restrict__ off_dst,
+                      const unsigned char* __restrict__ off_tr, double* __restrict__ off_base,
+                      double* __restrict__ off_slot, double* __restrict__ Hll, double* __restrict__ bvec,
+                      int num_poses, int size_poses, int lm_begin, double* __restrict__ lpart) {
+  constexpr int D = F::D, DA = F::DA, DB = F::DB;
+  constexpr int SA = DA * (DA + 1) / 2 + DA, SH = DA * DB, SM = SA > SH ? SA : SH;
+  __shared__ __attribute__((aligned(16))) double stage[4][64 * SM];
+  __shared__ int lmid[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wave = blockIdx.x * 4 + w;
+  if (wave >= nchunks) return;  // wave-uniform
+  const int4 ch = chunks[wave];
+  const int ebase = ch.x, nw = ch.y;
+  const int e = ebase + lane;
+  const bool in = lane < nw;
+  double* sw = stage[w];
+  const int pv = in ? d.v0[e] : -1;
+  const int hA = in ? h0[pv] : -1;
+  const bool nfA = hA >= 0, nfB = in && h1[d.v1[e]] >= 0;
+  double err[D], A[D * DA], B[D * DB], Om[D * D];
+  if (nfA || nfB) edge_terms<F>(d, e, err, A, B, Om);
+  double wr[D];
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    double s = 0;
+#pragma unroll
+    for (int c = 0; c < D; ++c) s += Om[r * D + c] * err[c];
+    wr[r] = -s;
+  }
+  double AtO[DA * D];
+#pragma unroll
+  for (int i = 0; i < DA; ++i)
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      double s = 0;
+#pragma unroll
+      for (int r = 0; r < D; ++r) s += A[r * DA + i] * Om[r * D + c];
+      AtO[i * D + c] = s;
+    }
+  // off-diagonal (Hpl) block, as k_linearize: a coalesced run through LDS when the wave's blocks are consecutive
+  {
+    constexpr long long SLOT_BIT = 1LL << 62;
+    const long long od_raw = (nfA && nfB) ? off_dst[e] : -1;
+    const bool in_slot = od_raw >= 0 && (od_raw & SLOT_BIT);
+    const long long od = od_raw >= 0 ? (od_raw & ~SLOT_BIT) : -1;
+    const bool tr = nfA && nfB && off_tr[e];
+    const long long od0 = __shfl(od, 0, 64);
+    const bool tr0 = __shfl((int)tr, 0, 64) != 0;
+    const bool slot0f = __shfl((int)in_slot, 0, 64) != 0;
+    const bool run = __all(!in || (od >= 0 && od0 >= 0 && od == od0 + (long long)lane * SH && tr == tr0 && in_slot == slot0f));
+    if (od >= 0) {
+      double* H = run ? sw + lane * SH : (in_slot ? off_slot : off_base) + od;
+      if (tr) {
+#pragma unroll
+        for (int i = 0; i < DA; ++i)
+#pragma unroll
+          for (int j = 0; j < DB; ++j) {
+            double s = 0;
+#pragma unroll
+            for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
+            H[i * DB + j] = s;
+          }
+      } else {
+#pragma unroll
+        for (int j = 0; j < DB; ++j)
+#pragma unroll
+          for (int i = 0; i < DA; ++i) {
+            double s = 0;
+#pragma unroll
+            for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
+            H[j * DA + i] = s;
+          }
+      }
+    }
+    if (run) {
+      wsync();
+      copy_out((slot0f ? off_slot : off_base) + od0, sw, nw * SH, lane);
+    }
+    wsync();
+  }
+  // landmark-side terms of every lane (zeros when the landmark is fixed), then segment sums in edge order
+  {
+    double* o = sw + lane * SA;
+    int k = 0;
+#pragma unroll
+    for (int c = 0; c < DA; ++c)
+#pragma unroll
+      for (int r = 0; r <= c; ++r) {
+        double s = 0;
+#pragma unroll
+        for (int t = 0; t < D; ++t) s += AtO[r * D + t] * A[t * DA + c];
+        o[k++] = nfA ? s : 0.0;
+      }
+#pragma unroll
+    for (int i = 0; i < DA; ++i) {
+      double s = 0;
+#pragma unroll
+      for (int r = 0; r < D; ++r) s += A[r * DA + i] * wr[r];
+      o[k++] = nfA ? s : 0.0;
+    }
+    lmid[w][lane] = pv;
+  }
+  wsync();
+  const bool head = in && (lane == 0 || lmid[w][lane - 1] != pv);
+  if (head && nfA) {
+    double acc[SA];
+#pragma unroll
+    for (int k = 0; k < SA; ++k) acc[k] = sw[lane * SA + k];
+    for (int j = lane + 1; j < nw && lmid[w][j] == pv; ++j)
+#pragma unroll
+      for (int k = 0; k < SA; ++k) acc[k] += sw[j * SA + k];
+    if (ch.z < 0) {
+      double* H = Hll + (size_t)(hA - num_poses - lm_begin) * DA * DA;
+      int k = 0;
+#pragma unroll
+      for (int c = 0; c < DA; ++c)
+#pragma unroll
+        for (int r = 0; r <= c; ++r) {
+          H[c * DA + r] = acc[k];
+          H[r * DA + c] = acc[k];
+          ++k;
+        }
+      double* bb = bvec + size_poses + (size_t)(hA - num_poses) * DA;
+#pragma unroll
+      for (int i = 0; i < DA; ++i) bb[i] = acc[DA * (DA + 1) / 2 + i];
+    } else {  // one landmark of > 64 observations: this chunk's partial
+#pragma unroll
+      for (int k = 0; k < SA; ++k) lpart[(size_t)ch.z * SA + k] = acc[k];
+    }
+  }
+}
+
+// split landmarks: fix = (hessian index, first partial, count); partials added in chunk order
+__global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restrict__ fix, const double* __restrict__ lpart,
+                                                  double* __restrict__ Hll, double* __restrict__ bvec, int num_poses,
+                                                  int size_poses, int lm_begin) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nfix) return;
+  const int4 f = fix[i];
+  constexpr int SA = 9;
+  double acc[SA];
+#pragma unroll
+  for (int k = 0; k < SA; ++k) acc[k] = 0.0;
+  for (int p = f.y; p < f.y + f.z; ++p)
+#pragma unroll
+    for (int k = 0; k < SA; ++k) acc[k] += lpart[(size_t)p * SA + k];
+  double* H = Hll + (size_t)(f.x - num_poses - lm_begin) * 9;
+  int k = 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r <= c; ++r) {
+      H[c * 3 + r] = acc[k];
+      H[r * 3 + c] = acc[k];
+      ++k;
+    }
+  double* bb = bvec + size_poses + (size_t)(f.x - num_poses) * 3;
+  bb[0] = acc[6]; bb[1] = acc[7]; bb[2] = acc[8];
+}
+
+// camera-side terms: one workgroup per pose, threads stride over its observations (camera-major copy of the
+// edge data, ascending landmark-major edge order), 27 accumulators per thread, fixed-tree reduction
+template <class F>
+__global__ void __launch_bounds__(256) k_cam_assemble(EdgeData d, const int* __restrict__ cm_ptr, int npose,
+                                                      double* __restrict__ Hpp, double* __restrict__ bvec) {
+  constexpr int D = F::D, DA = F::DA, DB = F::DB;
+  constexpr int SP = DB * (DB + 1) / 2, S = SP + DB;
+  __shared__ double red[4][S];
+  const int i = xcd_item(blockIdx.x, npose);  // neighbouring cameras share landmarks: one L2
+  if (i >= npose) return;  // workgroup-uniform
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double acc[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) acc[k] = 0.0;
+  const int p1 = cm_ptr[i + 1];
+  for (int p = cm_ptr[i] + tid; p < p1; p += 256) {
+    double err[D], A[D * DA], B[D * DB], Om[D * D];
+    edge_terms<F>(d, p, err, A, B, Om);
+    double wr[D];
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      double s = 0;
+#pragma unroll
+      for (int c = 0; c < D; ++c) s += Om[r * D + c] * err[c];
+      wr[r] = -s;
+    }
+    double BtO[DB * D];
+#pragma unroll
+    for (int j = 0; j < DB; ++j)
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        double s = 0;
+#pragma unroll
+        for (int r = 0; r < D; ++r) s += B[r * DB + j] * Om[r * D + c];
+        BtO[j * D + c] = s;
+      }
+    int k = 0;
+#pragma unroll
+    for (int c = 0; c < DB; ++c)
+#pragma unroll
+      for (int r = 0; r <= c; ++r) {
+        double s = 0;
+#pragma unroll
+        for (int t = 0; t < D; ++t) s += BtO[r * D + t] * B[t * DB + c];
+        acc[k++] += s;
+      }
+#pragma unroll
+    for (int j = 0; j < DB; ++j) {
+      double s = 0;
+#pragma unroll
+      for (int r = 0; r < D; ++r) s += B[r * DB + j] * wr[r];
+      acc[k++] += s;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+    for (int k = 0; k < S; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < S; ++k) red[w][k] = acc[k];
+  __syncthreads();
+  if (tid >= S) return;
+  const double t = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  if (tid < SP) {
+    int c = 0, base = 0;
+    while (tid >= base + c + 1) base += ++c;
+    const int r = tid - base;
+    double* H = Hpp + (size_t)i * DB * DB;
+    H[c * DB + r] = t;
+    H[r * DB + c] = t;
+  } else {
+    bvec[(size_t)i * DB + tid - SP] = t;
+  }
+}
+
+namespace launch {
+void linearize_fused(const EdgeArgs& a, const int4* chunks, int nchunks, const int* h0, const int* h1,
+                     const long long* off_dst, const unsigned char* off_tr, double* off_base, double* off_slot,
+                     double* Hll, double* b, int num_poses, int size_poses, int lm_begin, double* lpart,
+                     hipStream_t s) {
+  if (nchunks <= 0) return;
+  const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
+  hipLaunchKernelGGL(k_linearize_fused<FamilyBA>, grid_for(nchunks, 4), 256, 0, s, d, chunks, nchunks, h0, h1,
+                     off_dst, off_tr, off_base, off_slot, Hll, b, num_poses, size_poses, lm_begin, lpart);
+  KERNEL_CHECK();
+}
+void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, double* b, int num_poses, int size_poses,
+              int lm_begin, hipStream_t s) {
+  if (nfix <= 0) return;
+  hipLaunchKernelGGL(k_lm_fixup, grid_for(nfix, 256), 256, 0, s, nfix, fix, lpart, Hll, b, num_poses, size_poses,
+                     lm_begin);
+  KERNEL_CHECK();
+}
+void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, hipStream_t s) {
+  if (npose <= 0) return;
+  const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
+  hipLaunchKernelGGL(k_cam_assemble<FamilyBA>, npose, 256, 0, s, d, cm_ptr, npose, Hpp, b);
+  KERNEL_CHECK();
+}
+}  // namespace launch
+}  // namespace g2ohip

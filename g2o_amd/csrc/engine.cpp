@@ -1184,6 +1184,17 @@ void Engine::setup_edges_device() {
       ne += g.ne;
     }
   }
+  // fused BA assembly: the only edge group is BA and the Schur complement is formed (G2OHIP_ASM_FUSED=0 keeps the
+  // generic slot path, for A/B checks)
+  {
+    const char* fz = getenv("G2OHIP_ASM_FUSED");
+    ba_fused = do_schur && groups.size() == 1 && groups[0].family == FAM_BA && !(fz && atoi(fz) == 0);
+  }
+  if (ba_fused) {  // landmark-major edge order (stable: per landmark, the given order)
+    EGroup& g = groups[0];
+    const HEdgeSet& es = hg.esets[g.set];
+    std::stable_sort(g.edges.begin(), g.edges.end(), [&](int a, int b) { return hidx[es.ev0[a]] < hidx[es.ev0[b]]; });
+  }
   for (EGroup& g : groups) {
     const HEdgeSet& es = hg.esets[g.set];
     const int D = g.D, nm = es.nm, gne = g.ne;
@@ -1229,6 +1240,73 @@ void Engine::setup_edges_device() {
     g.params.upload(params, stream);
     if (g.family == FAM_HOSTJ) upload_group_payload(hg, g, stream);
     else g.meas.upload(meas, stream);
+  }
+  if (ba_fused) {
+    const EGroup& g = groups[0];
+    const HEdgeSet& es = hg.esets[g.set];
+    // wave chunks of whole landmarks (<= 64 edges); a landmark with more observations gets chunks of its own
+    // whose partial sums k_lm_fixup adds
+    std::vector<int4> chunks, fix;
+    int npart = 0;
+    int cb = 0, cn = 0;
+    auto close = [&]() {
+      if (cn) chunks.push_back(int4{cb, cn, -1, 0});
+      cn = 0;
+    };
+    for (int k = 0; k < g.ne;) {
+      int k2 = k + 1;
+      while (k2 < g.ne && es.ev0[g.edges[k2]] == es.ev0[g.edges[k]]) ++k2;
+      const int len = k2 - k;
+      if (len <= 64) {
+        if (cn + len > 64) close();
+        if (!cn) cb = k;
+        cn += len;
+      } else {
+        close();
+        const int h = hidx[es.ev0[g.edges[k]]];
+        const int p0 = npart;
+        for (int a = k; a < k2; a += 64) chunks.push_back(int4{a, std::min(64, k2 - a), npart++, 0});
+        if (h >= 0) fix.push_back(int4{h, p0, npart - p0, 0});
+      }
+      k = k2;
+    }
+    close();
+    fz_nchunks = (int)chunks.size();
+    fz_nfix = (int)fix.size();
+    fz_chunks.upload(chunks.empty() ? std::vector<int4>{int4{0, 0, -1, 0}} : chunks, stream);
+    fz_fix.upload(fix.empty() ? std::vector<int4>{int4{0, 0, 0, 0}} : fix, stream);
+    fz_lpart.resize((size_t)std::max(npart, 1) * 9);
+    // camera-major copy of the observations of every free camera (edge order within a camera: landmark-major)
+    std::vector<std::vector<int>> lists(num_poses);
+    for (int k = 0; k < g.ne; ++k) {
+      const int h = hidx[es.ev1[g.edges[k]]];
+      if (h >= 0 && h < num_poses) lists[h].push_back(k);
+    }
+    std::vector<int> ptr(num_poses + 1, 0), cv0, cv1;
+    std::vector<double> cmeas, cinfo, cpar;
+    for (int i = 0; i < num_poses; ++i) {
+      ptr[i + 1] = ptr[i] + (int)lists[i].size();
+      for (int k : lists[i]) {
+        const int e = g.edges[k];
+        cv0.push_back(hg.verts[es.ev0[e]].local);
+        cv1.push_back(hg.verts[es.ev1[e]].local);
+        cmeas.push_back(es.meas[(size_t)e * 2]);
+        cmeas.push_back(es.meas[(size_t)e * 2 + 1]);
+        const double* I = es.info.data() + (size_t)e * 4;
+        cinfo.push_back(I[0]);  // packed upper, column-major: (0,0) (0,1) (1,1)
+        cinfo.push_back(I[1]);
+        cinfo.push_back(I[3]);
+        for (int j = 0; j < 4; ++j) cpar.push_back(es.params[(size_t)e * 4 + j]);
+      }
+    }
+    auto nz_i = [](std::vector<int>& v) -> std::vector<int>& { if (v.empty()) v.push_back(0); return v; };
+    auto nz_d = [](std::vector<double>& v) -> std::vector<double>& { if (v.empty()) v.assign(4, 0.0); return v; };
+    cm_ptr.upload(ptr, stream);
+    cm_v0.upload(nz_i(cv0), stream);
+    cm_v1.upload(nz_i(cv1), stream);
+    cm_meas.upload(nz_d(cmeas), stream);
+    cm_info.upload(nz_d(cinfo), stream);
+    cm_params.upload(nz_d(cpar), stream);
   }
   long long maxp = std::max<long long>(vector_size(), 1);
   long long ptot = 0;
@@ -1394,8 +1472,8 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
   db.zero(stream);
   dx.resize(std::max<long long>(n, 1));
   dx.zero(stream);
-  dslot3.resize((size_t)std::max<long long>(nslot3, 1) * 9);
-  dslot6.resize((size_t)std::max<long long>(nslot6, 1) * 27);
+  dslot3.resize((size_t)std::max<long long>(ba_fused ? 1 : nslot3, 1) * 9);  // the fused BA path needs no slots
+  dslot6.resize((size_t)std::max<long long>(ba_fused ? 1 : nslot6, 1) * 27);
   // vertex incidence lists (hessian order): code = slot index in the arena of the vertex's dimension, in
   // group / edge order (a fixed summation order)
   {
@@ -1655,6 +1733,29 @@ int Engine::build_system() {  // block_solver.hpp:462-521
   }
   ensure_device_state();
   refresh_host_payload(true);
+  if (ba_fused) {  // assembly.hip: landmark side reduced inside the linearize waves, camera side recomputed per camera
+    const EGroup& g = groups[0];
+    const int lm_begin = local_lm.empty() ? 0 : local_lm.front();
+    timer.begin("linearize", stream);
+    launch::linearize_fused(group_args(g), fz_chunks.get(), fz_nchunks, d_hidx[g.vtA].get(), d_hidx[g.vtB].get(),
+                            g.off_dst.get(), g.off_tr.get(), dH.get(), doffslot.get(), dHll.get(), db.get(), num_poses,
+                            size_poses, lm_begin, fz_lpart.get(), stream);
+    timer.end(stream);
+    for (const OffRed& R : offred)
+      launch::offblock_reduce(R.nb, R.bsz, R.ptr.get(), R.soff.get(), doffslot.get(), dH.get(), R.dst.get(), stream);
+    timer.begin("vreduce", stream);
+    EdgeArgs ca = group_args(g);
+    ca.v0 = cm_v0.get();
+    ca.v1 = cm_v1.get();
+    ca.meas = cm_meas.get();
+    ca.info = cm_info.get();
+    ca.params = cm_params.get();
+    launch::cam_assemble(ca, cm_ptr.get(), num_poses, dH.get(), db.get(), stream);
+    launch::lm_fixup(fz_nfix, fz_fix.get(), fz_lpart.get(), dHll.get(), db.get(), num_poses, size_poses, lm_begin,
+                     stream);
+    timer.end(stream);
+    return G2OHIP_OK;
+  }
   timer.begin("linearize", stream);
   for (const EGroup& g : groups)
     launch::linearize(g.family, group_args(g), g.ne, d_hidx[g.vtA].get(), d_hidx[g.vtB].get(),
@@ -2231,10 +2332,12 @@ double Engine::kernel_bytes(const std::string& name) const {
   if (name == "schur_diag") return 2 * npl * pb + local_lm.size() * 9 * 8.0 + (double)num_poses * pd * pd * 8 * 2 +
                                    size_poses * 16.0;
   if (name == "schur_dinv") return local_lm.size() * ((9 + 3) * 8.0 + (9 + 6 + 3) * 8.0);
-  if (name == "linearize") {  // BA groups: edge data read, both slots + the Hpl block written
+  if (name == "linearize") {  // BA groups: edge data read, the Hpl block written (+ both slots, generic path)
     double by = 0;
     for (const EGroup& g : groups)
-      if (g.family == FAM_BA) by += g.ne * ((2 + 3 + 4) * 8.0 + 8 + (9.0 + 27.0 + pd * ld) * 8);
+      if (g.family == FAM_BA)
+        by += g.ne * ((2 + 3 + 4) * 8.0 + 8 + (ba_fused ? 0.0 : 9.0 + 27.0) * 8 + pd * ld * 8.0) +
+              (ba_fused ? local_lm.size() * 12 * 8.0 : 0.0);
     return by;
   }
   if (name == "backsub") return local_lm.size() * (3 * 8.0 * 2 + 72) + npl * (pb + 4) + size_poses * 8.0;

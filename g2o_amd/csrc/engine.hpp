@@ -246,6 +246,14 @@ class Engine {
   DevBuf<double> doffslot;
   struct OffRed { int nb = 0, bsz = 0; DevBuf<int> ptr; DevBuf<long long> soff, dst; };
   OffRed offred[2];  // [Hpp off-diagonal blocks (pd x pd), Hpl blocks (pd x ld)]
+  // fused BA assembly (assembly.hip): graphs whose only edge group is BA in Schur mode; edges landmark-major,
+  // wave chunks of whole landmarks, camera-major copies of the edge data for the camera-side pass
+  bool ba_fused = false;
+  DevBuf<int4> fz_chunks, fz_fix;
+  int fz_nchunks = 0, fz_nfix = 0;
+  DevBuf<double> fz_lpart;
+  DevBuf<int> cm_ptr, cm_v0, cm_v1;
+  DevBuf<double> cm_meas, cm_info, cm_params;
   // hessian storage
   int nHpp = 0, nHpl = 0;
   DevBuf<double> dH;             // [Hpp blocks | Hpl blocks]

@@ -33,6 +33,14 @@ void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, 
                    double* b, const int* boff, hipStream_t s);
 void offblock_reduce(int nb, int bsz, const int* ptr, const long long* soff, const double* slots, double* out,
                      const long long* dst, hipStream_t s);
+// fused BA assembly (assembly.hip): chunks = (first edge, edges, partial slot or -1, 0) of whole landmarks per wave
+void linearize_fused(const EdgeArgs& a, const int4* chunks, int nchunks, const int* h0, const int* h1,
+                     const long long* off_dst, const unsigned char* off_tr, double* off_base, double* off_slot,
+                     double* Hll, double* b, int num_poses, int size_poses, int lm_begin, double* lpart,
+                     hipStream_t s);
+void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, double* b, int num_poses, int size_poses,
+              int lm_begin, hipStream_t s);
+void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, hipStream_t s);
 void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
                 double* Ufac, double* cl_all, int* fail, hipStream_t s);
 // diagonal blocks + bschur (and G per observation): one workgroup per camera row over its observations (CSR rptr/robs)

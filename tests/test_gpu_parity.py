@@ -315,3 +315,13 @@ def test_linear_residual_small(g2o_amd_mod):
         assert opt.solve()
         assert opt.linear_residual() <= 1e-12
         opt.restore_diagonal()
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_ba_assembly_paths(g2o_amd_mod, oracle, monkeypatch, fused):
+    """BA assembly: the fused path (assembly.hip: landmark sums inside the linearize waves, camera blocks from a
+    camera-major pass; landmarks with > 64 observations split over chunks + fix-up) and the generic per-edge
+    slot path (G2OHIP_ASM_FUSED=0) both follow the oracle; points seen by 80 cameras exercise the split chunks."""
+    monkeypatch.setenv("G2OHIP_ASM_FUSED", fused)
+    for prob in (synth.ba(num_cameras=100, num_points=60, obs_per_point=80, window=100), _ragged_ba(seed=5)):
+        _check(*_run_both(g2o_amd_mod, oracle, prob, 4))

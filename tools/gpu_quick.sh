@@ -1,16 +1,12 @@
 #!/bin/bash
-# Quick GPU iteration: parity probe -> GPU test suite -> profiled C4 bench (kernel trace + stats).
+# quick GPU check after a kernel change: the -m gpu suite (minus PCG) + a C4 bench line (no CPU baseline)
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out
-mkdir -p $O
-timeout -k 10 300 python -u gpurun_probe.py > $O/probe.log 2>&1 || { echo PROBE_FAIL; tail -20 $O/probe.log; exit 1; }
-echo PROBE_OK
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 $O/pytest_gpu.log; exit 1; }
-echo PYTEST_OK
-rm -rf $O/prof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-posegraph ${BENCH_ARGS} > $O/bench_prof.json 2> $O/bench_prof.err || { echo PROF_FAIL; tail -20 $O/bench_prof.err; exit 1; }
-echo PROF_OK
-python -c "
-import json; d=json.load(open('$O/bench_prof.json')); print('it/s', round(d['value'],1), 'ms/lin', round(d['ms_per_linear_solve'],3)); print({k: round(v,4) for k,v in d['stages_ms_avg'].items()}); r=d['roofline']; print('roofline', r['kernel'], round(r['achieved'],1), round(r['frac'],4))"
-python tools_profsum.py $O/prof/run_kernel_stats.csv 14
+TAG=${1:-q}
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
+tail -2 gpurun_out/${TAG}_pytest.log
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-posegraph > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo BENCH_FAIL; tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/${TAG}_bench.json')); print('C4', round(d['value'],1), 'LM it/s', {k: round(v*1e3,1) for k,v in d['stages_ms_avg'].items()})"
+timeout -k 10 300 python bench.py --config C5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_bench_c5.json 2> gpurun_out/${TAG}_bench_c5.err || { echo BENCH_C5_FAIL; tail -20 gpurun_out/${TAG}_bench_c5.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/${TAG}_bench_c5.json')); print('C5', round(d['value'],1), 'LM it/s', {k: round(v*1e3,1) for k,v in d['stages_ms_avg'].items()})"

@@ -54,7 +54,7 @@ EXPORTS = [
     "g2ohip_graph_create", "g2ohip_graph_destroy", "g2ohip_add_vertices", "g2ohip_add_edges",
     "g2ohip_load_g2o", "g2ohip_save_g2o", "g2ohip_num_vertices", "g2ohip_num_edges",
     "g2ohip_set_robust_kernel", "g2ohip_set_host_jacobians", "g2ohip_set_host_edge_callback",
-    "g2ohip_solver_diag_absmax",
+    "g2ohip_solver_diag_absmax", "g2ohip_solver_set_eta", "g2ohip_solver_linear_iterations",
     "g2ohip_get_estimates", "g2ohip_set_estimates", "g2ohip_minimal_state", "g2ohip_set_algorithm",
     "g2ohip_initialize", "g2ohip_chi2", "g2ohip_optimize", "g2ohip_optimize_step",
     "g2ohip_solver_build_structure", "g2ohip_solver_build_system", "g2ohip_solver_set_lambda",
@@ -98,6 +98,8 @@ def lib() -> C.CDLL:
         "g2ohip_set_host_jacobians": ([P, I, P], I),
         "g2ohip_set_host_edge_callback": ([P, HOST_EDGE_FN, P], I),
         "g2ohip_solver_diag_absmax": ([P, P], I),
+        "g2ohip_solver_set_eta": ([P, D], I),
+        "g2ohip_solver_linear_iterations": ([P], I),
         "g2ohip_get_estimates": ([P, I, P, P], I),
         "g2ohip_set_estimates": ([P, I, P], I),
         "g2ohip_minimal_state": ([P, P], I),
@@ -341,6 +343,13 @@ class SparseOptimizer:
         out = np.zeros_like(src)
         _check(lib().g2ohip_solver_multiply_hessian(self.h, _p(out), _p(src)), "multiplyHessian")
         return out
+
+    def set_eta(self, eta: float):
+        """Solver::setEta: forcing term of the lm_pcg6_3_eigen CGLS (default 0.1)."""
+        _check(lib().g2ohip_solver_set_eta(self.h, float(eta)), "set_eta")
+
+    def linear_iterations(self) -> int:
+        return int(lib().g2ohip_solver_linear_iterations(self.h))
 
     def diag_absmax(self) -> float:
         """max |diag| of the vertex Hessians (computeLambdaInit's input) after buildSystem."""

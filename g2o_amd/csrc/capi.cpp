@@ -37,6 +37,8 @@ int algorithm_known(const std::string& n) {
   // g2o/solvers/pcg registry (solver_pcg.cpp:91-98): pcg (variable block size), pcg3_2, pcg6_3, pcg7_3.
   // Block-Jacobi PCG on the device replaces the Cholesky; pose blocks of 3 or 6 only.
   if (rest == "pcg" || rest == "pcg6_3") return 1;
+  // fork solvers/eigen/solver_eigen.cpp:80,126: JacobiSolver_6_3 + LinearSolverPCGEigen (matrix-free CGLS)
+  if (m == "lm_" && rest == "pcg6_3_eigen") return 1;
   if (rest == "pcg3_2" || rest == "pcg7_3") {
     g_err = n + ": fixed block sizes 3_2 / 7_3 are not supported by the device PCG (pose blocks of 3 or 6 only; "
                 "use " + m + "pcg)";
@@ -111,6 +113,12 @@ int g2ohip_set_host_edge_callback(g2ohip_graph* g, g2ohip_host_edge_fn fn, void*
   if (!g) return G2OHIP_ERR_ARG;
   return g->e->set_host_callback(fn, user);
 }
+int g2ohip_solver_set_eta(g2ohip_graph* g, double eta) {
+  if (!g || !(eta > 0)) return G2OHIP_ERR_ARG;
+  g->e->cgls.eta = eta;
+  return G2OHIP_OK;
+}
+int g2ohip_solver_linear_iterations(g2ohip_graph* g) { return g ? g->e->cgls.last_iterations : G2OHIP_ERR_ARG; }
 int g2ohip_solver_diag_absmax(g2ohip_graph* g, double* out) {
   if (!g || !out) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->diag_absmax(out); });

@@ -1284,9 +1284,11 @@ void Engine::setup_edges_device() {
     }
     std::vector<int> ptr(num_poses + 1, 0), cv0, cv1;
     std::vector<double> cmeas, cinfo, cpar;
+    cm_e_h.clear();
     for (int i = 0; i < num_poses; ++i) {
       ptr[i + 1] = ptr[i] + (int)lists[i].size();
       for (int k : lists[i]) {
+        cm_e_h.push_back(k);
         const int e = g.edges[k];
         cv0.push_back(hg.verts[es.ev0[e]].local);
         cv1.push_back(hg.verts[es.ev1[e]].local);
@@ -1301,6 +1303,16 @@ void Engine::setup_edges_device() {
     }
     auto nz_i = [](std::vector<int>& v) -> std::vector<int>& { if (v.empty()) v.push_back(0); return v; };
     auto nz_d = [](std::vector<double>& v) -> std::vector<double>& { if (v.empty()) v.assign(4, 0.0); return v; };
+    cm_ptr_h = ptr;
+    {  // per local landmark its edge range in the (landmark-major) group order
+      const int lm_b = local_lm.empty() ? 0 : local_lm.front();
+      lm_eptr_h.assign(local_lm.size() + 1, 0);
+      for (int k = 0; k < g.ne; ++k) {
+        const int h = hidx[es.ev0[g.edges[k]]];
+        if (h >= num_poses) lm_eptr_h[h - num_poses - lm_b + 1]++;
+      }
+      for (size_t l = 0; l < local_lm.size(); ++l) lm_eptr_h[l + 1] += lm_eptr_h[l];
+    }
     cm_ptr.upload(ptr, stream);
     cm_v0.upload(nz_i(cv0), stream);
     cm_v1.upload(nz_i(cv1), stream);
@@ -1677,8 +1689,22 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     dG.resize(std::max<long long>((long long)nHpl * 18, 1));  // G = Hpl U^-T per observation (6x3)
     dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
-    if (use_pcg()) pcg.setup(num_poses, pd, s_bi, s_bj, stream);
-    else chol.setup(num_poses, pd, s_bi, s_bj, stream);
+    if (use_cgls()) {  // the fork's JacobiSolver_6_3: CGLS on J, no reduced system to factor
+      if (!ba_fused || nranks > 1) throw DeviceError("lm_pcg6_3_eigen needs a single-GPU graph of BA edges only");
+      const EGroup& g = groups[0];
+      const HEdgeSet& es = hg.esets[g.set];
+      std::vector<int> ecam(g.ne), ept(g.ne);
+      for (int k = 0; k < g.ne; ++k) {
+        const int hc = hidx[es.ev1[g.edges[k]]], hl = hidx[es.ev0[g.edges[k]]];
+        ecam[k] = hc >= 0 && hc < num_poses ? hc : -1;
+        ept[k] = hl >= num_poses ? hl - num_poses - lm_begin : -1;
+      }
+      cgls.setup(num_poses, nLloc, g.ne, lm_eptr_h, cm_ptr_h, cm_e_h, ecam, ept, stream);
+    } else if (use_pcg()) {
+      pcg.setup(num_poses, pd, s_bi, s_bj, stream);
+    } else {
+      chol.setup(num_poses, pd, s_bi, s_bj, stream);
+    }
   } else if (use_pcg()) {
     pcg.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
   } else {
@@ -1754,6 +1780,11 @@ int Engine::build_system() {  // block_solver.hpp:462-521
     launch::lm_fixup(fz_nfix, fz_fix.get(), fz_lpart.get(), dHll.get(), db.get(), num_poses, size_poses, lm_begin,
                      stream);
     timer.end(stream);
+    if (use_cgls()) {  // JacobiSolver::buildSystem's J (jacobi_solver.hpp:479-700)
+      timer.begin("cgls_jacobian", stream);
+      cgls.build(group_args(g), d_hidx[g.vtA].get(), d_hidx[g.vtB].get(), stream);
+      timer.end(stream);
+    }
     return G2OHIP_OK;
   }
   timer.begin("linearize", stream);
@@ -1813,6 +1844,15 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
     timer.begin("chol_solve", stream);
     chol.solve(dx.get(), stream);
     timer.end(stream);
+    if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
+    return;
+  }
+  if (use_cgls()) {  // LinearSolverPCGEigen::solve on J (x for poses and landmarks at once, no Schur)
+    if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
+    timer.begin("cgls", stream);
+    cgls.solve(dscal.get(), db.get(), dx.get(), stream);
+    timer.end(stream);
+    if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
     if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
     return;
   }
@@ -1946,6 +1986,13 @@ int Engine::diag_absmax(double* out) {  // the vertex Hessian diagonal computeLa
 double Engine::lambda_init() { return 1e-5 * max_diagonal(); }  // optimization_algorithm_levenberg.cpp:152-175
 
 double Engine::max_diagonal() {
+  if (use_cgls()) {  // JacobiSolver leaves the vertex Hessians empty: max |diag(J^T J)| (:165-172)
+    cgls.diag_max(dpartial.get(), dscal.get() + 3, stream);
+    double m = 0;
+    HIP_CHECK(hipMemcpyAsync(&m, dscal.get() + 3, sizeof(double), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    return m;
+  }
   // Hpp diagonal blocks are partial per rank when sharded: reduce them first (copy)
   const double* Hp = dH.get();
   DevBuf<double> tmp;

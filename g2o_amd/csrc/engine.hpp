@@ -12,6 +12,7 @@
 #include "comm.hpp"
 #include "common.hpp"
 #include "kernels.hpp"
+#include "cgls.hpp"
 #include "pcg.hpp"
 #include "symbolic.hpp"
 
@@ -254,6 +255,7 @@ class Engine {
   DevBuf<double> fz_lpart;
   DevBuf<int> cm_ptr, cm_v0, cm_v1;
   DevBuf<double> cm_meas, cm_info, cm_params;
+  std::vector<int> cm_ptr_h, cm_e_h, lm_eptr_h;  // host copies for the CGLS setup (camera lists, landmark edge ranges)
   // hessian storage
   int nHpp = 0, nHpl = 0;
   DevBuf<double> dH;             // [Hpp blocks | Hpl blocks]
@@ -280,7 +282,11 @@ class Engine {
   BlockSymv symv_hpp, symv_s;
   DevBuf<double> dtmp;
   DevicePCG pcg;  // {lm,gn}_pcg* algorithms (linear_solver_pcg.hpp)
-  bool use_pcg() const { return algorithm.find("_pcg") != std::string::npos; }
+  bool use_cgls() const { return algorithm.size() > 12 && algorithm.compare(algorithm.size() - 12, 12, "pcg6_3_eigen") == 0; }
+  bool use_pcg() const { return algorithm.find("_pcg") != std::string::npos && !use_cgls(); }
+ public:
+  DeviceCGLS cgls;  // lm_pcg6_3_eigen: the fork's matrix-free CGLS (JacobiSolver_6_3 + LinearSolverPCGEigen)
+ private:
   // scalars: [0] lambda, [1] chi2, [2] scale, [3] maxdiag
   DevBuf<double> dscal;
   DevBuf<double> dpartial;

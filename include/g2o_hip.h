@@ -11,7 +11,9 @@
  *        + SparseOptimizer::optimize (core/sparse_optimizer.cpp:374-439) ... g2ohip_optimize
  *   OptimizableGraph::load / save (core/optimizable_graph.cpp:397-679) .. g2ohip_load_g2o / g2ohip_save_g2o
  *   OptimizationAlgorithmFactory::construct (core/optimization_algorithm_factory.cpp:84-93)
- *        .. g2ohip_set_algorithm("lm_hip_fix6_3" | "lm_hip_fix3_3" | "lm_hip_fix6_6" | "lm_hip_var" | "gn_hip_*")
+ *        .. g2ohip_set_algorithm("lm_hip_fix6_3" | "lm_hip_fix3_3" | "lm_hip_fix6_6" | "lm_hip_var" | "gn_hip_*"
+ *           | "{lm,gn}_pcg" | "{lm,gn}_pcg6_3" (block-Jacobi PCG, solver_pcg.cpp:91-98)
+ *           | "lm_pcg6_3_eigen" (fork JacobiSolver_6_3 + LinearSolverPCGEigen CGLS, solver_eigen.cpp:80,126))
  *   G2OBatchStatistics (core/batch_stats.h:42-72) .. g2ohip_batch_stats
  *
  * Plain pointers and sizes only; no torch / HIP types cross the boundary.
@@ -156,6 +158,11 @@ int g2ohip_solver_multiply_hessian(g2ohip_graph* g, double* dest, const double* 
  * OptimizationAlgorithmLevenberg::computeLambdaInit reads through the vertices' mapped Hessians
  * (optimization_algorithm_levenberg.cpp:152-175) in the host-authoritative Solver mode. */
 int g2ohip_solver_diag_absmax(g2ohip_graph* g, double* out);
+/* Solver::setEta (core/solver.h:137, jacobi_solver.h:142): forcing term of the lm_pcg6_3_eigen CGLS (stop when
+ * s.s < eta s0.s0, linear_solver_pcg_eigen.h:170-176); default 0.1 (core/linear_solver.h:66). */
+int g2ohip_solver_set_eta(g2ohip_graph* g, double eta);
+/* G2OBatchStatistics::iterationsLinearSolver of the last lm_pcg6_3_eigen solve */
+int g2ohip_solver_linear_iterations(g2ohip_graph* g);
 /* ||(A + lambda I) x - b|| / ||b|| of the last Solver::solve, evaluated on the device (A = the Schur complement
  * with Schur, else Hpp): a size-independent check of the factorization at any problem size. */
 int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel);

@@ -58,9 +58,9 @@ EXPORTS = [
     "g2ohip_get_estimates", "g2ohip_set_estimates", "g2ohip_minimal_state", "g2ohip_set_algorithm",
     "g2ohip_initialize", "g2ohip_chi2", "g2ohip_optimize", "g2ohip_optimize_step",
     "g2ohip_solver_build_structure", "g2ohip_solver_build_system", "g2ohip_solver_set_lambda",
-    "g2ohip_solver_restore_diagonal", "g2ohip_solver_solve", "g2ohip_solver_vector_size",
+    "g2ohip_solver_restore_diagonal", "g2ohip_solver_solve", "g2ohip_solver_vector_size", "g2ohip_solver_block_dims",
     "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_solver_multiply_hessian",
-    "g2ohip_solver_linear_residual", "g2ohip_solver_factor_info", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
+    "g2ohip_solver_linear_residual", "g2ohip_solver_factor_info", "g2ohip_solver_compute_marginals", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
     "g2ohip_discard_top", "g2ohip_stage", "g2ohip_linear_solve_ccs", "g2ohip_comm_unique_id",
     "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
     "g2ohip_kernel_timing_only", "g2ohip_set_stats_level", "g2ohip_kernel_ms",
@@ -114,11 +114,13 @@ def lib() -> C.CDLL:
         "g2ohip_solver_restore_diagonal": ([P], I),
         "g2ohip_solver_solve": ([P], I),
         "g2ohip_solver_vector_size": ([P], LL),
+        "g2ohip_solver_block_dims": ([P, P], I),
         "g2ohip_solver_get_x": ([P, P], I),
         "g2ohip_solver_get_b": ([P, P], I),
         "g2ohip_solver_multiply_hessian": ([P, P, P], I),
         "g2ohip_solver_linear_residual": ([P, P], I),
         "g2ohip_solver_factor_info": ([P, P, I], I),
+        "g2ohip_solver_compute_marginals": ([P, I, P, P, P], I),
         "g2ohip_update": ([P, P], I),
         "g2ohip_push": ([P], I),
         "g2ohip_pop": ([P], I),
@@ -327,6 +329,12 @@ class SparseOptimizer:
     def vector_size(self) -> int:
         return int(lib().g2ohip_solver_vector_size(self.h))
 
+    def block_dims(self):
+        """[PoseDim, LandmarkDim, pose blocks, landmark blocks] of the built structure."""
+        d = np.zeros(4, np.int32)
+        _check(lib().g2ohip_solver_block_dims(self.h, _p(d)), "block_dims")
+        return [int(v) for v in d]
+
     def x(self) -> np.ndarray:
         out = np.zeros(self.vector_size())
         _check(lib().g2ohip_solver_get_x(self.h, _p(out)), "x")
@@ -362,6 +370,20 @@ class SparseOptimizer:
         r = np.zeros(1)
         _check(lib().g2ohip_solver_linear_residual(self.h, _p(r)), "linear_residual")
         return float(r[0])
+
+    def compute_marginals(self, block_indices):
+        """SparseOptimizer::computeMarginals(spinv, blockIndices) (sparse_optimizer.h:129): {(r, c): pd x pd block
+        of Hpp^-1} for the Hessian block index pairs, or None when the factorization fails (the reference's false)."""
+        pairs = [(int(r), int(c)) for r, c in block_indices]
+        rows = np.ascontiguousarray([p[0] for p in pairs] or [0], np.int32)
+        cols = np.ascontiguousarray([p[1] for p in pairs] or [0], np.int32)
+        pd = self.block_dims()[0]
+        out = np.zeros(max(len(pairs), 1) * pd * pd)
+        rc = lib().g2ohip_solver_compute_marginals(self.h, len(pairs), _p(rows), _p(cols), _p(out))
+        _check(min(rc, 0), "computeMarginals")
+        if rc == 0:
+            return None
+        return {p: out[k * pd * pd:(k + 1) * pd * pd].reshape(pd, pd).T.copy() for k, p in enumerate(pairs)}
 
     FACTOR_INFO_KEYS = ("n", "nnzL", "flops", "supernodes", "levels", "max_front", "blocked_fronts",
                         "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds")

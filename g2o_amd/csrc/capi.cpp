@@ -189,6 +189,10 @@ int g2ohip_solver_solve(g2ohip_graph* g) {
   return guarded([&] { return g->e->solve_sync(); });
 }
 long long g2ohip_solver_vector_size(g2ohip_graph* g) { return g ? g->e->vector_size() : G2OHIP_ERR_ARG; }
+int g2ohip_solver_block_dims(g2ohip_graph* g, int* dims) {
+  if (!g || !dims) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->block_dims(dims); });
+}
 int g2ohip_solver_get_x(g2ohip_graph* g, double* x) {
   if (!g || !x) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->get_x(x); });
@@ -208,6 +212,11 @@ int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel) {
 int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n) {
   if (!g || !out || n < 0) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->factor_info(out, n); });
+}
+int g2ohip_solver_compute_marginals(g2ohip_graph* g, int nblocks, const int* block_rows, const int* block_cols,
+                                    double* out) {
+  if (!g) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->compute_marginals(nblocks, block_rows, block_cols, out); });
 }
 int g2ohip_update(g2ohip_graph* g, const double* x_host) {
   if (!g) return G2OHIP_ERR_ARG;

@@ -348,6 +348,14 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     ll.insert(ll.end(), lv.begin(), lv.end());
     level_off.push_back((int)ll.size());
   }
+  lfronts.upload(ll.empty() ? std::vector<int>{0} : ll, s);
+  {
+    std::vector<long long> wo(std::max<size_t>(sym.sn.size(), 1), 0);
+    long long w = 0;
+    for (size_t k = 0; k < sym.sn.size(); ++k) { wo[k] = w; w += (long long)sym.sn[k].nr * 64; }
+    wpool = std::max(w, 1LL);
+    woff.upload(wo, s);
+  }
   // work lists per level: extend-add, first diagonal block, one step per 32-wide panel,
   // contribution blocks
   {
@@ -612,6 +620,16 @@ void DeviceCholesky::solve(double* x, hipStream_t s) {
     }
   }
   launch::chol_ipermute(sym.n, perm.get(), x_p.get(), x, s);
+}
+
+void DeviceCholesky::solve_multi(double* Y, double* W, double* T, int K, hipStream_t s) {
+  if (K < 1 || K > 64) throw std::runtime_error("solve_multi: K must be in [1, 64]");
+  for (size_t l = 0; l + 1 < level_off.size(); ++l)
+    launch::marg_forward(level_off[l + 1] - level_off[l], lfronts.get() + level_off[l], fd.get(), children.get(),
+                         relmap.get(), lbuf.get(), linv.get(), woff.get(), W, Y, T, sym.n, K, s);
+  for (size_t l = level_off.size() - 1; l-- > 0;)
+    launch::marg_backward(level_off[l + 1] - level_off[l], lfronts.get() + level_off[l], fd.get(), rows.get(),
+                          lbuf.get(), linv.get(), Y, T, sym.n, K, s);
 }
 
 // ------------------------------------------------------------------ Engine: graph
@@ -2355,6 +2373,78 @@ int Engine::linear_residual(double* out) {
   HIP_CHECK(hipStreamSynchronize(stream));
   *out = h[1] > 0 ? std::sqrt(h[0] / h[1]) : std::sqrt(h[0]);
   return G2OHIP_OK;
+}
+
+int Engine::compute_marginals(int nblocks, const int* brow, const int* bcol, double* out) {
+  if (!structure_built) return G2OHIP_ERR_STATE;
+  if (nranks > 1) return G2OHIP_ERR_UNSUPPORTED;  // Hpp diagonal blocks are partial per landmark shard
+  if (nblocks < 0 || (nblocks && (!brow || !bcol || !out))) return G2OHIP_ERR_ARG;
+  for (int k = 0; k < nblocks; ++k)
+    if (brow[k] < 0 || brow[k] >= num_poses || bcol[k] < 0 || bcol[k] >= num_poses) return G2OHIP_ERR_ARG;
+  // the LM's own factor is reused where it factors Hpp; otherwise (Schur complement, iterative solvers) a
+  // factor of Hpp's pattern is set up once
+  const bool own = !do_schur && !use_pcg() && !use_cgls();
+  DeviceCholesky& C = own ? chol : marg_chol;
+  if (!own && !marg_ready) {
+    marg_chol.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
+    marg_ready = true;
+  }
+  const int n = size_poses, K = 64 / pd * pd, bpb = K / pd;
+  dmarg.resize((size_t)2 * n * K + (size_t)C.wpool + n);
+  double* Y = dmarg.get();
+  double* T = Y + (size_t)n * K;
+  double* W = T + (size_t)n * K;
+  double* zrhs = W + C.wpool;
+  dmarg_fail.resize(1);
+  dmarg_fail.zero(stream);
+  HIP_CHECK(hipMemsetAsync(zrhs, 0, sizeof(double) * n, stream));
+  // Hpp + 0 I (dscal[5] holds 0): the reference factors Hpp as buildSystem left it, lambda removed
+  C.factor(dH.get(), dscal.get() + 5, zrhs, dmarg_fail.get(), stream);
+  int fail = 0;
+  HIP_CHECK(hipMemcpyAsync(&fail, dmarg_fail.get(), sizeof fail, hipMemcpyDeviceToHost, stream));
+  HIP_CHECK(hipStreamSynchronize(stream));
+  if (fail) return 0;
+  // distinct block columns, batched K / pd per multi-right-hand-side solve
+  std::vector<int> ucol(bcol, bcol + nblocks);
+  std::sort(ucol.begin(), ucol.end());
+  ucol.erase(std::unique(ucol.begin(), ucol.end()), ucol.end());
+  const std::vector<int>& pinv = C.sym.pinv;
+  const size_t bsz = (size_t)pd * pd;
+  std::vector<int> prow(K);
+  std::vector<long long> idx;
+  std::vector<double> vals;
+  for (size_t b0 = 0; b0 < ucol.size(); b0 += bpb) {
+    const int nb = (int)std::min<size_t>(bpb, ucol.size() - b0), k = nb * pd;
+    for (int c = 0; c < nb; ++c)
+      for (int j = 0; j < pd; ++j) prow[c * pd + j] = pinv[ucol[b0 + c] * pd + j];
+    HIP_CHECK(hipMemsetAsync(Y, 0, sizeof(double) * n * k, stream));
+    dmarg_idx.resize(std::max<size_t>((size_t)k, bsz * nblocks));
+    HIP_CHECK(hipMemcpyAsync(dmarg_idx.get(), prow.data(), sizeof(int) * k, hipMemcpyHostToDevice, stream));
+    launch::marg_unit(k, reinterpret_cast<const int*>(dmarg_idx.get()), Y, n, stream);
+    C.solve_multi(Y, W, T, k, stream);
+    // entry (i, j) of block (r, c): Y(pinv[r pd + i], column of c's j)
+    idx.clear();
+    std::vector<int> which;
+    for (int q = 0; q < nblocks; ++q) {
+      const size_t pos = std::lower_bound(ucol.begin() + b0, ucol.begin() + b0 + nb, bcol[q]) - ucol.begin();
+      if (pos >= b0 + nb || ucol[pos] != bcol[q]) continue;
+      which.push_back(q);
+      const int c = (int)(pos - b0);
+      for (int j = 0; j < pd; ++j)
+        for (int i = 0; i < pd; ++i) idx.push_back((long long)(c * pd + j) * n + pinv[brow[q] * pd + i]);
+    }
+    if (idx.empty()) continue;
+    HIP_CHECK(hipStreamSynchronize(stream));  // dmarg_idx held the unit rows until marg_unit ran
+    HIP_CHECK(hipMemcpyAsync(dmarg_idx.get(), idx.data(), sizeof(long long) * idx.size(), hipMemcpyHostToDevice, stream));
+    dmarg_out.resize(idx.size());
+    launch::marg_gather((long long)idx.size(), dmarg_idx.get(), Y, dmarg_out.get(), stream);
+    vals.resize(idx.size());
+    HIP_CHECK(hipMemcpyAsync(vals.data(), dmarg_out.get(), sizeof(double) * idx.size(), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    for (size_t w = 0; w < which.size(); ++w)
+      std::copy(vals.begin() + w * bsz, vals.begin() + (w + 1) * bsz, out + (size_t)which[w] * bsz);
+  }
+  return 1;
 }
 
 int Engine::factor_info(double* out, int n) {

@@ -116,6 +116,12 @@ struct DeviceCholesky {
   void factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s);
   // backward solve x = P^T L^-T y
   void solve(double* x, hipStream_t s);
+  // multi-right-hand-side solve with the factor in lbuf/linv (marginals.hip): Y (n x K, column-major, rows in
+  // the permuted order) <- L^-T L^-1 Y; W (wpool x 64) and T (n x K) scratch, K <= 64
+  DevBuf<int> lfronts;          // fronts in level order (level_off ranges)
+  DevBuf<long long> woff;       // per front: offset of its below-diagonal right-hand-side block in W
+  long long wpool = 0;
+  void solve_multi(double* Y, double* W, double* T, int K, hipStream_t s);
 };
 
 // y = (A + lam I) x for a symmetric block matrix held as upper blocks (multiplyHessian, residual checks)
@@ -202,6 +208,15 @@ class Engine {
   // [n, nnz(L), flops, supernodes, levels, max front, blocked fronts, in-place levels, pre-scattered levels,
   //  k_syrk launches, backward big-panel rounds]
   int factor_info(double* out, int n);
+  int block_dims(int* dims) const {
+    if (!structure_built) return G2OHIP_ERR_STATE;
+    dims[0] = pd; dims[1] = ld; dims[2] = num_poses; dims[3] = num_landmarks;
+    return G2OHIP_OK;
+  }
+  // Solver::computeMarginals (block_solver.hpp:451 -> solvePattern, linear_solver_csparse.h:190-225): the pd x pd
+  // blocks (rows[k], cols[k]) of Hpp^-1 (Hpp of the last buildSystem, no lambda), column-major, into out;
+  // 1 done, 0 Hpp not positive definite (the reference's bool), < 0 a status code
+  int compute_marginals(int nblocks, const int* rows, const int* cols, double* out);
 
   // comm
   int set_comm(const unsigned char* uid, int rank, int nranks);
@@ -279,6 +294,11 @@ class Engine {
   DevBuf<int> sch_rptr, sch_robs, sch_obs_lm, sch_sdiag;
   std::vector<int> s_bi, s_bj, hpp_bi, hpp_bj;
   DeviceCholesky chol;
+  DeviceCholesky marg_chol;  // factor of Hpp for computeMarginals where `chol` factors S (or is not set up)
+  bool marg_ready = false;
+  DevBuf<double> dmarg, dmarg_out;  // [Y | T | W | zero rhs], gathered blocks
+  DevBuf<int> dmarg_fail;
+  DevBuf<long long> dmarg_idx;
   BlockSymv symv_hpp, symv_s;
   DevBuf<double> dtmp;
   DevicePCG pcg;  // {lm,gn}_pcg* algorithms (linear_solver_pcg.hpp)

@@ -141,5 +141,13 @@ void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double
                 hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only
 constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 16, CHOL_BW = 4;
+// computeMarginals multi-right-hand-side solves (marginals.hip): one launch per tree level, one workgroup per front
+void marg_forward(int nf, const int* lfronts, const FrontDesc* fd, const int* children, const int* relmap,
+                  const double* lbuf, const double* linv, const long long* woff, double* W, double* Y, double* T, int n,
+                  int K, hipStream_t s);
+void marg_backward(int nf, const int* lfronts, const FrontDesc* fd, const int* rows, const double* lbuf,
+                   const double* linv, double* Y, double* T, int n, int K, hipStream_t s);
+void marg_unit(int K, const int* prow, double* Y, int n, hipStream_t s);
+void marg_gather(long long cnt, const long long* idx, const double* Y, double* out, hipStream_t s);
 }  // namespace launch
 }  // namespace g2ohip

@@ -148,6 +148,9 @@ int g2ohip_solver_set_lambda(g2ohip_graph* g, double lambda, int backup); /* Sol
 int g2ohip_solver_restore_diagonal(g2ohip_graph* g);            /* Solver::restoreDiagonal */
 int g2ohip_solver_solve(g2ohip_graph* g);                       /* Solver::solve: 1 ok, 0 not PD, <0 error */
 long long g2ohip_solver_vector_size(g2ohip_graph* g);           /* Solver::vectorSize */
+/* BlockSolver<p, l> traits after build_structure: dims = [PoseDim, LandmarkDim, pose blocks, landmark blocks]
+ * (block_solver.h:44-60; Solver::additionalVectorSpace etc. not needed) */
+int g2ohip_solver_block_dims(g2ohip_graph* g, int* dims);
 int g2ohip_solver_get_x(g2ohip_graph* g, double* x);            /* Solver::x() (host copy) */
 int g2ohip_solver_get_b(g2ohip_graph* g, double* b);            /* Solver::b() (host copy) */
 /* BlockSolverBase::multiplyHessian (core/block_solver.h:94,146; used by OptimizationAlgorithmDogleg
@@ -170,6 +173,15 @@ int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel);
  * supernodes, tree levels, largest front, blocked fronts, levels assembled in place, pre-scattered levels,
  * trailing-update launches, big-panel backward rounds. Returns the number of entries available. */
 int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n);
+/* Solver::computeMarginals (core/solver.h:108; BlockSolver::computeMarginals block_solver.hpp:451-460 ->
+ * LinearSolverCSparse::solvePattern linear_solver_csparse.h:190-225, MarginalCovarianceCholesky): the pose-block
+ * entries (block_rows[k], block_cols[k]) (Hessian indices) of Hpp^-1, Hpp as the last build_system left it (no
+ * lambda), each a pd x pd column-major block written to out + k * pd * pd. The whole pose system is factored on the
+ * device (the LM's own factor when it factors Hpp), then one multi-right-hand-side supernodal solve per 64 / pd
+ * requested block columns. Returns 1, or 0 when Hpp is not positive definite (the reference's bool), or a
+ * negative status (unsupported on sharded graphs). */
+int g2ohip_solver_compute_marginals(g2ohip_graph* g, int nblocks, const int* block_rows, const int* block_cols,
+                                    double* out);
 /* SparseOptimizer::update(x) + push/pop/discardTop on the device-resident state */
 int g2ohip_update(g2ohip_graph* g, const double* x_host /* NULL: use device x */);
 int g2ohip_push(g2ohip_graph* g);

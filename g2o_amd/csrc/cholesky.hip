@@ -6,7 +6,8 @@
 // at :47-52) behind LinearSolver::solve (linear_solver.h:65).  The symbolic
 // analysis (symbolic.cpp) fixes ordering, supernodes and frontal maps once per
 // structure.  Storage: `fronts` holds each front (m x m col-major, m = ns + nr) as the
-// Schur updates progress; the finished factor columns [L11; L21] (m x ns, ld m) go to `lbuf`,
+// Schur updates progress; the finished factor columns [L11; L21] (m x ns, ld m) go to `lbuf` (the
+// 32x32 diagonal blocks of L11 as their inverses in `linv` only),
 // so no kernel ever reads a column another workgroup of the same launch is rewriting.
 // Each LM trial runs
 //   k_permute + k_vec_init   rhs -> P rhs -> front vectors (own rows)
@@ -217,13 +218,14 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, d
 }
 
 // Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid) and
-// forward-solve vy (LDS, kb values); L goes to L (leading dimension ldl, the block's first entry) and y to
-// ysol straight from the registers.
+// forward-solve vy (LDS, kb values); y goes to ysol straight from the registers.
 // Lanes 32..63 run the same instruction stream on the identity: lane 32 + c ends holding column c
-// of L^-1 (right-looking substitution on the broadcast columns of L), written row-major to linv.
+// of L^-1 (right-looking substitution on the broadcast columns of L), left transposed in D
+// (D[c * DS + i] = L^-1(i, c)) for publish_inverse, which the whole workgroup runs after a barrier.
+// The diagonal block of L itself is not stored: every consumer of the factor (tile TRSM, next-diagonal
+// update, inverse tasks, backward and multi-right-hand-side solves) uses L^-1 for diagonal blocks.
 __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, double* col, int lane, int* fail,
-                                             double* linv, double* X, int ldx, double* L, int ldl, double* ysol,
-                                             unsigned long long* ph = nullptr) {
+                                             double* ysol, unsigned long long* ph = nullptr) {
   double row[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
@@ -235,23 +237,27 @@ __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, doub
   const bool ok = chol32(row, y, lane, col);
   if (ph) { asm volatile("" : "+v"(row[NB - 1])); ph[6] = __builtin_amdgcn_s_memtime(); }
   if (lane == 0 && !ok) *fail = 1;
-  if (lane < kb) {  // publish L (column c: lanes c..kb-1 store consecutive rows) and y straight from registers
+  if (lane < kb) ysol[lane] = y;
+  if (lane >= NB) {  // every read of D (the row loads above) is done: this wave's LDS traffic is in order
 #pragma unroll
-    for (int c = 0; c < NB; ++c)
-      if (c <= lane) L[(size_t)c * ldl + lane] = row[c];
-    ysol[lane] = y;
-  }
-  if (lane >= NB) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) linv[i * NB + (lane - NB)] = row[i];
-    if (lane - NB < kb) {  // diagonal block of X = L11^-1, column-major with leading dimension ldx
-      double* xc = X + (size_t)(lane - NB) * ldx;
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-        if (i < kb) xc[i] = row[i];
-    }
+    for (int i = 0; i < NB; ++i) D[(lane - NB) * DS + i] = row[i];
   }
 }
+// After factor_block and a workgroup barrier: L_kk^-1 row-major to linv and the diagonal block of
+// X = L11^-1 (column-major, leading dimension ldx), both coalesced over the 256 threads.
+__device__ __forceinline__ void publish_inverse(const double* D, int kb, int tid, double* linv, double* X, int ldx) {
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = tid + 256 * u, i = e >> 5, c = e & (NB - 1);
+    linv[e] = D[c * DS + i];  // row i, column c of L^-1 (identity-padded past kb)
+  }
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = tid + 256 * u, c = e >> 5, i = e & (NB - 1);
+    if (c < kb && i < kb) X[(size_t)c * ldx + i] = D[c * DS + i];
+  }
+}
+
 // ---------------------------------------------------------------------------- assembly + extend-add
 // One launch per level assembles every front of the level from scratch (no front-pool memset, no
 // separate scatter pass), with two kinds of workgroup:
@@ -360,9 +366,9 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
       }
     }
     PH(2)
-    if (tid < 64)
-      factor_block(D, kb0, vy, col, tid, fail, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns,
-                   lbuf + me.l_off, m, ysol + me.c0, PH_REC);
+    if (tid < 64) factor_block(D, kb0, vy, col, tid, fail, ysol + me.c0, PH_REC);
+    __syncthreads();
+    publish_inverse(D, kb0, tid, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns);
     PH(3)
     PH(4)
     return;
@@ -509,7 +515,8 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
 // 8 the tile may reach into the contribution block (columns >= ns: no separate k_syrk pass),
 // 16 an inverse task: block (tj, ti) of X = L11^-1 (see below).
 // Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
-__global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, double* __restrict__ fronts,
+__global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, const launch::StepHead head,
+                                              double* __restrict__ fronts,
                                               double* __restrict__ lbuf, double* __restrict__ vecs,
                                               double* __restrict__ ysol, double* __restrict__ linv,
                                               double* __restrict__ xinv, int* __restrict__ fail) {
@@ -521,7 +528,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   __shared__ double vn[NB];
   PH_BEGIN(2)
   PH1_BEGIN(3)
-  const StepTask t = tasks[blockIdx.x];
+  const StepTask t = (int)blockIdx.x < head.n ? head.t[blockIdx.x] : tasks[blockIdx.x];
   const int m = t.m, ns = t.ns;
   double* F = fronts + t.f_off;
   double* L = lbuf + t.l_off;
@@ -603,9 +610,9 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     }
     __syncthreads();
     PH(2)
-    if (tid < 64)
-      factor_block(Dn, kbn, vn, col, tid, fail, linv + (size_t)(t.c0 + r0) * (NB * NB),
-                   xinv + t.x_off + (size_t)r0 * ns + r0, ns, L + (size_t)r0 * m + r0, m, ysol + t.c0 + r0, PH_REC);
+    if (tid < 64) factor_block(Dn, kbn, vn, col, tid, fail, ysol + t.c0 + r0, PH_REC);
+    __syncthreads();
+    publish_inverse(Dn, kbn, tid, linv + (size_t)(t.c0 + r0) * (NB * NB), xinv + t.x_off + (size_t)r0 * ns + r0, ns);
     PH(3)
     PH(4)
     return;
@@ -918,10 +925,10 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
                        lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }
-void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
-               double* linv, double* xinv, int* fail, hipStream_t s) {
+void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs,
+               double* ysol, double* linv, double* xinv, int* fail, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_step, ntasks, 256, 0, s, tasks, fronts, lbuf, vecs, ysol, linv, xinv, fail);
+  hipLaunchKernelGGL(k_step, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {

@@ -570,6 +570,16 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     }
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
+    heads.assign(ops.size(), launch::StepHead{});
+    for (size_t k = 0; k < ops.size(); ++k) {
+      if (ops[k].kind != 2) continue;
+      launch::StepHead& h = heads[k];
+      h.n = 0;
+      while (h.n < launch::CHOL_HEAD && h.n < ops[k].count && (stk[ops[k].off + h.n].flags & 4)) {
+        h.t[h.n] = stk[ops[k].off + h.n];
+        ++h.n;
+      }
+    }
   }
   children.upload(sym.children.empty() ? std::vector<int>{0} : sym.children, s);
   relmap.upload(sym.relmap.empty() ? std::vector<int>{0} : sym.relmap, s);
@@ -600,7 +610,8 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
                                       ent_row.get(),
                                       ent_src.get(), vals, lam, fronts.get(), vecs.get(),
                                       lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 0 ? 0 : (op.kind == 5 ? 2 : 1), s); break;
-      case 2: launch::chol_step(op.count, step_tasks.get() + op.off, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),
+      case 2: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
+                                vecs.get(), y_p.get(),
                                 linv.get(), xinv.get(), fail, s);
         break;
       default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;

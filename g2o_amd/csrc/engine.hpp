@@ -107,6 +107,7 @@ struct DeviceCholesky {
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
   struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add, 2 panel step, 3 syrk
   std::vector<Op> ops;
+  std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
   DevBuf<launch::Task> tasks;
   DevBuf<launch::StepTask> step_tasks;
   DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, t_p, lbuf, linv, xinv;

@@ -114,6 +114,13 @@ struct StepTask {  // k_step work item, self-contained so a workgroup needs one 
               // 32 no next-diagonal task this step (blocked front, big-panel boundary): writers update every row
   int clim;   // tile updates stop at this front column (ns, m when fused, the big-panel end when blocked)
 };
+// the launch's first (next-diagonal) tasks by value in the kernel arguments: the critical chain's workgroups
+// read their task with the kernel arguments instead of one more dependent global load
+constexpr int CHOL_HEAD = 8;
+struct StepHead {
+  StepTask t[CHOL_HEAD];
+  int n;
+};
 // zero ranges (offset, length pairs) of the front pool, then scatter input entries: fronts[dst[k]] =
 // vals[src[k] & 0x7fffffff] (+ lambda when src[k] < 0)
 void chol_prescatter(int nzero, const long long* zr, long long nent, const double* vals, const long long* dst,
@@ -126,7 +133,7 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
                      const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
                      int assemble, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place, 2 in place (m <= 512)
-void chol_step(int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
+void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs, double* ysol,
                double* linv, double* xinv, int* fail, hipStream_t s);
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
 // the contribution block, K = [0, ns)); columns stop at ns unless kb = ns (then m)

@@ -304,7 +304,28 @@ int run(const double* A, double* out, unsigned long long* cyc, const char* name)
   printf("%-28s %7llu cycles  (%5.1f per column)\n", name, best, best / 32.0);
   return 0;
 }
+__global__ void k_clock(unsigned long long* o, double* sink) {
+  double a = threadIdx.x * 1e-3;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < 200000; ++i) a = __builtin_fma(a, 0.999999, 1e-7);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  sink[threadIdx.x] = a;
+  if (threadIdx.x == 0) { o[0] = t1 - t0; o[1] = r1 - r0; }
+}
+
 int main() {
+  {
+    unsigned long long* o; double* sk;
+    CK(hipMalloc(&o, 16)); CK(hipMalloc(&sk, 64 * 8));
+    for (int r = 0; r < 3; ++r) {
+      hipLaunchKernelGGL(k_clock, 1, 64, 0, 0, o, sk);
+      CK(hipDeviceSynchronize());
+      unsigned long long h[2];
+      CK(hipMemcpy(h, o, 16, hipMemcpyDeviceToHost));
+      printf("clock: %llu memtime ticks / %llu realtime ticks (100 MHz) -> %.3f GHz; dependent fma %.1f cycles\n", h[0], h[1],
+             h[0] / (h[1] * 1e-2) * 1e-3, h[0] / 200000.0);
+    }
+  }
   double h[NB * NB];
   for (int i = 0; i < NB; ++i)
     for (int j = 0; j < NB; ++j) h[i * NB + j] = (i == j ? NB + 1.0 : 0.0) + 1.0 / (1 + i + j);

@@ -568,24 +568,17 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     if (tid < NB) yk[tid] = ykv;
     __syncthreads();
     const int lr = lane & 15, lk = lane >> 4;
-    dx4 x0 = {0.0, 0.0, 0.0, 0.0}, x1 = x0;
-    if (w < 2) {  // X rows 16w..16w+15
+    {  // X = P L_kk^-T: wave w owns the 16x16 tile (w & 1, w >> 1), one MFMA pipe per tile
+      const int xr = w & 1, xc = w >> 1;
+      dx4 x0 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int kk = 0; kk < NB / 4; ++kk) {
         const int k = kk * 4 + lk;
-        const double a = Pa[(16 * w + lr) * PS + k];
-        x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Li[lr * PS + k], x0, 0, 0, 0);
-        x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Li[(16 + lr) * PS + k], x1, 0, 0, 0);
+        x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(Pa[(16 * xr + lr) * PS + k], Li[(16 * xc + lr) * PS + k], x0, 0, 0, 0);
       }
-    }
-    __syncthreads();
-    if (w < 2) {
+      __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * w + lk + 4 * i;
-        Pa[r * PS + lr] = x0[i];
-        Pa[r * PS + 16 + lr] = x1[i];
-      }
+      for (int i = 0; i < 4; ++i) Pa[(16 * xr + lk + 4 * i) * PS + 16 * xc + lr] = x0[i];
     }
     __syncthreads();
     {  // D' -= X X^T: wave w owns the 16x16 tile (w & 1, w >> 1)

@@ -575,7 +575,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       if (ops[k].kind != 2) continue;
       launch::StepHead& h = heads[k];
       h.n = 0;
-      while (h.n < launch::CHOL_HEAD && h.n < ops[k].count && (stk[ops[k].off + h.n].flags & 4)) {
+      while (h.n < launch::CHOL_HEAD && h.n < ops[k].count) {  // the first workgroups (diagonal tasks among them)
         h.t[h.n] = stk[ops[k].off + h.n];
         ++h.n;
       }

@@ -114,7 +114,7 @@ struct StepTask {  // k_step work item, self-contained so a workgroup needs one 
               // 32 no next-diagonal task this step (blocked front, big-panel boundary): writers update every row
   int clim;   // tile updates stop at this front column (ns, m when fused, the big-panel end when blocked)
 };
-// the launch's first (next-diagonal) tasks by value in the kernel arguments: the critical chain's workgroups
+// the launch's first CHOL_HEAD tasks (the next-diagonal tasks among them) by value in the kernel arguments: those workgroups
 // read their task with the kernel arguments instead of one more dependent global load
 constexpr int CHOL_HEAD = 8;
 struct StepHead {

@@ -65,24 +65,29 @@ __device__ unsigned int g_phase_n;
     ph_k_ = atomicAdd(&g_phase_n, 1u) % 4096u;                             \
     g_phase[ph_k_][0] = (id);                                              \
     g_phase[ph_k_][1] = __builtin_amdgcn_s_memtime();                      \
-    for (int q_ = 2; q_ < 8; ++q_) g_phase[ph_k_][q_] = 0;                 \
+    for (int q_ = 2; q_ < 7; ++q_) g_phase[ph_k_][q_] = 0;                 \
+    g_phase[ph_k_][7] = __builtin_amdgcn_s_memrealtime();                  \
   }
 #define PH(i) \
   if (ph_on_) g_phase[ph_k_][i] = __builtin_amdgcn_s_memtime();
 #define PH_REC (ph_on_ ? g_phase[ph_k_] : nullptr)
-// second record for workgroup 1 (k_step: the first tile task)
+// second record for the launch's last workgroup (k_step: when the last-dispatched task starts and ends)
 #define PH1_BEGIN(id)                                                      \
-  const bool ph1_on_ = threadIdx.x == 0 && blockIdx.x == 1;                \
+  const bool ph1_on_ = threadIdx.x == 0 && blockIdx.x == gridDim.x - 1 && gridDim.x > 1; \
   unsigned ph1_k_ = 0;                                                     \
   if (ph1_on_) {                                                           \
     ph1_k_ = atomicAdd(&g_phase_n, 1u) % 4096u;                            \
     g_phase[ph1_k_][0] = (id);                                             \
     g_phase[ph1_k_][1] = __builtin_amdgcn_s_memtime();                     \
     for (int q_ = 2; q_ < 8; ++q_) g_phase[ph1_k_][q_] = 0;                \
+    g_phase[ph1_k_][6] = __builtin_amdgcn_s_memrealtime();                 \
   }
 #define PH1(i) \
   if (ph1_on_) g_phase[ph1_k_][i] = __builtin_amdgcn_s_memtime();
+#define PH1R(i) \
+  if (ph1_on_) g_phase[ph1_k_][i] = __builtin_amdgcn_s_memrealtime();
 #else
+#define PH1R(i)
 #define PH1_BEGIN(id)
 #define PH1(i)
 #define PH_REC nullptr
@@ -659,6 +664,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
         const int r = 16 * tr + lk + 4 * i, c = 16 * tc + lr;
         if (r < kbp) Xf[(size_t)(NB * j + c) * ns + NB * pp + r] = acc[i];
       }
+      PH1R(7)
       return;
     }
     __syncthreads();  // every read of Ts done
@@ -676,6 +682,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
       const int r = 16 * tr + lk + 4 * i, c = 16 * tc + lr;
       if (r < kbp) Xf[(size_t)(NB * j + c) * ns + NB * pp + r] = -xo[i];
     }
+    PH1R(7)
     return;
   }
 
@@ -753,7 +760,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     }
   }
   PH1(3)
-  if (!upd) return;
+  if (!upd) { PH1R(7) return; }
 
   // ---- C[I, J] -= P_I P_J^T (columns inside the supernode, lower triangle)
   MfmaTile T;
@@ -770,6 +777,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     if (gi < m && gj < climit && gi >= gj && !dblk) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
   }
   PH1(4)
+  PH1R(7)
 }
 
 // ---------------------------------------------------------------------------- contribution block

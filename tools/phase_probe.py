@@ -26,6 +26,7 @@ def main():
     a = np.frombuffer(buf, dtype=np.uint64, count=8 * n).reshape(n, 8).astype(np.int64)
     print(f"{n} records")
     periods(a)
+    tail(a)
     for kid, name, labels in ((1, "k_extend_add block-0 task", ["stage+assemble", "factor", "publish"]),
                               (2, "k_step(diag task)", ["stage+trsm+syrk", "factor", "publish"]),
                               (3, "k_step(tile 0,0)", ["stage", "trsm+L21", "update+store"])):
@@ -45,6 +46,25 @@ def main():
             ok = (t[:, i + 1] > 0) & (t[:, i] > 0)
             if ok.any():
                 print(f"   {lab:16s} median {np.median(d[ok]) / CLK:7.2f} us  mean {np.mean(d[ok]) / CLK:7.2f} us  (n={ok.sum()})")
+
+
+def tail(a):
+    """Per k_step launch: start of the last-dispatched workgroup and its end, relative to the diagonal task's start."""
+    ids = a[:, 0]
+    rs, re_, span = [], [], []
+    for k in range(1, len(a)):
+        if ids[k] == 3 and ids[k - 1] == 2 and a[k, 7] > 0:  # s_memrealtime (100 MHz, chip-wide) stamps
+            rs.append((a[k, 6] - a[k - 1, 7]) / 100.0)
+            re_.append((a[k, 7] - a[k - 1, 7]) / 100.0)
+            span.append((a[k - 1, 4] - a[k - 1, 1]) / CLK)
+    if rs:
+        print(f"last workgroup vs diagonal task (n={len(rs)}): start +{np.median(rs):.2f} us, end +{np.median(re_):.2f} us "
+              f"(max {np.max(re_):.2f}), diagonal task span {np.median(span):.2f} us")
+    r = a[ids == 2]
+    for q in range(min(len(r), 60)):
+        t = r[q]
+        print(f"   diag {q:3d}: stage {(t[2] - t[1]) / CLK:5.2f}  pre-chol {(t[5] - t[2]) / CLK:5.2f}  chol32 {(t[6] - t[5]) / CLK:5.2f}"
+              f"  post {(t[3] - t[6]) / CLK:5.2f}" + (f"  | last end +{re_[q]:5.2f}" if q < len(re_) else ""))
 
 
 def periods(a):

@@ -6,6 +6,8 @@ Parity status: the reference PCG is header-only C++ over Eigen (absent here), so
 pinned by construction against np.linalg.solve (tests/test_pcg_oracle.py) — "parity unpinned" against
 reference outputs; the GPU path is checked against this restatement.
 """
+import math
+
 import numpy as np
 
 
@@ -49,3 +51,45 @@ def pcg_solve(A, b, pd, tolerance=1e-6, absolute_tolerance=True, residual=-1.0, 
         d = s + (dn / dold) * d
         it += 1
     return x, it, 0.5 * dn
+
+
+def pcg_lm(host, iterations, pd, max_trials=10, tolerance=1e-6):
+    """OptimizationAlgorithmLevenberg (optimization_algorithm_levenberg.cpp:58-184) around LinearSolverPCG on a
+    pose graph (no Schur): the reduced system of every trial from the oracle's stage(lambda) (Hpp + lambda I, b), the
+    PCG's `_residual` carried across every trial and iteration (set once by init(), linear_solver_pcg.h:66).
+    host: an oracle graph. Returns [(chi2, trials, lambda, pcg_iterations_of_the_last_trial)]."""
+    stats = []
+    lam, ni, carry = None, 2.0, -1.0
+    for it in range(iterations):
+        current = host.chi2()
+        if it == 0:  # computeLambdaInit: tau * max diagonal entry of the Hessian (:152-175)
+            H0 = host.stage(0.0)["Hschur"]
+            lam = 1e-5 * float(np.max(np.abs(np.diag(H0))))
+            ni = 2.0
+        q, rho, cg = 0, 0.0, 0
+        while True:
+            st = host.stage(lam)
+            b = st["bschur"]
+            x, cg, carry = pcg_solve(st["Hschur"], b, pd, tolerance=tolerance, residual=carry)
+            host.push()
+            host.update(x)
+            temp = host.chi2()
+            rho = (current - temp) / (float(x @ (lam * x + b)) + 1e-3)  # computeScale (:177-184)
+            if rho > 0 and math.isfinite(temp):
+                lam *= max(1.0 / 3.0, min(1.0 - (2 * rho - 1) ** 3, 2.0 / 3.0))
+                ni = 2.0
+                current = temp
+                host.discard_top()
+            else:
+                lam *= ni
+                ni *= 2
+                host.pop()
+                if not math.isfinite(lam):
+                    break
+            q += 1
+            if not (rho < 0 and q < max_trials):
+                break
+        stats.append((host.chi2(), q, lam, cg))
+        if q == max_trials or rho == 0 or not math.isfinite(lam):
+            break
+    return stats

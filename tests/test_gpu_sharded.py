@@ -16,10 +16,12 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-6
 
 
-def _run_sharded(g2o_amd_mod, prob, nranks, iters):
+def _run_sharded(g2o_amd_mod, prob, nranks, iters, algo=None):
     key = uuid.uuid4().hex
     opts = [g2o_amd_mod.SparseOptimizer(0).add_problem(prob) for _ in range(nranks)]
     for r, o in enumerate(opts):
+        if algo:
+            o.set_algorithm(algo)
         o.set_comm_local(key, r, nranks)
     res, errs = [None] * nranks, []
 
@@ -100,3 +102,26 @@ def test_sharded_stage_reduced_system(g2o_amd_mod, oracle):
         assert g["ok"] == 1
         assert np.linalg.norm(g["Hschur"] - ref["Hschur"]) <= 1e-11 * np.linalg.norm(ref["Hschur"])
         assert np.linalg.norm(g["bschur"] - ref["bschur"]) <= 1e-9 * np.linalg.norm(ref["bschur"])
+
+
+def test_sharded_pcg_matches_single(g2o_amd_mod):
+    """lm_pcg6_3 on 2 landmark shards: every rank runs the block-Jacobi PCG on the all-reduced S (identical on
+    all ranks), so the LM decisions and the trajectory follow the single-GPU PCG run (S summed in a different
+    order: not bitwise, within the trajectory tolerance)."""
+    prob = synth.by_name("C4", "small")
+    iters = 5
+    opts, res = _run_sharded(g2o_amd_mod, prob, 2, iters, algo="lm_pcg6_3")
+    single = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    single.set_algorithm("lm_pcg6_3")
+    n1, st1 = single.optimize(iters)
+    for r in range(2):
+        n, st = res[r]
+        assert n == n1
+        for a, b in zip(st, st1):
+            assert a.levenbergIterations == b.levenbergIterations
+            assert abs(a.chi2 - b.chi2) <= RTOL * b.chi2, (a.chi2, b.chi2)
+    x, states = _gather_state(prob, opts)
+    C = prob.vertices[0].ids.size
+    assert np.array_equal(states[1][:6 * C], states[0][:6 * C])
+    xs = single.minimal_state()
+    assert np.linalg.norm(x - xs) <= RTOL * np.linalg.norm(xs)

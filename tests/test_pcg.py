@@ -42,6 +42,48 @@ def test_pcg_restatement_absolute_residual_carry():
     assert it3 == 2
 
 
+def test_pcg_restatement_indefinite_block():
+    """An indefinite diagonal block (the Jacobi preconditioner is its plain inverse, linear_solver_pcg.hpp:92-96):
+    r.(J r) < 0 at the start satisfies dn <= tol dn at once — zero iterations, x = 0 — both here and on the
+    device (k_pcg_start: the same test); a singular block gives a non-finite preconditioner and a NaN x,
+    which the LM rejects like a failed factorization."""
+    A, b = _block_spd(10, 3, 4)
+    A[:3, :3] = np.diag([1.0, -2.0, 3.0])
+    # make r.(J r) negative: b concentrated on the negative direction of the indefinite block
+    b = np.zeros_like(b)
+    b[1] = 1.0
+    x, it, res = pcg_ref.pcg_solve(A, b, 3)
+    assert it == 0 and not np.any(x) and res < 0
+    A[:3, :3] = 0.0
+    with np.errstate(all="ignore"):
+        try:
+            x, it, _ = pcg_ref.pcg_solve(A, b, 3)
+            assert not np.all(np.isfinite(x))
+        except np.linalg.LinAlgError:  # numpy refuses the singular block outright
+            pass
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,pd,rtol", [("C1", 6, 1e-6), ("C2", 3, 1e-4)])
+def test_gpu_pcg_lm_matches_restatement(g2o_amd_mod, oracle, name, pd, rtol):
+    """The whole LM loop around the PCG (lm_pcg) against pcg_ref.pcg_lm: per-iteration chi2, lambda and trial
+    counts, with the PCG's absolute-tolerance residual carried across every trial and iteration.
+    Both sides see the same reduced systems up to summation order. On C1 (14-60 CG iterations) chi2 and lambda
+    agree to 1e-6; the SE2 grid (150-210 iterations per solve on an ill-conditioned system) amplifies the
+    summation-order rounding to ~1e-5 in chi2 — even two runs of the multithreaded oracle differ that much."""
+    prob = synth.by_name(name, "small")
+    iters = 6 if name == "C1" else 4
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm("lm_pcg")
+    n, st = opt.optimize(iters)
+    ref = pcg_ref.pcg_lm(oracle.OracleGraph(prob), iters, pd)
+    assert n == len(ref)
+    for a, (chi2, trials, lam, _) in zip(st, ref):
+        assert a.levenbergIterations == trials
+        assert abs(a.chi2 - chi2) <= rtol * chi2, (a.chi2, chi2)
+        assert abs(a.lambda_ - lam) <= rtol * lam, (a.lambda_, lam)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,algo,pd", [("C4", "lm_pcg6_3", 6), ("C1", "lm_pcg", 6), ("C2", "lm_pcg", 3)])
 def test_gpu_pcg_matches_restatement(g2o_amd_mod, name, algo, pd):

@@ -18,13 +18,16 @@ import os
 import sys
 from collections import defaultdict
 
-STAGES = {  # substring of the kernel name -> stage name used by bench.py
+STAGES = {  # substring of the kernel name -> stage name used by bench.py (a stage's kernels each run once per
+    # iteration: the stage's traffic per launch is the sum of its kernels' per-dispatch means)
     "k_schur_rows": "schur_rows",
     "k_schur_prep": "schur_dinv",
     "k_schur_diag": "schur_diag",
     "k_linearize": "linearize",
     "k_backsub": "backsub",
     "k_vertex_reduce": "vreduce",
+    "k_cam_assemble": "vreduce",  # fused BA assembly (assembly.hip): the camera pass + landmark fix-ups
+    "k_lm_fixup": "vreduce",
 }
 
 
@@ -39,15 +42,19 @@ def read_counter(d, counter):
             if r.get("Counter_Name") != counter:
                 continue
             name = r.get("Kernel_Name", "")
-            for sub, stage in STAGES.items():
+            for sub in STAGES:
                 if sub in name:
-                    per[stage].append(float(r["Counter_Value"]))
+                    per[sub].append(float(r["Counter_Value"]))
             if any("::" + k + "(" in name or "::" + k + "<" in name for k in FACTOR):
                 fsum += float(r["Counter_Value"])
                 nfac += "::k_vec_init(" in name
+    st = defaultdict(list)
+    for sub, vals in per.items():  # per stage: sum of its kernels' per-dispatch means, one entry per dispatch
+        st[STAGES[sub]].append((sum(vals) / len(vals), len(vals)))
+    out = {k: [sum(m for m, _ in v)] * max(n for _, n in v) for k, v in st.items()}
     if nfac:
-        per["chol_factor"] = [fsum / nfac] * nfac
-    return per
+        out["chol_factor"] = [fsum / nfac] * nfac
+    return out
 
 
 def main():

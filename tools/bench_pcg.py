@@ -1,5 +1,7 @@
-"""Dev measurement: LM with the GPU PCG linear solver (lm_pcg6_3) vs the Cholesky (lm_hip_fix6_3) on a
-BASELINE config. Not the bench.py contract line; prints one JSON line per algorithm."""
+"""Dev measurement: LM with the GPU iterative linear solvers — g2o's block-Jacobi PCG on S (lm_pcg6_3) and the
+fork's matrix-free CGLS on J (lm_pcg6_3_eigen) — vs the Cholesky (lm_hip_fix6_3) on a BASELINE config.
+Not the bench.py contract line; prints one JSON line per algorithm.
+    python tools/bench_pcg.py [CONFIG [ITERS [ALGO...]]]"""
 import json
 import os
 import sys
@@ -12,7 +14,8 @@ from g2o_amd import synth  # noqa: E402
 name = sys.argv[1] if len(sys.argv) > 1 else "C4"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 prob = synth.by_name(name)
-for algo in ("lm_hip_fix6_3", "lm_pcg6_3"):
+algos = sys.argv[3:] or ["lm_hip_fix6_3", "lm_pcg6_3", "lm_pcg6_3_eigen"]
+for algo in algos:
     opt = g2o_amd.SparseOptimizer(0).add_problem(prob)
     opt.set_algorithm(algo)
     opt.initialize_optimization()
@@ -24,5 +27,7 @@ for algo in ("lm_hip_fix6_3", "lm_pcg6_3"):
     dt = time.perf_counter() - t
     print(json.dumps({"config": name, "algorithm": algo, "iterations": iters,
                       "levenberg_trials": int(sum(s.levenbergIterations for s in st)),
-                      "ms_per_iteration": 1e3 * dt / iters, "final_chi2": st[-1].chi2}), flush=True)
+                      "ms_per_iteration": 1e3 * dt / iters, "final_chi2": st[-1].chi2,
+                      "linear_iterations_last_solve": opt.linear_iterations() if algo != "lm_hip_fix6_3" else None}),
+          flush=True)
     opt.close()

@@ -141,7 +141,7 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 // the scaled column l_j = row[j] r_j, its two-column look-ahead (l_{j+1,j}, l_{j+2,j} are chain
 // values, no broadcast), the rest of column j-1's rank-1 update (through LDS, one column late,
 // columns >= j+2), cut into chunks that sched_barriers pin between the chain's dependent steps.
-// The forward solve L y = b rides along: y holds b(lane) on entry and y(lane) on return. Entries
+// The block's forward solve is not in this loop (publish_inverse multiplies by L^-1). Entries
 // above a lane's diagonal may collect garbage; they are never read. One template instance per
 // column keeps every register index a compile-time constant.
 #define CHOL_SB() __builtin_amdgcn_sched_barrier(0)
@@ -164,7 +164,7 @@ __device__ __forceinline__ void c32_fill(double (&row)[NB], const C32State& st) 
   }
 }
 template <int J>
-__device__ __forceinline__ void c32_step(double (&row)[NB], double& y, int lane, double* col, C32State& st) {
+__device__ __forceinline__ void c32_step(double (&row)[NB], int lane, double* col, C32State& st) {
   if constexpr (J < NB) {
     const double d = st.dn;
     st.ok &= d > 0.0;
@@ -193,8 +193,6 @@ __device__ __forceinline__ void c32_step(double (&row)[NB], double& y, int lane,
       col[(J & 1) * 2 * NB + lane] = lj;  // every lane writes (lanes >= 32 into the unused half)
     }
     if constexpr (J + 2 < NB) row[J + 2] -= lj * l2;
-    const double yj = rlane(y, J) * r;
-    y = lane == J ? yj : (lane > J ? y - lj * yj : y);
     CHOL_SB();
     if constexpr (J + 1 < NB) {  // column j for the next column's deferred update (entries >= j+3)
       constexpr int n0 = (J + 3) & ~1;
@@ -207,10 +205,10 @@ __device__ __forceinline__ void c32_step(double (&row)[NB], double& y, int lane,
     if constexpr (J + 2 < NB) { st.a1 = rlane(row[J + 2], J + 2); st.b1 = rlane(row[J + 1], J + 2); }
     if constexpr (J + 3 < NB) st.c2 = rlane(row[J + 1], J + 3);
     CHOL_SB();
-    c32_step<J + 1>(row, y, lane, col, st);
+    c32_step<J + 1>(row, lane, col, st);
   }
 }
-__device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, double* col) {
+__device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col) {
   C32State st;
   st.ok = true;
   st.lp = 0.0;
@@ -218,18 +216,17 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], double& y, int lane, d
   st.a1 = rlane(row[1], 1);
   st.b1 = rlane(row[0], 1);
   st.c2 = rlane(row[0], 2);
-  c32_step<0>(row, y, lane, col, st);
+  c32_step<0>(row, lane, col, st);
   return st.ok;
 }
 
-// Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid) and
-// forward-solve vy (LDS, kb values); y goes to ysol straight from the registers.
+// Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid).
 // Lanes 32..63 run the same instruction stream on the identity: lane 32 + c ends holding column c
 // of L^-1 (right-looking substitution on the broadcast columns of L), left transposed in D
 // (D[c * DS + i] = L^-1(i, c)) for publish_inverse, which the whole workgroup runs after a barrier.
 // The diagonal block of L itself is not stored: every consumer of the factor (tile TRSM, next-diagonal
 // update, inverse tasks, backward and multi-right-hand-side solves) uses L^-1 for diagonal blocks.
-__device__ __forceinline__ void factor_block(double* D, int kb, double* vy, double* col, int lane, int* fail,
+__device__ __forceinline__ void factor_block(double* D, int kb, const double* vy, double* col, int lane, int* fail,
                                              double* ysol, unsigned long long* ph = nullptr) {
   double row[NB];
 #pragma unroll
@@ -237,15 +234,28 @@ __device__ __forceinline__ void factor_block(double* D, int kb, double* vy, doub
     const double a = ld0(D, lane * DS + c, lane < kb && c <= lane);
     row[c] = ((lane >= kb && c == lane) || lane - NB == c) ? 1.0 : a;
   }
-  double y = ld0(vy, lane, lane < kb);
   if (ph) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); ph[5] = __builtin_amdgcn_s_memtime(); }
-  const bool ok = chol32(row, y, lane, col);
+  const bool ok = chol32(row, lane, col);
   if (ph) { asm volatile("" : "+v"(row[NB - 1])); ph[6] = __builtin_amdgcn_s_memtime(); }
   if (lane == 0 && !ok) *fail = 1;
-  if (lane < kb) ysol[lane] = y;
   if (lane >= NB) {  // every read of D (the row loads above) is done: this wave's LDS traffic is in order
 #pragma unroll
     for (int i = 0; i < NB; ++i) D[(lane - NB) * DS + i] = row[i];
+  }
+  // the block's forward solve y = L^-1 v (v in LDS, kb values) as a product with the inverse the same wave
+  // just wrote (in-order LDS traffic, no barrier) — a substitution inside chol32's column loop cost ~50
+  // cycles per column on the critical chain; ysol leaves before the inverse stores
+  if (lane < NB) {
+    double y4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int c0 = 0; c0 < NB; c0 += 8) {
+      double dv[8], vv[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) { dv[c] = D[(c0 + c) * DS + lane]; vv[c] = vy[c0 + c]; }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) y4[c & 3] += (c0 + c <= lane ? dv[c] : 0.0) * (c0 + c < kb ? vv[c] : 0.0);
+    }
+    if (lane < kb) ysol[lane] = (y4[0] + y4[1]) + (y4[2] + y4[3]);
   }
 }
 // After factor_block and a workgroup barrier: L_kk^-1 row-major to linv and the diagonal block of

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cassert>
 #include <cstdio>
+#include <cstdlib>
 #include <numeric>
 #include <stdexcept>
 
@@ -17,9 +18,11 @@ struct NDState {
   std::vector<int> dist, mark;
   int next_id = 1;
   int leaf;
-  bool do_refine;
-  explicit NDState(const BlockPattern& p, int leaf_, bool refine_)
-      : P(p), part(p.nb, 0), dist(p.nb, -1), mark(p.nb, 0), leaf(leaf_), do_refine(refine_) {}
+  bool do_refine, do_windows, part_degree;
+  std::vector<int> rank;  // scratch: position of a vertex in its part's BFS visitation order
+  explicit NDState(const BlockPattern& p, int leaf_, bool refine_, bool windows_, bool part_degree_)
+      : P(p), part(p.nb, 0), dist(p.nb, -1), mark(p.nb, 0), leaf(leaf_), do_refine(refine_), do_windows(windows_),
+        part_degree(part_degree_), rank(p.nb, -1) {}
 
   // Exact minimum-degree elimination on a small vertex set.
   void min_degree(const std::vector<int>& vs) {
@@ -157,7 +160,11 @@ struct NDState {
       depth = (int)lv.size();
       int best = lv.back()[0], bd = 1 << 30;
       for (int v : lv.back()) {
-        int d = P.adjp[v + 1] - P.adjp[v];
+        int d = 0;  // degree inside the part (global degrees do not tell a part's ends from its middle)
+        if (part_degree)
+          for (int p = P.adjp[v]; p < P.adjp[v + 1]; ++p) d += part[P.adji[p]] == id;
+        else
+          d = P.adjp[v + 1] - P.adjp[v];
         if (d < bd) { bd = d; best = v; }
       }
       root = best;
@@ -179,10 +186,77 @@ struct NDState {
       const double cost = (double)lv[k].size() * (1.0 + std::abs(a - b) / (double)N);
       if (cost < best) { best = cost; kbest = k; }
     }
+    const int kbest_balanced = kbest;
     if (kbest < 0) {  // fall back to the median level
       for (int k = 1; k < h - 1; ++k)
         if (before[k + 1] >= N / 2) { kbest = k; break; }
       if (kbest < 0) kbest = h / 2;
+    }
+    // window separators (position-aware): in the BFS visitation order, the vertices [x, reach(x)] —
+    // everything ranked after x that a vertex ranked before x touches — separate [0, x) from the rest, at any
+    // offset x, not only at BFS-level starts. On band-like graphs (C4's cameras: a path of one-bandwidth
+    // BFS levels) a level separator can only cut at multiples of the bandwidth, so the halves come out up to
+    // one bandwidth apart and the tree one level deeper than an exact split; the window at the vertex-count
+    // middle has the same size and balances exactly.
+    if (do_windows) {
+      // within a level, vertices with fewer neighbours in the next level first (ties: discovery order), so the
+      // reach of a prefix grows gradually instead of jumping to the end of the next level
+      std::vector<int> ord;
+      ord.reserve(N);
+      for (int k = 0; k < h; ++k) {
+        for (int v : lv[k]) rank[v] = k;  // level index, temporarily
+        std::vector<std::pair<int, int>> key;
+        key.reserve(lv[k].size());
+        for (size_t q = 0; q < lv[k].size(); ++q) key.push_back({0, (int)q});
+        ord.insert(ord.end(), lv[k].begin(), lv[k].end());
+      }
+      for (int k = 0, base = 0; k < h; base += (int)lv[k].size(), ++k) {
+        std::vector<std::pair<int, int>> key(lv[k].size());
+        for (size_t q = 0; q < lv[k].size(); ++q) {
+          const int v = lv[k][q];
+          int nn = 0;
+          for (int p = P.adjp[v]; p < P.adjp[v + 1]; ++p) nn += part[P.adji[p]] == id && rank[P.adji[p]] == k + 1;
+          key[q] = {nn, (int)q};
+        }
+        std::sort(key.begin(), key.end());
+        for (size_t q = 0; q < key.size(); ++q) ord[base + q] = lv[k][key[q].second];
+      }
+      for (int k = 0; k < N; ++k) rank[ord[k]] = k;
+      // balanced windows as the level candidates (both sides >= 20 %); failing that, on a part too small to
+      // split in balance (a leaf-sized band segment a bit wider than the bandwidth), the window that shortens
+      // the chain through the part (separator + larger side < whole part), so leaves come out small instead of
+      // one bandwidth plus a sliver
+      int reach = -1, xbest = -1, wend = -1, xs = -1, ws = -1;
+      double wcost = best, chain = 0.97 * N;
+      for (int x = 1; x < N - 1; ++x) {
+        const int v = ord[x - 1];
+        for (int p = P.adjp[v]; p < P.adjp[v + 1]; ++p) {
+          const int u = P.adji[p];
+          if (part[u] == id) reach = std::max(reach, rank[u]);
+        }
+        if (reach < x || reach >= N - 1) continue;  // disconnected prefix / nothing left on the far side
+        const int a = x, b = N - 1 - reach, w = reach - x + 1;
+        if (a >= 0.2 * N && b >= 0.2 * N) {
+          const double cost = (double)w * (1.0 + std::abs(a - b) / (double)N);
+          if (cost < wcost * (1.0 - 1e-9)) { wcost = cost; xbest = x; wend = reach; }
+        }
+        if (w + std::max(a, b) < chain) { chain = w + std::max(a, b); xs = x; ws = reach; }
+      }
+      if (xbest < 0 && kbest_balanced < 0 && xs >= 0) { xbest = xs; wend = ws; }
+      for (int v : ord) rank[v] = -1;
+      if (xbest >= 0) {
+        int idA = next_id++, idB = next_id++, idS = next_id++;
+        std::vector<int> A(ord.begin(), ord.begin() + xbest), S(ord.begin() + xbest, ord.begin() + wend + 1),
+            B(ord.begin() + wend + 1, ord.end());
+        for (int v : A) part[v] = idA;
+        for (int v : B) part[v] = idB;
+        for (int v : S) part[v] = idS;
+        run(A, idA);
+        run(B, idB);
+        std::sort(S.begin(), S.end());
+        for (int v : S) order.push_back(v);
+        return;
+      }
     }
     // refine: separator = vertices of level k with a neighbour in level k+1
     int idA = next_id++, idB = next_id++, idS = next_id++;
@@ -215,8 +289,8 @@ struct NDState {
 
 }  // namespace
 
-std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size, bool refine) {
-  NDState st(P, std::max(leaf_size, 1), refine);
+std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size, bool refine, bool windows, bool part_degree) {
+  NDState st(P, std::max(leaf_size, 1), refine, windows, part_degree || windows);
   std::vector<int> all(P.nb);
   std::iota(all.begin(), all.end(), 0);
   st.run(all, 0);
@@ -237,11 +311,21 @@ double gpu_cost(const Symbolic& S) {
 Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, int relax_max_blocks) {
   const int nb = P.nb;
   if (bperm.empty() && nb > 0) {
-    // nested dissection with and without separator refinement; the ordering with the lower modelled GPU
-    // factor time (flops at the MFMA rate + the level-synchronous panel-step chain) wins
-    Symbolic a = analyze(P, nested_dissection(P, 48, false), relax, relax_max_blocks);
-    Symbolic b = analyze(P, nested_dissection(P, 48, true), relax, relax_max_blocks);
-    return gpu_cost(b) < 0.95 * gpu_cost(a) ? b : a;  // the unrefined order unless clearly worse
+    // nested dissection variants; the ordering with the lowest modelled GPU factor time (flops at the MFMA
+    // rate + the level-synchronous panel-step chain) wins, the plain one unless another is clearly (5 %) better:
+    // with / without separator refinement, pseudo-peripheral roots by global or by in-part degree, and
+    // position-aware window separators (see NDState::run)
+    Symbolic best = analyze(P, nested_dissection(P, 48, false), relax, relax_max_blocks);
+    if (getenv("G2OHIP_ND_PLAIN")) return best;  // dev A/B: round-1 ordering
+    const double base = gpu_cost(best);
+    double bc = base;
+    const bool var[4][3] = {{true, false, false}, {false, false, true}, {true, false, true}, {false, true, true}};
+    for (const auto& v : var) {
+      Symbolic c = analyze(P, nested_dissection(P, 48, v[0], v[1], v[2]), relax, relax_max_blocks);
+      const double cc = gpu_cost(c);
+      if (cc < 0.95 * base && cc < bc) { bc = cc; best = std::move(c); }
+    }
+    return best;
   }
   Symbolic S;
   S.nb = nb;

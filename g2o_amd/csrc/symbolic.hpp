@@ -56,7 +56,8 @@ struct Symbolic {
 
 // Nested-dissection ordering of the block graph. leaf_size: subgraphs at most this
 // large are ordered by minimum degree; refine: greedy separator refinement after each bisection.
-std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size = 48, bool refine = false);
+std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size = 48, bool refine = false, bool windows = false,
+                                   bool part_degree = false);
 
 // Modelled GPU factor time of a symbolic analysis (seconds): flops at the MFMA rate plus the
 // level-synchronous panel-step chain.

@@ -20,6 +20,7 @@ struct NDState {
   int leaf;
   bool do_refine, do_windows, part_degree;
   std::vector<int> rank;  // scratch: position of a vertex in its part's BFS visitation order
+  const bool no_small_windows = getenv("G2OHIP_ND_NO_SMALLWIN") != nullptr;  // dev A/B
   explicit NDState(const BlockPattern& p, int leaf_, bool refine_, bool windows_, bool part_degree_)
       : P(p), part(p.nb, 0), dist(p.nb, -1), mark(p.nb, 0), leaf(leaf_), do_refine(refine_), do_windows(windows_),
         part_degree(part_degree_), rank(p.nb, -1) {}
@@ -242,7 +243,7 @@ struct NDState {
         }
         if (w + std::max(a, b) < chain) { chain = w + std::max(a, b); xs = x; ws = reach; }
       }
-      if (xbest < 0 && kbest_balanced < 0 && xs >= 0) { xbest = xs; wend = ws; }
+      if (xbest < 0 && kbest_balanced < 0 && xs >= 0 && !no_small_windows) { xbest = xs; wend = ws; }
       for (int v : ord) rank[v] = -1;
       if (xbest >= 0) {
         int idA = next_id++, idB = next_id++, idS = next_id++;
@@ -311,6 +312,7 @@ double gpu_cost(const Symbolic& S) {
 Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, int relax_max_blocks) {
   const int nb = P.nb;
   if (bperm.empty() && nb > 0) {
+    if (const char* rm = getenv("G2OHIP_ND_RMAX")) relax_max_blocks = atoi(rm);  // dev A/B
     // nested dissection variants; the ordering with the lowest modelled GPU factor time (flops at the MFMA
     // rate + the level-synchronous panel-step chain) wins, the plain one unless another is clearly (5 %) better:
     // with / without separator refinement, pseudo-peripheral roots by global or by in-part degree, and

@@ -173,10 +173,10 @@ def symbolic_analyze(nblocks: int, bdim: int, bi, bj):
     bi = np.ascontiguousarray(bi, np.int32)
     bj = np.ascontiguousarray(bj, np.int32)
     perm = np.zeros(nblocks * bdim, np.int32)
-    st = np.zeros(4)
+    st = np.zeros(5)
     n = lib().g2ohip_symbolic_analyze(nblocks, bdim, len(bi), _p(bi), _p(bj), _p(perm), _p(st))
     _check(n, "symbolic_analyze")
-    return perm, dict(nnzL=st[0], flops=st[1], supernodes=int(st[2]), levels=int(st[3]))
+    return perm, dict(nnzL=st[0], flops=st[1], supernodes=int(st[2]), levels=int(st[3]), panel_steps=int(st[4]))
 
 
 def linear_solve_ccs(n, Ap, Ai, Ax, b, block_dim=1, device=0):

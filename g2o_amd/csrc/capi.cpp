@@ -350,6 +350,13 @@ int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, cons
       stats[1] = S.flops;
       stats[2] = (double)S.sn.size();
       stats[3] = (double)S.num_levels;
+      int lsteps = 0;  // level-synchronous 32-column panel steps (the factor's dependent launch chain)
+      for (const auto& lv : S.levels) {
+        int mx = 0;
+        for (int sn : lv) mx = std::max(mx, (S.sn[sn].ns + 31) / 32);
+        lsteps += mx;
+      }
+      stats[4] = (double)lsteps;
     }
     return S.n;
   } catch (const std::exception& ex) {

@@ -212,7 +212,7 @@ int g2ohip_set_comm_local(g2ohip_graph* g, const char* group_key, int rank, int 
 /* ---- host-only symbolic analysis (no GPU needed) ----
  * Block pattern of a symmetric matrix given as upper blocks (bi[k] <= bj[k]) of a uniform block
  * size bdim: returns n = nblocks*bdim, fills perm[n] (new -> old scalar) and
- * stats[4] = {nnz(L), factor flops, #supernodes, #levels}. */
+ * stats[5] = {nnz(L), factor flops, #supernodes, #levels, level-synchronous 32-column panel steps}. */
 int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int* perm, double* stats);
 
 /* ---- measurement hooks ---- */

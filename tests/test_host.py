@@ -109,6 +109,21 @@ def test_symbolic_disconnected_and_trivial(g2o_amd_mod):
     assert perm1.tolist() == list(range(6)) and st1["supernodes"] == 1
 
 
+def test_symbolic_band_windows(g2o_amd_mod):
+    """C4's reduced camera system is a band (cameras within a 64-camera window share points): 998 camera blocks
+    of dimension 6, half-bandwidth 63 blocks — a path of 15.8 bandwidths. Level separators from a path's end cut
+    only at multiples of the bandwidth (5 levels of 12 panel steps); the window separators at the exact middles
+    give the optimum for the band: 3 separator levels over 8 segments, each segment split once more into a
+    separator and two small leaves — 1 + 4 x 12 = 49 level-synchronous panel steps."""
+    nb, w = 998, 63
+    bi = [i for i in range(nb) for j in range(i, min(nb, i + w + 1))]
+    bj = [j for i in range(nb) for j in range(i, min(nb, i + w + 1))]
+    perm, st = g2o_amd_mod.symbolic_analyze(nb, 6, bi, bj)
+    assert sorted(perm.tolist()) == list(range(nb * 6))
+    assert st["panel_steps"] <= 50, st
+    assert st["levels"] == 5, st
+
+
 def test_symbolic_rejects_bad_input(g2o_amd_mod):
     with pytest.raises(g2o_amd_mod.G2OHipError):
         g2o_amd_mod.symbolic_analyze(2, 3, [0, 5], [1, 1])

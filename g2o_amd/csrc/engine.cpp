@@ -405,8 +405,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       if (pre)
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
-          const long long len = (long long)(q.ns + q.nr) * (q.ns + q.nr);
-          for (long long o = 0; o < len; o += 65536) { zr.push_back(q.front_off + o); zr.push_back(std::min(65536LL, len - o)); }
+          // only the lower triangle is ever read (tiles, contribution passes and extend-add touch rows >= columns):
+          // zero column j's rows [j, m), whole small fronts in one range
+          const long long m = q.ns + q.nr, len = m * m;
+          if (m <= 64)
+            for (long long o = 0; o < len; o += 65536) { zr.push_back(q.front_off + o); zr.push_back(std::min(65536LL, len - o)); }
+          else
+            for (long long j = 0; j < m; ++j) { zr.push_back(q.front_off + j * m + j); zr.push_back(m - j); }
           for (int c = q.c0; c < q.c0 + q.ns; ++c)
             for (int e = cpv[c]; e < cpv[c + 1]; ++e) {
               pdst.push_back(edsts[e]);

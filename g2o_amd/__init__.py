@@ -273,6 +273,12 @@ class SparseOptimizer:
     def load(self, path: str, marginalize_xyz: bool = True):
         _check(lib().g2ohip_load_g2o(self.h, path.encode(), int(marginalize_xyz)), "load")
 
+    def num_vertices(self) -> int:
+        return int(lib().g2ohip_num_vertices(self.h))
+
+    def num_edges(self) -> int:
+        return int(lib().g2ohip_num_edges(self.h))
+
     def save(self, path: str):
         _check(lib().g2ohip_save_g2o(self.h, path.encode()), "save")
 

@@ -29,18 +29,19 @@ int guarded(F&& f) {
 }
 // 1 known, 0 unknown, -1 a reference name this backend does not build (with g_err set)
 int algorithm_known(const std::string& n) {
-  // {gn,lm}_hip_{var,fix6_3,fix3_3,fix6_6} (cf. solver_csparse.cpp:51-84 name parsing)
+  // {gn,lm}_hip_{var,fix6_3,fix3_2,fix3_3,fix6_6} (cf. solver_csparse.cpp:51-84 name parsing)
   if (n.size() < 6) return 0;
   const std::string m = n.substr(0, 3), rest = n.substr(3);
   if (m != "lm_" && m != "gn_") return 0;
-  if (rest == "hip_var" || rest == "hip_fix6_3" || rest == "hip_fix3_3" || rest == "hip_fix6_6") return 1;
+  if (rest == "hip_var" || rest == "hip_fix6_3" || rest == "hip_fix3_2" || rest == "hip_fix3_3" || rest == "hip_fix6_6")
+    return 1;
   // g2o/solvers/pcg registry (solver_pcg.cpp:91-98): pcg (variable block size), pcg3_2, pcg6_3, pcg7_3.
   // Block-Jacobi PCG on the device replaces the Cholesky; pose blocks of 3 or 6 only.
-  if (rest == "pcg" || rest == "pcg6_3") return 1;
+  if (rest == "pcg" || rest == "pcg6_3" || rest == "pcg3_2") return 1;
   // fork solvers/eigen/solver_eigen.cpp:80,126: JacobiSolver_6_3 + LinearSolverPCGEigen (matrix-free CGLS)
   if (m == "lm_" && rest == "pcg6_3_eigen") return 1;
-  if (rest == "pcg3_2" || rest == "pcg7_3") {
-    g_err = n + ": fixed block sizes 3_2 / 7_3 are not supported by the device PCG (pose blocks of 3 or 6 only; "
+  if (rest == "pcg7_3") {
+    g_err = n + ": fixed block size 7_3 is not supported by the device PCG (pose blocks of 3 or 6 only; "
                 "use " + m + "pcg)";
     return -1;
   }

@@ -3,6 +3,7 @@
 //   EdgeSE3ProjectXYZ  types/sba/types_six_dof_expmap.h:201-229, .cpp:395-455
 //   EdgeSE3 (QUAT)     types/slam3d/edge_se3.cpp:77-103, isometry3d_gradients.h:194-260
 //   EdgeSE2            types/slam2d/edge_se2.h:46-52, edge_se2.cpp:77-103
+//   EdgeSE2PointXY     types/slam2d/edge_se2_pointxy.h:41-75, edge_se2_pointxy.cpp:63-87
 //   oplus              types_six_dof_expmap.h:97-100 (SE3Quat::exp * T, se3quat.h:217-257),
 //                      types_sba.h:149-153, vertex_se3.h:105-113, vertex_se2.h:51-58
 //
@@ -11,6 +12,7 @@
 //   XYZ point       [3]
 //   Isometry3 pose  [12] R (row-major 3x3) tx ty tz
 //   SE2 pose        [3]  x y theta
+//   XY point        [2]
 // Jacobians are produced row-major (D x dim) in registers; nothing is stored.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -526,6 +528,41 @@ struct FamilySE2 {
     const double Z[9] = {rc, -rs, 0, rs, rc, 0, 0, 0, 1};
     mat3mul(Z, A, Ji);
     mat3mul(Z, B, Jj);
+  }
+};
+
+// ---- EdgeSE2PointXY (BlockSolver_3_2 landmark edge): v0 = SE2 pose (3), v1 = XY point (2); meas x y, info packed 3.
+// error = v0^-1 * l - z (edge_se2_pointxy.h:44-49, SE2::inverse se2.h:82-87, SE2 * Vector2 = t + R v se2.h:77-80),
+// Jacobians edge_se2_pointxy.cpp:63-87 ----
+struct FamilySE2XY {
+  static constexpr int D = 2, DA = 3, DB = 2, MEAS = 2, INFO = 3;
+  DI static void error(const EdgeData& d, int e, double* err) {
+    const double* xi = d.s0 + (size_t)d.v0[e] * 3;
+    const double* l = d.s1 + (size_t)d.v1[e] * 2;
+    const double* m = d.meas + (size_t)e * 2;
+    const double a[3] = {xi[0], xi[1], xi[2]};
+    double ai[3];
+    FamilySE2::inverse(a, ai);
+    const double c = cos(ai[2]), s = sin(ai[2]), l0 = l[0], l1 = l[1];
+    err[0] = (ai[0] + (c * l0 - s * l1)) - m[0];
+    err[1] = (ai[1] + (s * l0 + c * l1)) - m[1];
+  }
+  DI static void linearize(const EdgeData& d, int e, double* err, double* Ji, double* Jj) {
+    error(d, e, err);
+    const double* xi = d.s0 + (size_t)d.v0[e] * 3;
+    const double* l = d.s1 + (size_t)d.v1[e] * 2;
+    const double x1 = xi[0], y1 = xi[1], x2 = l[0], y2 = l[1];
+    const double c = cos(xi[2]), s = sin(xi[2]);
+    Ji[0] = -c;
+    Ji[1] = -s;
+    Ji[2] = c * y2 - c * y1 - s * x2 + s * x1;
+    Ji[3] = s;
+    Ji[4] = -c;
+    Ji[5] = -s * y2 + s * y1 - c * x2 + c * x1;
+    Jj[0] = c;
+    Jj[1] = s;
+    Jj[2] = -s;
+    Jj[3] = c;
   }
 };
 

@@ -29,25 +29,29 @@ static double wall() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int vertex_dim(int t) { return t == G2OHIP_V_SE3_EXPMAP || t == G2OHIP_V_SE3_QUAT ? 6 : (t == G2OHIP_V_XYZ || t == G2OHIP_V_SE2 ? 3 : -1); }
-int vertex_est_dim(int t) { return t == G2OHIP_V_SE3_EXPMAP || t == G2OHIP_V_SE3_QUAT ? 7 : 3; }
+int vertex_dim(int t) {
+  return t == G2OHIP_V_SE3_EXPMAP || t == G2OHIP_V_SE3_QUAT ? 6
+         : (t == G2OHIP_V_XYZ || t == G2OHIP_V_SE2 ? 3 : (t == G2OHIP_V_XY ? 2 : -1));
+}
+int vertex_est_dim(int t) { return t == G2OHIP_V_SE3_EXPMAP || t == G2OHIP_V_SE3_QUAT ? 7 : (t == G2OHIP_V_XY ? 2 : 3); }
 int vertex_state_stride(int t) {
   switch (t) {
     case G2OHIP_V_SE3_EXPMAP: return 8;
     case G2OHIP_V_XYZ: return 3;
     case G2OHIP_V_SE3_QUAT: return 12;
     case G2OHIP_V_SE2: return 3;
+    case G2OHIP_V_XY: return 2;
   }
   return 0;
 }
 static bool is_hostj(int e) { return e > G2OHIP_E_HOSTJ(0) && e <= G2OHIP_E_HOSTJ(6); }
 int edge_dim(int e) {
   if (is_hostj(e)) return e - G2OHIP_E_HOSTJ(0);
-  return e == G2OHIP_E_SE3_PROJECT_XYZ ? 2 : (e == G2OHIP_E_SE3_QUAT ? 6 : (e == G2OHIP_E_SE2 ? 3 : -1));
+  return e == G2OHIP_E_SE3_PROJECT_XYZ || e == G2OHIP_E_SE2_XY ? 2 : (e == G2OHIP_E_SE3_QUAT ? 6 : (e == G2OHIP_E_SE2 ? 3 : -1));
 }
 int edge_meas_dim(int e) {
   if (is_hostj(e)) return 0;
-  return e == G2OHIP_E_SE3_PROJECT_XYZ ? 2 : (e == G2OHIP_E_SE3_QUAT ? 7 : 3);
+  return e == G2OHIP_E_SE3_PROJECT_XYZ || e == G2OHIP_E_SE2_XY ? 2 : (e == G2OHIP_E_SE3_QUAT ? 7 : 3);
 }
 
 // ------------------------------------------------------------------ host-side math for I/O
@@ -127,6 +131,7 @@ void set_state_from_est(int vt, const double* est, double* st) {
       st[9] = est[0]; st[10] = est[1]; st[11] = est[2];
       break;
     case G2OHIP_V_SE2: st[0] = est[0]; st[1] = est[1]; st[2] = est[2]; break;
+    case G2OHIP_V_XY: st[0] = est[0]; st[1] = est[1]; break;
   }
 }
 void est_from_state(int vt, const double* st, double* est) {
@@ -142,7 +147,9 @@ void est_from_state(int vt, const double* st, double* est) {
       est[3] = q[0] / n; est[4] = q[1] / n; est[5] = q[2] / n; est[6] = q[3] / n;
       break;
     }
-    default: est[0] = st[0]; est[1] = st[1]; est[2] = st[2]; break;
+    default:
+      for (int k = 0; k < vertex_est_dim(vt); ++k) est[k] = st[k];
+      break;
   }
 }
 void minimal_from_state(int vt, const double* st, double* out) {
@@ -159,7 +166,9 @@ void minimal_from_state(int vt, const double* st, double* out) {
       out[3] = sg * q[0] / n; out[4] = sg * q[1] / n; out[5] = sg * q[2] / n;
       break;
     }
-    default: out[0] = st[0]; out[1] = st[1]; out[2] = st[2]; break;
+    default:
+      for (int k = 0; k < vertex_dim(vt); ++k) out[k] = st[k];
+      break;
   }
 }
 
@@ -817,6 +826,10 @@ void parse_chunk(const char* b, const char* e, ParsedChunk& out) {
       ParsedVertex v{tag == "VERTEX_XYZ" ? G2OHIP_V_XYZ : G2OHIP_V_SE2, c.i(), {}};
       for (int k = 0; k < 3; ++k) v.est[k] = c.d();
       out.verts.push_back(v);
+    } else if (tag == "VERTEX_XY") {  // vertex_point_xy.cpp:46-50
+      ParsedVertex v{G2OHIP_V_XY, c.i(), {}};
+      for (int k = 0; k < 2; ++k) v.est[k] = c.d();
+      out.verts.push_back(v);
     } else if (tag == "FIX") {
       while (c.more()) {
         const int id = c.i();
@@ -830,6 +843,12 @@ void parse_chunk(const char* b, const char* e, ParsedChunk& out) {
       const double o0 = c.d(), o1 = c.d(), o2 = c.d();
       ed.info[0] = o0; ed.info[1] = o1; ed.info[2] = o1; ed.info[3] = o2;
       for (double& x : ed.p) x = c.d();
+      out.edges.push_back(ed);
+    } else if (tag == "EDGE_SE2_XY") {  // edge_se2_pointxy.cpp:46-52
+      ParsedEdge ed{G2OHIP_E_SE2_XY, c.i(), c.i(), {}, {}, {}};
+      ed.m[0] = c.d(); ed.m[1] = c.d();
+      const double o0 = c.d(), o1 = c.d(), o2 = c.d();
+      ed.info[0] = o0; ed.info[1] = o1; ed.info[2] = o1; ed.info[3] = o2;
       out.edges.push_back(ed);
     } else if (tag == "EDGE_SE3:QUAT" || tag == "EDGE_SE2") {  // edge_se3.cpp:42-65, edge_se2.cpp:41-53
       const bool se3 = tag == "EDGE_SE3:QUAT";
@@ -906,7 +925,7 @@ int Engine::load(const char* path, int marginalize_xyz) {
       ids.push_back(v.id);
       est.insert(est.end(), v.est, v.est + vertex_est_dim(v.type));
       fx.push_back(0);
-      mg.push_back(v.type == G2OHIP_V_XYZ && marginalize_xyz ? 1 : 0);
+      mg.push_back((v.type == G2OHIP_V_XYZ || v.type == G2OHIP_V_XY) && marginalize_xyz ? 1 : 0);
     }
   if (int r = flush_v(cur)) return r;
   // edges in file order, batched per run of one type
@@ -962,6 +981,7 @@ int Engine::save(const char* path) {
         fprintf(f, "VERTEX_SE3:QUAT %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", v.id, e[0], e[1], e[2], e[3], e[4], e[5], e[6]);
         break;
       case G2OHIP_V_SE2: fprintf(f, "VERTEX_SE2 %d %.17g %.17g %.17g\n", v.id, e[0], e[1], e[2]); break;
+      case G2OHIP_V_XY: fprintf(f, "VERTEX_XY %d %.17g %.17g\n", v.id, e[0], e[1]); break;
     }
     if (v.fixed) fprintf(f, "FIX %d\n", v.id);
   }
@@ -975,7 +995,9 @@ int Engine::save(const char* path) {
       const int a = hg.verts[es.ev0[k]].id, b = hg.verts[es.ev1[k]].id;
       const double* m = es.meas.data() + k * nm;
       const double* I = es.info.data() + k * D * D;
-      if (es.type == G2OHIP_E_SE3_PROJECT_XYZ) {
+      if (es.type == G2OHIP_E_SE2_XY) {
+        fprintf(f, "EDGE_SE2_XY %d %d %.17g %.17g %.17g %.17g %.17g\n", a, b, m[0], m[1], I[0], I[1], I[3]);
+      } else if (es.type == G2OHIP_E_SE3_PROJECT_XYZ) {
         const double* p = es.params.data() + k * 4;
         fprintf(f, "EDGE_SE3_PROJECT_XYZ:EXPMAP %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", a, b, m[0],
                 m[1], I[0], I[1], I[3], p[0], p[1], p[2], p[3]);
@@ -993,7 +1015,7 @@ int Engine::save(const char* path) {
 
 void Engine::ensure_device_state() {
   if (!device_state_dirty) return;
-  for (int t = 1; t <= 4; ++t)
+  for (int t = 1; t < NVT; ++t)
     if (!hg.st[t].empty()) dstate[t].upload(hg.st[t], stream);
   if (!hg.nopl.empty()) dnopl.upload(hg.nopl, stream);
   device_state_dirty = false;
@@ -1003,7 +1025,7 @@ void Engine::ensure_device_state() {
 
 void Engine::sync_host_state() {
   if (!host_state_stale) return;
-  for (int t = 1; t <= 4; ++t)
+  for (int t = 1; t < NVT; ++t)
     if (!hg.st[t].empty()) dstate[t].download(hg.st[t].data(), hg.st[t].size(), stream);
   if (!hg.nopl.empty()) dnopl.download(hg.nopl.data(), hg.nopl.size(), stream);
   HIP_CHECK(hipStreamSynchronize(stream));
@@ -1052,6 +1074,7 @@ static int family_of(int etype, int& vtA, int& vtB) {
     case G2OHIP_E_SE3_PROJECT_XYZ: vtA = G2OHIP_V_XYZ; vtB = G2OHIP_V_SE3_EXPMAP; return FAM_BA;
     case G2OHIP_E_SE3_QUAT: vtA = vtB = G2OHIP_V_SE3_QUAT; return FAM_SE3;
     case G2OHIP_E_SE2: vtA = vtB = G2OHIP_V_SE2; return FAM_SE2;
+    case G2OHIP_E_SE2_XY: vtA = G2OHIP_V_SE2; vtB = G2OHIP_V_XY; return FAM_SE2XY;
   }
   vtA = vtB = 0;
   return is_hostj(etype) ? FAM_HOSTJ : FAM_NONE;
@@ -1095,8 +1118,8 @@ int Engine::initialize() {  // sparse_optimizer.cpp:201-279 + buildIndexMapping 
       pd = v.dim;
       ++num_poses;
     } else {
-      if (v.dim != 3) return G2OHIP_ERR_UNSUPPORTED;
-      ld = 3;
+      if (ld && ld != v.dim) return G2OHIP_ERR_UNSUPPORTED;  // one landmark block size
+      ld = v.dim;
       ++num_landmarks;
     }
   }
@@ -1104,7 +1127,8 @@ int Engine::initialize() {  // sparse_optimizer.cpp:201-279 + buildIndexMapping 
   size_poses = num_poses * pd;
   size_landmarks = num_landmarks * ld;
   do_schur = num_landmarks > 0;  // optimization_algorithm_with_hessian.cpp:48-73
-  if (do_schur && pd != 6) return G2OHIP_ERR_UNSUPPORTED;  // the Schur kernels are BlockSolver_6_3
+  // the Schur kernels are instantiated for BlockSolver_6_3 and BlockSolver_3_2 (block_solver.h:188-201)
+  if (do_schur && !((pd == 6 && ld == 3) || (pd == 3 && ld == 2))) return G2OHIP_ERR_UNSUPPORTED;
   // landmark-landmark edges have no place in BlockSolver's Schur layout here
   for (const HEdgeSet& es : hg.esets)
     for (size_t k = 0; k < es.ev0.size(); ++k) {
@@ -1234,7 +1258,7 @@ void Engine::setup_edges_device() {
     const int D = g.D, nm = es.nm, gne = g.ne;
     std::vector<int> v0(std::max(gne, 1), 0), v1(std::max(gne, 1), 0);
     const int minfo = D * (D + 1) / 2;
-    const int mmeas = g.family == FAM_BA ? 2 : (g.family == FAM_SE3 ? 12 : (g.family == FAM_SE2 ? 3 : 0));
+    const int mmeas = g.family == FAM_BA || g.family == FAM_SE2XY ? 2 : (g.family == FAM_SE3 ? 12 : (g.family == FAM_SE2 ? 3 : 0));
     std::vector<double> meas((size_t)std::max(gne, 1) * std::max(mmeas, 1)), info((size_t)std::max(gne, 1) * minfo),
         params(g.family == FAM_BA ? (size_t)gne * 4 : 1);
     for (int k = 0; k < gne; ++k) {
@@ -1261,6 +1285,8 @@ void Engine::setup_edges_device() {
         mo[0] = c * (-m[0]) - s * (-m[1]);
         mo[1] = s * (-m[0]) + c * (-m[1]);
         mo[2] = th;
+      } else if (g.family == FAM_SE2XY) {
+        mo[0] = m[0]; mo[1] = m[1];
       }
       const double* I = es.info.data() + (size_t)e * D * D;
       double* io = info.data() + (size_t)k * minfo;
@@ -1372,7 +1398,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
   // per-type hessian index and x offsets
   const int lm_begin = local_lm.empty() ? 0 : local_lm.front();
   const int lm_end = local_lm.empty() ? 0 : local_lm.back() + 1;
-  for (int t = 1; t <= 4; ++t) {
+  for (int t = 1; t < NVT; ++t) {
     const auto& lst = hg.by_type[t];
     std::vector<int> hx(std::max<size_t>(lst.size(), 1), -1), xo(std::max<size_t>(lst.size(), 1), -1);
     for (size_t k = 0; k < lst.size(); ++k) {
@@ -1489,12 +1515,12 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
   }
   doffslot.resize((size_t)std::max<long long>(nslotd, 1));
   // per-vertex-side slots: arena by vertex dimension, each group's sides contiguous
-  nslot3 = nslot6 = 0;
+  for (long long& c : nslot) c = 0;
   for (EGroup& g : groups) {
-    long long& ca = g.DA == 3 ? nslot3 : nslot6;
+    long long& ca = nslot[g.DA];
     g.slotA = ca;
     ca += g.ne;
-    long long& cb = g.DB == 3 ? nslot3 : nslot6;
+    long long& cb = nslot[g.DB];
     g.slotB = cb;
     cb += g.ne;
   }
@@ -1511,15 +1537,15 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
   dH.resize(std::max<long long>((long long)nHpp * pd * pd + (long long)nHpl * pd * ld, 1));
   dH.zero(stream);
   const int nLloc = (int)local_lm.size();
-  dHll.resize(std::max(nLloc * 9, 1));
+  dHll.resize(std::max(nLloc * ld * ld, 1));
   dHll.zero(stream);
   const long long n = vector_size();
   db.resize(std::max<long long>(n, 1));
   db.zero(stream);
   dx.resize(std::max<long long>(n, 1));
   dx.zero(stream);
-  dslot3.resize((size_t)std::max<long long>(ba_fused ? 1 : nslot3, 1) * 9);  // the fused BA path needs no slots
-  dslot6.resize((size_t)std::max<long long>(ba_fused ? 1 : nslot6, 1) * 27);
+  for (int d : {2, 3, 6})  // the fused BA path needs no slots
+    dslot[d].resize((size_t)std::max<long long>(ba_fused ? 1 : nslot[d], 1) * (d * (d + 1) / 2 + d));
   // vertex incidence lists (hessian order): code = slot index in the arena of the vertex's dimension, in
   // group / edge order (a fixed summation order)
   {
@@ -1718,9 +1744,9 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       nHppUsed += shpp[t] >= 0;
     }
     ds_hpp.upload(shpp, stream);
-    dDinv.resize(std::max(nLloc * 9, 1));
-    dUfac.resize(std::max(nLloc * 6, 1));
-    dG.resize(std::max<long long>((long long)nHpl * 18, 1));  // G = Hpl U^-T per observation (6x3)
+    dDinv.resize(std::max(nLloc * ld * ld, 1));
+    dUfac.resize(std::max(nLloc * launch::schur_ufac_stride(ld), 1));
+    dG.resize(std::max<long long>((long long)nHpl * pd * ld, 1));  // G = Hpl U^-T per observation (pd x ld)
     dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
     if (use_cgls()) {  // the fork's JacobiSolver_6_3: CGLS on J, no reduced system to factor
@@ -1896,15 +1922,15 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   double* S = dS.get();
   double* bschur = dS.get() + (size_t)nS * pd * pd;
   timer.begin("schur_dinv", stream);
-  launch::schur_prep(nLloc, lm_begin, dHll.get(), db.get() + size_poses, dscal.get(), dDinv.get(), dUfac.get(),
+  launch::schur_prep(ld, nLloc, lm_begin, dHll.get(), db.get() + size_poses, dscal.get(), dDinv.get(), dUfac.get(),
                      dCl.get(), failp() + 1, stream);
   timer.end(stream);
   timer.begin("schur_diag", stream);
-  launch::schur_diag(num_poses, sch_rptr.get(), sch_robs.get(), sch_obs_lm.get(), lm_begin, Hpl, dUfac.get(), dCl.get(),
+  launch::schur_diag(pd, ld, num_poses, sch_rptr.get(), sch_robs.get(), sch_obs_lm.get(), lm_begin, Hpl, dUfac.get(), dCl.get(),
                      sch_sdiag.get(), ds_hpp.get(), dH.get(), db.get(), dscal.get() + 4, S, bschur, dG.get(), stream);
   timer.end(stream);
   timer.begin("schur_rows", stream);
-  launch::schur_rows(nsch_tasks, sch_tasks.get(), sch_batches.get(), sch_st_obs.get(), sch_pairs.get(), sch_pp.get(),
+  launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(), sch_st_obs.get(), sch_pairs.get(), sch_pp.get(),
                      dG.get(), ds_hpp.get(), dH.get(), S, stream);
   timer.end(stream);
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
@@ -1925,7 +1951,7 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   }
   if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
   timer.begin("backsub", stream);
-  launch::backsub(nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get(), size_poses, lm_begin, dx.get(),
+  launch::backsub(pd, ld, nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get(), size_poses, lm_begin, dx.get(),
                   stream);
   timer.end(stream);
 }
@@ -1942,7 +1968,7 @@ int Engine::solve_sync() {
 
 void Engine::update_async() {  // sparse_optimizer.cpp:441-454
   timer.begin("oplus", stream);
-  for (int t = 1; t <= 4; ++t) {
+  for (int t = 1; t < NVT; ++t) {
     const int n = (int)hg.by_type[t].size();
     if (!n) continue;
     launch::oplus(t, n, d_xoff[t].get(), dx.get(), dstate[t].get(), t == G2OHIP_V_SE3_QUAT ? dnopl.get() : nullptr, stream);
@@ -1977,10 +2003,10 @@ int Engine::get_b(double* b) {
 
 int Engine::push() {  // base_vertex.h:93-95 for all active vertices (stream-ordered device copy)
   ensure_device_state();
-  if ((int)stack_.size() <= stack_depth_) stack_.emplace_back(5);
+  if ((int)stack_.size() <= stack_depth_) stack_.emplace_back(NVT);
   auto& lvl = stack_[stack_depth_++];
   launch::CopyList cl{};
-  for (int t = 1; t <= 4; ++t) {
+  for (int t = 1; t < NVT; ++t) {
     if (!dstate[t].size()) continue;
     lvl[t].resize(dstate[t].size());
     cl.src[cl.n] = dstate[t].get();
@@ -1994,7 +2020,7 @@ int Engine::pop() {
   if (stack_depth_ == 0) return G2OHIP_ERR_STATE;
   auto& lvl = stack_[--stack_depth_];
   launch::CopyList cl{};
-  for (int t = 1; t <= 4; ++t)
+  for (int t = 1; t < NVT; ++t)
     if (lvl[t].size()) {
       cl.src[cl.n] = lvl[t].get();
       cl.dst[cl.n] = dstate[t].get();

@@ -18,6 +18,7 @@
 
 namespace g2ohip {
 
+constexpr int NVT = 6;  // vertex type codes 1..5 (G2OHIP_V_*)
 int vertex_dim(int vtype);
 int vertex_est_dim(int vtype);
 int vertex_state_stride(int vtype);
@@ -46,8 +47,8 @@ struct HEdgeSet {
 struct HostGraph {
   std::vector<HVertex> verts;
   std::unordered_map<int, int> idmap;
-  std::vector<double> st[5];            // per type, device layout
-  std::vector<std::vector<int>> by_type = std::vector<std::vector<int>>(5);  // local -> vertex
+  std::vector<double> st[NVT];            // per type, device layout
+  std::vector<std::vector<int>> by_type = std::vector<std::vector<int>>(NVT);  // local -> vertex
   std::vector<int> nopl;                // VertexSE3 oplus counters (per local SE3QUAT vertex)
   std::vector<HEdgeSet> esets;          // in first-seen type order
   long long num_edges() const {
@@ -246,19 +247,19 @@ class Engine {
   std::vector<int> local_lm;     // landmark (hessian - num_poses) this rank owns
 
   // device state
-  DevBuf<double> dstate[5];
+  DevBuf<double> dstate[NVT];
   DevBuf<int> dnopl;
   std::vector<std::vector<DevBuf<double>>> stack_;  // per push level: per type (buffers reused)
   int stack_depth_ = 0;
   bool edges_ready = false;
   hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};  // schur start, factor start, factor end, solve end
   bool ev_valid_ = false;
-  DevBuf<int> d_xoff[5];         // per type local -> x offset or -1
-  DevBuf<int> d_hidx[5];         // per type local -> hessian index (-1 fixed)
-  // per-vertex-side slot arenas by vertex dimension (3, 6): packed upper H + b, one slot per (edge, side)
-  DevBuf<double> dslot3, dslot6;
-  long long nslot3 = 0, nslot6 = 0;
-  double* slot_arena(int dim) { return dim == 3 ? dslot3.get() : dslot6.get(); }
+  DevBuf<int> d_xoff[NVT];         // per type local -> x offset or -1
+  DevBuf<int> d_hidx[NVT];         // per type local -> hessian index (-1 fixed)
+  // per-vertex-side slot arenas by vertex dimension (2, 3, 6): packed upper H + b, one slot per (edge, side)
+  DevBuf<double> dslot[7];
+  long long nslot[7] = {0, 0, 0, 0, 0, 0, 0};
+  double* slot_arena(int dim) { return dslot[dim].get(); }
   // off-diagonal blocks several local edges share: per-edge slots reduced in edge order, one launch per block size
   DevBuf<double> doffslot;
   struct OffRed { int nb = 0, bsz = 0; DevBuf<int> ptr; DevBuf<long long> soff, dst; };

@@ -19,6 +19,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
+#include <type_traits>
 
 #include "common.hpp"
 #include "device_types.hpp"
@@ -359,60 +361,103 @@ __global__ void __launch_bounds__(256)
 }
 
 // ------------------------------------------------------------------------------ Schur
-// Landmark pass (block_solver.hpp:341-360): Dinv = (Hll + lambda I)^-1 (cofactor inverse, as
-// Eigen's 3x3 inverse; kept for the back-substitution) and the symmetric split
-//   Hll + lambda I = U U^T (3x3 Cholesky),  G_a = Hpl_a U^-T,  c_l = U^-1 b_l,
+// Landmark pass (block_solver.hpp:341-360): Dinv = (Hll + lambda I)^-1 (Eigen's fixed-size inverse: cofactors for
+// 3x3, the closed form for 2x2; kept for the back-substitution) and the symmetric split
+//   Hll + lambda I = U U^T (LD x LD Cholesky),  G_a = Hpl_a U^-T,  c_l = U^-1 b_l,
 // so that Hpl Dinv Hpl^T = G G^T and Hpl Dinv b_l = G c_l. k_schur_diag forms G once per observation
-// (for its own sums and, stored, for k_schur_rows). Ufac per landmark: r0 r1 r2 u10 u20 u21
-// (r = reciprocal pivots of U).
+// (for its own sums and, stored, for k_schur_rows). Ufac per landmark (UF doubles, r = reciprocal pivots of U):
+// LD = 3: r0 r1 r2 u10 u20 u21, LD = 2: r0 r1 u10 0. The Schur kernels are instantiated for the reference's
+// BlockSolver_6_3 (PD = 6, LD = 3) and BlockSolver_3_2 (PD = 3, LD = 2) (block_solver.h:188-201).
+template <int LD>
+struct LmTraits;
+template <>
+struct LmTraits<3> { static constexpr int UF = 6; };
+template <>
+struct LmTraits<2> { static constexpr int UF = 4; };
+
+template <int LD>
 __global__ void __launch_bounds__(256)
     k_schur_prep(int nl, int lm0, const double* __restrict__ Hll, const double* __restrict__ bl_all,
                  const double* __restrict__ lam, double* __restrict__ Dinv, double* __restrict__ Ufac,
                  double* __restrict__ cl_all, int* __restrict__ fail) {
+  constexpr int UF = LmTraits<LD>::UF;
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= nl) return;
   const double lambda = *lam;
-  const double* Hm = Hll + (size_t)l * 9;
-  double a[9];
+  const double* Hm = Hll + (size_t)l * LD * LD;
+  double a[LD * LD];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) a[k] = Hm[k];
-  a[0] += lambda; a[4] += lambda; a[8] += lambda;
-  auto m = [&](int r, int c) { return a[c * 3 + r]; };
-  const double c00 = m(1, 1) * m(2, 2) - m(1, 2) * m(2, 1);
-  const double c10 = m(0, 2) * m(2, 1) - m(0, 1) * m(2, 2);
-  const double c20 = m(0, 1) * m(1, 2) - m(0, 2) * m(1, 1);
-  const double det = c00 * m(0, 0) + c10 * m(1, 0) + c20 * m(2, 0);
-  const double inv = 1.0 / det;
-  double Di[9];  // col-major
-  Di[0] = c00 * inv; Di[3] = c10 * inv; Di[6] = c20 * inv;
-  Di[1] = (m(1, 2) * m(2, 0) - m(1, 0) * m(2, 2)) * inv;
-  Di[4] = (m(0, 0) * m(2, 2) - m(0, 2) * m(2, 0)) * inv;
-  Di[7] = (m(0, 2) * m(1, 0) - m(0, 0) * m(1, 2)) * inv;
-  Di[2] = (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0)) * inv;
-  Di[5] = (m(0, 1) * m(2, 0) - m(0, 0) * m(2, 1)) * inv;
-  Di[8] = (m(0, 0) * m(1, 1) - m(0, 1) * m(1, 0)) * inv;
-  double* Do = Dinv + (size_t)l * 9;
+  for (int k = 0; k < LD * LD; ++k) a[k] = Hm[k];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) Do[k] = Di[k];
-  // U (lower): reciprocal pivots u_ii^-1
-  const double d0 = m(0, 0);
-  const double r0 = 1.0 / sqrt(d0);
-  const double u10 = m(1, 0) * r0, u20 = m(2, 0) * r0;
-  const double d1 = m(1, 1) - u10 * u10;
-  const double r1 = 1.0 / sqrt(d1);
-  const double u21 = (m(2, 1) - u20 * u10) * r1;
-  const double d2 = m(2, 2) - u20 * u20 - u21 * u21;
-  const double r2 = 1.0 / sqrt(d2);
-  if (!(det != 0.0) || !isfinite(inv) || !(d0 > 0.0) || !(d1 > 0.0) || !(d2 > 0.0)) *fail = 1;
-  double* U = Ufac + (size_t)l * 6;
-  U[0] = r0; U[1] = r1; U[2] = r2; U[3] = u10; U[4] = u20; U[5] = u21;
-  // c_l = U^-1 b_l
-  const double* bl = bl_all + (size_t)(lm0 + l) * 3;
-  const double g0 = bl[0] * r0;
-  const double g1 = (bl[1] - u10 * g0) * r1;
-  const double g2 = (bl[2] - u20 * g0 - u21 * g1) * r2;
-  double* co = cl_all + (size_t)(lm0 + l) * 3;
-  co[0] = g0; co[1] = g1; co[2] = g2;
+  for (int i = 0; i < LD; ++i) a[i * LD + i] += lambda;
+  auto m = [&](int r, int c) { return a[c * LD + r]; };
+  double* Do = Dinv + (size_t)l * LD * LD;  // col-major
+  double* U = Ufac + (size_t)l * UF;
+  const double* bl = bl_all + (size_t)(lm0 + l) * LD;
+  double* co = cl_all + (size_t)(lm0 + l) * LD;
+  bool bad;
+  if constexpr (LD == 3) {
+    const double c00 = m(1, 1) * m(2, 2) - m(1, 2) * m(2, 1);
+    const double c10 = m(0, 2) * m(2, 1) - m(0, 1) * m(2, 2);
+    const double c20 = m(0, 1) * m(1, 2) - m(0, 2) * m(1, 1);
+    const double det = c00 * m(0, 0) + c10 * m(1, 0) + c20 * m(2, 0);
+    const double inv = 1.0 / det;
+    Do[0] = c00 * inv; Do[3] = c10 * inv; Do[6] = c20 * inv;
+    Do[1] = (m(1, 2) * m(2, 0) - m(1, 0) * m(2, 2)) * inv;
+    Do[4] = (m(0, 0) * m(2, 2) - m(0, 2) * m(2, 0)) * inv;
+    Do[7] = (m(0, 2) * m(1, 0) - m(0, 0) * m(1, 2)) * inv;
+    Do[2] = (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0)) * inv;
+    Do[5] = (m(0, 1) * m(2, 0) - m(0, 0) * m(2, 1)) * inv;
+    Do[8] = (m(0, 0) * m(1, 1) - m(0, 1) * m(1, 0)) * inv;
+    const double d0 = m(0, 0);
+    const double r0 = 1.0 / sqrt(d0);
+    const double u10 = m(1, 0) * r0, u20 = m(2, 0) * r0;
+    const double d1 = m(1, 1) - u10 * u10;
+    const double r1 = 1.0 / sqrt(d1);
+    const double u21 = (m(2, 1) - u20 * u10) * r1;
+    const double d2 = m(2, 2) - u20 * u20 - u21 * u21;
+    const double r2 = 1.0 / sqrt(d2);
+    bad = !(det != 0.0) || !isfinite(inv) || !(d0 > 0.0) || !(d1 > 0.0) || !(d2 > 0.0);
+    U[0] = r0; U[1] = r1; U[2] = r2; U[3] = u10; U[4] = u20; U[5] = u21;
+    const double g0 = bl[0] * r0;
+    const double g1 = (bl[1] - u10 * g0) * r1;
+    const double g2 = (bl[2] - u20 * g0 - u21 * g1) * r2;
+    co[0] = g0; co[1] = g1; co[2] = g2;
+  } else {  // Eigen compute_inverse_size2: adjugate / (m00 m11 - m10 m01)
+    const double det = m(0, 0) * m(1, 1) - m(1, 0) * m(0, 1);
+    const double inv = 1.0 / det;
+    Do[0] = m(1, 1) * inv; Do[1] = -m(1, 0) * inv; Do[2] = -m(0, 1) * inv; Do[3] = m(0, 0) * inv;
+    const double d0 = m(0, 0);
+    const double r0 = 1.0 / sqrt(d0);
+    const double u10 = m(1, 0) * r0;
+    const double d1 = m(1, 1) - u10 * u10;
+    const double r1 = 1.0 / sqrt(d1);
+    bad = !(det != 0.0) || !isfinite(inv) || !(d0 > 0.0) || !(d1 > 0.0);
+    U[0] = r0; U[1] = r1; U[2] = u10; U[3] = 0.0;
+    const double g0 = bl[0] * r0;
+    co[0] = g0;
+    co[1] = (bl[1] - u10 * g0) * r1;
+  }
+  if (bad) *fail = 1;
+}
+
+// G = Hpl U^-T in place: g (PD x LD col-major) holds Hpl on entry, G on exit; row r solves U g_r = h_r
+template <int PD, int LD>
+__device__ __forceinline__ void form_G(double* g, const double* U) {
+#pragma unroll
+  for (int r = 0; r < PD; ++r) {
+    if constexpr (LD == 3) {
+      const double g0 = g[r] * U[0];
+      const double g1 = (g[PD + r] - U[3] * g0) * U[1];
+      g[2 * PD + r] = (g[2 * PD + r] - U[4] * g0 - U[5] * g1) * U[2];
+      g[r] = g0;
+      g[PD + r] = g1;
+    } else {
+      const double g0 = g[r] * U[0];
+      g[PD + r] = (g[PD + r] - U[2] * g0) * U[1];
+      g[r] = g0;
+    }
+  }
 }
 
 // Diagonal blocks of the reduced system (block_solver.hpp:361-400, the j == i terms):
@@ -420,6 +465,7 @@ __global__ void __launch_bounds__(256)
 // one workgroup per camera row, its 256 lanes striding over the row's observations (landmark
 // order), G formed in registers from Hpl and U_l (and stored, for k_schur_rows); a fixed butterfly
 // per wave and the four wave sums added in wave order (bitwise reproducible).
+template <int PD, int LD>
 __global__ void __launch_bounds__(256)
     k_schur_diag(int nrows, const int* __restrict__ rptr, const int* __restrict__ robs,
                  const int* __restrict__ obs_lm, int lm0, const double* __restrict__ Hpl,
@@ -427,79 +473,85 @@ __global__ void __launch_bounds__(256)
                  const int* __restrict__ s_hpp, const double* __restrict__ Hpp, const double* __restrict__ b,
                  const double* __restrict__ lam, double* __restrict__ S, double* __restrict__ bschur,
                  double* __restrict__ G) {
-  __shared__ double red[4][27];
-  __shared__ __attribute__((aligned(16))) double gst[4][64 * 18];  // per-wave image of 64 G blocks
+  constexpr int GB = PD * LD, UF = LmTraits<LD>::UF, NPK = PD * (PD + 1) / 2, NA = NPK + PD;
+  static_assert(GB % 2 == 0 && UF % 2 == 0, "16-byte block loads");
+  __shared__ double red[4][NA];
+  __shared__ __attribute__((aligned(16))) double gst[4][64 * GB];  // per-wave image of 64 G blocks
   // XCD-contiguous camera rows: the observations of one landmark (neighbours in Hpl) are read by
   // rows of nearby cameras, i.e. mostly behind one L2
   const int row = xcd_item(blockIdx.x, nrows), tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double acc[27];  // packed upper of G G^T (21, col-major) | G c (6)
+  double acc[NA];  // packed upper of G G^T (col-major) | G c
 #pragma unroll
-  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  for (int k = 0; k < NA; ++k) acc[k] = 0.0;
   const int p1 = rptr[row + 1];
   for (int pb = rptr[row] + w * 64; pb < p1; pb += 256) {  // the wave's blocks [pb, pb + nw)
     const int p = pb + lane, nw = min(64, p1 - pb);
     if (p < p1) {
       const int a = robs[p], l = obs_lm[a];
-      const double2* h2 = reinterpret_cast<const double2*>(Hpl + (size_t)a * 18);
-      const double2* u2 = reinterpret_cast<const double2*>(Ufac + (size_t)l * 6);
-      double g[18], U[6], c[3];
+      const double2* h2 = reinterpret_cast<const double2*>(Hpl + (size_t)a * GB);
+      const double2* u2 = reinterpret_cast<const double2*>(Ufac + (size_t)l * UF);
+      double g[GB], U[UF], c[LD];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) { const double2 v = h2[k]; g[2 * k] = v.x; g[2 * k + 1] = v.y; }
+      for (int k = 0; k < GB / 2; ++k) { const double2 v = h2[k]; g[2 * k] = v.x; g[2 * k + 1] = v.y; }
 #pragma unroll
-      for (int k = 0; k < 3; ++k) { const double2 v = u2[k]; U[2 * k] = v.x; U[2 * k + 1] = v.y; }
-      const double* cp = cl_all + (size_t)(lm0 + l) * 3;
-      c[0] = cp[0]; c[1] = cp[1]; c[2] = cp[2];
+      for (int k = 0; k < UF / 2; ++k) { const double2 v = u2[k]; U[2 * k] = v.x; U[2 * k + 1] = v.y; }
+      const double* cp = cl_all + (size_t)(lm0 + l) * LD;
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {  // row r of G = Hpl U^-T
-        const double g0 = g[r] * U[0];
-        const double g1 = (g[6 + r] - U[3] * g0) * U[1];
-        g[12 + r] = (g[12 + r] - U[4] * g0 - U[5] * g1) * U[2];
-        g[r] = g0;
-        g[6 + r] = g1;
-      }
+      for (int k = 0; k < LD; ++k) c[k] = cp[k];
+      form_G<PD, LD>(g, U);
       {  // every observation lies in exactly one camera row: G is written once, in camera-row order,
          // for k_schur_rows; the wave's blocks leave as one contiguous coalesced run (below)
-        double2* go = reinterpret_cast<double2*>(gst[w] + lane * 18);
+        double2* go = reinterpret_cast<double2*>(gst[w] + lane * GB);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) go[k] = double2{g[2 * k], g[2 * k + 1]};
+        for (int k = 0; k < GB / 2; ++k) go[k] = double2{g[2 * k], g[2 * k + 1]};
       }
       int k = 0;
 #pragma unroll
-      for (int cc = 0; cc < 6; ++cc)
+      for (int cc = 0; cc < PD; ++cc)
 #pragma unroll
-        for (int r = 0; r <= cc; ++r) acc[k++] += g[r] * g[cc] + g[6 + r] * g[6 + cc] + g[12 + r] * g[12 + cc];
+        for (int r = 0; r <= cc; ++r) {
+          double s = g[r] * g[cc];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) acc[21 + r] += g[r] * c[0] + g[6 + r] * c[1] + g[12 + r] * c[2];
+          for (int kk = 1; kk < LD; ++kk) s += g[kk * PD + r] * g[kk * PD + cc];
+          acc[k++] += s;
+        }
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        double s = g[r] * c[0];
+#pragma unroll
+        for (int kk = 1; kk < LD; ++kk) s += g[kk * PD + r] * c[kk];
+        acc[NPK + r] += s;
+      }
     }
     wave_sync();  // converged: the whole wave copies the image out
-    wave_copy_out(G + (size_t)pb * 18, gst[w], nw * 18, lane);
+    wave_copy_out(G + (size_t)pb * GB, gst[w], nw * GB, lane);
     wave_sync();
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1)
 #pragma unroll
-    for (int k = 0; k < 27; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
+    for (int k = 0; k < NA; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
   if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 27; ++k) red[w][k] = acc[k];
+    for (int k = 0; k < NA; ++k) red[w][k] = acc[k];
   }
   __syncthreads();
-  if (tid >= 27) return;
+  if (tid >= NA) return;
   const double v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-  if (tid >= 21) {
-    const int r = tid - 21;
-    bschur[(size_t)row * 6 + r] = b[(size_t)row * 6 + r] - v;
+  if (tid >= NPK) {
+    const int r = tid - NPK;
+    bschur[(size_t)row * PD + r] = b[(size_t)row * PD + r] - v;
     return;
   }
   const int sidx = sdiag[row], hp = s_hpp[sidx];
-  const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * 36;
-  double* So = S + (size_t)sidx * 36;
+  const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * PD * PD;
+  double* So = S + (size_t)sidx * PD * PD;
   int cc = 0, r = tid;  // packed upper index tid -> (r, cc), r <= cc
   while (r > cc) { r -= cc + 1; ++cc; }
-  const double h0 = hp >= 0 ? Hh[cc * 6 + r] : 0.0;
+  const double h0 = hp >= 0 ? Hh[cc * PD + r] : 0.0;
   const double o = (r == cc ? h0 + *lam : h0) - v;
-  So[cc * 6 + r] = o;
-  So[r * 6 + cc] = o;
+  So[cc * PD + r] = o;
+  So[r * PD + cc] = o;
 }
 
 // Off-diagonal blocks, row-stationary (block_solver.hpp:361-391, j > i): one workgroup per (camera
@@ -508,26 +560,29 @@ __global__ void __launch_bounds__(256)
 // observation by k_schur_diag, in camera-row order) of the row's own observation a = (l, i) and of
 // its partners (l, j), j > i, into LDS by LDS-DMA
 // (global_load_lds_dwordx4: 1 KiB lane-linear per wave instruction, no register staging). Two LDS
-// buffers: batch k+1 lands while batch k is reduced. Four threads per slot, each three columns of
-// the block over every second pair of the slot's list (landmark order), the two parities combined by
+// buffers: batch k+1 lands while batch k is reduced. Four threads per slot, each half of the block's
+// columns over every second pair of the slot's list (landmark order), the two parities combined by
 // one fixed shuffle: every output has one owner and a fixed summation order (no atomics, bitwise
 // reproducible).
 namespace {
 constexpr int SCH_SB = launch::SCHUR_SB;  // staged G blocks per batch
-constexpr int SCH_GB = 18;                // doubles per staged block: G, 6x3 col-major (9 x 16 B)
 constexpr int SCH_SL = launch::SCHUR_SL;  // off-diagonal slots per task
 constexpr int SCH_PPB = SCH_SL + 1;       // slot-CSR entries per batch
 constexpr int SCH_NI = (SCH_SB + 255) / 256;
-constexpr int SCH_NC = (SCH_SB * 9 + 255) / 256;  // 16-B pieces per thread per batch
-static_assert(SCH_SB * 9 % 64 == 0, "a wave's LDS-DMA pieces must tile the batch image");
 }  // namespace
 
+template <int PD, int LD>
 __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
                  const int* __restrict__ st_obs, const int* __restrict__ pairs, const int* __restrict__ pp,
                  const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,
                  double* __restrict__ S, int mode) {
-  __shared__ __attribute__((aligned(16))) double Gs[2][SCH_SB * SCH_GB];
+  constexpr int GB = PD * LD;                        // doubles per staged block: G, PD x LD col-major
+  constexpr int NPC = GB / 2;                        // 16-B pieces per block
+  constexpr int NC = (SCH_SB * NPC + 255) / 256;     // 16-B pieces per thread per batch
+  constexpr int CW = (PD + 1) / 2;                   // output columns (and rows) per half
+  static_assert(SCH_SB * NPC % 64 == 0, "a wave's LDS-DMA pieces must tile the batch image");
+  __shared__ __attribute__((aligned(16))) double Gs[2][SCH_SB * GB];
   __shared__ int so[2][SCH_SB];  // staged observation per block
   __shared__ int sp[2][SCH_SB];  // pair lists (posA | posB << 16), slot-sorted
   __shared__ int spp[2][SCH_PPB];
@@ -535,9 +590,9 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
   const int nb = t.b1 - t.b0;
   const int tid = threadIdx.x, w = tid >> 6;
   const int ls = tid >> 2, q = tid & 3;
-  double acc[18];  // 6 x 3: rows 0..5 of columns h3..h3+2
+  double acc[CW * PD];  // columns c0 .. c0 + CW - 1 of the block, all PD rows
 #pragma unroll
-  for (int k = 0; k < 18; ++k) acc[k] = 0.0;
+  for (int k = 0; k < CW * PD; ++k) acc[k] = 0.0;
   // records past the task's end read the next task's (or the trailing dummy) record and go unused
   auto rec = [&](int k) { return batches[t.b0 + min(k, nb)]; };
   int ov[SCH_NI], pv[SCH_NI], ppv = 0;
@@ -559,41 +614,52 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     if (tid < SCH_PPB) spp[buf][tid] = ppv;
   };
   auto stage = [&](const launch::SchurBatch B, int buf) {  // so[buf] holds B's observations
-    const int n9 = B.nst * 9;
+    const int np = B.nst * NPC;
 #pragma unroll
-    for (int u = 0; u < SCH_NC; ++u) {
+    for (int u = 0; u < NC; ++u) {
       const int i = tid + 256 * u;
-      if (i < n9) {
-        const int item = i / 9, ch = i - item * 9;
+      if (i < np) {
+        const int item = i / NPC, ch = i - item * NPC;
         __builtin_amdgcn_global_load_lds(
-            (const void*)(G + (size_t)so[buf][item] * SCH_GB + 2 * ch),
+            (const void*)(G + (size_t)so[buf][item] * GB + 2 * ch),
             (__attribute__((address_space(3))) void*)(&Gs[buf][(256 * u + 64 * w) * 2]), 16, 0, 0);
       }
     }
   };
-  // thread q of a slot: columns 3h..3h+2 of the block (h = q & 1) over the pairs of parity q >> 1
-  const int h3 = (q & 1) * 3, par = q >> 1;
+  // thread q of a slot: columns c0 .. c0 + CW - 1 of the block (h = q & 1) over the pairs of parity q >> 1
+  const int c0 = (q & 1) * CW, par = q >> 1;
   auto compute = [&](int buf) {
     if (ls >= t.noff) return;
     const int p1 = spp[buf][ls + 1];
     for (int p = spp[buf][ls] + par; p < p1; p += 2) {
       const int pr = sp[buf][p];
-      const double* ga = &Gs[buf][(pr & 0xffff) * SCH_GB];
-      const double* gb = &Gs[buf][(pr >> 16) * SCH_GB + h3];
+      const double* ga = &Gs[buf][(pr & 0xffff) * GB];
+      const double* gb = &Gs[buf][(pr >> 16) * GB + c0];
 #pragma unroll
-      for (int kk = 0; kk < 3; ++kk) {  // one column of G_a and three entries of G_b at a time
-        double A[6], Bm[3];
+      for (int kk = 0; kk < LD; ++kk) {  // one column of G_a and CW entries of G_b at a time
+        double A[PD], Bm[CW];
+        if constexpr (PD % 2 == 0) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const double2 x = *reinterpret_cast<const double2*>(ga + kk * 6 + 2 * k);
-          A[2 * k] = x.x; A[2 * k + 1] = x.y;
+          for (int k = 0; k < PD / 2; ++k) {
+            const double2 x = *reinterpret_cast<const double2*>(ga + kk * PD + 2 * k);
+            A[2 * k] = x.x; A[2 * k + 1] = x.y;
+          }
+#pragma unroll
+          for (int j = 0; j < CW; ++j) Bm[j] = gb[kk * PD + j];
+        } else {  // odd PD: the second half has CW - 1 columns (the spare one reads column c0 and is zeroed)
+#pragma unroll
+          for (int r = 0; r < PD; ++r) A[r] = ga[kk * PD + r];
+#pragma unroll
+          for (int j = 0; j < CW; ++j) {
+            const bool in = c0 + j < PD;
+            const double v = gb[kk * PD + (in ? j : 0)];
+            Bm[j] = in ? v : 0.0;
+          }
         }
 #pragma unroll
-        for (int j = 0; j < 3; ++j) Bm[j] = gb[kk * 6 + j];
+        for (int j = 0; j < CW; ++j)
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-          for (int r = 0; r < 6; ++r) acc[j * 6 + r] += A[r] * Bm[j];
+          for (int r = 0; r < PD; ++r) acc[j * PD + r] += A[r] * Bm[j];
       }
     }
   };
@@ -625,28 +691,29 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     B1 = B2;
     B2 = B3;
   }
-  // even + odd pairs (fixed order); thread (h, par) stores rows 3 par..3 par+2 of its three columns
+  // even + odd pairs (fixed order); thread (h, par) stores rows [0, CW) (par 0) or [CW, PD) (par 1) of its columns
 #pragma unroll
-  for (int k = 0; k < 18; ++k) acc[k] += __shfl_xor(acc[k], 2, 4);
+  for (int k = 0; k < CW * PD; ++k) acc[k] += __shfl_xor(acc[k], 2, 4);
   if (ls < t.noff) {
     const int sidx = t.soff + ls;
     const int hp = s_hpp[sidx];
-    const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * 36;
-    double* So = S + (size_t)sidx * 36;
+    const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * PD * PD;
+    double* So = S + (size_t)sidx * PD * PD;
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < CW; ++j)
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        if ((r >= 3) != (par == 1)) continue;
-        const int k = (h3 + j) * 6 + r;
-        So[k] = (hp >= 0 ? Hh[k] : 0.0) - acc[j * 6 + r];
+      for (int r = 0; r < PD; ++r) {
+        if ((r >= CW) != (par == 1)) continue;
+        if (PD % 2 != 0 && c0 + j >= PD) continue;
+        const int k = (c0 + j) * PD + r;
+        So[k] = (hp >= 0 ? Hh[k] : 0.0) - acc[j * PD + r];
       }
   }
 }
 
 // back-substitution: x_l = Dinv_l (b_l - sum_a Hpl_a^T x_pose(a)); LANES lanes per landmark stride over
 // its observations, combined by a fixed butterfly (bitwise reproducible)
-template <int PD, int LANES>
+template <int PD, int LD, int LANES>
 __global__ void __launch_bounds__(256)
     k_backsub(int nl, const int* __restrict__ lm_ptr, const int* __restrict__ blk_pose, const double* __restrict__ Hpl,
               const double* __restrict__ Dinv, const double* __restrict__ b, int size_poses, int lm0,
@@ -654,37 +721,44 @@ __global__ void __launch_bounds__(256)
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int l = gid / LANES, q = gid % LANES;  // local landmark; global index lm0 + l
   const bool active = l < nl;
-  double c0 = 0, c1 = 0, c2 = 0;
+  double c[LD];
+#pragma unroll
+  for (int k = 0; k < LD; ++k) c[k] = 0.0;
   if (active) {
     const int a1 = lm_ptr[l + 1];
     for (int a = lm_ptr[l] + q; a < a1; a += LANES) {
-      const double* Bm = Hpl + (size_t)a * PD * 3;
+      const double* Bm = Hpl + (size_t)a * PD * LD;
       const double* xp = x + (size_t)blk_pose[a] * PD;
-      double s0 = 0, s1 = 0, s2 = 0;
+      double s[LD];
+#pragma unroll
+      for (int k = 0; k < LD; ++k) s[k] = 0.0;
 #pragma unroll
       for (int r = 0; r < PD; ++r) {
         const double xr = -xp[r];
-        s0 += Bm[r] * xr;
-        s1 += Bm[PD + r] * xr;
-        s2 += Bm[2 * PD + r] * xr;
+#pragma unroll
+        for (int k = 0; k < LD; ++k) s[k] += Bm[k * PD + r] * xr;
       }
-      c0 += s0; c1 += s1; c2 += s2;
+#pragma unroll
+      for (int k = 0; k < LD; ++k) c[k] += s[k];
     }
   }
 #pragma unroll
-  for (int m = LANES / 2; m >= 1; m >>= 1) {
-    c0 += __shfl_xor(c0, m, LANES);
-    c1 += __shfl_xor(c1, m, LANES);
-    c2 += __shfl_xor(c2, m, LANES);
-  }
+  for (int m = LANES / 2; m >= 1; m >>= 1)
+#pragma unroll
+    for (int k = 0; k < LD; ++k) c[k] += __shfl_xor(c[k], m, LANES);
   if (!active || q != 0) return;
-  const double* bl = b + size_poses + (size_t)(lm0 + l) * 3;
-  c0 += bl[0]; c1 += bl[1]; c2 += bl[2];
-  const double* D = Dinv + (size_t)l * 9;
-  double* xl = x + size_poses + (size_t)(lm0 + l) * 3;
-  xl[0] = D[0] * c0 + D[3] * c1 + D[6] * c2;
-  xl[1] = D[1] * c0 + D[4] * c1 + D[7] * c2;
-  xl[2] = D[2] * c0 + D[5] * c1 + D[8] * c2;
+  const double* bl = b + size_poses + (size_t)(lm0 + l) * LD;
+#pragma unroll
+  for (int k = 0; k < LD; ++k) c[k] += bl[k];
+  const double* D = Dinv + (size_t)l * LD * LD;
+  double* xl = x + size_poses + (size_t)(lm0 + l) * LD;
+#pragma unroll
+  for (int r = 0; r < LD; ++r) {
+    double s = D[r] * c[0];
+#pragma unroll
+    for (int k = 1; k < LD; ++k) s += D[k * LD + r] * c[k];
+    xl[r] = s;
+  }
 }
 
 // ------------------------------------------------------------------------------ oplus
@@ -760,6 +834,15 @@ __global__ void k_oplus_se2(int n, const int* __restrict__ xoff, const double* _
   s[0] += u[0];
   s[1] += u[1];
   s[2] = normalize_theta(s[2] + u[2]);
+}
+
+__global__ void k_oplus_xy(int n, const int* __restrict__ xoff, const double* __restrict__ x, double* __restrict__ st) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;  // vertex_point_xy.h:77-81
+  if (v >= n || xoff[v] < 0) return;
+  const double* u = x + xoff[v];
+  double* s = st + (size_t)v * 2;
+  s[0] += u[0];
+  s[1] += u[1];
 }
 
 // ------------------------------------------------------------------------------ reductions
@@ -920,18 +1003,20 @@ static EdgeData mk(const EdgeArgs& a) {
   return EdgeData{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
 }
 
-// host-Jacobian families: runtime (D, DA, DB) -> FamilyHostJ<D, DA, DB> (vertex dims 3 or 6, D = 1..6)
+// host-Jacobian families: runtime (D, DA, DB) -> FamilyHostJ<D, DA, DB> (vertex dims 2, 3 or 6, D = 1..6)
 template <int D, int DA, class Fn>
 static void hj_b(int DB, Fn& fn) {
-  if (DB == 3) fn(FamilyHostJ<D, DA, 3>{});
+  if (DB == 2) fn(FamilyHostJ<D, DA, 2>{});
+  else if (DB == 3) fn(FamilyHostJ<D, DA, 3>{});
   else if (DB == 6) fn(FamilyHostJ<D, DA, 6>{});
-  else throw std::runtime_error("host-Jacobian edge: vertex dimension must be 3 or 6");
+  else throw std::runtime_error("host-Jacobian edge: vertex dimension must be 2, 3 or 6");
 }
 template <int D, class Fn>
 static void hj_a(int DA, int DB, Fn& fn) {
-  if (DA == 3) hj_b<D, 3>(DB, fn);
+  if (DA == 2) hj_b<D, 2>(DB, fn);
+  else if (DA == 3) hj_b<D, 3>(DB, fn);
   else if (DA == 6) hj_b<D, 6>(DB, fn);
-  else throw std::runtime_error("host-Jacobian edge: vertex dimension must be 3 or 6");
+  else throw std::runtime_error("host-Jacobian edge: vertex dimension must be 2, 3 or 6");
 }
 template <class Fn>
 static void family_dispatch(int family, const EdgeArgs& a, Fn&& fn) {
@@ -939,6 +1024,7 @@ static void family_dispatch(int family, const EdgeArgs& a, Fn&& fn) {
     case FAM_BA: fn(FamilyBA{}); break;
     case FAM_SE3: fn(FamilySE3{}); break;
     case FAM_SE2: fn(FamilySE2{}); break;
+    case FAM_SE2XY: fn(FamilySE2XY{}); break;
     case FAM_HOSTJ:
       switch (a.D) {
         case 1: hj_a<1>(a.DA, a.DB, fn); break;
@@ -1002,7 +1088,8 @@ static void vreduce_dim(int nv, int lanes, const int* ptr, const int* code, cons
 void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, const double* slots, double* H,
                    double* b, const int* boff, hipStream_t s) {
   if (nv <= 0) return;
-  if (dim == 3) vreduce_dim<3>(nv, lanes, ptr, code, slots, H, b, boff, s);
+  if (dim == 2) vreduce_dim<2>(nv, lanes, ptr, code, slots, H, b, boff, s);
+  else if (dim == 3) vreduce_dim<3>(nv, lanes, ptr, code, slots, H, b, boff, s);
   else if (dim == 6) vreduce_dim<6>(nv, lanes, ptr, code, slots, H, b, boff, s);
   else throw std::runtime_error("vertex_reduce: unsupported dim");
 }
@@ -1014,32 +1101,54 @@ void offblock_reduce(int nb, int bsz, const int* ptr, const long long* soff, con
   KERNEL_CHECK();
 }
 
-void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
+// (pose, landmark) block sizes with Schur kernels: BlockSolver_6_3 and BlockSolver_3_2
+template <class Fn>
+static void pl_dispatch(int pd, int ld, Fn&& fn) {
+  if (pd == 6 && ld == 3) fn(std::integral_constant<int, 6>{}, std::integral_constant<int, 3>{});
+  else if (pd == 3 && ld == 2) fn(std::integral_constant<int, 3>{}, std::integral_constant<int, 2>{});
+  else throw std::runtime_error("Schur complement: (pose, landmark) dimensions must be (6, 3) or (3, 2)");
+}
+void schur_prep(int ld, int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
                 double* Ufac, double* cl_all, int* fail, hipStream_t s) {
   if (nl <= 0) return;
-  hipLaunchKernelGGL(k_schur_prep, grid_for(nl, 256), 256, 0, s, nl, lm0, Hll, bl_all, lam, Dinv, Ufac, cl_all, fail);
+  if (ld == 3)
+    hipLaunchKernelGGL(k_schur_prep<3>, grid_for(nl, 256), 256, 0, s, nl, lm0, Hll, bl_all, lam, Dinv, Ufac, cl_all, fail);
+  else if (ld == 2)
+    hipLaunchKernelGGL(k_schur_prep<2>, grid_for(nl, 256), 256, 0, s, nl, lm0, Hll, bl_all, lam, Dinv, Ufac, cl_all, fail);
+  else
+    throw std::runtime_error("schur_prep: landmark dimension must be 2 or 3");
   KERNEL_CHECK();
 }
-void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0, const double* Hpl,
-                const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp, const double* Hpp,
-                const double* b, const double* lam, double* S, double* bschur, double* G, hipStream_t s) {
+int schur_ufac_stride(int ld) { return ld == 3 ? LmTraits<3>::UF : LmTraits<2>::UF; }
+void schur_diag(int pd, int ld, int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0,
+                const double* Hpl, const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp,
+                const double* Hpp, const double* b, const double* lam, double* S, double* bschur, double* G,
+                hipStream_t s) {
   if (nrows <= 0) return;
-  hipLaunchKernelGGL(k_schur_diag, nrows, 256, 0, s, nrows, rptr, robs, obs_lm, lm0, Hpl, Ufac, cl_all,
-                     sdiag, s_hpp, Hpp, b, lam, S, bschur, G);
+  pl_dispatch(pd, ld, [&](auto P, auto L) {
+    hipLaunchKernelGGL((k_schur_diag<decltype(P)::value, decltype(L)::value>), nrows, 256, 0, s, nrows, rptr, robs,
+                       obs_lm, lm0, Hpl, Ufac, cl_all, sdiag, s_hpp, Hpp, b, lam, S, bschur, G);
+  });
   KERNEL_CHECK();
 }
-void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs, const int* pairs,
-                const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S, hipStream_t s) {
+void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
+                const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
+                hipStream_t s) {
   if (ntasks <= 0) return;
   static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;  // dev A/B only
-  hipLaunchKernelGGL(k_schur_rows, ntasks, 256, 0, s, tasks, batches, st_obs, pairs, pp, G, s_hpp, Hpp, S, mode);
+  pl_dispatch(pd, ld, [&](auto P, auto L) {
+    hipLaunchKernelGGL((k_schur_rows<decltype(P)::value, decltype(L)::value>), ntasks, 256, 0, s, tasks, batches,
+                       st_obs, pairs, pp, G, s_hpp, Hpp, S, mode);
+  });
   KERNEL_CHECK();
 }
-void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
-             int size_poses, int lm0, double* x, hipStream_t s) {
+void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv,
+             const double* b, int size_poses, int lm0, double* x, hipStream_t s) {
   if (nl <= 0) return;
-  hipLaunchKernelGGL((k_backsub<6, 4>), grid_for((size_t)nl * 4, 256), 256, 0, s, nl, lm_ptr, blk_pose, Hpl, Dinv, b,
-                     size_poses, lm0, x);
+  pl_dispatch(pd, ld, [&](auto P, auto L) {
+    hipLaunchKernelGGL((k_backsub<decltype(P)::value, decltype(L)::value, 4>), grid_for((size_t)nl * 4, 256), 256, 0,
+                       s, nl, lm_ptr, blk_pose, Hpl, Dinv, b, size_poses, lm0, x);
+  });
   KERNEL_CHECK();
 }
 
@@ -1051,6 +1160,7 @@ void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* 
     case 2: hipLaunchKernelGGL(k_oplus_xyz, g, 256, 0, s, n, xoff, x, st); break;
     case 3: hipLaunchKernelGGL(k_oplus_se3quat, g, 256, 0, s, n, xoff, x, st, nopl); break;
     case 4: hipLaunchKernelGGL(k_oplus_se2, g, 256, 0, s, n, xoff, x, st); break;
+    case 5: hipLaunchKernelGGL(k_oplus_xy, g, 256, 0, s, n, xoff, x, st); break;
   }
   KERNEL_CHECK();
 }

@@ -7,7 +7,7 @@
 
 namespace g2ohip {
 
-enum Family { FAM_NONE = 0, FAM_BA = 1, FAM_SE3 = 2, FAM_SE2 = 3, FAM_HOSTJ = 4 };
+enum Family { FAM_NONE = 0, FAM_BA = 1, FAM_SE3 = 2, FAM_SE2 = 3, FAM_HOSTJ = 4, FAM_SE2XY = 5 };
 
 struct EdgeArgs {
   const int* v0;
@@ -41,12 +41,15 @@ void linearize_fused(const EdgeArgs& a, const int4* chunks, int nchunks, const i
 void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, double* b, int num_poses, int size_poses,
               int lm_begin, hipStream_t s);
 void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, hipStream_t s);
-void schur_prep(int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
+// Schur kernels for (pd, ld) = (6, 3) (BlockSolver_6_3) and (3, 2) (BlockSolver_3_2)
+void schur_prep(int ld, int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
                 double* Ufac, double* cl_all, int* fail, hipStream_t s);
+int schur_ufac_stride(int ld);  // doubles of the per-landmark U factor record
 // diagonal blocks + bschur (and G per observation): one workgroup per camera row over its observations (CSR rptr/robs)
-void schur_diag(int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0, const double* Hpl,
-                const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp, const double* Hpp,
-                const double* b, const double* lam, double* S, double* bschur, double* G, hipStream_t s);
+void schur_diag(int pd, int ld, int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0,
+                const double* Hpl, const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp,
+                const double* Hpp, const double* b, const double* lam, double* S, double* bschur, double* G,
+                hipStream_t s);
 // row-stationary off-diagonal Schur pass (k_schur_rows): task = (camera row, <= SCHUR_SL off-diagonal
 // slots), batch = <= SCHUR_SB staged observation blocks of the row's landmarks
 constexpr int SCHUR_SB = 128, SCHUR_SL = 64;  // 128: 4 workgroups per CU (LDS), 150 vs 172 us at C4
@@ -60,10 +63,11 @@ struct SchurBatch {
   int st0, nst;  // staged blocks (st_obs)
   int pr0, npr;  // pairs (posA | posB << 16), slot CSR in pp[batch * (SCHUR_SL + 1) ...]
 };
-void schur_rows(int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs, const int* pairs,
-                const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S, hipStream_t s);
-void backsub(int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv, const double* b,
-             int size_poses, int lm0, double* x, hipStream_t s);
+void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
+                const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
+                hipStream_t s);
+void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv,
+             const double* b, int size_poses, int lm0, double* x, hipStream_t s);
 void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s);
 size_t sum_partials(long long n);
 void sum(const double* v, long long n, double* partial, double* out, hipStream_t s);

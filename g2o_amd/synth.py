@@ -10,6 +10,8 @@ Recipes:
     EDGE_SE3:QUAT), optionally with the extra lap f-2 loop closures of config C3.
   * ``se2_grid`` - SE2 lattice random walk with odometry plus up to 3 spatially
     local loop closures per pose (config C2).
+  * ``slam2d``  - 2D landmark SLAM for BlockSolver_3_2 (VERTEX_SE2 poses, VERTEX_XY landmarks, EDGE_SE2
+    odometry, EDGE_SE2_XY range-limited point observations), the shape of g2o/examples/tutorial_slam2d.
   * ``ba``      - BAL-style bundle adjustment after ``g2o/examples/ba/ba_demo.cpp:86-300``
     (VERTEX_SE3:EXPMAP cameras, VERTEX_XYZ points, EDGE_SE3_PROJECT_XYZ:EXPMAP),
     each point observed by exactly k cameras of a window of W consecutive ones.
@@ -25,11 +27,11 @@ import numpy as np
 SEED = 20261015
 
 # vertex / edge type codes (include/g2o_hip.h)
-V_SE3_EXPMAP, V_XYZ, V_SE3_QUAT, V_SE2 = 1, 2, 3, 4
-E_SE3_PROJECT_XYZ, E_SE3_QUAT, E_SE2 = 1, 2, 3
-EST_DIM = {V_SE3_EXPMAP: 7, V_XYZ: 3, V_SE3_QUAT: 7, V_SE2: 3}
-MEAS_DIM = {E_SE3_PROJECT_XYZ: 2, E_SE3_QUAT: 7, E_SE2: 3}
-ERR_DIM = {E_SE3_PROJECT_XYZ: 2, E_SE3_QUAT: 6, E_SE2: 3}
+V_SE3_EXPMAP, V_XYZ, V_SE3_QUAT, V_SE2, V_XY = 1, 2, 3, 4, 5
+E_SE3_PROJECT_XYZ, E_SE3_QUAT, E_SE2, E_SE2_XY = 1, 2, 3, 5
+EST_DIM = {V_SE3_EXPMAP: 7, V_XYZ: 3, V_SE3_QUAT: 7, V_SE2: 3, V_XY: 2}
+MEAS_DIM = {E_SE3_PROJECT_XYZ: 2, E_SE3_QUAT: 7, E_SE2: 3, E_SE2_XY: 2}
+ERR_DIM = {E_SE3_PROJECT_XYZ: 2, E_SE3_QUAT: 6, E_SE2: 3, E_SE2_XY: 2}
 
 
 @dataclasses.dataclass
@@ -291,6 +293,90 @@ def se2_grid(num_poses: int = 1000, loops_per_pose: int = 3, radius: float = 2.0
     verts = VertexSet(V_SE2, np.arange(N, dtype=np.int32), est, fixed, np.zeros(N, np.int32))
     edges = EdgeSet(E_SE2, a.astype(np.int32), b.astype(np.int32), meas, np.broadcast_to(info, (m, 3, 3)).copy())
     return Problem(f"se2grid{N}", [verts], [edges], 3, 0)
+
+
+# ---------------------------------------------------------------- 2D landmark SLAM (BlockSolver_3_2)
+def slam2d(num_poses: int = 1000, landmarks_per_cell: float = 1.0, sensor_range: float = 2.5,
+           max_obs_per_pose: int = 8, odo_noise=(0.05, 0.05, 0.01), point_noise=(0.05, 0.05),
+           seed: int = SEED) -> Problem:
+    """SE2 lattice random walk (as ``se2_grid``) with XY landmarks scattered over the visited area
+    (``landmarks_per_cell`` per unit cell); every pose observes up to ``max_obs_per_pose`` nearest landmarks
+    within ``sensor_range`` (EdgeSE2PointXY: z = x_i^-1 * l + noise), consecutive poses are joined by EdgeSE2
+    odometry. Landmarks nobody observes are dropped; pose 0 is fixed; landmarks are marginalised (Schur).
+    Initial estimates: chained noisy odometry for the poses, each landmark from its first observation."""
+    rng = _rng(seed, 4)
+    N = num_poses
+    turns = rng.choice([-1, 0, 0, 1], size=N)
+    heading = np.zeros(N, np.int64)
+    pos = np.zeros((N, 2), np.int64)
+    dirs = np.array([[1, 0], [0, 1], [-1, 0], [0, -1]])
+    for i in range(1, N):
+        heading[i] = (heading[i - 1] + turns[i]) % 4
+        pos[i] = pos[i - 1] + dirs[heading[i]]
+    th = np.mod(heading * (np.pi / 2) + np.pi, 2 * np.pi) - np.pi
+    gt = np.stack([pos[:, 0].astype(float), pos[:, 1].astype(float), th], axis=1)
+    # landmarks: uniform over the cells within sensor range of the trajectory
+    r = int(math.ceil(sensor_range))
+    cells = {(int(x) + dx, int(y) + dy) for x, y in pos for dx in range(-r, r + 1) for dy in range(-r, r + 1)}
+    cells = sorted(cells)
+    nper = rng.poisson(landmarks_per_cell, size=len(cells))
+    lm = np.concatenate([np.asarray(c, float)[None] + rng.random((k, 2)) for c, k in zip(cells, nper) if k > 0])
+    grid: dict = {}
+    for j, (x, y) in enumerate(lm):
+        grid.setdefault((int(math.floor(x)), int(math.floor(y))), []).append(j)
+    oa, ob = [], []
+    for i in range(N):
+        px, py = gt[i, 0], gt[i, 1]
+        cand = [j for dx in range(-r - 1, r + 2) for dy in range(-r - 1, r + 2)
+                for j in grid.get((int(math.floor(px)) + dx, int(math.floor(py)) + dy), ())]
+        if not cand:
+            continue
+        cand = np.asarray(cand)
+        d2 = (lm[cand, 0] - px) ** 2 + (lm[cand, 1] - py) ** 2
+        keep = cand[d2 <= sensor_range ** 2]
+        keep = keep[np.argsort(d2[d2 <= sensor_range ** 2], kind="stable")][:max_obs_per_pose]
+        for j in np.sort(keep):
+            oa.append(i)
+            ob.append(j)
+    oa = np.asarray(oa, np.int64)
+    ob = np.asarray(ob, np.int64)
+    used = np.unique(ob)
+    remap = -np.ones(len(lm), np.int64)
+    remap[used] = np.arange(len(used))
+    lm = lm[used]
+    ob = remap[ob]
+    L = len(lm)
+    # measurements
+    c, s_ = np.cos(gt[oa, 2]), np.sin(gt[oa, 2])
+    dx, dy = lm[ob, 0] - gt[oa, 0], lm[ob, 1] - gt[oa, 1]
+    zo = np.stack([c * dx + s_ * dy, -s_ * dx + c * dy], axis=1) + rng.standard_normal((len(oa), 2)) * np.asarray(point_noise)
+    a = np.arange(N - 1)
+    rel = _se2_between(gt[a], gt[a + 1])
+    zodo = rel + rng.standard_normal((N - 1, 3)) * np.asarray(odo_noise)
+    zodo[:, 2] = np.mod(zodo[:, 2] + np.pi, 2 * np.pi) - np.pi
+    est = np.empty((N, 3))
+    est[0] = gt[0]
+    for i in range(1, N):
+        est[i] = _se2_compose(est[i - 1], zodo[i - 1])
+    lest = np.zeros((L, 2))
+    seen = np.zeros(L, bool)
+    for k in range(len(oa)):
+        j = ob[k]
+        if seen[j]:
+            continue
+        seen[j] = True
+        i = oa[k]
+        cc, ss = math.cos(est[i, 2]), math.sin(est[i, 2])
+        lest[j] = [est[i, 0] + cc * zo[k, 0] - ss * zo[k, 1], est[i, 1] + ss * zo[k, 0] + cc * zo[k, 1]]
+    fixed = np.zeros(N, np.int32)
+    fixed[0] = 1
+    pose_ids = np.arange(N, dtype=np.int32)
+    lm_ids = (N + np.arange(L)).astype(np.int32)
+    poses = VertexSet(V_SE2, pose_ids, est, fixed, np.zeros(N, np.int32))
+    points = VertexSet(V_XY, lm_ids, lest, np.zeros(L, np.int32), np.ones(L, np.int32))
+    odo = EdgeSet(E_SE2, pose_ids[a], pose_ids[a + 1], zodo, np.broadcast_to(np.diag(1.0 / np.square(odo_noise)), (N - 1, 3, 3)).copy())
+    obs = EdgeSet(E_SE2_XY, pose_ids[oa], lm_ids[ob], zo, np.broadcast_to(np.diag(1.0 / np.square(point_noise)), (len(oa), 2, 2)).copy())
+    return Problem(f"slam2d{N}x{L}", [poses, points], [odo, obs], 3, 2)
 
 
 # ---------------------------------------------------------------- BA

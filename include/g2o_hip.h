@@ -33,13 +33,16 @@ extern "C" {
 #define G2OHIP_V_XYZ 2        /* VertexSBAPointXYZ, types_sba.h:137: x y z */
 #define G2OHIP_V_SE3_QUAT 3   /* VertexSE3, vertex_se3.h:50: x y z qx qy qz qw (toVectorQT) */
 #define G2OHIP_V_SE2 4        /* VertexSE2, vertex_se2.h:40: x y theta */
+#define G2OHIP_V_XY 5         /* VertexPointXY, vertex_point_xy.h:39-88: x y (a BlockSolver_3_2 landmark) */
 /* ---- edge types ---- */
 #define G2OHIP_E_SE3_PROJECT_XYZ 1 /* EdgeSE3ProjectXYZ, types_six_dof_expmap.h:201-229: v0 point, v1 camera;
                                       meas u v; info 2x2; params fx fy cx cy */
 #define G2OHIP_E_SE3_QUAT 2        /* EdgeSE3, edge_se3.h: meas x y z qx qy qz qw; info 6x6 */
 #define G2OHIP_E_SE2 3             /* EdgeSE2, edge_se2.h:46-52: meas x y theta; info 3x3 */
+#define G2OHIP_E_SE2_XY 5          /* EdgeSE2PointXY, edge_se2_pointxy.h:41-75: v0 SE2 pose, v1 XY point; meas x y;
+                                      info 2x2 */
 /* An edge type the device does not know (any BaseBinaryEdge<D, E, Vi, Vj> between registered vertices of
- * dimension 3 or 6): the host's own linearizeOplus (the type's analytic one, or BaseBinaryEdge's numeric
+ * dimension 2, 3 or 6): the host's own linearizeOplus (the type's analytic one, or BaseBinaryEdge's numeric
  * central differences, base_binary_edge.hpp:198-266) supplies the error and both Jacobians, see
  * g2ohip_set_host_jacobians; the device assembles, marginalises and solves. meas unused (may be NULL);
  * info D*D. Several host-J types (different D) may coexist with the device types in one graph. */

@@ -242,6 +242,7 @@ int vdim(int type) {
     case ORACLE_V_XYZ: return 3;
     case ORACLE_V_SE3_QUAT: return 6;
     case ORACLE_V_SE2: return 3;
+    case ORACLE_V_XY: return 2;
   }
   return -1;
 }
@@ -251,6 +252,7 @@ int edim(int type) {
     case ORACLE_E_SE3_QUAT: return 6;
     case ORACLE_E_SE2: return 3;
     case ORACLE_E_SE3_EXPMAP: return 6;
+    case ORACLE_E_SE2_XY: return 2;
   }
   return -1;
 }
@@ -584,6 +586,10 @@ void vertexOplus(Vertex& v, const double* u) {
       v.est.se2.th = normalize_theta(v.est.se2.th + u[2]);
       break;
     }
+    case ORACLE_V_XY:  // vertex_point_xy.h:77-81
+      v.est.p.x += u[0];
+      v.est.p.y += u[1];
+      break;
   }
 }
 void vpush(Vertex& v) { v.stack.push_back(v.est); }
@@ -625,6 +631,13 @@ void computeError(const Graph& G, Edge& e) {
       e.err[0] = delta.x;
       e.err[1] = delta.y;
       e.err[2] = delta.th;
+      break;
+    }
+    case ORACLE_E_SE2_XY: {  // edge_se2_pointxy.h:44-49: v1^-1 * l - z (se2.h:77-80 SE2 * Vector2 = t + R v)
+      const SE2 inv = se2inv(a.est.se2);
+      const double c = std::cos(inv.th), s = std::sin(inv.th);
+      e.err[0] = (inv.x + (c * b.est.p.x - s * b.est.p.y)) - e.meas[0];
+      e.err[1] = (inv.y + (s * b.est.p.x + c * b.est.p.y)) - e.meas[1];
       break;
     }
   }
@@ -756,6 +769,22 @@ void linearizeOplus(const Graph& G, const Edge& e, double* Ji, double* Jj) {
           Ji[r * 3 + cc] = a;
           Jj[r * 3 + cc] = b;
         }
+      break;
+    }
+    case ORACLE_E_SE2_XY: {  // edge_se2_pointxy.cpp:63-87
+      const double x1 = va.est.se2.x, y1 = va.est.se2.y, th1 = va.est.se2.th;
+      const double x2 = vb.est.p.x, y2 = vb.est.p.y;
+      const double aux_1 = std::cos(th1), aux_2 = -aux_1, aux_3 = std::sin(th1);
+      Ji[0] = aux_2;
+      Ji[1] = -aux_3;
+      Ji[2] = aux_1 * y2 - aux_1 * y1 - aux_3 * x2 + aux_3 * x1;
+      Ji[3] = aux_3;
+      Ji[4] = aux_2;
+      Ji[5] = -aux_3 * y2 + aux_3 * y1 - aux_1 * x2 + aux_1 * x1;
+      Jj[0] = aux_1;
+      Jj[1] = aux_3;
+      Jj[2] = -aux_3;
+      Jj[3] = aux_1;
       break;
     }
   }
@@ -1143,7 +1172,13 @@ bool BlockSolver::solve(int threads, oracle_batch_stats* st) {  // :314-447
     double* Dinv = DInv.data() + DInvOff[l];
     if (ld == 3) {
       inverse3(Dm, Dinv);
-    } else {  // generic: Gauss-Jordan (only used for non-3 landmark dims)
+    } else if (ld == 2) {  // Eigen compute_inverse_size2 (BlockSolver_3_2's Matrix2 inverse)
+      const double invdet = 1.0 / (Dm[0] * Dm[3] - Dm[1] * Dm[2]);
+      Dinv[0] = Dm[3] * invdet;
+      Dinv[1] = -Dm[1] * invdet;
+      Dinv[2] = -Dm[2] * invdet;
+      Dinv[3] = Dm[0] * invdet;
+    } else {  // generic: Gauss-Jordan (only used for other landmark dims)
       std::vector<double> M(Dm, Dm + ld * ld), I(ld * ld, 0.0);
       for (int k = 0; k < ld; ++k) I[k * ld + k] = 1;
       for (int c = 0; c < ld; ++c) {
@@ -1378,7 +1413,7 @@ int addEdgeRaw(Graph& G, int type, int id0, int id1, const double* meas, const d
   e.D = edim(type);
   e.v[0] = a->second;
   e.v[1] = b->second;
-  const int nm = type == ORACLE_E_SE3_PROJECT_XYZ ? 2 : (type == ORACLE_E_SE3_QUAT || type == ORACLE_E_SE3_EXPMAP ? 7 : 3);
+  const int nm = type == ORACLE_E_SE3_PROJECT_XYZ || type == ORACLE_E_SE2_XY ? 2 : (type == ORACLE_E_SE3_QUAT || type == ORACLE_E_SE3_EXPMAP ? 7 : 3);
   std::memcpy(e.meas, meas, sizeof(double) * nm);
   e.numeric = type == ORACLE_E_SE3_EXPMAP;  // no analytic Jacobian restated: base_binary_edge.hpp:198-266
   std::memcpy(e.info, info, sizeof(double) * e.D * e.D);
@@ -1402,9 +1437,12 @@ void setVertexEstimate(Vertex& v, const double* est) {
     case ORACLE_V_XYZ: v.est.p = {est[0], est[1], est[2]}; break;
     case ORACLE_V_SE3_QUAT: v.est.iso = fromVectorQT(est); break;  // vertex_se3.cpp:49-55
     case ORACLE_V_SE2: v.est.se2.x = est[0]; v.est.se2.y = est[1]; v.est.se2.th = est[2]; break;
+    case ORACLE_V_XY: v.est.p = {est[0], est[1], 0.0}; break;
   }
 }
-int estDim(int type) { return type == ORACLE_V_SE3_EXPMAP || type == ORACLE_V_SE3_QUAT ? 7 : 3; }
+int estDim(int type) {
+  return type == ORACLE_V_SE3_EXPMAP || type == ORACLE_V_SE3_QUAT ? 7 : (type == ORACLE_V_XY ? 2 : 3);
+}
 void getVertexEstimate(const Vertex& v, double* out) {
   switch (v.type) {
     case ORACLE_V_SE3_EXPMAP:
@@ -1414,6 +1452,7 @@ void getVertexEstimate(const Vertex& v, double* out) {
     case ORACLE_V_XYZ: out[0] = v.est.p.x; out[1] = v.est.p.y; out[2] = v.est.p.z; break;
     case ORACLE_V_SE3_QUAT: toVectorQT(v.est.iso, out); break;
     case ORACLE_V_SE2: out[0] = v.est.se2.x; out[1] = v.est.se2.y; out[2] = v.est.se2.th; break;
+    case ORACLE_V_XY: out[0] = v.est.p.x; out[1] = v.est.p.y; break;
   }
 }
 void minimalEstimate(const Vertex& v, double* out) {
@@ -1465,7 +1504,7 @@ int oracle_add_edges(OracleGraph* og, int type, int n, const int* v0, const int*
   Graph& G = og->g;
   const int D = edim(type);
   if (D < 0) return -1;
-  const int nm = type == ORACLE_E_SE3_PROJECT_XYZ ? 2 : (type == ORACLE_E_SE3_QUAT || type == ORACLE_E_SE3_EXPMAP ? 7 : 3);
+  const int nm = type == ORACLE_E_SE3_PROJECT_XYZ || type == ORACLE_E_SE2_XY ? 2 : (type == ORACLE_E_SE3_QUAT || type == ORACLE_E_SE3_EXPMAP ? 7 : 3);
   G.edges.reserve(G.edges.size() + n);
   for (int k = 0; k < n; ++k) {
     int r = addEdgeRaw(G, type, v0[k], v1[k], meas + (size_t)k * nm, info + (size_t)k * D * D,
@@ -1509,6 +1548,11 @@ int oracle_load_g2o(OracleGraph* og, const char* path, int marginalize_xyz) {
       ss >> id >> v[0] >> v[1] >> v[2];
       int z = 0;
       oracle_add_vertices(og, ORACLE_V_SE2, 1, &id, v, &z, &z);
+    } else if (tag == "VERTEX_XY") {  // vertex_point_xy.cpp:46-50
+      int id; double v[2];
+      ss >> id >> v[0] >> v[1];
+      int z = 0, m = marginalize_xyz ? 1 : 0;
+      oracle_add_vertices(og, ORACLE_V_XY, 1, &id, v, &z, &m);
     } else if (tag == "FIX") {
       int id;
       while (ss >> id) fixIds.push_back(id);
@@ -1529,6 +1573,11 @@ int oracle_load_g2o(OracleGraph* og, const char* path, int marginalize_xyz) {
       for (int i = 0; i < 3; ++i)
         for (int j = i; j < 3; ++j) { ss >> info[i * 3 + j]; info[j * 3 + i] = info[i * 3 + j]; }
       if (addEdgeRaw(G, ORACLE_E_SE2, a, b, m, info, nullptr)) return -3;
+    } else if (tag == "EDGE_SE2_XY") {  // edge_se2_pointxy.cpp:46-52
+      int a, b; double m[2], o[3];
+      ss >> a >> b >> m[0] >> m[1] >> o[0] >> o[1] >> o[2];
+      double info[4] = {o[0], o[1], o[1], o[2]};
+      if (addEdgeRaw(G, ORACLE_E_SE2_XY, a, b, m, info, nullptr)) return -3;
     }
   }
   for (int id : fixIds) {
@@ -1554,6 +1603,8 @@ int oracle_save_g2o(OracleGraph* og, const char* path) {
     } else if (v.type == ORACLE_V_SE3_QUAT) {
       fprintf(f, "VERTEX_SE3:QUAT %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", v.id, e[0], e[1], e[2], e[3], e[4],
               e[5], e[6]);
+    } else if (v.type == ORACLE_V_XY) {
+      fprintf(f, "VERTEX_XY %d %.17g %.17g\n", v.id, e[0], e[1]);
     } else {
       fprintf(f, "VERTEX_SE2 %d %.17g %.17g %.17g\n", v.id, e[0], e[1], e[2]);
     }
@@ -1566,8 +1617,8 @@ int oracle_save_g2o(OracleGraph* og, const char* path) {
               e.meas[0], e.meas[1], e.info[0], e.info[1], e.info[3], e.params[0], e.params[1], e.params[2],
               e.params[3]);
     } else {
-      const char* tag = e.type == ORACLE_E_SE3_QUAT ? "EDGE_SE3:QUAT" : "EDGE_SE2";
-      int nm = e.type == ORACLE_E_SE3_QUAT ? 7 : 3;
+      const char* tag = e.type == ORACLE_E_SE3_QUAT ? "EDGE_SE3:QUAT" : (e.type == ORACLE_E_SE2_XY ? "EDGE_SE2_XY" : "EDGE_SE2");
+      int nm = e.type == ORACLE_E_SE3_QUAT ? 7 : (e.type == ORACLE_E_SE2_XY ? 2 : 3);
       fprintf(f, "%s %d %d", tag, a, b);
       for (int k = 0; k < nm; ++k) fprintf(f, " %.17g", e.meas[k]);
       for (int i = 0; i < e.D; ++i)

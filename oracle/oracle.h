@@ -14,12 +14,15 @@ extern "C" {
 #define ORACLE_V_XYZ 2        /* est: x y z */
 #define ORACLE_V_SE3_QUAT 3   /* est: x y z qx qy qz qw (toVectorQT) */
 #define ORACLE_V_SE2 4        /* est: x y theta */
+#define ORACLE_V_XY 5         /* VertexPointXY (slam2d/vertex_point_xy.h:39-88), est: x y */
 /* edge types */
 #define ORACLE_E_SE3_PROJECT_XYZ 1 /* v0 = point, v1 = camera; meas u v; info 2x2; params fx fy cx cy */
 #define ORACLE_E_SE3_QUAT 2        /* meas x y z qx qy qz qw; info 6x6 */
 #define ORACLE_E_SE2 3             /* meas x y theta; info 3x3 */
 #define ORACLE_E_SE3_EXPMAP 4      /* EdgeSE3Expmap (types_six_dof_expmap.h:108-127) between two VertexSE3Expmap:
                                       meas tx ty tz qx qy qz qw; info 6x6; Jacobians always numeric here */
+#define ORACLE_E_SE2_XY 5          /* EdgeSE2PointXY (slam2d/edge_se2_pointxy.h:41-75): v0 = SE2 pose, v1 = XY point;
+                                      meas x y; info 2x2 */
 
 typedef struct {
   int iteration;
@@ -80,7 +83,7 @@ int oracle_optimize(OracleGraph* g, const oracle_config* cfg, int iterations, or
  *   dims[2]=nl (landmark scalars).  Any output pointer may be NULL. */
 int oracle_stage(OracleGraph* g, const oracle_config* cfg, double lambda, double* b, double* x, double* Hschur,
                  double* bschur, long long* dims);
-/* Dense Hessian blocks: Hpp[np*np] (full sym), Hll[nl*3] (diag blocks, col-major per landmark),
+/* Dense Hessian blocks: Hpp[np*np] (full sym), Hll[nl*l] (diag blocks, col-major per landmark, l = dim),
  * Hpl[np*nl] dense.  Small problems only. */
 int oracle_hessian_dense(OracleGraph* g, double* Hpp, double* Hll_diag, double* Hpl);
 

@@ -68,6 +68,38 @@ def test_edge_se2_jacobian_vs_numeric(oracle, trials):
     assert worst < 1e-6, worst
 
 
+@pytest.mark.parametrize("trials", [2000])
+def test_edge_se2_pointxy_jacobian_vs_numeric(oracle, trials):
+    """unit_test/slam2d/jacobians_slam2d.cpp:123-150 (EdgeSE2PointXYJacobian): analytic vs numeric, 1e-6."""
+    worst = 0.0
+    for _ in range(trials):
+        vs = [synth.VertexSet(synth.V_SE2, np.array([0], np.int32), random_se2()[None], np.zeros(1, np.int32),
+                              np.zeros(1, np.int32)),
+              synth.VertexSet(synth.V_XY, np.array([1], np.int32), RNG.uniform(-1, 1, (1, 2)), np.zeros(1, np.int32),
+                              np.ones(1, np.int32))]
+        es = synth.EdgeSet(synth.E_SE2_XY, np.array([0], np.int32), np.array([1], np.int32),
+                           RNG.uniform(-1, 1, (1, 2)), np.eye(2)[None])
+        g = oracle.OracleGraph(synth.Problem("j", vs, [es], 3, 2))
+        _, Ja, Jb, Na, Nb = g.edge_jacobians(0, 2, 3, 2)
+        worst = max(worst, np.abs(Ja - Na).max(), np.abs(Jb - Nb).max())
+    assert worst < 1e-6, worst
+
+
+def test_slam2d_oracle_file_roundtrip(oracle, tmp_path):
+    """VERTEX_XY / EDGE_SE2_XY reader and writer of the oracle (vertex_point_xy.cpp:46-56,
+    edge_se2_pointxy.cpp:46-61): same chi2 after a save/load cycle, and the LM converges."""
+    prob = synth.slam2d(200)
+    g = oracle.OracleGraph(prob)
+    path = str(tmp_path / "s.g2o")
+    g.save(path)
+    h = oracle.OracleGraph.load(path)
+    chi0 = g.chi2()
+    assert abs(h.chi2() - chi0) <= 1e-12 * chi0
+    n, st = h.optimize(8)
+    assert n == 8 and st[-1].chi2 < 0.05 * chi0
+    assert st[-1].hessianPoseDimension == 3 * 199 and st[-1].hessianLandmarkDimension == 2 * prob.vertices[1].ids.size
+
+
 def test_edge_se3_project_xyz_jacobian_vs_numeric(oracle):
     prob = synth.ba(12, 300, 5, 8)
     g = oracle.OracleGraph(prob)

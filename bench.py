@@ -31,7 +31,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="C4", help="C4 (default, BASELINE metric) or C5/C3/C2/C1")
+    ap.add_argument("--config", default="C4", help="C4 (default, BASELINE metric) or C5/C3/C2/C1; C4R (random covisibility), S2 (BlockSolver_3_2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=6, help="timed oracle LM iterations (after iteration 0)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="OpenMP threads for the CPU baseline (0 = all)")
@@ -224,7 +224,8 @@ def main():
     prob = make_problem(args.config)
     gen_s = time.time() - t0
     opt = g2o_amd.SparseOptimizer(local).add_problem(prob)
-    opt.set_algorithm("lm_hip_fix6_3" if prob.landmark_dim else ("lm_hip_fix6_6" if prob.pose_dim == 6 else "lm_hip_fix3_3"))
+    pd, ldim = prob.pose_dim, prob.landmark_dim
+    opt.set_algorithm(f"lm_hip_fix{pd}_{ldim}" if ldim else f"lm_hip_fix{pd}_{pd}")
     if world > 1:
         uid = g2o_amd.SparseOptimizer.comm_unique_id() if rank == 0 else None
         uid = bcast_bytes(uid, world)

@@ -407,9 +407,17 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       // k_extend_add: every front's first-diagonal-block task first, then the slabs
       // small levels (all fronts <= pre_max bytes together) are zeroed + scattered before the first level
       // (two massively parallel passes off the critical chain); large ones are assembled in place
-      long long lbytes = 0;
-      for (int sn : lv) lbytes += 8LL * (sym.sn[sn].ns + sym.sn[sn].nr) * (sym.sn[sn].ns + sym.sn[sn].nr);
-      const bool pre = lbytes <= pre_max;
+      // levels whose fronts are mostly input entries (a dense reduced system: few children) are pre-scattered
+      // too, whatever their size: one thread per entry instead of a dependent gather chain per front column
+      long long lbytes = 0, lent = 0, ltri = 0;
+      for (int sn : lv) {
+        const Supernode& q = sym.sn[sn];
+        const long long m = q.ns + q.nr;
+        lbytes += 8LL * m * m;
+        lent += cpv[q.c0 + q.ns] - cpv[q.c0];
+        ltri += (long long)q.ns * (2 * m - q.ns + 1) / 2;
+      }
+      const bool pre = lbytes <= pre_max || 2 * lent >= ltri;
       (pre ? n_pre_levels : n_inplace_levels)++;
       if (pre)
         for (int sn : lv) {

@@ -450,6 +450,10 @@ def by_name(name: str, scale: str = "full") -> Problem:
         return ba(40, 1500) if small else ba(1000, 100_000)
     if name == "C5":
         return ba(80, 4000) if small else ba(4000, 1_000_000)
+    if name == "C4R":  # C4 with random covisibility (dense reduced camera system)
+        return ba(120, 3000, window=120) if small else ba(1000, 100_000, window=1000)
+    if name == "S2":  # BlockSolver_3_2: 2D landmark SLAM (not a BASELINE config)
+        return slam2d(300) if small else slam2d(100_000)
     raise KeyError(name)
 
 

@@ -164,6 +164,17 @@ def test_lm_blocked_fronts_sphere2500(g2o_amd_mod, oracle, monkeypatch, pre_max)
     _check(*_run_both(g2o_amd_mod, oracle, prob, 3))
 
 
+def test_lm_ba_random_covisibility(g2o_amd_mod, oracle):
+    """SURVEY.md §8d's C4 variant covis=random at reduced size: every point seen by 10 of all 450 cameras, so the
+    reduced camera system is dense (2688 columns, one wide supernode) and takes the blocked dense-front schedule
+    (big panels, rank-256 trailing updates) with the default settings."""
+    prob = synth.ba(450, 8000, window=450)
+    opt, n, st, ref, nr, sr = _run_both(g2o_amd_mod, oracle, prob, 2, threads=16)
+    _check(opt, n, st, ref, nr, sr)
+    fi = opt.factor_info()
+    assert fi["blocked_fronts"] >= 1 and fi["max_front"] >= 2000, fi
+
+
 def test_g2o_file_roundtrip_parity(g2o_amd_mod, oracle, tmp_path):
     prob = synth.by_name("C4", "small")
     path = str(tmp_path / "ba.g2o")

@@ -62,15 +62,17 @@ __device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err
 }
 }  // namespace
 
-template <class F>
+template <class F, bool FG>
 __global__ void __launch_bounds__(256)
     k_linearize_fused(EdgeData d, const int4* __restrict__ chunks, int nchunks, const int* __restrict__ h0,
                       const int* __restrict__ h1, const long long* __restrict__ off_dst,
                       const unsigned char* __restrict__ off_tr, double* __restrict__ off_base,
                       double* __restrict__ off_slot, double* __restrict__ Hll, double* __restrict__ bvec,
-                      int num_poses, int size_poses, int lm_begin, double* __restrict__ lpart) {
+                      int num_poses, int size_poses, int lm_begin, double* __restrict__ lpart, launch::SchurSplit sp) {
   constexpr int D = F::D, DA = F::DA, DB = F::DB;
   constexpr int SA = DA * (DA + 1) / 2 + DA, SH = DA * DB, SM = SA > SH ? SA : SH;
+  constexpr int UF = 2 * DA;  // U record of a DA = 3 landmark (FG instantiations are BA only)
+  static_assert(!FG || (DA == 3 && 64 * SA + 64 * UF <= 64 * SM), "U records live behind the landmark terms");
   __shared__ __attribute__((aligned(16))) double stage[4][64 * SM];
   __shared__ int lmid[4][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -104,20 +106,24 @@ __global__ void __launch_bounds__(256)
       for (int r = 0; r < D; ++r) s += A[r * DA + i] * Om[r * D + c];
       AtO[i * D + c] = s;
     }
-  // off-diagonal (Hpl) block, as k_linearize: a coalesced run through LDS when the wave's blocks are consecutive
-  {
+  // off-diagonal (Hpl) block, as k_linearize: a coalesced run through LDS when the wave's blocks are consecutive.
+  // With a Schur split it is G = Hpl U^-T instead (U of the lane's landmark, known after the landmark sums below;
+  // split landmarks store Hpl and k_lm_fixup forms their G)
+  auto off_block = [&](const double* U) {
     constexpr long long SLOT_BIT = 1LL << 62;
     const long long od_raw = (nfA && nfB) ? off_dst[e] : -1;
     const bool in_slot = od_raw >= 0 && (od_raw & SLOT_BIT);
-    const long long od = od_raw >= 0 ? (od_raw & ~SLOT_BIT) : -1;
+    const long long od = od_raw >= 0 ? (od_raw & ~SLOT_BIT) - (FG ? sp.hpl_base : 0) : -1;
+    double* base = FG ? sp.G : off_base;
     const bool tr = nfA && nfB && off_tr[e];
     const long long od0 = __shfl(od, 0, 64);
     const bool tr0 = __shfl((int)tr, 0, 64) != 0;
     const bool slot0f = __shfl((int)in_slot, 0, 64) != 0;
     const bool run = __all(!in || (od >= 0 && od0 >= 0 && od == od0 + (long long)lane * SH && tr == tr0 && in_slot == slot0f));
     if (od >= 0) {
-      double* H = run ? sw + lane * SH : (in_slot ? off_slot : off_base) + od;
-      if (tr) {
+      double* H = run ? sw + lane * SH : (in_slot ? off_slot : base) + od;
+      if (FG || tr) {  // (pose, landmark) block, column-major: H[i * DB + j] = (A^T Omega B)(i, j)
+        double g[SH];
 #pragma unroll
         for (int i = 0; i < DA; ++i)
 #pragma unroll
@@ -125,8 +131,13 @@ __global__ void __launch_bounds__(256)
             double s = 0;
 #pragma unroll
             for (int r = 0; r < D; ++r) s += AtO[i * D + r] * B[r * DB + j];
-            H[i * DB + j] = s;
+            g[i * DB + j] = s;
           }
+        if constexpr (FG) {
+          if (ch.z < 0) form_G<DB, DA>(g, U);
+        }
+#pragma unroll
+        for (int k = 0; k < SH; ++k) H[k] = g[k];
       } else {
 #pragma unroll
         for (int j = 0; j < DB; ++j)
@@ -141,10 +152,11 @@ __global__ void __launch_bounds__(256)
     }
     if (run) {
       wsync();
-      copy_out((slot0f ? off_slot : off_base) + od0, sw, nw * SH, lane);
+      copy_out((slot0f ? off_slot : base) + od0, sw, nw * SH, lane);
     }
     wsync();
-  }
+  };
+  if constexpr (!FG) off_block(nullptr);
   // landmark-side terms of every lane (zeros when the landmark is fixed), then segment sums in edge order
   {
     double* o = sw + lane * SA;
@@ -190,17 +202,56 @@ __global__ void __launch_bounds__(256)
       double* bb = bvec + size_poses + (size_t)(hA - num_poses) * DA;
 #pragma unroll
       for (int i = 0; i < DA; ++i) bb[i] = acc[DA * (DA + 1) / 2 + i];
+      if constexpr (FG) {  // Hll + lambda I = U U^T, c = U^-1 b_l (k_schur_prep's arithmetic)
+        double a[DA * DA];
+        int q = 0;
+#pragma unroll
+        for (int c = 0; c < DA; ++c)
+#pragma unroll
+          for (int r = 0; r <= c; ++r) {
+            a[c * DA + r] = acc[q];
+            a[r * DA + c] = acc[q];
+            ++q;
+          }
+#pragma unroll
+        for (int i = 0; i < DA; ++i) a[i * DA + i] += sp.lam;
+        double U[UF], cl[DA];
+        if (!lm_ufac<DA>(a, acc + DA * (DA + 1) / 2, U, cl)) *sp.fail = 1;
+        double* Uo = sp.Ufac + (size_t)(hA - num_poses - lm_begin) * UF;
+        double* co = sp.cl + (size_t)(hA - num_poses) * DA;
+#pragma unroll
+        for (int k2 = 0; k2 < UF; ++k2) {
+          Uo[k2] = U[k2];
+          sw[64 * SA + lane * UF + k2] = U[k2];
+        }
+#pragma unroll
+        for (int i = 0; i < DA; ++i) co[i] = cl[i];
+      }
     } else {  // one landmark of > 64 observations: this chunk's partial
 #pragma unroll
       for (int k = 0; k < SA; ++k) lpart[(size_t)ch.z * SA + k] = acc[k];
     }
   }
+  if constexpr (FG) {
+    wsync();
+    // the lane's segment head: the highest head lane at or below it
+    const unsigned long long hm = __ballot(head);
+    const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1);
+    const int hl = 63 - __clzll(hm & le);
+    double U[UF];
+#pragma unroll
+    for (int k = 0; k < UF; ++k) U[k] = sw[64 * SA + (hl & 63) * UF + k];
+    wsync();  // every U read before the run image reuses the stage
+    off_block(U);
+  }
 }
 
-// split landmarks: fix = (hessian index, first partial, count); partials added in chunk order
+// split landmarks: fix = (hessian index, first partial, count); partials added in chunk order. With a Schur split the
+// landmark's U, c follow, and its G blocks (stored as Hpl by the linearize chunks) are formed in place.
+template <bool FG>
 __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restrict__ fix, const double* __restrict__ lpart,
                                                   double* __restrict__ Hll, double* __restrict__ bvec, int num_poses,
-                                                  int size_poses, int lm_begin) {
+                                                  int size_poses, int lm_begin, launch::SchurSplit sp) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nfix) return;
   const int4 f = fix[i];
@@ -211,7 +262,8 @@ __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restri
   for (int p = f.y; p < f.y + f.z; ++p)
 #pragma unroll
     for (int k = 0; k < SA; ++k) acc[k] += lpart[(size_t)p * SA + k];
-  double* H = Hll + (size_t)(f.x - num_poses - lm_begin) * 9;
+  const int l = f.x - num_poses - lm_begin;
+  double* H = Hll + (size_t)l * 9;
   int k = 0;
 #pragma unroll
   for (int c = 0; c < 3; ++c)
@@ -223,24 +275,61 @@ __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restri
     }
   double* bb = bvec + size_poses + (size_t)(f.x - num_poses) * 3;
   bb[0] = acc[6]; bb[1] = acc[7]; bb[2] = acc[8];
+  if constexpr (FG) {
+    double a[9];
+    int q = 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int r = 0; r <= c; ++r) {
+        a[c * 3 + r] = acc[q];
+        a[r * 3 + c] = acc[q];
+        ++q;
+      }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) a[j * 3 + j] += sp.lam;
+    double U[6], cl[3];
+    if (!lm_ufac<3>(a, acc + 6, U, cl)) *sp.fail = 1;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) sp.Ufac[(size_t)l * 6 + j] = U[j];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sp.cl[(size_t)(f.x - num_poses) * 3 + j] = cl[j];
+    for (int a2 = sp.lm_ptr[l]; a2 < sp.lm_ptr[l + 1]; ++a2) {
+      double g[18];
+      double* gp = sp.G + (size_t)a2 * 18;
+#pragma unroll
+      for (int j = 0; j < 18; ++j) g[j] = gp[j];
+      form_G<6, 3>(g, U);
+#pragma unroll
+      for (int j = 0; j < 18; ++j) gp[j] = g[j];
+    }
+  }
 }
 
 // camera-side terms: one workgroup per pose, threads stride over its observations (camera-major copy of the
-// edge data, ascending landmark-major edge order), 27 accumulators per thread, fixed-tree reduction
-template <class F>
+// edge data, ascending landmark-major edge order), 27 accumulators per thread, fixed-tree reduction. With a Schur
+// split the same pass forms each observation's G = Hpl U^-T (the linearize lane's arithmetic, U and c of its
+// landmark) and accumulates the diagonal Schur terms G G^T and G c (k_schur_diag's order: thread t takes the
+// camera's observations t, t + 256, ...): S(i,i) = Hpp(i,i) + lambda I - sum G G^T, bschur_i = b_i - sum G c.
+template <class F, bool FG>
 __global__ void __launch_bounds__(256) k_cam_assemble(EdgeData d, const int* __restrict__ cm_ptr, int npose,
-                                                      double* __restrict__ Hpp, double* __restrict__ bvec) {
+                                                      double* __restrict__ Hpp, double* __restrict__ bvec,
+                                                      int num_poses, int lm_begin, launch::SchurSplit sp) {
   constexpr int D = F::D, DA = F::DA, DB = F::DB;
-  constexpr int SP = DB * (DB + 1) / 2, S = SP + DB;
-  __shared__ double red[4][S];
+  constexpr int SP = DB * (DB + 1) / 2, S = SP + DB, NS = FG ? 2 * S : S;
+  constexpr int GB = DA * DB, UF = 2 * DA;
+  __shared__ double red[4][NS];
+  __shared__ double fin[NS];
   const int i = xcd_item(blockIdx.x, npose);  // neighbouring cameras share landmarks: one L2
   if (i >= npose) return;  // workgroup-uniform
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double acc[S];
+  double acc[NS];
 #pragma unroll
-  for (int k = 0; k < S; ++k) acc[k] = 0.0;
+  for (int k = 0; k < NS; ++k) acc[k] = 0.0;
   const int p1 = cm_ptr[i + 1];
   for (int p = cm_ptr[i] + tid; p < p1; p += 256) {
+    int hl = -1;
+    if constexpr (FG) hl = sp.hl[d.v0[p]];
     double err[D], A[D * DA], B[D * DB], Om[D * D];
     edge_terms<F>(d, p, err, A, B, Om);
     double wr[D];
@@ -278,26 +367,93 @@ __global__ void __launch_bounds__(256) k_cam_assemble(EdgeData d, const int* __r
       for (int r = 0; r < D; ++r) s += B[r * DB + j] * wr[r];
       acc[k++] += s;
     }
+    if constexpr (FG) {
+      if (hl >= 0) {
+        const double2* u2 = reinterpret_cast<const double2*>(sp.Ufac + (size_t)(hl - num_poses - lm_begin) * UF);
+        const double* cp = sp.cl + (size_t)(hl - num_poses) * DA;
+        double U[UF], cl[DA];
+#pragma unroll
+        for (int q = 0; q < UF / 2; ++q) { const double2 v = u2[q]; U[2 * q] = v.x; U[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int q = 0; q < DA; ++q) cl[q] = cp[q];
+        double AtO[DA * D];
+#pragma unroll
+        for (int a = 0; a < DA; ++a)
+#pragma unroll
+          for (int c = 0; c < D; ++c) {
+            double s = 0;
+#pragma unroll
+            for (int r = 0; r < D; ++r) s += A[r * DA + a] * Om[r * D + c];
+            AtO[a * D + c] = s;
+          }
+        double g[GB];
+#pragma unroll
+        for (int a = 0; a < DA; ++a)
+#pragma unroll
+          for (int j = 0; j < DB; ++j) {
+            double s = 0;
+#pragma unroll
+            for (int r = 0; r < D; ++r) s += AtO[a * D + r] * B[r * DB + j];
+            g[a * DB + j] = s;
+          }
+        form_G<DB, DA>(g, U);
+        int q = S;
+#pragma unroll
+        for (int cc = 0; cc < DB; ++cc)
+#pragma unroll
+          for (int r = 0; r <= cc; ++r) {
+            double s = g[r] * g[cc];
+#pragma unroll
+            for (int kk = 1; kk < DA; ++kk) s += g[kk * DB + r] * g[kk * DB + cc];
+            acc[q++] += s;
+          }
+#pragma unroll
+        for (int r = 0; r < DB; ++r) {
+          double s = g[r] * cl[0];
+#pragma unroll
+          for (int kk = 1; kk < DA; ++kk) s += g[kk * DB + r] * cl[kk];
+          acc[q++] += s;
+        }
+      }
+    }
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1)
 #pragma unroll
-    for (int k = 0; k < S; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
+    for (int k = 0; k < NS; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
   if (lane == 0)
 #pragma unroll
-    for (int k = 0; k < S; ++k) red[w][k] = acc[k];
+    for (int k = 0; k < NS; ++k) red[w][k] = acc[k];
   __syncthreads();
-  if (tid >= S) return;
-  const double t = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  if (tid < NS) fin[tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  if constexpr (FG) __syncthreads();
+  if (tid >= NS) return;
+  const double t = fin[tid];
+  auto unpack = [](int k, int& r, int& c) {  // packed upper index -> (r, c), r <= c
+    c = 0;
+    int base = 0;
+    while (k >= base + c + 1) base += ++c;
+    r = k - base;
+  };
   if (tid < SP) {
-    int c = 0, base = 0;
-    while (tid >= base + c + 1) base += ++c;
-    const int r = tid - base;
+    int r, c;
+    unpack(tid, r, c);
     double* H = Hpp + (size_t)i * DB * DB;
     H[c * DB + r] = t;
     H[r * DB + c] = t;
-  } else {
+  } else if (tid < S) {
     bvec[(size_t)i * DB + tid - SP] = t;
+  } else if (tid < S + SP) {
+    int r, c;
+    unpack(tid - S, r, c);
+    const double h = fin[tid - S];
+    const double o = (r == c ? h + sp.lam_rank : h) - t;
+    double* So = sp.S + (size_t)sp.sdiag[i] * DB * DB;
+    So[c * DB + r] = o;
+    So[r * DB + c] = o;
+  } else {
+    const int r = tid - S - SP;
+    sp.bschur[(size_t)i * DB + r] = fin[SP + r] - t;
   }
 }
 
@@ -305,24 +461,41 @@ namespace launch {
 void linearize_fused(const EdgeArgs& a, const int4* chunks, int nchunks, const int* h0, const int* h1,
                      const long long* off_dst, const unsigned char* off_tr, double* off_base, double* off_slot,
                      double* Hll, double* b, int num_poses, int size_poses, int lm_begin, double* lpart,
-                     hipStream_t s) {
+                     const SchurSplit* sp, hipStream_t s) {
   if (nchunks <= 0) return;
   const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
-  hipLaunchKernelGGL(k_linearize_fused<FamilyBA>, grid_for(nchunks, 4), 256, 0, s, d, chunks, nchunks, h0, h1,
-                     off_dst, off_tr, off_base, off_slot, Hll, b, num_poses, size_poses, lm_begin, lpart);
+  const SchurSplit z = sp ? *sp : SchurSplit{};
+  if (sp)
+    hipLaunchKernelGGL((k_linearize_fused<FamilyBA, true>), grid_for(nchunks, 4), 256, 0, s, d, chunks, nchunks, h0, h1,
+                       off_dst, off_tr, off_base, off_slot, Hll, b, num_poses, size_poses, lm_begin, lpart, z);
+  else
+    hipLaunchKernelGGL((k_linearize_fused<FamilyBA, false>), grid_for(nchunks, 4), 256, 0, s, d, chunks, nchunks, h0,
+                       h1, off_dst, off_tr, off_base, off_slot, Hll, b, num_poses, size_poses, lm_begin, lpart, z);
   KERNEL_CHECK();
 }
 void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, double* b, int num_poses, int size_poses,
-              int lm_begin, hipStream_t s) {
+              int lm_begin, const SchurSplit* sp, hipStream_t s) {
   if (nfix <= 0) return;
-  hipLaunchKernelGGL(k_lm_fixup, grid_for(nfix, 256), 256, 0, s, nfix, fix, lpart, Hll, b, num_poses, size_poses,
-                     lm_begin);
+  const SchurSplit z = sp ? *sp : SchurSplit{};
+  if (sp)
+    hipLaunchKernelGGL(k_lm_fixup<true>, grid_for(nfix, 256), 256, 0, s, nfix, fix, lpart, Hll, b, num_poses,
+                       size_poses, lm_begin, z);
+  else
+    hipLaunchKernelGGL(k_lm_fixup<false>, grid_for(nfix, 256), 256, 0, s, nfix, fix, lpart, Hll, b, num_poses,
+                       size_poses, lm_begin, z);
   KERNEL_CHECK();
 }
-void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, hipStream_t s) {
+void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, int num_poses, int lm_begin,
+                  const SchurSplit* sp, hipStream_t s) {
   if (npose <= 0) return;
   const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
-  hipLaunchKernelGGL(k_cam_assemble<FamilyBA>, npose, 256, 0, s, d, cm_ptr, npose, Hpp, b);
+  const SchurSplit z = sp ? *sp : SchurSplit{};
+  if (sp)
+    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
+                       lm_begin, z);
+  else
+    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, false>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
+                       lm_begin, z);
   KERNEL_CHECK();
 }
 }  // namespace launch

@@ -1668,7 +1668,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
 
       std::vector<launch::SchurTask> tasks;
       std::vector<launch::SchurBatch> batches;
-      std::vector<int> st_obs, prs, pp;
+      std::vector<int> st_obs, st_obs_h, prs, pp;
       std::vector<int> camslot(num_poses, -1);
       struct P3 { int ls, a, b; };
       std::vector<P3> cur;
@@ -1719,9 +1719,11 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
             if ((int)st_obs.size() - bst0 + need > SB) flush();
             const int posA = (int)st_obs.size() - bst0;
             st_obs.push_back(gpos[a]);
+            st_obs_h.push_back(a);
             for (auto& [a2, sl] : tmp) {
               const int posB = (int)st_obs.size() - bst0;
               st_obs.push_back(gpos[a2]);
+              st_obs_h.push_back(a2);
               cur.push_back(P3{sl, posA, posB});
             }
           }
@@ -1738,6 +1740,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       batches.push_back(launch::SchurBatch{});  // trailing dummy: k_schur_rows reads one record ahead
       sch_batches.upload(batches, stream);
       sch_st_obs.upload(nz(st_obs), stream);
+      sch_st_obs_h.upload(nz(st_obs_h), stream);
       sch_pairs.upload(nz(prs), stream);
       sch_pp.upload(nz(pp), stream);
     }
@@ -1757,6 +1760,11 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     dG.resize(std::max<long long>((long long)nHpl * pd * ld, 1));  // G = Hpl U^-T per observation (pd x ld)
     dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
+    {  // landmark side of the Schur complement formed during assembly (G2OHIP_SCHUR_SPLIT=0: the plain passes, A/B)
+      const char* ev = getenv("G2OHIP_SCHUR_SPLIT");
+      fz_split_ok = ba_fused && nslotd == 0 && pd == 6 && ld == 3 && !use_cgls() && !(ev && atoi(ev) == 0);
+      fz_lambda = std::numeric_limits<double>::quiet_NaN();
+    }
     if (use_cgls()) {  // the fork's JacobiSolver_6_3: CGLS on J, no reduced system to factor
       if (!ba_fused || nranks > 1) throw DeviceError("lm_pcg6_3_eigen needs a single-GPU graph of BA edges only");
       const EGroup& g = groups[0];
@@ -1820,33 +1828,55 @@ double Engine::chi2() {
   return chi2_sync();
 }
 
-int Engine::build_system() {  // block_solver.hpp:462-521
+int Engine::build_system() { return build_system_split(std::numeric_limits<double>::quiet_NaN()); }
+
+int Engine::build_system_split(double lambda) {  // block_solver.hpp:462-521
   if (!structure_built) {
     int r = build_structure();
     if (r) return r;
   }
   ensure_device_state();
   refresh_host_payload(true);
+  fz_lambda = std::numeric_limits<double>::quiet_NaN();
   if (ba_fused) {  // assembly.hip: landmark side reduced inside the linearize waves, camera side recomputed per camera
     const EGroup& g = groups[0];
     const int lm_begin = local_lm.empty() ? 0 : local_lm.front();
+    launch::SchurSplit sp{};
+    const bool split = fz_split_ok && std::isfinite(lambda);
+    if (split) {  // block_solver.hpp:341-400 (the landmark pass and the diagonal terms) at lambda, during assembly
+      sp.lam = lambda;
+      sp.lam_rank = rank == 0 ? lambda : 0.0;
+      sp.Ufac = dUfac.get();
+      sp.cl = dCl.get();
+      sp.G = dG.get();
+      sp.hpl_base = (long long)nHpp * pd * pd;
+      sp.lm_ptr = d_lm_ptr.get();
+      sp.hl = d_hidx[g.vtA].get();
+      sp.sdiag = sch_sdiag.get();
+      sp.S = dS.get();
+      sp.bschur = dS.get() + (size_t)nS * pd * pd;
+      sp.fail = failp() + 1;
+      fz_lambda = lambda;
+    }
     timer.begin("linearize", stream);
     launch::linearize_fused(group_args(g), fz_chunks.get(), fz_nchunks, d_hidx[g.vtA].get(), d_hidx[g.vtB].get(),
                             g.off_dst.get(), g.off_tr.get(), dH.get(), doffslot.get(), dHll.get(), db.get(), num_poses,
-                            size_poses, lm_begin, fz_lpart.get(), stream);
+                            size_poses, lm_begin, fz_lpart.get(), split ? &sp : nullptr, stream);
     timer.end(stream);
     for (const OffRed& R : offred)
       launch::offblock_reduce(R.nb, R.bsz, R.ptr.get(), R.soff.get(), doffslot.get(), dH.get(), R.dst.get(), stream);
     timer.begin("vreduce", stream);
+    // split landmarks first: the camera pass reads every landmark's U and c
+    launch::lm_fixup(fz_nfix, fz_fix.get(), fz_lpart.get(), dHll.get(), db.get(), num_poses, size_poses, lm_begin,
+                     split ? &sp : nullptr, stream);
     EdgeArgs ca = group_args(g);
     ca.v0 = cm_v0.get();
     ca.v1 = cm_v1.get();
     ca.meas = cm_meas.get();
     ca.info = cm_info.get();
     ca.params = cm_params.get();
-    launch::cam_assemble(ca, cm_ptr.get(), num_poses, dH.get(), db.get(), stream);
-    launch::lm_fixup(fz_nfix, fz_fix.get(), fz_lpart.get(), dHll.get(), db.get(), num_poses, size_poses, lm_begin,
-                     stream);
+    launch::cam_assemble(ca, cm_ptr.get(), num_poses, dH.get(), db.get(), num_poses, lm_begin, split ? &sp : nullptr,
+                         stream);
     timer.end(stream);
     if (use_cgls()) {  // JacobiSolver::buildSystem's J (jacobi_solver.hpp:479-700)
       timer.begin("cgls_jacobian", stream);
@@ -1929,17 +1959,25 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   const double* Hpl = dH.get() + (long long)nHpp * pd * pd;
   double* S = dS.get();
   double* bschur = dS.get() + (size_t)nS * pd * pd;
-  timer.begin("schur_dinv", stream);
-  launch::schur_prep(ld, nLloc, lm_begin, dHll.get(), db.get() + size_poses, dscal.get(), dDinv.get(), dUfac.get(),
-                     dCl.get(), failp() + 1, stream);
-  timer.end(stream);
-  timer.begin("schur_diag", stream);
-  launch::schur_diag(pd, ld, num_poses, sch_rptr.get(), sch_robs.get(), sch_obs_lm.get(), lm_begin, Hpl, dUfac.get(), dCl.get(),
-                     sch_sdiag.get(), ds_hpp.get(), dH.get(), db.get(), dscal.get() + 4, S, bschur, dG.get(), stream);
-  timer.end(stream);
+  // Schur split formed at assembly: usable as is when this trial's lambda is the one it was formed with; a trial at
+  // another lambda re-assembles at the same (popped) state with its lambda. Otherwise the plain passes over Hpl.
+  bool split = !std::isnan(fz_lambda);
+  if (split && fz_lambda != lambda_host) split = build_system_split(lambda_host) == G2OHIP_OK && !std::isnan(fz_lambda);
+  if (!split) {
+    timer.begin("schur_dinv", stream);
+    launch::schur_prep(ld, nLloc, lm_begin, dHll.get(), db.get() + size_poses, dscal.get(), dDinv.get(), dUfac.get(),
+                       dCl.get(), failp() + 1, stream);
+    timer.end(stream);
+    timer.begin("schur_diag", stream);
+    launch::schur_diag(pd, ld, num_poses, sch_rptr.get(), sch_robs.get(), sch_obs_lm.get(), lm_begin, Hpl, dUfac.get(),
+                       dCl.get(), sch_sdiag.get(), ds_hpp.get(), dH.get(), db.get(), dscal.get() + 4, S, bschur, dG.get(),
+                       stream);
+    timer.end(stream);
+  }
   timer.begin("schur_rows", stream);
-  launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(), sch_st_obs.get(), sch_pairs.get(), sch_pp.get(),
-                     dG.get(), ds_hpp.get(), dH.get(), S, stream);
+  launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(),
+                     split ? sch_st_obs_h.get() : sch_st_obs.get(), sch_pairs.get(), sch_pp.get(), dG.get(),
+                     ds_hpp.get(), dH.get(), S, stream);
   timer.end(stream);
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
   if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
@@ -1959,8 +1997,12 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   }
   if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
   timer.begin("backsub", stream);
-  launch::backsub(pd, ld, nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get(), size_poses, lm_begin, dx.get(),
-                  stream);
+  if (split)
+    launch::backsub_g(pd, ld, nLloc, d_lm_ptr.get(), d_blk_pose.get(), dG.get(), dUfac.get(), dCl.get(), size_poses,
+                      lm_begin, dx.get(), stream);
+  else
+    launch::backsub(pd, ld, nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get(), size_poses, lm_begin,
+                    dx.get(), stream);
   timer.end(stream);
 }
 
@@ -2098,7 +2140,9 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   double tempChi = currentChi;
   hipEvent_t e0 = lm_ev_[0], e1 = lm_ev_[1], e2 = lm_ev_[2], e3 = lm_ev_[3], q0 = lm_ev_[4], q1 = lm_ev_[5];
   if (st && stats_level >= 2) HIP_CHECK(hipEventRecord(q0, stream));
-  if (built_ver != state_ver || iteration == 0) build_system();  // else enqueued by the previous iteration
+  // else enqueued by the previous iteration; lambda is known from iteration 1 on (iteration 0 derives it from H)
+  if (built_ver != state_ver || iteration == 0)
+    build_system_split(iteration == 0 ? std::numeric_limits<double>::quiet_NaN() : current_lambda);
   if (st && stats_level >= 2) HIP_CHECK(hipEventRecord(q1, stream));  // timeQuadraticForm from events
   built_ver = 0;
   if (iteration == 0) {
@@ -2186,7 +2230,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   // while the host returns to the caller (skipped when the loop is about to stop)
   const bool more = !(qmax == maxTrials || rho == 0 || !std::isfinite(current_lambda));
   if (more) {
-    build_system();
+    build_system_split(current_lambda);
     built_ver = state_ver;
   }
   if (qmax == maxTrials || rho == 0 || !std::isfinite(current_lambda)) return 1;  // Terminate

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <limits>
 #include <map>
 #include <memory>
 #include <string>
@@ -191,6 +192,9 @@ class Engine {
   int optimize_step(const g2ohip_config* cfg, int iteration, g2ohip_batch_stats* stats);
   int build_structure();
   int build_system();
+  // buildSystem with lambda known (the LM loop): where eligible the landmark side of the Schur complement is formed
+  // during assembly (kernels.hpp SchurSplit); solve_async re-assembles when a trial's lambda differs
+  int build_system_split(double lambda);
   int set_lambda(double lambda, int backup);
   int restore_diagonal();
   int solve_sync();  // 1 ok / 0 not PD
@@ -270,6 +274,10 @@ class Engine {
   DevBuf<int4> fz_chunks, fz_fix;
   int fz_nchunks = 0, fz_nfix = 0;
   DevBuf<double> fz_lpart;
+  // Schur split at assembly: eligible graphs (fused BA, no shared off-diagonal blocks, a Cholesky / PCG on S), and the
+  // lambda the stored G = Hpl U^-T, S(i,i) and bschur were formed with (NaN: Hpl stored, the plain Schur passes run)
+  bool fz_split_ok = false;
+  double fz_lambda = std::numeric_limits<double>::quiet_NaN();
   DevBuf<int> cm_ptr, cm_v0, cm_v1;
   DevBuf<double> cm_meas, cm_info, cm_params;
   std::vector<int> cm_ptr_h, cm_e_h, lm_eptr_h;  // host copies for the CGLS setup (camera lists, landmark edge ranges)
@@ -291,6 +299,7 @@ class Engine {
   DevBuf<launch::SchurTask> sch_tasks;
   DevBuf<launch::SchurBatch> sch_batches;
   DevBuf<int> sch_st_obs, sch_pairs, sch_pp;
+  DevBuf<int> sch_st_obs_h;  // the same staged blocks as Hpl block indices (G in Hpl's order, Schur split)
   int nsch_tasks = 0;
   // diagonal Schur blocks (k_schur_diag): per camera row its observations in landmark order
   DevBuf<int> sch_rptr, sch_robs, sch_obs_lm, sch_sdiag;

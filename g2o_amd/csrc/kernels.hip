@@ -409,55 +409,20 @@ __global__ void __launch_bounds__(256)
     Do[2] = (m(1, 0) * m(2, 1) - m(1, 1) * m(2, 0)) * inv;
     Do[5] = (m(0, 1) * m(2, 0) - m(0, 0) * m(2, 1)) * inv;
     Do[8] = (m(0, 0) * m(1, 1) - m(0, 1) * m(1, 0)) * inv;
-    const double d0 = m(0, 0);
-    const double r0 = 1.0 / sqrt(d0);
-    const double u10 = m(1, 0) * r0, u20 = m(2, 0) * r0;
-    const double d1 = m(1, 1) - u10 * u10;
-    const double r1 = 1.0 / sqrt(d1);
-    const double u21 = (m(2, 1) - u20 * u10) * r1;
-    const double d2 = m(2, 2) - u20 * u20 - u21 * u21;
-    const double r2 = 1.0 / sqrt(d2);
-    bad = !(det != 0.0) || !isfinite(inv) || !(d0 > 0.0) || !(d1 > 0.0) || !(d2 > 0.0);
-    U[0] = r0; U[1] = r1; U[2] = r2; U[3] = u10; U[4] = u20; U[5] = u21;
-    const double g0 = bl[0] * r0;
-    const double g1 = (bl[1] - u10 * g0) * r1;
-    const double g2 = (bl[2] - u20 * g0 - u21 * g1) * r2;
-    co[0] = g0; co[1] = g1; co[2] = g2;
+    bad = !(det != 0.0) || !isfinite(inv);
   } else {  // Eigen compute_inverse_size2: adjugate / (m00 m11 - m10 m01)
     const double det = m(0, 0) * m(1, 1) - m(1, 0) * m(0, 1);
     const double inv = 1.0 / det;
     Do[0] = m(1, 1) * inv; Do[1] = -m(1, 0) * inv; Do[2] = -m(0, 1) * inv; Do[3] = m(0, 0) * inv;
-    const double d0 = m(0, 0);
-    const double r0 = 1.0 / sqrt(d0);
-    const double u10 = m(1, 0) * r0;
-    const double d1 = m(1, 1) - u10 * u10;
-    const double r1 = 1.0 / sqrt(d1);
-    bad = !(det != 0.0) || !isfinite(inv) || !(d0 > 0.0) || !(d1 > 0.0);
-    U[0] = r0; U[1] = r1; U[2] = u10; U[3] = 0.0;
-    const double g0 = bl[0] * r0;
-    co[0] = g0;
-    co[1] = (bl[1] - u10 * g0) * r1;
+    bad = !(det != 0.0) || !isfinite(inv);
   }
-  if (bad) *fail = 1;
-}
-
-// G = Hpl U^-T in place: g (PD x LD col-major) holds Hpl on entry, G on exit; row r solves U g_r = h_r
-template <int PD, int LD>
-__device__ __forceinline__ void form_G(double* g, const double* U) {
+  double Ur[UF], cr[LD];
+  if (!lm_ufac<LD>(a, bl, Ur, cr)) bad = true;
 #pragma unroll
-  for (int r = 0; r < PD; ++r) {
-    if constexpr (LD == 3) {
-      const double g0 = g[r] * U[0];
-      const double g1 = (g[PD + r] - U[3] * g0) * U[1];
-      g[2 * PD + r] = (g[2 * PD + r] - U[4] * g0 - U[5] * g1) * U[2];
-      g[r] = g0;
-      g[PD + r] = g1;
-    } else {
-      const double g0 = g[r] * U[0];
-      g[PD + r] = (g[PD + r] - U[2] * g0) * U[1];
-      g[r] = g0;
-    }
-  }
+  for (int k = 0; k < UF; ++k) U[k] = Ur[k];
+#pragma unroll
+  for (int k = 0; k < LD; ++k) co[k] = cr[k];
+  if (bad) *fail = 1;
 }
 
 // Diagonal blocks of the reduced system (block_solver.hpp:361-400, the j == i terms):
@@ -758,6 +723,60 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int k = 1; k < LD; ++k) s += D[k * LD + r] * c[k];
     xl[r] = s;
+  }
+}
+
+// the same from the symmetric split of a Schur pass whose G blocks were formed at assembly (G = Hpl U^-T stored in
+// place of Hpl, same block order): Dinv (b_l - Hpl^T x_p) = U^-T (c_l - G^T x_p), c_l = U^-1 b_l
+template <int PD, int LD, int LANES>
+__global__ void __launch_bounds__(256)
+    k_backsub_g(int nl, const int* __restrict__ lm_ptr, const int* __restrict__ blk_pose, const double* __restrict__ G,
+                const double* __restrict__ Ufac, const double* __restrict__ cl_all, int size_poses, int lm0,
+                double* __restrict__ x) {
+  constexpr int UF = LmTraits<LD>::UF;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int l = gid / LANES, q = gid % LANES;
+  const bool active = l < nl;
+  double c[LD];
+#pragma unroll
+  for (int k = 0; k < LD; ++k) c[k] = 0.0;
+  if (active) {
+    const int a1 = lm_ptr[l + 1];
+    for (int a = lm_ptr[l] + q; a < a1; a += LANES) {
+      const double* Bm = G + (size_t)a * PD * LD;
+      const double* xp = x + (size_t)blk_pose[a] * PD;
+      double s[LD];
+#pragma unroll
+      for (int k = 0; k < LD; ++k) s[k] = 0.0;
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        const double xr = -xp[r];
+#pragma unroll
+        for (int k = 0; k < LD; ++k) s[k] += Bm[k * PD + r] * xr;
+      }
+#pragma unroll
+      for (int k = 0; k < LD; ++k) c[k] += s[k];
+    }
+  }
+#pragma unroll
+  for (int m = LANES / 2; m >= 1; m >>= 1)
+#pragma unroll
+    for (int k = 0; k < LD; ++k) c[k] += __shfl_xor(c[k], m, LANES);
+  if (!active || q != 0) return;
+  const double* cl = cl_all + (size_t)(lm0 + l) * LD;
+  const double* U = Ufac + (size_t)l * UF;
+#pragma unroll
+  for (int k = 0; k < LD; ++k) c[k] += cl[k];
+  double* xl = x + size_poses + (size_t)(lm0 + l) * LD;
+  if constexpr (LD == 3) {  // U^T x = y, U = [[1/r0, 0, 0], [u10, 1/r1, 0], [u20, u21, 1/r2]]
+    const double x2 = c[2] * U[2];
+    const double x1 = (c[1] - U[5] * x2) * U[1];
+    const double x0 = (c[0] - U[3] * x1 - U[4] * x2) * U[0];
+    xl[0] = x0; xl[1] = x1; xl[2] = x2;
+  } else {
+    const double x1 = c[1] * U[1];
+    const double x0 = (c[0] - U[2] * x1) * U[0];
+    xl[0] = x0; xl[1] = x1;
   }
 }
 
@@ -1148,6 +1167,15 @@ void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, con
   pl_dispatch(pd, ld, [&](auto P, auto L) {
     hipLaunchKernelGGL((k_backsub<decltype(P)::value, decltype(L)::value, 4>), grid_for((size_t)nl * 4, 256), 256, 0,
                        s, nl, lm_ptr, blk_pose, Hpl, Dinv, b, size_poses, lm0, x);
+  });
+  KERNEL_CHECK();
+}
+void backsub_g(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* G, const double* Ufac,
+               const double* cl_all, int size_poses, int lm0, double* x, hipStream_t s) {
+  if (nl <= 0) return;
+  pl_dispatch(pd, ld, [&](auto P, auto L) {
+    hipLaunchKernelGGL((k_backsub_g<decltype(P)::value, decltype(L)::value, 4>), grid_for((size_t)nl * 4, 256), 256,
+                       0, s, nl, lm_ptr, blk_pose, G, Ufac, cl_all, size_poses, lm0, x);
   });
   KERNEL_CHECK();
 }

@@ -34,13 +34,32 @@ void vertex_reduce(int dim, int nv, int lanes, const int* ptr, const int* code, 
 void offblock_reduce(int nb, int bsz, const int* ptr, const long long* soff, const double* slots, double* out,
                      const long long* dst, hipStream_t s);
 // fused BA assembly (assembly.hip): chunks = (first edge, edges, partial slot or -1, 0) of whole landmarks per wave
+// With a SchurSplit (sp != nullptr, lambda known at assembly, no shared off-diagonal blocks) the landmark side of the
+// Schur complement is formed during assembly: the linearize waves factor each landmark's Hll + lambda I = U U^T and
+// store G = Hpl U^-T in place of Hpl (in G's buffer, Hpl's block order), the camera pass adds S(i,i) and bschur_i
+// beside Hpp(i,i) and b_i. No Hpl is stored then.
+struct SchurSplit {
+  double lam;            // lambda of every landmark block
+  double lam_rank;       // lambda on S's diagonal (rank 0 only when sharded)
+  double* Ufac;          // per local landmark U record (6 doubles)
+  double* cl;            // c = U^-1 b_l, global landmark index
+  double* G;             // Hpl's block order
+  long long hpl_base;    // offset of the first Hpl block in off_base (the Hessian)
+  const int* lm_ptr;     // local landmark -> its Hpl/G block range (split landmarks' fixup)
+  const int* hl;         // landmark vertex (local id) -> hessian index (-1 fixed), for the camera pass
+  const int* sdiag;      // camera row -> S index of its diagonal block
+  double* S;             // [S blocks | bschur]
+  double* bschur;
+  int* fail;             // landmark block not positive definite (informational, as k_schur_prep)
+};
 void linearize_fused(const EdgeArgs& a, const int4* chunks, int nchunks, const int* h0, const int* h1,
                      const long long* off_dst, const unsigned char* off_tr, double* off_base, double* off_slot,
                      double* Hll, double* b, int num_poses, int size_poses, int lm_begin, double* lpart,
-                     hipStream_t s);
+                     const SchurSplit* sp, hipStream_t s);
 void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, double* b, int num_poses, int size_poses,
-              int lm_begin, hipStream_t s);
-void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, hipStream_t s);
+              int lm_begin, const SchurSplit* sp, hipStream_t s);
+void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, int num_poses, int lm_begin,
+                  const SchurSplit* sp, hipStream_t s);
 // Schur kernels for (pd, ld) = (6, 3) (BlockSolver_6_3) and (3, 2) (BlockSolver_3_2)
 void schur_prep(int ld, int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
                 double* Ufac, double* cl_all, int* fail, hipStream_t s);
@@ -68,6 +87,9 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
                 hipStream_t s);
 void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv,
              const double* b, int size_poses, int lm0, double* x, hipStream_t s);
+// back-substitution from the G blocks of an assembly-time Schur split: x_l = U^-T (c_l - G^T x_p)
+void backsub_g(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* G, const double* Ufac,
+               const double* cl_all, int size_poses, int lm0, double* x, hipStream_t s);
 void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s);
 size_t sum_partials(long long n);
 void sum(const double* v, long long n, double* partial, double* out, hipStream_t s);

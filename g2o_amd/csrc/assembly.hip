@@ -307,19 +307,19 @@ __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restri
 }
 
 // camera-side terms: one workgroup per pose, threads stride over its observations (camera-major copy of the
-// edge data, ascending landmark-major edge order), 27 accumulators per thread, fixed-tree reduction. With a Schur
-// split the same pass forms each observation's G = Hpl U^-T (the linearize lane's arithmetic, U and c of its
-// landmark) and accumulates the diagonal Schur terms G G^T and G c (k_schur_diag's order: thread t takes the
-// camera's observations t, t + 256, ...): S(i,i) = Hpp(i,i) + lambda I - sum G G^T, bschur_i = b_i - sum G c.
+// edge data, ascending landmark-major edge order), 27 accumulators per thread, fixed-tree reduction: Hpp(i,i), b_i.
+// With a Schur split the pass forms the diagonal Schur block directly instead of Hpp(i,i): per observation with a free
+// landmark, G G^T = B^T M B and G c_l = B^T W c_l with W = Omega A U^-T (D x LD), M = W W^T = Omega A (Hll + lambda I)^-1
+// A^T Omega, so S(i,i) = lambda I + sum B^T (Omega - M) B and bschur_i = sum B^T (omega_r - W c_l), beside b_i
+// (block_solver.hpp:361-400's j == i terms in 33 accumulators; Hpp is left to a plain buildSystem).
 template <class F, bool FG>
-__global__ void __launch_bounds__(256) k_cam_assemble(EdgeData d, const int* __restrict__ cm_ptr, int npose,
+__global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* __restrict__ cm_ptr, int npose,
                                                       double* __restrict__ Hpp, double* __restrict__ bvec,
                                                       int num_poses, int lm_begin, launch::SchurSplit sp) {
   constexpr int D = F::D, DA = F::DA, DB = F::DB;
-  constexpr int SP = DB * (DB + 1) / 2, S = SP + DB, NS = FG ? 2 * S : S;
-  constexpr int GB = DA * DB, UF = 2 * DA;
+  constexpr int SP = DB * (DB + 1) / 2, S = SP + DB, NS = FG ? S + DB : S;
+  constexpr int UF = 2 * DA;
   __shared__ double red[4][NS];
-  __shared__ double fin[NS];
   const int i = xcd_item(blockIdx.x, npose);  // neighbouring cameras share landmarks: one L2
   if (i >= npose) return;  // workgroup-uniform
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -340,15 +340,59 @@ __global__ void __launch_bounds__(256) k_cam_assemble(EdgeData d, const int* __r
       for (int c = 0; c < D; ++c) s += Om[r * D + c] * err[c];
       wr[r] = -s;
     }
-    double BtO[DB * D];
+    double N[D * D];  // Omega, minus M with a Schur split
+    double v[D];      // omega_r - W c_l with a Schur split
+#pragma unroll
+    for (int k = 0; k < D * D; ++k) N[k] = Om[k];
+#pragma unroll
+    for (int r = 0; r < D; ++r) v[r] = wr[r];
+    if constexpr (FG) {
+      if (hl >= 0) {
+        const double2* u2 = reinterpret_cast<const double2*>(sp.Ufac + (size_t)(hl - num_poses - lm_begin) * UF);
+        const double* cp = sp.cl + (size_t)(hl - num_poses) * DA;
+        double U[UF], cl[DA];
+#pragma unroll
+        for (int q = 0; q < UF / 2; ++q) { const double2 x = u2[q]; U[2 * q] = x.x; U[2 * q + 1] = x.y; }
+#pragma unroll
+        for (int q = 0; q < DA; ++q) cl[q] = cp[q];
+        double W[D * DA];  // Omega A, column-major D x DA, then U^-T applied to each row
+#pragma unroll
+        for (int a = 0; a < DA; ++a)
+#pragma unroll
+          for (int r = 0; r < D; ++r) {
+            double s = 0;
+#pragma unroll
+            for (int c = 0; c < D; ++c) s += Om[r * D + c] * A[c * DA + a];
+            W[a * D + r] = s;
+          }
+        form_G<D, DA>(W, U);
+#pragma unroll
+        for (int r = 0; r < D; ++r)
+#pragma unroll
+          for (int c = 0; c < D; ++c) {
+            double s = W[r] * W[c];
+#pragma unroll
+            for (int a = 1; a < DA; ++a) s += W[a * D + r] * W[a * D + c];
+            N[r * D + c] -= s;
+          }
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+          double s = W[r] * cl[0];
+#pragma unroll
+          for (int a = 1; a < DA; ++a) s += W[a * D + r] * cl[a];
+          v[r] -= s;
+        }
+      }
+    }
+    double BtN[DB * D];
 #pragma unroll
     for (int j = 0; j < DB; ++j)
 #pragma unroll
       for (int c = 0; c < D; ++c) {
         double s = 0;
 #pragma unroll
-        for (int r = 0; r < D; ++r) s += B[r * DB + j] * Om[r * D + c];
-        BtO[j * D + c] = s;
+        for (int r = 0; r < D; ++r) s += B[r * DB + j] * N[r * D + c];
+        BtN[j * D + c] = s;
       }
     int k = 0;
 #pragma unroll
@@ -357,7 +401,7 @@ __global__ void __launch_bounds__(256) k_cam_assemble(EdgeData d, const int* __r
       for (int r = 0; r <= c; ++r) {
         double s = 0;
 #pragma unroll
-        for (int t = 0; t < D; ++t) s += BtO[r * D + t] * B[t * DB + c];
+        for (int t = 0; t < D; ++t) s += BtN[r * D + t] * B[t * DB + c];
         acc[k++] += s;
       }
 #pragma unroll
@@ -368,52 +412,12 @@ __global__ void __launch_bounds__(256) k_cam_assemble(EdgeData d, const int* __r
       acc[k++] += s;
     }
     if constexpr (FG) {
-      if (hl >= 0) {
-        const double2* u2 = reinterpret_cast<const double2*>(sp.Ufac + (size_t)(hl - num_poses - lm_begin) * UF);
-        const double* cp = sp.cl + (size_t)(hl - num_poses) * DA;
-        double U[UF], cl[DA];
 #pragma unroll
-        for (int q = 0; q < UF / 2; ++q) { const double2 v = u2[q]; U[2 * q] = v.x; U[2 * q + 1] = v.y; }
+      for (int j = 0; j < DB; ++j) {
+        double s = 0;
 #pragma unroll
-        for (int q = 0; q < DA; ++q) cl[q] = cp[q];
-        double AtO[DA * D];
-#pragma unroll
-        for (int a = 0; a < DA; ++a)
-#pragma unroll
-          for (int c = 0; c < D; ++c) {
-            double s = 0;
-#pragma unroll
-            for (int r = 0; r < D; ++r) s += A[r * DA + a] * Om[r * D + c];
-            AtO[a * D + c] = s;
-          }
-        double g[GB];
-#pragma unroll
-        for (int a = 0; a < DA; ++a)
-#pragma unroll
-          for (int j = 0; j < DB; ++j) {
-            double s = 0;
-#pragma unroll
-            for (int r = 0; r < D; ++r) s += AtO[a * D + r] * B[r * DB + j];
-            g[a * DB + j] = s;
-          }
-        form_G<DB, DA>(g, U);
-        int q = S;
-#pragma unroll
-        for (int cc = 0; cc < DB; ++cc)
-#pragma unroll
-          for (int r = 0; r <= cc; ++r) {
-            double s = g[r] * g[cc];
-#pragma unroll
-            for (int kk = 1; kk < DA; ++kk) s += g[kk * DB + r] * g[kk * DB + cc];
-            acc[q++] += s;
-          }
-#pragma unroll
-        for (int r = 0; r < DB; ++r) {
-          double s = g[r] * cl[0];
-#pragma unroll
-          for (int kk = 1; kk < DA; ++kk) s += g[kk * DB + r] * cl[kk];
-          acc[q++] += s;
-        }
+        for (int r = 0; r < D; ++r) s += B[r * DB + j] * v[r];
+        acc[k++] += s;
       }
     }
   }
@@ -425,35 +429,26 @@ __global__ void __launch_bounds__(256) k_cam_assemble(EdgeData d, const int* __r
 #pragma unroll
     for (int k = 0; k < NS; ++k) red[w][k] = acc[k];
   __syncthreads();
-  if (tid < NS) fin[tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-  if constexpr (FG) __syncthreads();
   if (tid >= NS) return;
-  const double t = fin[tid];
-  auto unpack = [](int k, int& r, int& c) {  // packed upper index -> (r, c), r <= c
-    c = 0;
-    int base = 0;
-    while (k >= base + c + 1) base += ++c;
-    r = k - base;
-  };
+  const double t = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
   if (tid < SP) {
-    int r, c;
-    unpack(tid, r, c);
-    double* H = Hpp + (size_t)i * DB * DB;
-    H[c * DB + r] = t;
-    H[r * DB + c] = t;
+    int c = 0, base = 0;
+    while (tid >= base + c + 1) base += ++c;
+    const int r = tid - base;
+    if constexpr (FG) {  // S(i,i) = lambda I + sum B^T (Omega - M) B
+      const double o = r == c ? t + sp.lam_rank : t;
+      double* So = sp.S + (size_t)sp.sdiag[i] * DB * DB;
+      So[c * DB + r] = o;
+      So[r * DB + c] = o;
+    } else {
+      double* H = Hpp + (size_t)i * DB * DB;
+      H[c * DB + r] = t;
+      H[r * DB + c] = t;
+    }
   } else if (tid < S) {
     bvec[(size_t)i * DB + tid - SP] = t;
-  } else if (tid < S + SP) {
-    int r, c;
-    unpack(tid - S, r, c);
-    const double h = fin[tid - S];
-    const double o = (r == c ? h + sp.lam_rank : h) - t;
-    double* So = sp.S + (size_t)sp.sdiag[i] * DB * DB;
-    So[c * DB + r] = o;
-    So[r * DB + c] = o;
   } else {
-    const int r = tid - S - SP;
-    sp.bschur[(size_t)i * DB + r] = fin[SP + r] - t;
+    sp.bschur[(size_t)i * DB + tid - S] = t;
   }
 }
 

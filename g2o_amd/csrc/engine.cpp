@@ -1830,6 +1830,12 @@ double Engine::chi2() {
 
 int Engine::build_system() { return build_system_split(std::numeric_limits<double>::quiet_NaN()); }
 
+// a Schur-split assembly leaves Hpp's diagonal blocks unwritten (S(i,i) is formed directly): the entry points that
+// read Hpp get a plain buildSystem of the same state first
+void Engine::ensure_hpp() {
+  if (!std::isnan(fz_lambda)) build_system();
+}
+
 int Engine::build_system_split(double lambda) {  // block_solver.hpp:462-521
   if (!structure_built) {
     int r = build_structure();
@@ -2103,6 +2109,7 @@ double Engine::max_diagonal() {
     HIP_CHECK(hipStreamSynchronize(stream));
     return m;
   }
+  ensure_hpp();
   // Hpp diagonal blocks are partial per rank when sharded: reduce them first (copy)
   const double* Hp = dH.get();
   DevBuf<double> tmp;
@@ -2340,7 +2347,11 @@ int Engine::stage(double lambda, double* b, double* x, double* Hs, double* bs, l
   const long long n = vector_size();
   if (dims) { dims[0] = n; dims[1] = size_poses; dims[2] = size_landmarks; }
   if (!b && !x && !Hs && !bs) return 1;
-  build_system();
+  {  // G2OHIP_STAGE_SPLIT=1 (tests): stage through the Schur split formed at assembly, as the LM loop does
+    const char* ev = getenv("G2OHIP_STAGE_SPLIT");
+    if (ev && atoi(ev) == 1) build_system_split(lambda);
+    else build_system();
+  }
   set_lambda(lambda, 1);
   const int ok = solve_sync();
   if (b) db.download(b, n, stream);
@@ -2427,6 +2438,7 @@ void BlockSymv::setup(int nblocks, int bdim, const std::vector<int>& bi, const s
 int Engine::multiply_hessian(double* dest, const double* src) {  // block_solver.h:146
   if (!structure_built) return G2OHIP_ERR_STATE;
   if (nranks > 1) return G2OHIP_ERR_UNSUPPORTED;  // Hpp diagonal blocks are partial per landmark shard
+  ensure_hpp();
   if (symv_hpp.key != (const void*)&hpp_bi) {
     symv_hpp.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
     symv_hpp.key = &hpp_bi;
@@ -2475,6 +2487,7 @@ int Engine::compute_marginals(int nblocks, const int* brow, const int* bcol, dou
   if (nblocks < 0 || (nblocks && (!brow || !bcol || !out))) return G2OHIP_ERR_ARG;
   for (int k = 0; k < nblocks; ++k)
     if (brow[k] < 0 || brow[k] >= num_poses || bcol[k] < 0 || bcol[k] >= num_poses) return G2OHIP_ERR_ARG;
+  ensure_hpp();
   // the LM's own factor is reused where it factors Hpp; otherwise (Schur complement, iterative solvers) a
   // factor of Hpp's pattern is set up once
   const bool own = !do_schur && !use_pcg() && !use_cgls();

@@ -344,6 +344,7 @@ class Engine {
   double chi2_sync();
   double lambda_init();
   double max_diagonal();
+  void ensure_hpp();
   void solve_async(bool reset_fail);
   int* failp() const { return reinterpret_cast<int*>(dscal.get() + 8); }
   void update_async();

@@ -1,0 +1,94 @@
+"""Schur split formed at assembly (kernels.hpp SchurSplit): the LM loop's buildSystem knows lambda, so the
+linearize waves store G = Hpl U^-T (Hll + lambda I = U U^T) and the camera pass forms S(i,i) and bschur
+directly (block_solver.hpp:341-400). Checked against the oracle's BlockSolver at the stage level (reduced
+system, solution) and through LM trajectories whose rejected trials re-assemble at another lambda; the plain
+passes (G2OHIP_SCHUR_SPLIT=0) give the same trajectory.
+"""
+import numpy as np
+import pytest
+
+from g2o_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _stage(g2o_amd_mod, oracle, prob, lam, monkeypatch):
+    monkeypatch.setenv("G2OHIP_STAGE_SPLIT", "1")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    g = opt.stage(lam)
+    r = oracle.OracleGraph(prob).stage(lam)
+    assert g["ok"] == r["ok"] == 1
+    for k in ("b", "bschur", "x"):
+        assert np.linalg.norm(g[k] - r[k]) <= 1e-9 * np.linalg.norm(r[k]), k
+    assert np.linalg.norm(g["Hschur"] - r["Hschur"]) <= 1e-11 * np.linalg.norm(r["Hschur"])
+
+
+@pytest.mark.parametrize("name", ["C4", "C5"])
+def test_split_stage_reduced_system(g2o_amd_mod, oracle, name, monkeypatch):
+    _stage(g2o_amd_mod, oracle, synth.by_name(name, "small"), 1e-3, monkeypatch)
+
+
+def test_split_stage_long_tracks(g2o_amd_mod, oracle, monkeypatch):
+    """Landmarks seen by more than 64 cameras span several linearize waves: their U, c and G are formed by
+    k_lm_fixup after the partial sums (mixed with short tracks)."""
+    prob = synth.ba(num_cameras=140, num_points=300, obs_per_point=90, window=120, seed=7)
+    _stage(g2o_amd_mod, oracle, prob, 1e-2, monkeypatch)
+
+
+def _traj(g2o_amd_mod, oracle, prob, iters):
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    ref = oracle.OracleGraph(prob)
+    n, st = opt.optimize(iters)
+    nr, sr = ref.optimize(iters, oracle.make_config(threads=8))
+    assert n == nr
+    for a, b in zip(st, sr):
+        assert abs(a.chi2 - b.chi2) <= 1e-6 * abs(b.chi2), (a.chi2, b.chi2)
+        assert a.levenbergIterations == b.levenbergIterations
+    xg, xr = opt.minimal_state(), ref.minimal_state()
+    assert np.linalg.norm(xg - xr) <= 1e-6 * np.linalg.norm(xr)
+    return opt, st
+
+
+def test_split_trajectory_with_rejected_trials(g2o_amd_mod, oracle):
+    """Heavy pixel noise: iterations 0 and 1 reject a trial (oracle: [2, 2, 1, ...]); iteration 1's retry
+    re-assembles the split at the new lambda from the popped state."""
+    prob = synth.ba(num_cameras=40, num_points=1500, obs_per_point=8, window=24, cam_rot_noise=0.02,
+                    cam_trans_noise=0.05, point_noise=0.1, pixel_noise=200.0, seed=11)
+    _, st = _traj(g2o_amd_mod, oracle, prob, 10)
+    assert st[1].levenbergIterations > 1, "no rejected trial after iteration 0"
+
+
+def test_split_trajectory_long_tracks(g2o_amd_mod, oracle):
+    prob = synth.ba(num_cameras=140, num_points=300, obs_per_point=90, window=120, seed=7)
+    _traj(g2o_amd_mod, oracle, prob, 5)
+
+
+def test_split_equals_plain_passes(g2o_amd_mod, monkeypatch):
+    """The split and the plain passes (k_schur_prep / k_schur_diag over Hpl) follow the same trajectory."""
+    prob = synth.by_name("C4", "small")
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("G2OHIP_SCHUR_SPLIT", flag)
+        opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+        n, st = opt.optimize(6)
+        runs.append((n, [s.chi2 for s in st], [s.levenbergIterations for s in st], opt.minimal_state()))
+    (n1, c1, t1, x1), (n0, c0, t0, x0) = runs
+    assert n1 == n0 and t1 == t0
+    assert np.allclose(c1, c0, rtol=1e-10, atol=0)
+    assert np.linalg.norm(x1 - x0) <= 1e-10 * np.linalg.norm(x0)
+
+
+def test_split_hpp_consumers_after_optimize(g2o_amd_mod, oracle):
+    """After optimize() the engine holds a split assembly of the final state (no Hpp stored): multiplyHessian
+    and computeMarginals still see Hpp of that state (a plain buildSystem runs first)."""
+    prob = synth.by_name("C4", "small")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.optimize(3)
+    npose = opt.block_dims()[2] * 6
+    v = np.random.default_rng(0).standard_normal(npose)
+    y = opt.multiply_hessian(v)
+    ref = oracle.OracleGraph(prob)
+    ref.optimize(3, oracle.make_config(threads=8))
+    r = ref.stage(0.0)  # buildSystem at the optimized state
+    Hpp, _, _ = ref.hessian_dense(r["np"], r["nl"])
+    assert np.linalg.norm(y - Hpp @ v) <= 1e-8 * np.linalg.norm(Hpp @ v)

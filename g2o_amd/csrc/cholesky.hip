@@ -112,13 +112,13 @@ __global__ void __launch_bounds__(256) k_chol_scatter(long long nent, const doub
   fronts[dst[k]] = sr < 0 ? v + *lam : v;
 }
 
-// front vectors: v_s = [P rhs (own columns); 0]
-__global__ void __launch_bounds__(256) k_vec_init(const FrontDesc* __restrict__ fd, const double* __restrict__ rhs_p,
-                                                  double* __restrict__ vecs) {
+// front vectors: v_s = [P rhs (own columns); 0], the permutation applied on the fly
+__global__ void __launch_bounds__(256) k_vec_init(const FrontDesc* __restrict__ fd, const int* __restrict__ perm,
+                                                  const double* __restrict__ rhs, double* __restrict__ vecs) {
   const FrontDesc me = fd[blockIdx.x];
   const int m = me.ns + me.nr;
   double* v = vecs + me.vec_off;
-  for (int i = threadIdx.x; i < m; i += 256) v[i] = ld0(rhs_p, me.c0 + i, i < me.ns);
+  for (int i = threadIdx.x; i < m; i += 256) v[i] = i < me.ns ? rhs[perm[me.c0 + i]] : 0.0;
 }
 
 // ---------------------------------------------------------------------------- wave helpers
@@ -915,9 +915,9 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
     KERNEL_CHECK();
   }
 }
-void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double* vecs, hipStream_t s) {
+void chol_vec_init(int nfronts, const FrontDesc* fd, const int* perm, const double* rhs, double* vecs, hipStream_t s) {
   if (nfronts <= 0) return;
-  hipLaunchKernelGGL(k_vec_init, nfronts, 256, 0, s, fd, rhs_p, vecs);
+  hipLaunchKernelGGL(k_vec_init, nfronts, 256, 0, s, fd, perm, rhs, vecs);
   KERNEL_CHECK();
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,

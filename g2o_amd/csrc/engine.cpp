@@ -618,10 +618,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   x_p.resize(std::max(sym.n, 1));
 }
 
-void DeviceCholesky::factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s) {
-  launch::chol_permute(sym.n, perm.get(), rhs, rhs_p.get(), s);
-  launch::chol_vec_init((int)sym.sn.size(), fd.get(), rhs_p.get(), vecs.get(), s);
-  launch::chol_prescatter(nzero, zero_rng.get(), npre, vals, pre_dst.get(), pre_src.get(), lam, fronts.get(), s);
+void DeviceCholesky::factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s,
+                            bool prezeroed) {
+  launch::chol_vec_init((int)sym.sn.size(), fd.get(), perm.get(), rhs, vecs.get(), s);
+  launch::chol_prescatter(prezeroed ? 0 : nzero, zero_rng.get(), npre, vals, pre_dst.get(), pre_src.get(), lam,
+                          fronts.get(), s);
   for (const Op& op : ops) {
     const launch::Task* t = tasks.get() + op.off;
     switch (op.kind) {
@@ -1391,7 +1392,7 @@ void Engine::setup_edges_device() {
   long long maxp = std::max<long long>(vector_size(), 1);
   long long ptot = 0;
   for (auto& g : groups) ptot += (long long)launch::sum_partials(std::max(g.ne, 1));
-  dpartial.resize(std::max<size_t>(std::max<size_t>(launch::sum_partials(maxp), (size_t)ptot) + 64, 128));
+  dpartial.resize(std::max<size_t>(launch::sum_partials(maxp) + (size_t)ptot + 64, 128));  // chi2 + scale partials
   edges_ready = true;
   ++state_ver;  // the edge set (and so chi2) changed
 }
@@ -1797,7 +1798,7 @@ void Engine::allreduce_sum(double* p, size_t n) {
   comm->allreduce_sum(p, n, stream);
 }
 
-void Engine::compute_errors_async() {  // computeActiveErrors + activeRobustChi2 (sparse_optimizer.cpp:63-116)
+void Engine::compute_errors_async(bool reduce) {  // computeActiveErrors + activeRobustChi2 (sparse_optimizer.cpp:63-116)
   ensure_device_state();
   refresh_host_payload(false);
   timer.begin("error", stream);
@@ -1805,7 +1806,7 @@ void Engine::compute_errors_async() {  // computeActiveErrors + activeRobustChi2
   for (const EGroup& g : groups) np += launch::error_partials(g.family, group_args(g), g.ne, dpartial.get() + np, stream);
   launch::sum_final(dpartial.get(), np, dscal.get() + 1, stream);
   timer.end(stream);
-  if (do_schur) allreduce_sum(dscal.get() + 1, 1);
+  if (do_schur && reduce) allreduce_sum(dscal.get() + 1, 1);
 }
 
 double Engine::chi2_sync() {
@@ -1980,10 +1981,14 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
                        stream);
     timer.end(stream);
   }
+  // the Cholesky's pre-scattered fronts are cleared by extra workgroups of the Schur pass (they are dead since the
+  // last factorization), off the factorization's own chain
+  const bool zero_here = !use_pcg() && chol.nzero > 0;
   timer.begin("schur_rows", stream);
   launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(),
                      split ? sch_st_obs_h.get() : sch_st_obs.get(), sch_pairs.get(), sch_pp.get(), dG.get(),
-                     ds_hpp.get(), dH.get(), S, stream);
+                     ds_hpp.get(), dH.get(), S, zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(),
+                     stream);
   timer.end(stream);
   allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
   if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
@@ -1994,7 +1999,7 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
     if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
   } else {
     timer.begin("chol_factor", stream);
-    chol.factor(S, dscal.get() + 5, bschur, failp(), stream);
+    chol.factor(S, dscal.get() + 5, bschur, failp(), stream, zero_here);
     timer.end(stream);
     if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
     timer.begin("chol_solve", stream);
@@ -2024,11 +2029,18 @@ int Engine::solve_sync() {
 
 void Engine::update_async() {  // sparse_optimizer.cpp:441-454
   timer.begin("oplus", stream);
+  launch::OplusList L;
   for (int t = 1; t < NVT; ++t) {
     const int n = (int)hg.by_type[t].size();
     if (!n) continue;
-    launch::oplus(t, n, d_xoff[t].get(), dx.get(), dstate[t].get(), t == G2OHIP_V_SE3_QUAT ? dnopl.get() : nullptr, stream);
+    L.vt[L.cnt] = t;
+    L.n[L.cnt] = n;
+    L.xoff[L.cnt] = d_xoff[t].get();
+    L.st[L.cnt] = dstate[t].get();
+    if (t == G2OHIP_V_SE3_QUAT) L.nopl = dnopl.get();
+    ++L.cnt;
   }
+  launch::oplus_multi(L, dx.get(), stream);
   timer.end(stream);
   host_state_stale = true;
   ++state_ver;
@@ -2173,10 +2185,20 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     if (ev2) HIP_CHECK(hipEventRecord(e2, stream));
     // computeScale (:177-184) on the device, sum x (lambda x + b), while lambda is still set; the
     // restoreDiagonal that follows (:113) is the next setLambda (lambda is virtual, never in H)
-    launch::scale_sum(vector_size(), size_poses, dx.get(), db.get(), dscal.get(), dpartial.get(), dscal.get() + 2,
-                      stream);
-    allreduce_sum(dscal.get() + 2, 1);
-    compute_errors_async();
+    if (groups.size() == 1 && groups[0].family != FAM_HOSTJ) {  // chi2 and the scale sum in one pass + one final
+      timer.begin("error", stream);
+      const EGroup& g = groups[0];
+      launch::error_scale(g.family, group_args(g), g.ne, vector_size(), size_poses, dx.get(), db.get(), dscal.get(),
+                          dpartial.get(), dscal.get() + 1, dscal.get() + 2, stream);
+      timer.end(stream);
+    } else {
+      launch::scale_sum(vector_size(), size_poses, dx.get(), db.get(), dscal.get(), dpartial.get(), dscal.get() + 2,
+                        stream);
+      compute_errors_async(false);
+    }
+    // the same collectives on every rank whatever its edge groups: chi2 is per landmark shard only in Schur mode
+    if (do_schur) allreduce_sum(dscal.get() + 1, 2);
+    else allreduce_sum(dscal.get() + 2, 1);
     if (ev2) HIP_CHECK(hipEventRecord(e3, stream));
     double hs[12];  // lambda, chi2, scale, ... | fail flags (one readback per trial)
     HIP_CHECK(hipMemcpyAsync(hs, dscal.get(), sizeof hs, hipMemcpyDeviceToHost, stream));

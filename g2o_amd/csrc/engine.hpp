@@ -116,7 +116,8 @@ struct DeviceCholesky {
   long long lpool = 0;
   void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
   // numeric LL^T fused with the forward solve of rhs (y = L^-1 P rhs)
-  void factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s);
+  // prezeroed: the pre-scattered fronts were already cleared (zero_rng, nzero) by the caller's Schur pass
+  void factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s, bool prezeroed = false);
   // backward solve x = P^T L^-T y
   void solve(double* x, hipStream_t s);
   // multi-right-hand-side solve with the factor in lbuf/linv (marginals.hip): Y (n x K, column-major, rows in
@@ -338,7 +339,7 @@ class Engine {
   void ensure_device_state();
   void sync_host_state();
   void setup_edges_device();
-  void compute_errors_async();
+  void compute_errors_async(bool reduce = true);  // reduce: the chi2 all-reduce over landmark shards
   void refresh_host_payload(bool jacobians);  // host-J groups: payload at the current state (callback), upload
   EdgeArgs group_args(const EGroup& g) const;
   double chi2_sync();

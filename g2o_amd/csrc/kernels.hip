@@ -541,7 +541,8 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
                  const int* __restrict__ st_obs, const int* __restrict__ pairs, const int* __restrict__ pp,
                  const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,
-                 double* __restrict__ S, int mode) {
+                 double* __restrict__ S, int mode, int ntasks, const long long* __restrict__ zr,
+                 double* __restrict__ fronts) {
   constexpr int GB = PD * LD;                        // doubles per staged block: G, PD x LD col-major
   constexpr int NPC = GB / 2;                        // 16-B pieces per block
   constexpr int NC = (SCH_SB * NPC + 255) / 256;     // 16-B pieces per thread per batch
@@ -551,7 +552,12 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
   __shared__ int so[2][SCH_SB];  // staged observation per block
   __shared__ int sp[2][SCH_SB];  // pair lists (posA | posB << 16), slot-sorted
   __shared__ int spp[2][SCH_PPB];
-  const launch::SchurTask t = tasks[xcd_item(blockIdx.x, gridDim.x)];  // XCD-contiguous rows
+  if ((int)blockIdx.x >= ntasks) {  // side job: zero one range of the factorization's front pool
+    const long long off = zr[2 * (blockIdx.x - ntasks)], len = zr[2 * (blockIdx.x - ntasks) + 1];
+    for (long long i = threadIdx.x; i < len; i += 256) fronts[off + i] = 0.0;
+    return;
+  }
+  const launch::SchurTask t = tasks[xcd_item(blockIdx.x, ntasks)];  // XCD-contiguous rows
   const int nb = t.b1 - t.b0;
   const int tid = threadIdx.x, w = tid >> 6;
   const int ls = tid >> 2, q = tid & 3;
@@ -781,10 +787,9 @@ __global__ void __launch_bounds__(256)
 }
 
 // ------------------------------------------------------------------------------ oplus
-__global__ void k_oplus_se3expmap(int n, const int* __restrict__ xoff, const double* __restrict__ x,
-                                  double* __restrict__ st) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= n || xoff[v] < 0) return;
+__device__ __forceinline__ void d_oplus_se3expmap(int v, const int* __restrict__ xoff, const double* __restrict__ x,
+                                            double* __restrict__ st, int* __restrict__ nopl) {
+  if (xoff[v] < 0) return;
   const double* u = x + xoff[v];
   double uu[6] = {u[0], u[1], u[2], u[3], u[4], u[5]};
   double qe[4], te[3];
@@ -800,18 +805,17 @@ __global__ void k_oplus_se3expmap(int n, const int* __restrict__ xoff, const dou
   s[3] = qn[0]; s[4] = qn[1]; s[5] = qn[2]; s[6] = qn[3];
 }
 
-__global__ void k_oplus_xyz(int n, const int* __restrict__ xoff, const double* __restrict__ x, double* __restrict__ st) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= n || xoff[v] < 0) return;
+__device__ __forceinline__ void d_oplus_xyz(int v, const int* __restrict__ xoff, const double* __restrict__ x,
+                                            double* __restrict__ st, int* __restrict__ nopl) {
+  if (xoff[v] < 0) return;
   const double* u = x + xoff[v];
   double* s = st + (size_t)v * 3;
   s[0] += u[0]; s[1] += u[1]; s[2] += u[2];
 }
 
-__global__ void k_oplus_se3quat(int n, const int* __restrict__ xoff, const double* __restrict__ x,
-                                double* __restrict__ st, int* __restrict__ nopl) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= n || xoff[v] < 0) return;
+__device__ __forceinline__ void d_oplus_se3quat(int v, const int* __restrict__ xoff, const double* __restrict__ x,
+                                            double* __restrict__ st, int* __restrict__ nopl) {
+  if (xoff[v] < 0) return;
   const double* u = x + xoff[v];
   // increment = fromVectorMQT(u) (isometry3d_mappings.cpp:106-111)
   double inc[12];
@@ -845,9 +849,9 @@ __global__ void k_oplus_se3quat(int n, const int* __restrict__ xoff, const doubl
   for (int k = 0; k < 12; ++k) s[k] = Y[k];
 }
 
-__global__ void k_oplus_se2(int n, const int* __restrict__ xoff, const double* __restrict__ x, double* __restrict__ st) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= n || xoff[v] < 0) return;
+__device__ __forceinline__ void d_oplus_se2(int v, const int* __restrict__ xoff, const double* __restrict__ x,
+                                            double* __restrict__ st, int* __restrict__ nopl) {
+  if (xoff[v] < 0) return;
   const double* u = x + xoff[v];
   double* s = st + (size_t)v * 3;
   s[0] += u[0];
@@ -855,13 +859,28 @@ __global__ void k_oplus_se2(int n, const int* __restrict__ xoff, const double* _
   s[2] = normalize_theta(s[2] + u[2]);
 }
 
-__global__ void k_oplus_xy(int n, const int* __restrict__ xoff, const double* __restrict__ x, double* __restrict__ st) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;  // vertex_point_xy.h:77-81
-  if (v >= n || xoff[v] < 0) return;
+__device__ __forceinline__ void d_oplus_xy(int v, const int* __restrict__ xoff, const double* __restrict__ x,
+                                            double* __restrict__ st, int* __restrict__ nopl) {  // vertex_point_xy.h:77-81
+  if (xoff[v] < 0) return;
   const double* u = x + xoff[v];
   double* s = st + (size_t)v * 2;
   s[0] += u[0];
   s[1] += u[1];
+}
+
+// SparseOptimizer::update (sparse_optimizer.cpp:441-454) over every vertex type in one launch: block ranges per type
+__global__ void __launch_bounds__(256) k_oplus_multi(launch::OplusList L, const double* __restrict__ x) {
+  int t = 0;
+  while (t + 1 < L.cnt && (int)blockIdx.x >= L.blk0[t + 1]) ++t;
+  const int v = ((int)blockIdx.x - L.blk0[t]) * 256 + threadIdx.x;
+  if (v >= L.n[t]) return;
+  switch (L.vt[t]) {
+    case 1: d_oplus_se3expmap(v, L.xoff[t], x, L.st[t], L.nopl); break;
+    case 2: d_oplus_xyz(v, L.xoff[t], x, L.st[t], L.nopl); break;
+    case 3: d_oplus_se3quat(v, L.xoff[t], x, L.st[t], L.nopl); break;
+    case 4: d_oplus_se2(v, L.xoff[t], x, L.st[t], L.nopl); break;
+    case 5: d_oplus_xy(v, L.xoff[t], x, L.st[t], L.nopl); break;
+  }
 }
 
 // ------------------------------------------------------------------------------ reductions
@@ -948,6 +967,78 @@ __global__ void __launch_bounds__(RED_BLOCK) k_error_partial(EdgeData d, int ne,
     __syncthreads();
   }
   if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+// computeActiveErrors (one edge group) and computeScale in one launch: blocks [0, npe) are k_error_partial's
+// chunks, the rest k_scale_partial's (same chunking and trees: the same sums bit for bit); k_sum_final2 finishes both
+template <class F>
+__global__ void __launch_bounds__(RED_BLOCK) k_error_scale_partial(EdgeData d, int ne, int npe, long long n,
+                                                                   long long npose, const double* __restrict__ x,
+                                                                   const double* __restrict__ b,
+                                                                   const double* __restrict__ lam,
+                                                                   double* __restrict__ partial) {
+  __shared__ double sh[RED_BLOCK];
+  double s = 0;
+  if ((int)blockIdx.x < npe) {
+    const long long base = (long long)blockIdx.x * RED_BLOCK * RED_PER_THREAD;
+    for (int k = 0; k < RED_PER_THREAD; ++k) {
+      const long long e = base + (long long)k * RED_BLOCK + threadIdx.x;
+      if (e < ne) {
+        double err[F::D];
+        F::error(d, (int)e, err);
+        double Om[F::D * F::D];
+        load_info<F::D>(d.info + (size_t)e * F::INFO, Om);
+        double c = 0;
+#pragma unroll
+        for (int i = 0; i < F::D; ++i) {
+          double r = 0;
+#pragma unroll
+          for (int j = 0; j < F::D; ++j) r += Om[i * F::D + j] * err[j];
+          c += err[i] * r;
+        }
+        if (d.rk) {
+          double r0, r1;
+          robustify(d.rk, d.rk_delta, c, r0, r1);
+          c = r0;
+        }
+        s += c;
+      }
+    }
+  } else {
+    const double lp = lam[4], ll = lam[0];
+    const long long base = (long long)(blockIdx.x - npe) * RED_BLOCK * RED_PER_THREAD;
+#pragma unroll
+    for (int k = 0; k < RED_PER_THREAD; ++k) {
+      const long long i = base + (long long)k * RED_BLOCK + threadIdx.x;
+      if (i < n) {
+        const double l = i < npose ? lp : ll;
+        s += x[i] * (l * x[i] + b[i]);
+      }
+    }
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int m = RED_BLOCK / 2; m > 0; m >>= 1) {
+    if ((int)threadIdx.x < m) sh[threadIdx.x] += sh[threadIdx.x + m];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+// two k_sum_final in one launch: block 0 sums partial[0, n0) into out0, block 1 partial[n0, n0 + n1) into out1
+__global__ void __launch_bounds__(RED_BLOCK) k_sum_final2(const double* __restrict__ partial, int n0, int n1,
+                                                          double* __restrict__ out0, double* __restrict__ out1) {
+  __shared__ double sh[RED_BLOCK];
+  const double* p = blockIdx.x == 0 ? partial : partial + n0;
+  const int np = blockIdx.x == 0 ? n0 : n1;
+  double s = 0;
+  for (int i = threadIdx.x; i < np; i += RED_BLOCK) s += p[i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int m = RED_BLOCK / 2; m > 0; m >>= 1) {
+    if ((int)threadIdx.x < m) sh[threadIdx.x] += sh[threadIdx.x + m];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *(blockIdx.x == 0 ? out0 : out1) = sh[0];
 }
 
 // computeScale (optimization_algorithm_levenberg.cpp:177-184) fused with the first sum pass:
@@ -1152,12 +1243,13 @@ void schur_diag(int pd, int ld, int nrows, const int* rptr, const int* robs, con
 }
 void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
-                hipStream_t s) {
-  if (ntasks <= 0) return;
+                int nzero, const long long* zr, double* fronts, hipStream_t s) {
+  if (ntasks <= 0 && nzero <= 0) return;
   static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;  // dev A/B only
+  const int nz = nzero > 0 ? nzero : 0;
   pl_dispatch(pd, ld, [&](auto P, auto L) {
-    hipLaunchKernelGGL((k_schur_rows<decltype(P)::value, decltype(L)::value>), ntasks, 256, 0, s, tasks, batches,
-                       st_obs, pairs, pp, G, s_hpp, Hpp, S, mode);
+    hipLaunchKernelGGL((k_schur_rows<decltype(P)::value, decltype(L)::value>), ntasks + nz, 256, 0, s, tasks, batches,
+                       st_obs, pairs, pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
   });
   KERNEL_CHECK();
 }
@@ -1173,23 +1265,27 @@ void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, con
 void backsub_g(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* G, const double* Ufac,
                const double* cl_all, int size_poses, int lm0, double* x, hipStream_t s) {
   if (nl <= 0) return;
+  static const int lanes = getenv("G2OHIP_BACKSUB_LANES") ? atoi(getenv("G2OHIP_BACKSUB_LANES")) : 8;  // dev A/B (8: C4 48.5 -> 45.3 us)
   pl_dispatch(pd, ld, [&](auto P, auto L) {
-    hipLaunchKernelGGL((k_backsub_g<decltype(P)::value, decltype(L)::value, 4>), grid_for((size_t)nl * 4, 256), 256,
-                       0, s, nl, lm_ptr, blk_pose, G, Ufac, cl_all, size_poses, lm0, x);
+    if (lanes == 8)
+      hipLaunchKernelGGL((k_backsub_g<decltype(P)::value, decltype(L)::value, 8>), grid_for((size_t)nl * 8, 256), 256,
+                         0, s, nl, lm_ptr, blk_pose, G, Ufac, cl_all, size_poses, lm0, x);
+    else
+      hipLaunchKernelGGL((k_backsub_g<decltype(P)::value, decltype(L)::value, 4>), grid_for((size_t)nl * 4, 256), 256,
+                         0, s, nl, lm_ptr, blk_pose, G, Ufac, cl_all, size_poses, lm0, x);
   });
   KERNEL_CHECK();
 }
 
-void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s) {
-  if (n <= 0) return;
-  const unsigned g = grid_for(n, 256);
-  switch (vtype) {
-    case 1: hipLaunchKernelGGL(k_oplus_se3expmap, g, 256, 0, s, n, xoff, x, st); break;
-    case 2: hipLaunchKernelGGL(k_oplus_xyz, g, 256, 0, s, n, xoff, x, st); break;
-    case 3: hipLaunchKernelGGL(k_oplus_se3quat, g, 256, 0, s, n, xoff, x, st, nopl); break;
-    case 4: hipLaunchKernelGGL(k_oplus_se2, g, 256, 0, s, n, xoff, x, st); break;
-    case 5: hipLaunchKernelGGL(k_oplus_xy, g, 256, 0, s, n, xoff, x, st); break;
+void oplus_multi(const OplusList& L0, const double* x, hipStream_t s) {
+  OplusList L = L0;
+  int nb = 0;
+  for (int t = 0; t < L.cnt; ++t) {
+    L.blk0[t] = nb;
+    nb += (int)grid_for(L.n[t], 256);
   }
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(k_oplus_multi, nb, 256, 0, s, L, x);
   KERNEL_CHECK();
 }
 
@@ -1211,6 +1307,18 @@ int error_partials(int family, const EdgeArgs& a, int ne, double* partial, hipSt
   });
   KERNEL_CHECK();
   return np;
+}
+void error_scale(int family, const EdgeArgs& a, int ne, long long n, long long npose, const double* x, const double* b,
+                 const double* lam, double* partial, double* out_chi, double* out_scale, hipStream_t s) {
+  const int npe = (int)sum_partials(ne), nps = (int)sum_partials(n);
+  if (npe + nps > 0)
+    family_dispatch(family, a, [&](auto fam) {
+      using F = decltype(fam);
+      hipLaunchKernelGGL(k_error_scale_partial<F>, npe + nps, RED_BLOCK, 0, s, mk(a), ne, npe, n, npose, x, b, lam,
+                         partial);
+    });
+  hipLaunchKernelGGL(k_sum_final2, 2, RED_BLOCK, 0, s, partial, npe, nps, out_chi, out_scale);
+  KERNEL_CHECK();
 }
 void sum_final(const double* partial, int np, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_sum_final, 1, RED_BLOCK, 0, s, partial, np, out);

@@ -82,15 +82,25 @@ struct SchurBatch {
   int st0, nst;  // staged blocks (st_obs)
   int pr0, npr;  // pairs (posA | posB << 16), slot CSR in pp[batch * (SCHUR_SL + 1) ...]
 };
+// nzero > 0: nzero more workgroups (after the row tasks) zero the (offset, length) ranges zr of `fronts` — the
+// factorization's pre-scattered fronts, cleared beside the Schur pass instead of by a launch of the factor's own
 void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
-                hipStream_t s);
+                int nzero, const long long* zr, double* fronts, hipStream_t s);
 void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv,
              const double* b, int size_poses, int lm0, double* x, hipStream_t s);
 // back-substitution from the G blocks of an assembly-time Schur split: x_l = U^-T (c_l - G^T x_p)
 void backsub_g(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* G, const double* Ufac,
                const double* cl_all, int size_poses, int lm0, double* x, hipStream_t s);
-void oplus(int vtype, int n, const int* xoff, const double* x, double* st, int* nopl, hipStream_t s);
+// vertex oplus of every type in one launch: per type (vertex type id 1..5, count, x offsets, states)
+struct OplusList {
+  int cnt = 0;
+  int vt[5], n[5], blk0[5];
+  const int* xoff[5];
+  double* st[5];
+  int* nopl = nullptr;
+};
+void oplus_multi(const OplusList& L, const double* x, hipStream_t s);
 size_t sum_partials(long long n);
 void sum(const double* v, long long n, double* partial, double* out, hipStream_t s);
 void scale_terms(long long n, const double* x, const double* b, const double* lam, double* out, hipStream_t s);
@@ -98,6 +108,10 @@ void scale_terms(long long n, const double* x, const double* b, const double* la
 // writes the group's partials at partial[0..np) and returns np; sum_final adds all groups' partials in order
 int error_partials(int family, const EdgeArgs& a, int ne, double* partial, hipStream_t s);
 void sum_final(const double* partial, int np, double* out, hipStream_t s);
+// error_partials (one edge group) + scale_sum in one launch and both finals in a second: chi2 -> out_chi, the
+// computeScale sum -> out_scale (the same sums bit for bit)
+void error_scale(int family, const EdgeArgs& a, int ne, long long n, long long npose, const double* x, const double* b,
+                 const double* lam, double* partial, double* out_chi, double* out_scale, hipStream_t s);
 // computeScale + sum (same chunking/tree as sum(): deterministic)
 void scale_sum(long long n, long long npose, const double* x, const double* b, const double* lam, double* partial,
                double* out, hipStream_t s);
@@ -151,7 +165,8 @@ struct StepHead {
 // vals[src[k] & 0x7fffffff] (+ lambda when src[k] < 0)
 void chol_prescatter(int nzero, const long long* zr, long long nent, const double* vals, const long long* dst,
                      const int* src, const double* lam, double* fronts, hipStream_t s);
-void chol_vec_init(int nfronts, const FrontDesc* fd, const double* rhs_p, double* vecs, hipStream_t s);
+// front vectors v_s = [rhs(perm[c0 ..]) (own columns); 0]
+void chol_vec_init(int nfronts, const FrontDesc* fd, const int* perm, const double* rhs, double* vecs, hipStream_t s);
 // assembly + extend-add of a level (slab tasks, t.c == 0: columns [a, b)) with every front's first
 // diagonal block assembled, factored and forward-solved beside it (t.c == 1). Input entries of scalar
 // column c (permuted): ent_row/ent_src[colptr[c] .. colptr[c+1]) = row in the front | diag << 30, index in vals

@@ -44,7 +44,7 @@ template <class F>
 __device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err, double* A, double* B, double* Om) {
   constexpr int D = F::D;
   F::linearize(d, e, err, A, B);
-  load_info<D>(d.info + (size_t)e * F::INFO, Om);
+  load_info<D>(info_rec(d, e, F::INFO), Om);
   if (d.rk) {
     double chi = 0;
 #pragma unroll
@@ -458,7 +458,7 @@ void linearize_fused(const EdgeArgs& a, const int4* chunks, int nchunks, const i
                      double* Hll, double* b, int num_poses, int size_poses, int lm_begin, double* lpart,
                      const SchurSplit* sp, hipStream_t s) {
   if (nchunks <= 0) return;
-  const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
+  const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
   const SchurSplit z = sp ? *sp : SchurSplit{};
   if (sp)
     hipLaunchKernelGGL((k_linearize_fused<FamilyBA, true>), grid_for(nchunks, 4), 256, 0, s, d, chunks, nchunks, h0, h1,
@@ -483,7 +483,7 @@ void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, doubl
 void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, int num_poses, int lm_begin,
                   const SchurSplit* sp, hipStream_t s) {
   if (npose <= 0) return;
-  const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
+  const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
   const SchurSplit z = sp ? *sp : SchurSplit{};
   if (sp)
     hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,

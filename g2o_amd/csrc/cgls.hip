@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(B) k_cgls_jac(dev::EdgeData d, int ne, const i
   if (e >= ne) return;
   double err[2], A[6], Bm[12];
   dev::FamilyBA::linearize(d, e, err, A, Bm);
-  const double si = sqrt(d.info[(size_t)e * dev::FamilyBA::INFO]);  // sqrt(Omega(0,0)) (jacobi_solver.hpp:563)
+  const double si = sqrt(dev::info_rec(d, e, dev::FamilyBA::INFO)[0]);  // sqrt(Omega(0,0)) (jacobi_solver.hpp:563)
   const bool fa = h0[d.v0[e]] >= 0, fb = h1[d.v1[e]] >= 0;
 #pragma unroll
   for (int k = 0; k < 6; ++k) JA[(size_t)e * 6 + k] = fa ? A[k] * si : 0.0;
@@ -520,7 +520,7 @@ void DeviceCGLS::setup(int nc, int np_, int ne_, const std::vector<int>& ptp, co
 
 void DeviceCGLS::build(const EdgeArgs& a, const int* h0, const int* h1, hipStream_t s) {
   if (ne <= 0) return;
-  const dev::EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
+  const dev::EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
   hipLaunchKernelGGL(k_cgls_jac, grid_for(ne, B), B, 0, s, d, ne, h0, h1, JA.get(), JB.get());
   const int nce = (int)(JBc.size() / 12);
   hipLaunchKernelGGL(k_cgls_gather_cam, grid_for(nce, B), B, 0, s, nce, cam_e.get(), JB.get(), JBc.get());

@@ -242,7 +242,15 @@ struct EdgeData {
   const double* s1;         // state array of vertex-1 type
   int rk;                   // robust kernel of the edge set (G2OHIP_RK_*), 0 none
   double rk_delta;          // RobustKernel::delta
+  int ue = 0;               // uniform records: bit 0 one information record for every edge, bit 1 one intrinsics record
 };
+// an edge's packed information / intrinsics record (a single shared record when the edge group's are all equal)
+DI const double* info_rec(const EdgeData& d, int e, int stride) {
+  return d.info + ((d.ue & 1) ? 0 : (size_t)e * stride);
+}
+DI const double* param_rec(const EdgeData& d, int e, int stride) {
+  return d.params + ((d.ue & 2) ? 0 : (size_t)e * stride);
+}
 
 // RobustKernel*::robustify (robust_kernel_impl.cpp:65-200): rho[0] = rho(e2), rho[1] = rho'(e2) (rho'' is not
 // used on this path: base_edge.h:117-123 builds the weighted information from rho' only)
@@ -340,7 +348,7 @@ struct FamilyBA {
     const double pv[3] = {p[0], p[1], p[2]};
     qrot(q, pv, pc);
     pc[0] += c[0]; pc[1] += c[1]; pc[2] += c[2];
-    const double* K = d.params + (size_t)e * 4;
+    const double* K = param_rec(d, e, 4);
     err[0] = d.meas[(size_t)e * 2 + 0] - (pc[0] / pc[2] * K[0] + K[2]);
     err[1] = d.meas[(size_t)e * 2 + 1] - (pc[1] / pc[2] * K[1] + K[3]);
   }
@@ -352,7 +360,7 @@ struct FamilyBA {
     double pc[3];
     qrot(q, pv, pc);
     pc[0] += c[0]; pc[1] += c[1]; pc[2] += c[2];
-    const double* K = d.params + (size_t)e * 4;
+    const double* K = param_rec(d, e, 4);
     const double fx = K[0], fy = K[1];
     const double x = pc[0], y = pc[1], z = pc[2], z2 = z * z;
     err[0] = d.meas[(size_t)e * 2 + 0] - (x / z * fx + K[2]);

@@ -1158,6 +1158,7 @@ EdgeArgs Engine::group_args(const EGroup& g) const {
   a.D = g.D;
   a.DA = g.DA;
   a.DB = g.DB;
+  a.ue = g.ue;
   return a;
 }
 
@@ -1305,6 +1306,20 @@ void Engine::setup_edges_device() {
     }
     g.v0.upload(v0, stream);
     g.v1.upload(v1, stream);
+    {  // BA: edges sharing one information matrix / one set of intrinsics (the usual monocular case) read a single
+       // record instead of 24 + 32 bytes per edge (G2OHIP_UNIFORM_RECORDS=0 keeps per-edge records, A/B)
+      const char* ev = getenv("G2OHIP_UNIFORM_RECORDS");
+      g.ue = 0;
+      if (g.family == FAM_BA && gne > 1 && !(ev && atoi(ev) == 0)) {
+        auto uniform = [&](const std::vector<double>& v, int st) {
+          for (int k = 1; k < gne; ++k)
+            if (std::memcmp(v.data() + (size_t)k * st, v.data(), sizeof(double) * st) != 0) return false;
+          return true;
+        };
+        if (uniform(info, minfo)) { g.ue |= 1; info.resize(minfo); }
+        if (uniform(params, 4)) { g.ue |= 2; params.resize(4); }
+      }
+    }
     g.info.upload(info, stream);
     g.params.upload(params, stream);
     if (g.family == FAM_HOSTJ) upload_group_payload(hg, g, stream);
@@ -1386,6 +1401,8 @@ void Engine::setup_edges_device() {
     cm_v0.upload(nz_i(cv0), stream);
     cm_v1.upload(nz_i(cv1), stream);
     cm_meas.upload(nz_d(cmeas), stream);
+    if ((g.ue & 1) && cinfo.size() > 3) cinfo.resize(3);  // the shared record (see the group's upload)
+    if ((g.ue & 2) && cpar.size() > 4) cpar.resize(4);
     cm_info.upload(nz_d(cinfo), stream);
     cm_params.upload(nz_d(cpar), stream);
   }

@@ -71,6 +71,7 @@ struct EGroup {
   int ne = 0;
   DevBuf<int> v0, v1;                   // local vertex indices (per type)
   DevBuf<double> meas, info, params;    // meas: family payload (host-J: [e | Ji | Jj] per edge)
+  int ue = 0;                           // info / params stored as one shared record (bit 0 / bit 1): all edges equal
   long long slotA = 0, slotB = 0;       // first slot of the group's A / B sides in the arenas of dims DA / DB
   DevBuf<long long> off_dst;            // per edge: offset of its off-diagonal block (bit 62: a shared-block slot)
   DevBuf<unsigned char> off_tr;

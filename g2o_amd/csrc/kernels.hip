@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(256) k_error(EdgeData d, int ne, double* __res
   double err[F::D];
   F::error(d, e, err);
   double Om[F::D * F::D];
-  load_info<F::D>(d.info + (size_t)e * F::INFO, Om);
+  load_info<F::D>(info_rec(d, (int)e, F::INFO), Om);
   double s = 0;
 #pragma unroll
   for (int i = 0; i < F::D; ++i) {
@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(256)
   double err[D], A[D * DA], B[D * DB], Om[D * D];
   if (nfA || nfB) {
     F::linearize(d, e, err, A, B);
-    load_info<D>(d.info + (size_t)e * F::INFO, Om);
+    load_info<D>(info_rec(d, e, F::INFO), Om);
     if (d.rk) {  // robust branch of constructQuadraticForm (base_binary_edge.hpp:104-135): Omega, omega_r scaled by rho'
       double chi = 0;
 #pragma unroll
@@ -943,7 +943,7 @@ __global__ void __launch_bounds__(RED_BLOCK) k_error_partial(EdgeData d, int ne,
       double err[F::D];
       F::error(d, (int)e, err);
       double Om[F::D * F::D];
-      load_info<F::D>(d.info + (size_t)e * F::INFO, Om);
+      load_info<F::D>(info_rec(d, (int)e, F::INFO), Om);
       double c = 0;
 #pragma unroll
       for (int i = 0; i < F::D; ++i) {
@@ -987,7 +987,7 @@ __global__ void __launch_bounds__(RED_BLOCK) k_error_scale_partial(EdgeData d, i
         double err[F::D];
         F::error(d, (int)e, err);
         double Om[F::D * F::D];
-        load_info<F::D>(d.info + (size_t)e * F::INFO, Om);
+        load_info<F::D>(info_rec(d, (int)e, F::INFO), Om);
         double c = 0;
 #pragma unroll
         for (int i = 0; i < F::D; ++i) {
@@ -1110,7 +1110,7 @@ __global__ void __launch_bounds__(256)
 namespace launch {
 
 static EdgeData mk(const EdgeArgs& a) {
-  return EdgeData{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta};
+  return EdgeData{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
 }
 
 // host-Jacobian families: runtime (D, DA, DB) -> FamilyHostJ<D, DA, DB> (vertex dims 2, 3 or 6, D = 1..6)

@@ -20,6 +20,7 @@ struct EdgeArgs {
   int rk = 0;          // robust kernel (G2OHIP_RK_*), uniform over the edge group
   double rk_delta = 1.0;
   int D = 0, DA = 0, DB = 0;  // host-J family dimensions
+  int ue = 0;                 // uniform records (EdgeData::ue): bit 0 information, bit 1 intrinsics
 };
 
 namespace launch {

@@ -528,7 +528,10 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
 
 // Task flags: 1 update the tile (else TRSM + L21 store only), 4 the step's next-diagonal task,
 // 8 the tile may reach into the contribution block (columns >= ns: no separate k_syrk pass),
-// 16 an inverse task: block (tj, ti) of X = L11^-1 (see below).
+// 16 an inverse task: block (tj, ti) of X = L11^-1 (see below),
+// 64 lagged pair (odd steps of a lagged front, DeviceCholesky::setup): the update also applies the PREVIOUS
+//    panel (k0 - 32, whose L rows the strip tiles of the even step stored), so the trailing columns are read and
+//    written once per two panels (rank-64); the even steps update only the next panel's strip (clim = r0 + kbn).
 // Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
 __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, const launch::StepHead head,
                                               double* __restrict__ fronts,
@@ -563,13 +566,15 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     // D' = A(r0:r0+32, r0:r0+32) - X X^T with X = P(r0:r0+32) L_kk^-T, then its factor, inverse
     // and forward solve. Only the critical chain of the panel step lives here.
     const int kbn = min(NB, ns - r0);
-    double lv[NB * NB / 256], pv[NB * NB / 256], cdv[NB * NB / 256];
+    const bool pair = t.flags & 64;  // the block also lacks the previous panel's update (lagged front, odd step)
+    double lv[NB * NB / 256], pv[NB * NB / 256], cdv[NB * NB / 256], xpv[NB * NB / 256];
 #pragma unroll
     for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
       const int e = tid + 256 * u_, r = e & (NB - 1), c = e >> 5;
       lv[u_] = ld0(Lin, e, kb > 0);  // kb = 0: first block of a big panel, already fully updated
       pv[u_] = ld0(F, (k0 + c) * m + r0 + r, c < kb);
       cdv[u_] = ld0(F, (r0 + c) * m + r0 + r, r >= c && r < kbn);
+      xpv[u_] = ld0(L, (k0 - NB + c) * m + r0 + r, pair);  // L rows of the block in the previous panel
     }
     const double ykv = ld0(ysol, t.c0 + k0 + tid, tid < kb);
     const double vo = ld0(v, r0 + tid, tid < kbn);
@@ -579,6 +584,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
       Li[c * PS + r] = lv[u_];  // e = row * 32 + col of the row-major inverse: (c, r) = (row, col)
       Pa[r * PS + c] = pv[u_];
       Dn[r * DS + c] = cdv[u_];
+      Pb[r * PS + c] = xpv[u_];
     }
     if (tid < NB) yk[tid] = ykv;
     __syncthreads();
@@ -596,9 +602,16 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
       for (int i = 0; i < 4; ++i) Pa[(16 * xr + lk + 4 * i) * PS + 16 * xc + lr] = x0[i];
     }
     __syncthreads();
-    {  // D' -= X X^T: wave w owns the 16x16 tile (w & 1, w >> 1)
+    {  // D' -= X X^T (+ X_prev X_prev^T on a lagged odd step): wave w owns the 16x16 tile (w & 1, w >> 1)
       const int tr = w & 1, tc = w >> 1;
       dx4 acc = {0.0, 0.0, 0.0, 0.0};
+      if (pair) {
+#pragma unroll
+        for (int kk = 0; kk < NB / 4; ++kk) {
+          const int k = kk * 4 + lk;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Pb[(16 * tr + lr) * PS + k], Pb[(16 * tc + lr) * PS + k], acc, 0, 0, 0);
+        }
+      }
 #pragma unroll
       for (int kk = 0; kk < NB / 4; ++kk) {
         const int k = kk * 4 + lk;
@@ -696,6 +709,17 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     return;
   }
 
+  // ---- lagged pair: the previous panel's L rows of I and J (stored by the even step's strip tiles) go first
+  const bool pair = (t.flags & 64) && upd;
+  MfmaTile T;
+  T.zero();
+  double xpa[8], xpb[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+    xpa[u] = ld0(L, (k0 - NB + q) * m + I0 + r, pair && I0 + r < m);
+    xpb[u] = ld0(L, (k0 - NB + q) * m + J0 + r, pair && J0 + r < m);
+  }
   // ---- stage L_kk^-1, y_k, the raw panel rows of I (and J), prefetch the C tile: every global
   // load is issued before the first LDS store so the whole batch is in flight at once
   double lv[NB * NB / 256], pav[8], pbv[8], cv[16];
@@ -710,6 +734,17 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   }
   const int climit = t.clim;  // ns; m when the contribution block is fused; the big-panel end when blocked
   if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
+  if (pair) {  // C[I, J] -= X_prev,I X_prev,J^T into the accumulators first
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+      Pa[r * PS + q] = xpa[u];
+      Pb[r * PS + q] = xpb[u];
+    }
+    __syncthreads();
+    T.step(Pa, Pb, lane, w);
+    __syncthreads();  // Pa / Pb free for the current panel
+  }
 #pragma unroll
   for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
     const int e = tid + 256 * u_;
@@ -773,8 +808,6 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   if (!upd) { PH1R(7) return; }
 
   // ---- C[I, J] -= P_I P_J^T (columns inside the supernode, lower triangle)
-  MfmaTile T;
-  T.zero();
   T.step(Pa, Pb, lane, w);
   __syncthreads();
   T.store(sh, lane, w);

@@ -390,6 +390,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const int wide_pb = wp ? std::max(64, atoi(wp) / 64 * 64) : 128;
     const bool dev_noinv = getenv("G2OHIP_DEV_NOINV") != nullptr;  // timing experiments only (wrong solve)
     const bool dev_diagonly = getenv("G2OHIP_DEV_DIAGONLY") != nullptr;  // timing experiments only (wrong factor)
+    // lagged trailing updates on levels with a separate contribution pass (their steps are bound by the rank-32
+    // tile traffic, not the diagonal chain): even steps update only the next panel's column strip, odd steps
+    // apply two panels at once (rank 64) to the rest of the supernode's columns (G2OHIP_CHOL_LAG=0: every step
+    // updates every trailing column, A/B)
+    const char* lg = getenv("G2OHIP_CHOL_LAG");
+    const int lag_mode = lg ? atoi(lg) : 1;  // 0 off, 1 levels with a separate contribution pass, 2 every unblocked level
+    const bool lag_on = lag_mode != 0;
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
     const long long pre_max = pm ? atoll(pm) : (256LL << 20);
     std::vector<long long> zr, pdst;
@@ -475,16 +482,22 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           const bool blk = blocked(q);
           const int pend = blk ? std::min((k0 / lpb + 1) * lpb, q.ns) : q.ns;  // big-panel end
           const bool bnd = blk && r0 == pend && r0 < q.ns;  // next block starts a big panel: no diag task
+          // fused contribution (lag mode 2): the contribution columns ride with the pairs; an even LAST step updates
+          // every trailing column with its own panel (nothing may stay behind for the parent)
+          const bool lagged = lag_on && !blk && (!fused_contrib || lag_mode >= 2);
+          const bool last = r0 >= q.ns;
+          const bool strip = lagged && (p % 2 == 0) && !(fused_contrib && last), pair = lagged && (p % 2 == 1);
           // fused: every panel step also applies its rank-kb update to the contribution block (the
-          // step is latency-bound on the diagonal chain, the extra tiles run in its shadow)
-          const int clim = fused_contrib ? m : pend;
+          // step is latency-bound on the diagonal chain, the extra tiles run in its shadow); lagged even steps
+          // stop at the next panel's strip
+          const int clim = strip ? std::min(q.ns, r0 + NB) : (fused_contrib ? m : pend);
           const int T = (m - r0 + TT - 1) / TT, TJ = (clim - r0 + TT - 1) / TT;
-          const int fl = (fused_contrib ? 8 : 0) | (bnd ? 32 : 0);
+          const int fl = (fused_contrib ? 8 : 0) | (bnd ? 32 : 0) | (pair ? 64 : 0);
           auto mk = [&](int tile, int flags) {
             return launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns, q.c0,
                                     k0 | (kb << 16), tile, flags, clim};
           };
-          if (r0 < q.ns && !bnd) diag_t.push_back(mk(0, 4));
+          if (r0 < q.ns && !bnd) diag_t.push_back(mk(0, 4 | (pair ? 64 : 0)));
           for (int tj = 0; tj < std::max(TJ, 1); ++tj)
             for (int ti = tj; ti < T; ++ti) tile_t.push_back(mk(ti | (tj << 16), (tj < TJ ? 1 : 0) | fl));
           // inverse tasks: block row p-1's term into every pending block (bp, j), bp >= p, j < p;

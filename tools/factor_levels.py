@@ -21,12 +21,16 @@ for r in seg:
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     cur['k'][name] += d
     cur['n'][name] += 1
+    if name == 'k_step':
+        cur.setdefault('steps', []).append(d)
     cur['t1'] = int(r['End_Timestamp'])
 tot = collections.defaultdict(float)
 for l, c in enumerate(levels):
     span = (c['t1'] - c['t0']) / 1e3
     parts = '  '.join('%s %.0f(%d)' % (k[2:], v, c['n'][k]) for k, v in sorted(c['k'].items()))
     print('lev %2d span %8.0f us  %s' % (l, span, parts))
+    if c.get('steps'):
+        print('        k_step us: ' + ' '.join('%.1f' % v for v in c['steps']))
     for k, v in c['k'].items():
         tot[k] += v
 print('total', {k: round(v) for k, v in tot.items()}, 'span %.0f us' % ((int(seg[-1]['End_Timestamp']) - int(seg[0]['Start_Timestamp'])) / 1e3))

@@ -395,8 +395,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     // apply two panels at once (rank 64) to the rest of the supernode's columns (G2OHIP_CHOL_LAG=0: every step
     // updates every trailing column, A/B)
     const char* lg = getenv("G2OHIP_CHOL_LAG");
-    const int lag_mode = lg ? atoi(lg) : 1;  // 0 off, 1 levels with a separate contribution pass, 2 every unblocked level
+    const int lag_mode = lg ? atoi(lg) : 1;  // 0 off, 1 throughput-bound levels, 2 every unblocked level
     const bool lag_on = lag_mode != 0;
+    // fused-contribution levels are lagged when their first step has more tiles than one per CU (C4: the 4-front
+    // level, 183 -> 161 us; the 1- and 2-front levels are bound by the diagonal chain and lose ~6 us each)
+    const char* lfm = getenv("G2OHIP_CHOL_LAG_FUSED_MIN");
+    const long long lag_fused_min = lag_mode >= 2 ? 0 : (lfm ? atoll(lfm) : 256);
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
     const long long pre_max = pm ? atoll(pm) : (256LL << 20);
     std::vector<long long> zr, pdst;
@@ -484,7 +488,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           const bool bnd = blk && r0 == pend && r0 < q.ns;  // next block starts a big panel: no diag task
           // fused contribution (lag mode 2): the contribution columns ride with the pairs; an even LAST step updates
           // every trailing column with its own panel (nothing may stay behind for the parent)
-          const bool lagged = lag_on && !blk && (!fused_contrib || lag_mode >= 2);
+          const bool lagged = lag_on && !blk && (!fused_contrib || tiles0 > lag_fused_min);
           const bool last = r0 >= q.ns;
           const bool strip = lagged && (p % 2 == 0) && !(fused_contrib && last), pair = lagged && (p % 2 == 1);
           // fused: every panel step also applies its rank-kb update to the contribution block (the

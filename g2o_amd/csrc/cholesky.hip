@@ -533,6 +533,9 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
 //    panel (k0 - 32, whose L rows the strip tiles of the even step stored), so the trailing columns are read and
 //    written once per two panels (rank-64); the even steps update only the next panel's strip (clim = r0 + kbn).
 // Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
+// PAIRS: the launch may hold lagged-pair tasks (flag 64); without them the pair code is compiled out (166 instead of
+// ~180 VGPRs: three workgroups per CU instead of two)
+template <bool PAIRS>
 __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, const launch::StepHead head,
                                               double* __restrict__ fronts,
                                               double* __restrict__ lbuf, double* __restrict__ vecs,
@@ -566,7 +569,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     // D' = A(r0:r0+32, r0:r0+32) - X X^T with X = P(r0:r0+32) L_kk^-T, then its factor, inverse
     // and forward solve. Only the critical chain of the panel step lives here.
     const int kbn = min(NB, ns - r0);
-    const bool pair = t.flags & 64;  // the block also lacks the previous panel's update (lagged front, odd step)
+    const bool pair = PAIRS && (t.flags & 64);  // the block also lacks the previous panel's update (lagged, odd step)
     double lv[NB * NB / 256], pv[NB * NB / 256], cdv[NB * NB / 256], xpv[NB * NB / 256];
 #pragma unroll
     for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
@@ -710,10 +713,10 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   }
 
   // ---- lagged pair: the previous panel's L rows of I and J (stored by the even step's strip tiles) go first
-  const bool pair = (t.flags & 64) && upd;
+  const bool pair = PAIRS && (t.flags & 64) && upd;
   MfmaTile T;
   T.zero();
-  double xpa[8], xpb[8];
+  double xpa[8], xpb[8];  // (the PAIRS = false instantiation drops them: 166 VGPRs, three workgroups per CU)
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
@@ -734,7 +737,7 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   }
   const int climit = t.clim;  // ns; m when the contribution block is fused; the big-panel end when blocked
   if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
-  if (pair) {  // C[I, J] -= X_prev,I X_prev,J^T into the accumulators first
+  if (pair) {  // C[I, J] -= X_prev,I X_prev,J^T into the accumulators first, the current panel's loads in flight
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
@@ -970,9 +973,12 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
   KERNEL_CHECK();
 }
 void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs,
-               double* ysol, double* linv, double* xinv, int* fail, hipStream_t s) {
+               double* ysol, double* linv, double* xinv, int* fail, bool pairs, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_step, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
+  if (pairs)
+    hipLaunchKernelGGL(k_step<true>, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
+  else
+    hipLaunchKernelGGL(k_step<false>, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {

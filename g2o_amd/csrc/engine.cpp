@@ -519,6 +519,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         if (!dev_diagonly) stk.insert(stk.end(), tile_t.begin(), tile_t.end());
         if (!dev_diagonly) stk.insert(stk.end(), inv_t.begin(), inv_t.end());
         st.count = (int)stk.size() - st.off;
+        for (int k = st.off; k < st.off + st.count; ++k)
+          if (stk[k].flags & 64) st.kind = 6;
         if (st.count) ops.push_back(st);
         if ((p + 1) * NB % lpb) continue;
         // end of a big panel: trailing update of the blocked fronts, then their next first blocks
@@ -611,7 +613,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
     heads.assign(ops.size(), launch::StepHead{});
     for (size_t k = 0; k < ops.size(); ++k) {
-      if (ops[k].kind != 2) continue;
+      if (ops[k].kind != 2 && ops[k].kind != 6) continue;
       launch::StepHead& h = heads[k];
       h.n = 0;
       while (h.n < launch::CHOL_HEAD && h.n < ops[k].count) {  // the first workgroups (diagonal tasks among them)
@@ -650,9 +652,9 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
                                       ent_row.get(),
                                       ent_src.get(), vals, lam, fronts.get(), vecs.get(),
                                       lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 0 ? 0 : (op.kind == 5 ? 2 : 1), s); break;
-      case 2: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
-                                vecs.get(), y_p.get(),
-                                linv.get(), xinv.get(), fail, s);
+      case 2:
+      case 6: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
+                                vecs.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 6, s);
         break;
       default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;
     }

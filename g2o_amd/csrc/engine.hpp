@@ -108,7 +108,8 @@ struct DeviceCholesky {
   // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
   // trailing-update (k_syrk) launches, big-panel backward rounds
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
-  struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add, 2 panel step, 3 syrk
+  struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add, 2 panel step
+                                        // (6: with lagged-pair tasks), 3 syrk
   std::vector<Op> ops;
   std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
   DevBuf<launch::Task> tasks;

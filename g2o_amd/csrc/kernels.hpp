@@ -176,7 +176,7 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
                      int assemble, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place, 2 in place (m <= 512)
 void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs, double* ysol,
-               double* linv, double* xinv, int* fail, hipStream_t s);
+               double* linv, double* xinv, int* fail, bool pairs, hipStream_t s);  // pairs: lagged-pair tasks present
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
 // the contribution block, K = [0, ns)); columns stop at ns unless kb = ns (then m)
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s);

@@ -62,7 +62,7 @@ EXPORTS = [
     "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_solver_multiply_hessian",
     "g2ohip_solver_linear_residual", "g2ohip_solver_factor_info", "g2ohip_solver_compute_marginals", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
     "g2ohip_discard_top", "g2ohip_stage", "g2ohip_linear_solve_ccs", "g2ohip_comm_unique_id",
-    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
+    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_comm_selftest", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
     "g2ohip_kernel_timing_only", "g2ohip_set_stats_level", "g2ohip_kernel_ms",
     "g2ohip_kernel_count", "g2ohip_kernel_bytes", "g2ohip_kernel_flops", "g2ohip_last_error",
     "g2ohip_version",
@@ -130,6 +130,7 @@ def lib() -> C.CDLL:
         "g2ohip_comm_unique_id": ([P], I),
         "g2ohip_set_comm": ([P, P, I, I], I),
         "g2ohip_set_comm_local": ([P, C.c_char_p, I, I], I),
+        "g2ohip_comm_selftest": ([I, P, I, P, P], I),
         "g2ohip_debug_phases": ([P, I], I),
         "g2ohip_symbolic_analyze": ([I, I, I, P, P, P, P], I),
         "g2ohip_enable_kernel_timing": ([P, I], None),
@@ -413,6 +414,15 @@ class SparseOptimizer:
         buf = (C.c_ubyte * 128)()
         _check(lib().g2ohip_comm_unique_id(buf), "comm_unique_id")
         return bytes(buf)
+
+    @staticmethod
+    def comm_selftest(values, device: int = 0):
+        """RCCL binding smoke test on one device (one-rank communicator): [allreduce sum | allreduce max]."""
+        v = np.ascontiguousarray(values, np.float64)
+        out = np.zeros(2 * v.size)
+        uid = (C.c_ubyte * 128).from_buffer_copy(SparseOptimizer.comm_unique_id())
+        _check(lib().g2ohip_comm_selftest(device, uid, v.size, _p(v), _p(out)), "comm_selftest")
+        return out[: v.size], out[v.size:]
 
     def set_comm(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_ubyte * 128).from_buffer_copy(uid)

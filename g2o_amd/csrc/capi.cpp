@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <map>
+#include <memory>
 #include <vector>
 #include <cstring>
 #include <string>
@@ -308,6 +309,29 @@ int g2ohip_comm_unique_id(unsigned char out[128]) {
 int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int nranks) {
   if (!g || !uid || rank < 0 || rank >= nranks) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->set_comm(uid, rank, nranks); });
+}
+int g2ohip_comm_selftest(int device, const unsigned char uid[128], int n, const double* in, double* out) {
+  if (!uid || n <= 0 || !in || !out) return G2OHIP_ERR_ARG;
+  return guarded([&] {
+    HIP_CHECK(hipSetDevice(device));
+    std::string err;
+    std::unique_ptr<g2ohip::Comm> c(g2ohip::make_rccl_comm(uid, 0, 1, err));
+    if (!c) throw g2ohip::DeviceError(err);
+    hipStream_t s = nullptr;
+    HIP_CHECK(hipStreamCreate(&s));
+    double* d = nullptr;
+    HIP_CHECK(hipMalloc(&d, sizeof(double) * 2 * (size_t)n));
+    HIP_CHECK(hipMemcpyAsync(d, in, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(d + n, in, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    c->allreduce_sum(d, (size_t)n, s);
+    c->allreduce_max(d + n, (size_t)n, s);
+    HIP_CHECK(hipMemcpyAsync(out, d, sizeof(double) * 2 * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipFree(d));
+    HIP_CHECK(hipStreamDestroy(s));
+    c.reset();  // ncclCommDestroy
+    return G2OHIP_OK;
+  });
 }
 int g2ohip_set_comm_local(g2ohip_graph* g, const char* key, int rank, int nranks) {
   if (!g || !key || rank < 0 || rank >= nranks) return G2OHIP_ERR_ARG;

@@ -125,3 +125,12 @@ def test_sharded_pcg_matches_single(g2o_amd_mod):
     assert np.array_equal(states[1][:6 * C], states[0][:6 * C])
     xs = single.minimal_state()
     assert np.linalg.norm(x - xs) <= RTOL * np.linalg.norm(xs)
+
+
+def test_rccl_binding_single_rank(g2o_amd_mod):
+    """The RCCL transport itself (RcclComm: ncclGetUniqueId, ncclCommInitRank, ncclAllReduce sum / max on a HIP
+    stream, ncclCommDestroy) on a one-rank communicator: a one-GPU box cannot host two ranks of one RCCL
+    communicator (RCCL refuses duplicate GPUs), so the multi-rank path is covered by the LocalComm tests above."""
+    v = np.linspace(-3.0, 5.0, 1000)
+    s, m = g2o_amd_mod.SparseOptimizer.comm_selftest(v)
+    assert np.array_equal(s, v) and np.array_equal(m, v)

@@ -536,7 +536,7 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
 // PAIRS: the launch may hold lagged-pair tasks (flag 64); without them the pair code is compiled out (166 instead of
 // ~180 VGPRs: three workgroups per CU instead of two)
 template <bool PAIRS>
-__global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks, const launch::StepHead head,
+__global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ tasks, const launch::StepHead head,
                                               double* __restrict__ fronts,
                                               double* __restrict__ lbuf, double* __restrict__ vecs,
                                               double* __restrict__ ysol, double* __restrict__ linv,
@@ -716,12 +716,15 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
   const bool pair = PAIRS && (t.flags & 64) && upd;
   MfmaTile T;
   T.zero();
-  double xpa[8], xpb[8];  // (the PAIRS = false instantiation drops them: 166 VGPRs, three workgroups per CU)
+  if (pair) {  // staged before the current panel's loads are issued: the two batches never share registers
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-    xpa[u] = ld0(L, (k0 - NB + q) * m + I0 + r, pair && I0 + r < m);
-    xpb[u] = ld0(L, (k0 - NB + q) * m + J0 + r, pair && J0 + r < m);
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+      const double xa = ld0(L, (k0 - NB + q) * m + I0 + r, I0 + r < m);
+      const double xb = ld0(L, (k0 - NB + q) * m + J0 + r, J0 + r < m);
+      Pa[r * PS + q] = xa;
+      Pb[r * PS + q] = xb;
+    }
   }
   // ---- stage L_kk^-1, y_k, the raw panel rows of I (and J), prefetch the C tile: every global
   // load is issued before the first LDS store so the whole batch is in flight at once
@@ -736,18 +739,12 @@ __global__ void __launch_bounds__(256) k_step(const StepTask* __restrict__ tasks
     pbv[u] = ld0(F, (k0 + q) * m + J0 + r, upd && q < kb && J0 + r < m);
   }
   const int climit = t.clim;  // ns; m when the contribution block is fused; the big-panel end when blocked
-  if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
   if (pair) {  // C[I, J] -= X_prev,I X_prev,J^T into the accumulators first, the current panel's loads in flight
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-      Pa[r * PS + q] = xpa[u];
-      Pb[r * PS + q] = xpb[u];
-    }
     __syncthreads();
     T.step(Pa, Pb, lane, w);
     __syncthreads();  // Pa / Pb free for the current panel
   }
+  if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
 #pragma unroll
   for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
     const int e = tid + 256 * u_;

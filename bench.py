@@ -291,7 +291,12 @@ def main():
     if tf and os.path.exists(tf):
         traffic_all = json.load(open(tf))
 
+    # PMC traffic is measured on one workload (its _meta.config): other configs report null
+    traffic_cfg = traffic_all.get("_meta", {}).get("config", "C4")
+
     def traffic(k):
+        if traffic_cfg != args.config:
+            return None
         rec = traffic_all.get(k)
         return rec.get("bytes_per_launch") if isinstance(rec, dict) else rec
 

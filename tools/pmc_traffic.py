@@ -88,6 +88,8 @@ def main():
         }
         if stage == "chol_factor":
             res[stage]["launches"] = "factorizations (sum over the factor's kernel chain)"
+    res["_meta"] = {"config": os.environ.get("G2OHIP_TRAFFIC_CONFIG", "C4"),
+                    "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py, tools/pmc_traffic.py"}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))

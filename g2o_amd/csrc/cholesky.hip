@@ -877,7 +877,8 @@ __global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks
 
 __global__ void __launch_bounds__(256) k_bwd_x(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                const double* __restrict__ xinv, const double* __restrict__ tsol,
-                                               double* __restrict__ xsol) {
+                                               double* __restrict__ xsol, const int* __restrict__ perm,
+                                               double* __restrict__ xout) {
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int ns = me.ns;
@@ -896,7 +897,10 @@ __global__ void __launch_bounds__(256) k_bwd_x(const Task* __restrict__ tasks, c
   double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (lane == 0) xsol[me.c0 + j] = acc;
+  if (lane == 0) {
+    xsol[me.c0 + j] = acc;
+    xout[perm[me.c0 + j]] = acc;  // the solution in the caller's order (no separate inverse permutation)
+  }
 }
 
 // blocked fronts: t_j -= sum_{i in [t.b, ns)} L(i, j) x_i for the columns j of one big panel (the later big
@@ -1006,9 +1010,9 @@ void chol_bwd_inner(int ntasks, const Task* tasks, const FrontDesc* fd, const do
   KERNEL_CHECK();
 }
 void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,
-                hipStream_t s) {
+                const int* perm, double* xout, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_bwd_x, ntasks, 256, 0, s, tasks, fd, xinv, tsol, xsol);
+  hipLaunchKernelGGL(k_bwd_x, ntasks, 256, 0, s, tasks, fd, xinv, tsol, xsol, perm, xout);
   KERNEL_CHECK();
 }
 

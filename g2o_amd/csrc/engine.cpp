@@ -666,13 +666,14 @@ void DeviceCholesky::solve(double* x, hipStream_t s) {
     const BwdLevel& bl = bwd_ops[l];
     launch::chol_bwd_gemv(bl.gemv.second, tasks.get() + bl.gemv.first, fd.get(), rows.get(), lbuf.get(), y_p.get(),
                           x_p.get(), t_p.get(), s);
-    launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), t_p.get(), x_p.get(), s);
+    launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
+                       perm.get(), x, s);
     for (const auto& rd : bl.rounds) {
       launch::chol_bwd_inner(rd.first.second, tasks.get() + rd.first.first, fd.get(), lbuf.get(), x_p.get(), t_p.get(), s);
-      launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), t_p.get(), x_p.get(), s);
+      launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
+                         perm.get(), x, s);
     }
   }
-  launch::chol_ipermute(sym.n, perm.get(), x_p.get(), x, s);
 }
 
 void DeviceCholesky::solve_multi(double* Y, double* W, double* T, int K, hipStream_t s) {

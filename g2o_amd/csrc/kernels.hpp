@@ -186,8 +186,9 @@ void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int
                    const double* ysol, const double* xsol, double* tsol, hipStream_t s);
 void chol_bwd_inner(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* xsol, double* tsol,
                     hipStream_t s);
+// x = X^T t per front column; each x also lands at xout[perm[k]] (the caller's order)
 void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,
-                hipStream_t s);
+                const int* perm, double* xout, hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only
 constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 16, CHOL_BW = 4;
 // computeMarginals multi-right-hand-side solves (marginals.hip): one launch per tree level, one workgroup per front

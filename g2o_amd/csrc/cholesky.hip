@@ -716,15 +716,12 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   const bool pair = PAIRS && (t.flags & 64) && upd;
   MfmaTile T;
   T.zero();
-  if (pair) {  // staged before the current panel's loads are issued: the two batches never share registers
+  double xpa[8], xpb[8];  // issued with the current panel's loads (one round trip), staged before the C prefetch
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-      const double xa = ld0(L, (k0 - NB + q) * m + I0 + r, I0 + r < m);
-      const double xb = ld0(L, (k0 - NB + q) * m + J0 + r, J0 + r < m);
-      Pa[r * PS + q] = xa;
-      Pb[r * PS + q] = xb;
-    }
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+    xpa[u] = ld0(L, (k0 - NB + q) * m + I0 + r, pair && I0 + r < m);
+    xpb[u] = ld0(L, (k0 - NB + q) * m + J0 + r, pair && J0 + r < m);
   }
   // ---- stage L_kk^-1, y_k, the raw panel rows of I (and J), prefetch the C tile: every global
   // load is issued before the first LDS store so the whole batch is in flight at once
@@ -740,6 +737,12 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   }
   const int climit = t.clim;  // ns; m when the contribution block is fused; the big-panel end when blocked
   if (pair) {  // C[I, J] -= X_prev,I X_prev,J^T into the accumulators first, the current panel's loads in flight
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+      Pa[r * PS + q] = xpa[u];
+      Pb[r * PS + q] = xpb[u];
+    }
     __syncthreads();
     T.step(Pa, Pb, lane, w);
     __syncthreads();  // Pa / Pb free for the current panel

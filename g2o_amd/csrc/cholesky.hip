@@ -840,7 +840,11 @@ __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, co
   const int m = me.ns + me.nr, ns = me.ns;
   const int ti = t.b & 0xffff, tj = t.b >> 16;
   const int ka = t.a, kb = t.c ? t.c : ns, climit = kb == ns ? m : ns;
-  SyrkTile::run(lbuf + me.l_off, m, fronts + me.front_off, m, m, climit, kb + ti * TT, kb + tj * TT, ka, kb, sh);
+  // a childless front's contribution block holds nothing before this pass (its rows and columns are ancestors'
+  // variables: no input entries, no children): written, not read
+  const bool overwrite = t.c == 0 && me.child_begin == me.child_end;
+  SyrkTile::run(lbuf + me.l_off, m, fronts + me.front_off, m, m, climit, kb + ti * TT, kb + tj * TT, ka, kb, sh,
+                overwrite);
 }
 
 __global__ void k_permute(int n, const int* __restrict__ perm, const double* __restrict__ in, double* __restrict__ out) {

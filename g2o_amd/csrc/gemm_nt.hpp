@@ -28,8 +28,12 @@ struct GemmNT {
 
   // rows [I0, I0+BM) x columns [J0, J0+BN) of C, K = [ka, kb); entries outside rows < mrows,
   // columns < climit or above the diagonal are left untouched. lds: LDS_DOUBLES doubles.
+  // overwrite: C is known to be zero (a childless front's contribution block): C = -A A^T without reading it.
+  // Short-K tiles (their time is the C traffic) stage the tile in LDS (once it holds no K chunk) and move C a column
+  // per wave instruction: 16-lane segments of the MFMA layout would touch 16 columns 32 bytes at a time.
+  static constexpr bool LDS_EPILOGUE = (long long)BM * (BN + 1) <= LDS_DOUBLES && NT % BM == 0;
   __device__ static void run(const double* __restrict__ A, int lda, double* __restrict__ C, int ldc, int mrows,
-                             int climit, int I0, int J0, int ka, int kb, double* lds) {
+                             int climit, int I0, int J0, int ka, int kb, double* lds, bool overwrite = false) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w % WM, wc = w / WM;
     const int lr = lane & 15, lk = lane >> 4;
@@ -98,6 +102,33 @@ struct GemmNT {
       stash(b ^ 1);
       __syncthreads();
     }
+    // (short K only: with a long K loop the tile's own epilogue measured faster, C4 K = 384 pass 48 vs 51 us)
+    if (LDS_EPILOGUE && (overwrite || kb - ka <= 2 * KC)) {
+      // acc -> LDS tile (row-major, stride BN + 1), then thread t owns row t % BM of columns t / BM, + NT / BM, ...
+      constexpr int CS = BN + 1, CPI = NT / BM;  // columns per pass
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            lds[(wr * (BM / WM) + 16 * i + lk + 4 * q) * CS + wc * (BN / WN) + 16 * j + lr] = acc[i][j][q];
+      __syncthreads();
+      const int r = tid % BM, gi = I0 + r;
+      constexpr int NP = BN / CPI;
+      double cv[NP];
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const int c = tid / BM + CPI * u, gj = J0 + c;
+        cv[u] = overwrite ? 0.0 : ld0(C, gj * ldc + gi, gi < mrows && gj < climit && gi >= gj);
+      }
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const int c = tid / BM + CPI * u, gj = J0 + c;
+        if (gi < mrows && gj < climit && gi >= gj) C[(size_t)gj * ldc + gi] = cv[u] - lds[r * CS + c];
+      }
+      return;
+    }
     // epilogue: C -= acc, lane holds D[lk + 4q][lr] of each 16x16 block; one block column at a time
     // (all loads of the column in flight, then the stores)
 #pragma unroll
@@ -109,7 +140,7 @@ struct GemmNT {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int gi = I0 + wr * (BM / WM) + 16 * i + lk + 4 * q;
-          cv[i][q] = ld0(C, gj * ldc + gi, gi < mrows && gj < climit && gi >= gj);
+          cv[i][q] = overwrite ? 0.0 : ld0(C, gj * ldc + gi, gi < mrows && gj < climit && gi >= gj);
         }
 #pragma unroll
       for (int i = 0; i < MI; ++i)

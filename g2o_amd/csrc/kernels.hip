@@ -740,25 +740,47 @@ __global__ void __launch_bounds__(256)
                 const double* __restrict__ Ufac, const double* __restrict__ cl_all, int size_poses, int lm0,
                 double* __restrict__ x) {
   constexpr int UF = LmTraits<LD>::UF;
+  constexpr int GB = PD * LD, GP = GB / 2;  // doubles / 16-B pieces per block
+  constexpr int CH = 32;                    // blocks per staged chunk (per wave)
+  static_assert(GB % 2 == 0, "blocks are whole 16-B pieces");
+  // A wave's landmarks own one contiguous run of G blocks (Hpl order is landmark-major). The run is staged through
+  // the wave's LDS slice in lane-linear 16-B pieces (1 KiB per load instruction): a lane reading its own 144-B blocks
+  // directly touches a different cache line per lane and piece, and refetches lines from L2 many times (C5 422 -> 362
+  // us; prefetching the next chunk into registers measured no faster at half the occupancy).
+  __shared__ __attribute__((aligned(16))) double2 gs[4][CH * GP];
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int l = gid / LANES, q = gid % LANES;
+  const int l = gid / LANES, q = gid % LANES, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lw0 = (gid - lane) / LANES;  // the wave's first landmark
+  if (lw0 >= nl) return;                 // wave-uniform
   const bool active = l < nl;
+  const int A0 = lm_ptr[lw0], A1 = lm_ptr[min(lw0 + 64 / LANES, nl)];
+  int a = active ? lm_ptr[l] + q : 0;
+  const int ae = active ? lm_ptr[l + 1] : 0;
   double c[LD];
 #pragma unroll
   for (int k = 0; k < LD; ++k) c[k] = 0.0;
-  if (active) {
-    const int a1 = lm_ptr[l + 1];
-    for (int a = lm_ptr[l] + q; a < a1; a += LANES) {
-      const double* Bm = G + (size_t)a * PD * LD;
+  double2* gw = gs[w];
+  for (int c0 = A0; c0 < A1; c0 += CH) {  // wave-uniform chunks; a lane's cursor stays in observation order
+    const int n = min(CH, A1 - c0);
+    const double2* src = reinterpret_cast<const double2*>(G + (size_t)c0 * GB);
+    __builtin_amdgcn_wave_barrier();  // every lane's reads of the previous chunk precede these writes (LDS in order)
+    asm volatile("" ::: "memory");
+    for (int i = lane; i < n * GP; i += 64) gw[i] = src[i];
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    for (; a < ae && a < c0 + n; a += LANES) {
+      const double2* Bm = gw + (a - c0) * GP;
       const double* xp = x + (size_t)blk_pose[a] * PD;
-      double s[LD];
+      double bv[GB], s[LD];
+#pragma unroll
+      for (int i = 0; i < GP; ++i) { const double2 v = Bm[i]; bv[2 * i] = v.x; bv[2 * i + 1] = v.y; }
 #pragma unroll
       for (int k = 0; k < LD; ++k) s[k] = 0.0;
 #pragma unroll
       for (int r = 0; r < PD; ++r) {
         const double xr = -xp[r];
 #pragma unroll
-        for (int k = 0; k < LD; ++k) s[k] += Bm[k * PD + r] * xr;
+        for (int k = 0; k < LD; ++k) s[k] += bv[k * PD + r] * xr;
       }
 #pragma unroll
       for (int k = 0; k < LD; ++k) c[k] += s[k];

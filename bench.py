@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="OpenMP threads for the CPU baseline (0 = all)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-posegraph", action="store_true", help="skip the C3 (100k-pose SE3) secondary leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (4k x 1M x 10M BA) secondary leg")
     return ap.parse_args()
 
 
@@ -46,6 +47,9 @@ def make_problem(cfg):
 
 
 def dist_setup(n):
+    """torch.distributed (gloo, CPU only) is the multi-process control plane: uid broadcast, barriers, max over
+    ranks. libg2o_hip.so is loaded BEFORE torch so its HIP runtime and RCCL are /opt/rocm's (ROCm 7.2, the ones it
+    was built against) and not the copies torch bundles; torch never touches the GPU here."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -189,8 +193,61 @@ def posegraph_leg(local, steps=5, warmup=1):
         "factor": {"bound": "mfma", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                    "frac": tf / PEAK_FP64_TFLOPS, "flops_per_launch": flops,
                    "flops_convention": "reference cs_amd sum c_k^2" if ref else "backend ordering",
-                   "backend_ordering_flops": own, "avg_launch_ms": fms},
+                   "backend_ordering_flops": own,
+                   "backend_ordering_achieved": own / (fms * 1e-3) / 1e12 if fms > 0 else 0.0,
+                   "backend_ordering_frac": own / (fms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if fms > 0 else 0.0,
+                   "avg_launch_ms": fms},
     }
+
+
+def c5_leg(local, steps=10, warmup=2):
+    """BASELINE config C5 (4k cameras x 1M points x 10M observations, the multi-GPU target) on this GPU, measured like
+    the headline: LM it/s, ms/linear-solve, the factorization's time and its stage split."""
+    import g2o_amd
+    t0 = time.time()
+    prob = make_problem("C5")
+    gen = time.time() - t0
+    opt = g2o_amd.SparseOptimizer(local).add_problem(prob)
+    opt.set_algorithm("lm_hip_fix6_3")
+    it = 0
+    for _ in range(max(warmup, 1)):
+        opt.optimize_step(it)
+        it += 1
+    opt.set_stats_level(1)
+    g2o_amd.device_synchronize(local)
+    t0 = time.perf_counter()
+    timed = []
+    for _ in range(steps):
+        timed.append(opt.optimize_step(it)[1])
+        it += 1
+    g2o_amd.device_synchronize(local)
+    dt = time.perf_counter() - t0
+    names = ["linearize", "vreduce", "schur_rows", "chol_factor", "chol_solve", "backsub", "error", "oplus"]
+    opt.enable_kernel_timing(True)
+    opt.set_stats_level(2)
+    for _ in range(2):
+        opt.optimize_step(it)
+        it += 1
+    kt = {k: opt.kernel_ms(k) for k in names}
+    cf = load_json("chol_flops.json").get("C5", {}).get("ref_cs_amd", {}).get("flops")
+    own = opt.kernel_flops("chol_factor")
+    fms = kt["chol_factor"]
+    lin = [1e3 * s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
+    out = {
+        "workload": f"C5: {prob.name} ({prob.num_vertices} vertices, {prob.num_edges} edges), {solver_name(prob)}, "
+                    f"{int(prob.vertices[0].fixed.sum())} fixed cameras, 1 GPU",
+        "value": steps / dt, "unit": "LM it/s", "steps": steps, "warmup": warmup,
+        "ms_per_step": 1e3 * dt / steps, "ms_per_linear_solve": float(np.median(lin)),
+        "levenberg_trials": sum(s.levenbergIterations for s in timed), "final_chi2": timed[-1].chi2,
+        "stages_ms_avg": kt,
+        "factor": {"bound": "mfma", "avg_launch_ms": fms, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                   "ref_order_flops": cf, "backend_ordering_flops": own,
+                   "achieved": (cf or own) / (fms * 1e-3) / 1e12 if fms > 0 else 0.0,
+                   "backend_ordering_achieved": own / (fms * 1e-3) / 1e12 if fms > 0 else 0.0},
+        "generate_s": gen,
+    }
+    opt.close()
+    return out
 
 
 def load_json(name):
@@ -203,22 +260,32 @@ def load_json(name):
 
 def stage_bytes(prob):
     """SURVEY.md §8d algorithmic bytes per launch of the assembly and Schur stages (BA configs):
-    assembly: per edge 80 B read (meas, Omega, intrinsics, 2 ids) + 144 B Hpl written, per point 24 B
+    assembly: per edge 80 B read (meas 16, Omega 24, intrinsics 32, 2 ids 8) + 144 B Hpl written, per point 24 B
     read + 96 B (Hll, b_l) written, per camera 56 B read + 336 B (Hpp block, b_p) written;
-    Schur: per point k*144 + 96 B read, 288 B per upper Hschur block written once."""
+    Schur: per point k*144 + 96 B read, 288 B per upper Hschur block written once.
+    Omega and the intrinsics are counted once, not per edge, when every edge of the group holds the same record:
+    the engine then stores and reads ONE shared record (EdgeData::ue, DESIGN.md §3), so those bytes never move."""
     if not prob.landmark_dim:
         return None
     cams, pts = prob.vertices
-    ne = prob.edges[0].v0.size
+    es = prob.edges[0]
+    ne = es.v0.size
     nc, npt = int((cams.fixed == 0).sum()), pts.ids.size
-    asm = ne * (80 + 144) + npt * (24 + 96) + nc * (56 + 336)
-    return {"assembly": asm, "schur_read": ne * 144 + npt * 96}
+    info = np.asarray(es.info).reshape(ne, -1)
+    par = np.asarray(es.params).reshape(ne, -1) if es.params is not None else None
+    shared_info = bool(ne and (info == info[0]).all())
+    shared_par = bool(ne and par is not None and (par == par[0]).all())
+    per_edge = 16 + 8 + (0 if shared_info else 24) + (0 if shared_par else 32)
+    asm = ne * (per_edge + 144) + npt * (24 + 96) + nc * (56 + 336)
+    return {"assembly": asm, "schur_read": ne * 144 + npt * 96, "edge_read_bytes": per_edge,
+            "shared_records": {"information": shared_info, "intrinsics": shared_par}}
 
 
 def main():
     args = parse()
-    rank, world, local = dist_setup(args.gpus)
     import g2o_amd
+    g2o_amd.lib()  # bind the ROCm 7.2 HIP runtime + RCCL first (dist_setup imports torch)
+    rank, world, local = dist_setup(args.gpus)
 
     t0 = time.time()
     prob = make_problem(args.config)
@@ -230,11 +297,9 @@ def main():
         uid = g2o_amd.SparseOptimizer.comm_unique_id() if rank == 0 else None
         uid = bcast_bytes(uid, world)
         opt.set_comm(uid, rank, world)
-    try:
-        import torch
-        sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
-    except Exception:  # torch is plumbing only
-        sync = lambda: None  # noqa: E731
+    # device-wide synchronize in the product's own HIP runtime (the product does not use torch's)
+    def sync():
+        g2o_amd.device_synchronize(local)
 
     # warmup: iteration 0 builds the structure (symbolic analysis) and lambda0
     t0 = time.time()
@@ -294,11 +359,19 @@ def main():
     # PMC traffic is measured on one workload (its _meta.config): other configs report null
     traffic_cfg = traffic_all.get("_meta", {}).get("config", "C4")
 
-    def traffic(k):
+    # traffic: the raw PMC bytes (FETCH_SIZE + WRITE_SIZE); traffic_fetch_doubled: with the guide's gfx950 half-count
+    # correction of FETCH_SIZE, which is exact only for 16-B/lane streaming reads (tools/pmc_traffic.py)
+    def traffic(k, key="bytes_per_launch"):
         if traffic_cfg != args.config:
             return None
         rec = traffic_all.get(k)
-        return rec.get("bytes_per_launch") if isinstance(rec, dict) else rec
+        if not isinstance(rec, dict):
+            return None
+        if key == "bytes_per_launch" and "bytes_fetch_doubled" not in rec:  # older file: only the doubled figure
+            return (rec["fetch_size_kb_raw"] + rec["write_size_kb"]) * 1024.0
+        if key == "bytes_fetch_doubled" and key not in rec:
+            return rec.get("bytes_per_launch")
+        return rec.get(key)
 
     flops = ref_flops if ref_flops else own_flops
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
@@ -310,6 +383,7 @@ def main():
         "unit": "TFLOP/s",
         "frac": achieved / PEAK_FP64_TFLOPS,
         "traffic": traffic(dom),
+        "traffic_fetch_doubled": traffic(dom, "bytes_fetch_doubled"),
         "algorithmic_flops_per_launch": flops,
         "flops_convention": ("sum_k c_k^2 of the reference cs_amd block ordering (tools/chol_flops.py)" if ref_flops
                              else "backend ordering (reference count missing for this config)"),
@@ -327,6 +401,7 @@ def main():
             a = rows_bytes / (ms_rows * 1e-3) / 1e9
             secondary.append({"kernel": "schur_rows", "bound": "hbm", "achieved": a, "peak": PEAK_HBM_GBS,
                               "unit": "GB/s", "frac": a / PEAK_HBM_GBS, "traffic": traffic("schur_rows"),
+                              "traffic_fetch_doubled": traffic("schur_rows", "bytes_fetch_doubled"),
                               "algorithmic_bytes_per_launch": rows_bytes, "avg_launch_ms": ms_rows})
         nsblk = cf.get("blocks_upper")
         split = kt["schur_diag"]["count"] == 0  # Schur split formed at assembly (the LM loop's first trials)
@@ -356,11 +431,17 @@ def main():
                 by = sb["assembly"] + sb["schur_read"] + 288 * nsblk
                 a = by / (ms_as * 1e-3) / 1e9
                 tr = [traffic(k) for k in ("linearize", "vreduce", "schur_rows")]
+                td = [traffic(k, "bytes_fetch_doubled") for k in ("linearize", "vreduce", "schur_rows")]
                 secondary.append({"kernel": "assembly + schur (split at assembly: linearize, camera pass, rows)",
                                   "bound": "hbm", "achieved": a, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                   "frac": a / PEAK_HBM_GBS,
                                   "traffic": sum(tr) if all(t is not None for t in tr) else None,
+                                  "traffic_fetch_doubled": sum(td) if all(t is not None for t in td) else None,
+                                  "edge_read_bytes": sb["edge_read_bytes"], "shared_records": sb["shared_records"],
                                   "algorithmic_bytes_per_launch": by, "avg_launch_ms": ms_as})
+    runtime = g2o_amd.runtime_info()
+    runtime["mapped"] = sorted({ln.split()[-1] for ln in open("/proc/self/maps")
+                                if ("libamdhip64" in ln or "librccl" in ln) and "/" in ln})
     fixed = ""
     if prob.landmark_dim:
         fixed = f", {int(prob.vertices[0].fixed.sum())} fixed cameras (gauge + monocular scale; ba_demo.cpp fixes 1)"
@@ -390,12 +471,19 @@ def main():
         "roofline_secondary": secondary,
         "factor": finfo,
         "setup_s": {"generate": gen_s, "warmup_incl_structure": warm_s},
+        "runtime": runtime,
     }
     if rank == 0 and world == 1 and not args.no_posegraph and args.config == "C4":
         try:
             out["pose_graph"] = posegraph_leg(local)
         except Exception as ex:  # reported, not fatal
             out["pose_graph"] = {"error": repr(ex)}
+    if rank == 0 and world == 1 and not args.no_c5 and args.config == "C4":
+        try:
+            opt.close()
+            out["c5"] = c5_leg(local)
+        except Exception as ex:  # reported, not fatal
+            out["c5"] = {"error": repr(ex)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(prob, args.cpu_iters, args.cpu_threads)

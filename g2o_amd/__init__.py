@@ -65,7 +65,8 @@ EXPORTS = [
     "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_comm_selftest", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
     "g2ohip_kernel_timing_only", "g2ohip_set_stats_level", "g2ohip_kernel_ms",
     "g2ohip_kernel_count", "g2ohip_kernel_bytes", "g2ohip_kernel_flops", "g2ohip_last_error",
-    "g2ohip_version",
+    "g2ohip_version", "g2ohip_host_payload_len", "g2ohip_solver_save_hessian", "g2ohip_solver_set_write_debug",
+    "g2ohip_comm_local_reduce_host", "g2ohip_runtime_info", "g2ohip_device_synchronize",
 ]
 
 
@@ -142,6 +143,12 @@ def lib() -> C.CDLL:
         "g2ohip_kernel_flops": ([P, C.c_char_p], D),
         "g2ohip_last_error": ([], C.c_char_p),
         "g2ohip_version": ([], C.c_char_p),
+        "g2ohip_host_payload_len": ([P, I], LL),
+        "g2ohip_solver_save_hessian": ([P, C.c_char_p], I),
+        "g2ohip_solver_set_write_debug": ([P, I], I),
+        "g2ohip_comm_local_reduce_host": ([C.c_char_p, I, I, P, LL, I], I),
+        "g2ohip_runtime_info": ([C.c_char_p, I], I),
+        "g2ohip_device_synchronize": ([I], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -149,6 +156,25 @@ def lib() -> C.CDLL:
         f.restype = res
     _lib = L
     return L
+
+
+def runtime_info() -> dict:
+    """The HIP runtime / RCCL this library is bound to (resolved library paths + versions)."""
+    import json
+    buf = C.create_string_buffer(2048)
+    lib().g2ohip_runtime_info(buf, len(buf))
+    return json.loads(buf.value.decode())
+
+
+def device_synchronize(device: int = 0) -> None:
+    _check(lib().g2ohip_device_synchronize(device), "device_synchronize")
+
+
+def comm_local_reduce_host(group_key: str, rank: int, nranks: int, buf, is_max: bool = False):
+    """The in-process test transport's host reduction (collective-consistency checked); buf is reduced in place."""
+    _check(lib().g2ohip_comm_local_reduce_host(group_key.encode(), rank, nranks, _p(buf), buf.size, int(is_max)),
+           "comm_local_reduce_host")
+    return buf
 
 
 def _p(a):
@@ -256,6 +282,10 @@ class SparseOptimizer:
         def tramp(user, etype, with_jac, out):
             try:
                 pay = np.ascontiguousarray(fn(etype, bool(with_jac)), np.float64)
+                want = lib().g2ohip_host_payload_len(self.h, etype)
+                if want < 0 or pay.size != want:  # never write past the engine's payload buffer
+                    raise G2OHipError(f"host edge callback returned {pay.size} doubles for edge type {etype}, "
+                                      f"expected {want} (D * (1 + dim(v0) + dim(v1)) per edge)")
                 C.memmove(out, pay.ctypes.data, pay.nbytes)
                 return 0
             except Exception:  # reported as a failed callback by the engine
@@ -282,6 +312,14 @@ class SparseOptimizer:
 
     def save(self, path: str):
         _check(lib().g2ohip_save_g2o(self.h, path.encode()), "save")
+
+    def save_hessian(self, path: str) -> bool:
+        """Solver::saveHessian (block_solver.hpp:589-593): Hpp in Octave sparse-matrix text."""
+        return bool(_check(lib().g2ohip_solver_save_hessian(self.h, path.encode()), "saveHessian"))
+
+    def set_write_debug(self, on: bool = True):
+        """Solver::setWriteDebug: a not-PD factorization writes debug.txt (linear_solver_csparse.h:127-133)."""
+        _check(lib().g2ohip_solver_set_write_debug(self.h, int(on)), "setWriteDebug")
 
     def set_algorithm(self, name: str):
         _check(lib().g2ohip_set_algorithm(self.h, name.encode()), "set_algorithm")

@@ -1,4 +1,5 @@
 // extern "C" entry points of libg2o_hip.so (include/g2o_hip.h).
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -336,6 +337,59 @@ int g2ohip_comm_selftest(int device, const unsigned char uid[128], int n, const 
 int g2ohip_set_comm_local(g2ohip_graph* g, const char* key, int rank, int nranks) {
   if (!g || !key || rank < 0 || rank >= nranks) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->set_comm_local(key, rank, nranks); });
+}
+int g2ohip_comm_local_reduce_host(const char* key, int rank, int nranks, double* buf, long long n, int is_max) {
+  if (!key || rank < 0 || rank >= nranks || n < 0 || (n > 0 && !buf)) return G2OHIP_ERR_ARG;
+  return guarded([&] {
+    g2ohip::local_comm_reduce_host(key, rank, nranks, buf, (size_t)n, is_max != 0);
+    return G2OHIP_OK;
+  });
+}
+
+int g2ohip_runtime_info(char* out, int cap) {
+  // which HIP runtime and RCCL this library's calls actually bound to (dladdr of the resolved symbols), and their
+  // versions: a process that loaded another copy first (e.g. torch's bundled RCCL / HIP) is visible here
+  auto where = [](const void* sym) -> std::string {
+    Dl_info di;
+    return dladdr(sym, &di) && di.dli_fname ? di.dli_fname : "?";
+  };
+  int hipv = 0, ncv = 0;
+  (void)hipRuntimeGetVersion(&hipv);
+  (void)ncclGetVersion(&ncv);
+  const std::string s = std::string("{\"libamdhip64\": \"") + where((const void*)&hipStreamSynchronize) +
+                        "\", \"hip_runtime_version\": " + std::to_string(hipv) + ", \"librccl\": \"" +
+                        where((const void*)&ncclGetVersion) + "\", \"rccl_version\": " + std::to_string(ncv) +
+                        ", \"libg2o_hip\": \"" + where((const void*)&g2ohip_runtime_info) + "\"}";
+  if (out && cap > 0) {
+    std::strncpy(out, s.c_str(), (size_t)cap - 1);
+    out[cap - 1] = 0;
+  }
+  return (int)s.size() + 1;
+}
+int g2ohip_device_synchronize(int device) {
+  return guarded([&] {
+    HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipDeviceSynchronize());
+    return G2OHIP_OK;
+  });
+}
+long long g2ohip_host_payload_len(g2ohip_graph* g, int edge_type) {
+  if (!g) return G2OHIP_ERR_ARG;
+  try {
+    return g->e->host_payload_len(edge_type);
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return G2OHIP_ERR_DEVICE;
+  }
+}
+int g2ohip_solver_save_hessian(g2ohip_graph* g, const char* path) {
+  if (!g || !path) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->save_hessian(path); });
+}
+int g2ohip_solver_set_write_debug(g2ohip_graph* g, int on) {
+  if (!g) return G2OHIP_ERR_ARG;
+  g->e->write_debug = on != 0;
+  return G2OHIP_OK;
 }
 
 int g2ohip_debug_phases(unsigned long long* out, int max_records) {

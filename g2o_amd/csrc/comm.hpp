@@ -5,6 +5,11 @@
 //   LocalComm  test transport: N engines driven by N host threads of ONE process on one GPU;
 //              host-staged, summed in rank order. Lets the sharding logic run under pytest on
 //              a single-GPU box; never selected by the product path.
+//
+// Every collective carries a per-communicator call number. LocalComm always checks that all ranks
+// entered the same call (number, length, operation) and throws DeviceError on every rank otherwise (a
+// rank-dependent call sequence was a heap over-read here and a silent hang under RCCL); RcclComm runs
+// the same check as one extra 6-double max all-reduce per call when G2OHIP_COMM_CHECK=1.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -17,9 +22,13 @@ struct Comm {
   virtual ~Comm() = default;
   virtual void allreduce_sum(double* dptr, size_t n, hipStream_t s) = 0;
   virtual void allreduce_max(double* dptr, size_t n, hipStream_t s) = 0;
+  long long seq = 0;  // collectives issued so far on this communicator
 };
 
 Comm* make_rccl_comm(const unsigned char* uid128, int rank, int nranks, std::string& err);
 Comm* make_local_comm(const std::string& key, int rank, int nranks);
+// LocalComm's host-side reduction alone (no device copies): the collective-consistency check is testable on a
+// host without a GPU. Throws DeviceError on a mismatched call.
+void local_comm_reduce_host(const std::string& key, int rank, int nranks, double* buf, size_t n, bool is_max);
 
 }  // namespace g2ohip

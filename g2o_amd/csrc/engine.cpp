@@ -13,6 +13,7 @@
 
 
 #include <algorithm>
+#include <charconv>
 #include <cstdlib>
 #include <chrono>
 #include <cmath>
@@ -904,13 +905,14 @@ int Engine::load(const char* path, int marginalize_xyz) {
     std::fseek(f, 0, SEEK_END);
     const long sz = std::ftell(f);
     std::fseek(f, 0, SEEK_SET);
-    buf.resize(sz > 0 ? (size_t)sz : 0);
+    // one byte more than the file, NUL: strtod / strtol stop there even on a last line without its newline
+    buf.assign(sz > 0 ? (size_t)sz + 1 : 1, '\0');
     const size_t got = sz > 0 ? std::fread(buf.data(), 1, (size_t)sz, f) : 0;
     fclose(f);
-    if (got != buf.size()) return G2OHIP_ERR_ARG;
+    if (got + 1 != buf.size()) return G2OHIP_ERR_ARG;
   }
   const char* base = buf.data();
-  const size_t n = buf.size();
+  const size_t n = buf.size() - 1;
   const int nthreads = (int)std::max<size_t>(1, std::min<size_t>(16, n / (1 << 20)));
   std::vector<size_t> cut(nthreads + 1, n);
   cut[0] = 0;
@@ -990,56 +992,181 @@ int Engine::load(const char* path, int marginalize_xyz) {
   return G2OHIP_OK;
 }
 
+// OptimizableGraph::save (optimizable_graph.cpp:663-679): vertices in insertion order (each followed by its FIX line),
+// then the edges of every type. The lines are formatted in parallel — contiguous ranges of vertices / edges per thread,
+// std::to_chars shortest round-trip decimals (the value read back is bit-identical) — and written in order.
+namespace {
+struct LineBuf {
+  std::string s;
+  char tmp[64];
+  void tag(const char* t) { s += t; }
+  void i(int v) {
+    s += ' ';
+    const auto r = std::to_chars(tmp, tmp + sizeof tmp, v);
+    s.append(tmp, r.ptr);
+  }
+  void d(double v) {
+    s += ' ';
+    const auto r = std::to_chars(tmp, tmp + sizeof tmp, v);
+    s.append(tmp, r.ptr);
+  }
+  void nl() { s += '\n'; }
+};
+template <class F>
+void parallel_ranges(size_t n, int nthreads, F&& f) {
+  if (nthreads <= 1 || n < 4096) { f(0, 0, n); return; }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) th.emplace_back([&, t] { f(t, n * t / nthreads, n * (t + 1) / nthreads); });
+  for (auto& x : th) x.join();
+}
+}  // namespace
+
 int Engine::save(const char* path) {
   sync_host_state();
-  FILE* f = fopen(path, "w");
+  FILE* f = fopen(path, "wb");
   if (!f) return G2OHIP_ERR_ARG;
-  for (auto& v : hg.verts) {
-    const double* st = hg.st[v.type].data() + (size_t)v.local * vertex_state_stride(v.type);
-    double e[7];
-    est_from_state(v.type, st, e);
-    switch (v.type) {
-      case G2OHIP_V_SE3_EXPMAP: {
-        double c[7];
-        se3quat_inverse(e, c);
-        fprintf(f, "VERTEX_SE3:EXPMAP %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", v.id, c[0], c[1], c[2], c[3], c[4], c[5], c[6]);
-        break;
-      }
-      case G2OHIP_V_XYZ: fprintf(f, "VERTEX_XYZ %d %.17g %.17g %.17g\n", v.id, e[0], e[1], e[2]); break;
-      case G2OHIP_V_SE3_QUAT:
-        fprintf(f, "VERTEX_SE3:QUAT %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", v.id, e[0], e[1], e[2], e[3], e[4], e[5], e[6]);
-        break;
-      case G2OHIP_V_SE2: fprintf(f, "VERTEX_SE2 %d %.17g %.17g %.17g\n", v.id, e[0], e[1], e[2]); break;
-      case G2OHIP_V_XY: fprintf(f, "VERTEX_XY %d %.17g %.17g\n", v.id, e[0], e[1]); break;
+  const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<LineBuf> out(nt);
+  bool ok = true;
+  auto flush = [&] {
+    for (auto& o : out) {
+      if (!o.s.empty() && std::fwrite(o.s.data(), 1, o.s.size(), f) != o.s.size()) ok = false;
+      o.s.clear();
     }
-    if (v.fixed) fprintf(f, "FIX %d\n", v.id);
-  }
+  };
+  parallel_ranges(hg.verts.size(), nt, [&](int t, size_t lo, size_t hi) {
+    LineBuf& L = out[t];
+    L.s.reserve((hi - lo) * 96);
+    for (size_t k = lo; k < hi; ++k) {
+      const HVertex& v = hg.verts[k];
+      const double* st = hg.st[v.type].data() + (size_t)v.local * vertex_state_stride(v.type);
+      double e[7], c[7];
+      est_from_state(v.type, st, e);
+      int ne = 3;
+      switch (v.type) {
+        case G2OHIP_V_SE3_EXPMAP: L.tag("VERTEX_SE3:EXPMAP"); se3quat_inverse(e, c); std::memcpy(e, c, sizeof c); ne = 7; break;
+        case G2OHIP_V_XYZ: L.tag("VERTEX_XYZ"); break;
+        case G2OHIP_V_SE3_QUAT: L.tag("VERTEX_SE3:QUAT"); ne = 7; break;
+        case G2OHIP_V_SE2: L.tag("VERTEX_SE2"); break;
+        case G2OHIP_V_XY: L.tag("VERTEX_XY"); ne = 2; break;
+      }
+      L.i(v.id);
+      for (int q = 0; q < ne; ++q) L.d(e[q]);
+      L.nl();
+      if (v.fixed) { L.tag("FIX"); L.i(v.id); L.nl(); }
+    }
+  });
+  flush();
   for (const HEdgeSet& es : hg.esets) {
     if (is_hostj(es.type)) {  // the device does not know the host type's tag: the host saves those edges
       fprintf(stderr, "g2o_hip save: %zu host-Jacobian edges (type %d) not written\n", es.ev0.size(), es.type);
       continue;
     }
     const int D = es.D, nm = es.nm;
-    for (size_t k = 0; k < es.ev0.size(); ++k) {
-      const int a = hg.verts[es.ev0[k]].id, b = hg.verts[es.ev1[k]].id;
-      const double* m = es.meas.data() + k * nm;
-      const double* I = es.info.data() + k * D * D;
-      if (es.type == G2OHIP_E_SE2_XY) {
-        fprintf(f, "EDGE_SE2_XY %d %d %.17g %.17g %.17g %.17g %.17g\n", a, b, m[0], m[1], I[0], I[1], I[3]);
-      } else if (es.type == G2OHIP_E_SE3_PROJECT_XYZ) {
-        const double* p = es.params.data() + k * 4;
-        fprintf(f, "EDGE_SE3_PROJECT_XYZ:EXPMAP %d %d %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g %.17g\n", a, b, m[0],
-                m[1], I[0], I[1], I[3], p[0], p[1], p[2], p[3]);
-      } else {
-        fprintf(f, "%s %d %d", es.type == G2OHIP_E_SE3_QUAT ? "EDGE_SE3:QUAT" : "EDGE_SE2", a, b);
-        for (int i = 0; i < nm; ++i) fprintf(f, " %.17g", m[i]);
-        for (int i = 0; i < D; ++i) for (int j = i; j < D; ++j) fprintf(f, " %.17g", I[i * D + j]);
-        fprintf(f, "\n");
+    parallel_ranges(es.ev0.size(), nt, [&](int t, size_t lo, size_t hi) {
+      LineBuf& L = out[t];
+      L.s.reserve((hi - lo) * 200);
+      for (size_t k = lo; k < hi; ++k) {
+        const int a = hg.verts[es.ev0[k]].id, b = hg.verts[es.ev1[k]].id;
+        const double* m = es.meas.data() + k * nm;
+        const double* I = es.info.data() + k * D * D;
+        if (es.type == G2OHIP_E_SE2_XY) {  // edge_se2_pointxy.cpp:54-61
+          L.tag("EDGE_SE2_XY"); L.i(a); L.i(b);
+          L.d(m[0]); L.d(m[1]); L.d(I[0]); L.d(I[1]); L.d(I[3]);
+        } else if (es.type == G2OHIP_E_SE3_PROJECT_XYZ) {  // types_six_dof_expmap.cpp:380-393
+          const double* p = es.params.data() + k * 4;
+          L.tag("EDGE_SE3_PROJECT_XYZ:EXPMAP"); L.i(a); L.i(b);
+          L.d(m[0]); L.d(m[1]); L.d(I[0]); L.d(I[1]); L.d(I[3]);
+          for (int q = 0; q < 4; ++q) L.d(p[q]);
+        } else {  // edge_se3.cpp:67-75, edge_se2.cpp:55-63: measurement, upper triangle of the information row-wise
+          L.tag(es.type == G2OHIP_E_SE3_QUAT ? "EDGE_SE3:QUAT" : "EDGE_SE2"); L.i(a); L.i(b);
+          for (int q = 0; q < nm; ++q) L.d(m[q]);
+          for (int r = 0; r < D; ++r) for (int q = r; q < D; ++q) L.d(I[r * D + q]);
+        }
+        L.nl();
       }
-    }
+    });
+    flush();
   }
-  fclose(f);
-  return G2OHIP_OK;
+  if (std::fclose(f) != 0) ok = false;
+  return ok ? G2OHIP_OK : G2OHIP_ERR_ARG;
+}
+
+long long Engine::host_payload_len(int type) {
+  HEdgeSet* es = hg.set_of(type);
+  if (!es || !is_hostj(type)) return G2OHIP_ERR_ARG;
+  long long len = 0;
+  for (size_t k = 0; k < es->ev0.size(); ++k)
+    len += (long long)es->D * (1 + hg.verts[es->ev0[k]].dim + hg.verts[es->ev1[k]].dim);
+  return len;
+}
+
+// Octave sparse-matrix text of a symmetric matrix held as upper blocks (bi <= bj, pd x pd column-major): every entry of
+// every stored block and the mirror of the off-diagonal ones, sorted by (column, row), 1-based
+// (SparseBlockMatrix::writeOctave sparse_block_matrix.hpp:579-617; csparse_helper.cpp:62-111 for the debug dump,
+// whose input is the upper CCS of fillCCS: diagonal blocks contribute their upper triangle, mirrored).
+static bool write_octave_blocks(const char* path, const std::vector<int>& bi, const std::vector<int>& bj, int pd,
+                                const double* blocks, int nb, double diag_add, bool upper_diag_only, bool fixed9) {
+  struct Tr { int r, c; double x; };
+  std::vector<Tr> ent;
+  ent.reserve(bi.size() * pd * pd * 2);
+  for (size_t t = 0; t < bi.size(); ++t) {
+    const double* B = blocks + t * pd * pd;
+    const bool dg = bi[t] == bj[t];
+    for (int c = 0; c < pd; ++c)
+      for (int r = 0; r < pd; ++r) {
+        const int gr = bi[t] * pd + r, gc = bj[t] * pd + c;
+        if (dg) {
+          // symmetric diagonal block: the upper entry (min, max) as stored, both positions written
+          const double x = B[std::max(r, c) * pd + std::min(r, c)] + (r == c ? diag_add : 0.0);
+          if (upper_diag_only && r > c) continue;
+          ent.push_back({gr, gc, x});
+          if (upper_diag_only && r != c) ent.push_back({gc, gr, x});
+        } else {
+          ent.push_back({gr, gc, B[c * pd + r]});
+          ent.push_back({gc, gr, B[c * pd + r]});
+        }
+      }
+  }
+  std::sort(ent.begin(), ent.end(), [](const Tr& a, const Tr& b) { return a.c < b.c || (a.c == b.c && a.r < b.r); });
+  std::string name = path;
+  const size_t dot = name.find_last_of('.');
+  if (dot != std::string::npos) name = name.substr(0, dot);
+  FILE* f = std::fopen(path, "w");
+  if (!f) return false;
+  const int n = nb * pd;
+  std::fprintf(f, "# name: %s\n# type: sparse matrix\n# nnz: %zu\n# rows: %d\n# columns: %d\n\n", name.c_str(),
+               ent.size(), n, n);
+  for (const Tr& e : ent) std::fprintf(f, fixed9 ? "%d %d %.9f\n" : "%d %d %.9g\n", e.r + 1, e.c + 1, e.x);
+  return std::fclose(f) == 0;
+}
+
+int Engine::save_hessian(const char* path) {
+  if (!structure_built) return G2OHIP_ERR_STATE;
+  if (nranks > 1) return G2OHIP_ERR_UNSUPPORTED;  // Hpp diagonal blocks are partial per landmark shard
+  if (use_cgls()) return G2OHIP_ERR_UNSUPPORTED;  // JacobiSolver never assembles Hpp
+  ensure_hpp();
+  std::vector<double> blocks(hpp_bi.size() * pd * pd);
+  dH.download(blocks.data(), blocks.size(), stream);
+  HIP_CHECK(hipStreamSynchronize(stream));
+  // the reference's Hpp holds lambda between setLambda and restoreDiagonal; here lambda is virtual
+  return write_octave_blocks(path, hpp_bi, hpp_bj, pd, blocks.data(), num_poses, lambda_set ? lambda_host : 0.0, false,
+                             true)
+             ? 1
+             : 0;
+}
+
+void Engine::write_debug_dump() {
+  // the matrix the failed factorization saw: S (lambda already on its diagonal) or Hpp + lambda
+  const std::vector<int>& bi = do_schur ? s_bi : hpp_bi;
+  const std::vector<int>& bj = do_schur ? s_bj : hpp_bj;
+  std::vector<double> blocks(bi.size() * pd * pd);
+  if (do_schur) dS.download(blocks.data(), blocks.size(), stream);
+  else dH.download(blocks.data(), blocks.size(), stream);
+  HIP_CHECK(hipStreamSynchronize(stream));
+  fprintf(stderr, "Cholesky failure, writing %s (Hessian loadable by Octave)\n", debug_path.c_str());
+  write_octave_blocks(debug_path.c_str(), bi, bj, pd, blocks.data(), num_poses, do_schur ? 0.0 : lambda_host, true,
+                      false);
 }
 
 void Engine::ensure_device_state() {
@@ -1441,6 +1568,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
   }
   ensure_device_state();
   setup_edges_device();
+  ++structure_ver;  // every cache keyed on the block pattern (marginals factor, BlockSymv) is stale from here
   // per-type hessian index and x offsets
   const int lm_begin = local_lm.empty() ? 0 : local_lm.front();
   const int lm_end = local_lm.empty() ? 0 : local_lm.back() + 1;
@@ -2061,6 +2189,7 @@ int Engine::solve_sync() {
   HIP_CHECK(hipMemcpyAsync(f, failp(), sizeof f, hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
   timer.collect();
+  if (f[0] && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
   return f[0] ? 0 : 1;
 }
 
@@ -2245,6 +2374,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     int f[2];
     std::memcpy(f, hs + 8, sizeof f);
     const bool ok2 = f[0] == 0;
+    if (!ok2 && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
     if (ev2 && first_trial) {
       float mq = 0;
       HIP_CHECK(hipEventElapsedTime(&mq, q0, q1));
@@ -2338,6 +2468,7 @@ int Engine::gn_solve(int iteration, g2ohip_batch_stats* st) {
     st->timeUpdate = b * 1e-3;
   }
   levenberg_iterations = 0;
+  if (f[0] != 0 && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
   return f[0] == 0 ? 0 : 2;
 }
 
@@ -2498,9 +2629,9 @@ int Engine::multiply_hessian(double* dest, const double* src) {  // block_solver
   if (!structure_built) return G2OHIP_ERR_STATE;
   if (nranks > 1) return G2OHIP_ERR_UNSUPPORTED;  // Hpp diagonal blocks are partial per landmark shard
   ensure_hpp();
-  if (symv_hpp.key != (const void*)&hpp_bi) {
+  if (symv_hpp.key != structure_ver) {
     symv_hpp.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
-    symv_hpp.key = &hpp_bi;
+    symv_hpp.key = structure_ver;
   }
   const int n = size_poses;
   dtmp.resize(2 * (size_t)std::max(n, 1));
@@ -2514,13 +2645,14 @@ int Engine::multiply_hessian(double* dest, const double* src) {  // block_solver
 
 int Engine::linear_residual(double* out) {
   if (!structure_built || !out) return G2OHIP_ERR_STATE;
-  if (use_pcg()) return G2OHIP_ERR_UNSUPPORTED;
+  // the iterative solvers never form the factorized system: PCG keeps no residual here, CGLS never assembles S
+  if (use_pcg() || use_cgls()) return G2OHIP_ERR_UNSUPPORTED;
   const std::vector<int>& bi = do_schur ? s_bi : hpp_bi;
   const std::vector<int>& bj = do_schur ? s_bj : hpp_bj;
   BlockSymv& M = do_schur ? symv_s : symv_hpp;
-  if (M.key != (const void*)&bi) {
+  if (M.key != structure_ver) {
     M.setup(num_poses, pd, bi, bj, stream);
-    M.key = &bi;
+    M.key = structure_ver;
   }
   const int n = size_poses;
   // S already holds lambda on its diagonal (k_schur_diag); Hpp gets the virtual lambda like the factor
@@ -2551,9 +2683,9 @@ int Engine::compute_marginals(int nblocks, const int* brow, const int* bcol, dou
   // factor of Hpp's pattern is set up once
   const bool own = !do_schur && !use_pcg() && !use_cgls();
   DeviceCholesky& C = own ? chol : marg_chol;
-  if (!own && !marg_ready) {
+  if (!own && marg_ver != structure_ver) {
     marg_chol.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
-    marg_ready = true;
+    marg_ver = structure_ver;
   }
   const int n = size_poses, K = 64 / pd * pd, bpb = K / pd;
   dmarg.resize((size_t)2 * n * K + (size_t)C.wpool + n);

@@ -133,7 +133,7 @@ struct DeviceCholesky {
 // y = (A + lam I) x for a symmetric block matrix held as upper blocks (multiplyHessian, residual checks)
 struct BlockSymv {
   int nb = 0, pd = 0;
-  const void* key = nullptr;  // the block list it was built for
+  unsigned long long key = 0;  // Engine::structure_ver it was built for (0: never)
   DevBuf<int> rptr, diag;
   DevBuf<int2> ent;
   void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
@@ -182,6 +182,14 @@ class Engine {
   int diag_absmax(double* out);
   int load(const char* path, int marginalize_xyz);
   int save(const char* path);
+  // doubles of the host payload of a host-J edge type ([e | Ji | Jj] per edge, insertion order)
+  long long host_payload_len(int type);
+  // Solver::saveHessian (block_solver.hpp:589-593 -> SparseBlockMatrix::writeOctave, sparse_block_matrix.hpp:579-617)
+  int save_hessian(const char* path);
+  // Solver::setWriteDebug (block_solver.hpp:582-586): on a not-PD factorization the LM trial writes debug.txt
+  // (linear_solver_csparse.h:127-133, csparse_helper.cpp:62-111)
+  bool write_debug = false;
+  std::string debug_path = "debug.txt";
   int get_estimates(int type, double* out, int* ids);
   int set_estimates(int type, const double* est);
   int minimal_state(double* out);
@@ -237,6 +245,7 @@ class Engine {
  private:
   // structure
   bool initialized = false, structure_built = false, device_state_dirty = true, host_state_stale = false;
+  unsigned long long structure_ver = 0;  // bumped by every build_structure (block pattern, fronts, index maps)
   int pd = 0, ld = 0;
   int num_poses = 0, num_landmarks = 0, size_poses = 0, size_landmarks = 0;
   std::vector<int> active;       // active vertex indices sorted by id
@@ -309,7 +318,7 @@ class Engine {
   std::vector<int> s_bi, s_bj, hpp_bi, hpp_bj;
   DeviceCholesky chol;
   DeviceCholesky marg_chol;  // factor of Hpp for computeMarginals where `chol` factors S (or is not set up)
-  bool marg_ready = false;
+  unsigned long long marg_ver = 0;  // structure_ver marg_chol was set up for (0: never)
   DevBuf<double> dmarg, dmarg_out;  // [Y | T | W | zero rhs], gathered blocks
   DevBuf<int> dmarg_fail;
   DevBuf<long long> dmarg_idx;
@@ -355,6 +364,8 @@ class Engine {
   void allreduce_sum(double* dptr, size_t n);
   int lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats* st);
   int gn_solve(int iteration, g2ohip_batch_stats* st);
+  // upper blocks of the matrix the last factorization saw (S with lambda, or Hpp + lambda) as an Octave file
+  void write_debug_dump();
 };
 
 }  // namespace g2ohip

@@ -130,6 +130,10 @@ int g2ohip_set_host_jacobians(g2ohip_graph* g, int edge_type, const double* payl
  * with_jacobians = 0 only needs the errors. Return 0 on success. */
 typedef int (*g2ohip_host_edge_fn)(void* user, int edge_type, int with_jacobians, double* payload);
 int g2ohip_set_host_edge_callback(g2ohip_graph* g, g2ohip_host_edge_fn fn, void* user);
+/* Length in doubles of the payload buffer of a host-J edge type (the `payload` the callback fills and
+ * g2ohip_set_host_jacobians reads): sum over its edges of D * (1 + dim(v0) + dim(v1)). A callback must write exactly
+ * this many doubles. */
+long long g2ohip_host_payload_len(g2ohip_graph* g, int edge_type);
 
 /* OptimizationAlgorithmFactory::construct by name; default "lm_hip_var" */
 int g2ohip_set_algorithm(g2ohip_graph* g, const char* name);
@@ -196,6 +200,15 @@ int g2ohip_discard_top(g2ohip_graph* g);
 int g2ohip_stage(g2ohip_graph* g, double lambda, double* b, double* x, double* Hschur_dense, double* bschur,
                  long long* dims);
 
+/* Solver::saveHessian (core/block_solver.hpp:589-593 -> SparseBlockMatrix::writeOctave, sparse_block_matrix.hpp:579-617):
+ * Hpp of the last buildSystem (+ lambda while a setLambda is active) as an Octave sparse-matrix text file, every entry of
+ * every stored block plus the mirrored off-diagonal blocks, "%.9f". Returns 1 written, 0 not written, <0 error. */
+int g2ohip_solver_save_hessian(g2ohip_graph* g, const char* path);
+/* Solver::setWriteDebug (core/block_solver.hpp:582-586): when on, a factorization that meets a non-positive pivot
+ * writes the matrix it factored (S, or Hpp + lambda) to "debug.txt" in the format of csparse_helper.cpp:62-111, as
+ * LinearSolverCSparse::solve does (linear_solver_csparse.h:127-133). Default off. */
+int g2ohip_solver_set_write_debug(g2ohip_graph* g, int on);
+
 /* ---- LinearSolver-level plugin (core/linear_solver.h:42-105, LinearSolverCCS) ----
  * Solve A x = b for symmetric PD A given as UPPER CCS (n, Ap[n+1], Ai, Ax) of scalar entries,
  * with an optional block partition (nblocks, block_ends[] cumulative end offsets as in
@@ -215,6 +228,16 @@ int g2ohip_set_comm_local(g2ohip_graph* g, const char* group_key, int rank, int 
  * (the calls g2ohip_set_comm's ranks make) over n doubles of `in` on a stream of `device`; out = [sum | max].
  * A one-GPU box cannot host two ranks of one RCCL communicator, so this is the binding's smoke test there. */
 int g2ohip_comm_selftest(int device, const unsigned char uid[128], int n, const double* in, double* out);
+/* The test transport's rank-ordered host reduction alone (no GPU): `nranks` host threads that share `group_key` each
+ * call this with their buffer; every call is checked to be the same collective on every rank (call number, length,
+ * operation) and a mismatch returns G2OHIP_ERR_DEVICE on every rank (g2ohip_last_error says which) instead of reading
+ * past a buffer. RCCL ranks run the same check when G2OHIP_COMM_CHECK=1 is set. */
+int g2ohip_comm_local_reduce_host(const char* group_key, int rank, int nranks, double* buf, long long n, int is_max);
+/* JSON text naming the HIP runtime and RCCL libraries this library's calls are bound to (resolved paths) and their
+ * versions; returns the length needed including the NUL. */
+int g2ohip_runtime_info(char* out, int cap);
+/* hipDeviceSynchronize on `device` in this library's HIP runtime (the benchmark's bracket around its timed region). */
+int g2ohip_device_synchronize(int device);
 
 /* ---- host-only symbolic analysis (no GPU needed) ----
  * Block pattern of a symmetric matrix given as upper blocks (bi[k] <= bj[k]) of a uniform block

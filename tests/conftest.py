@@ -8,6 +8,17 @@ ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
+# Bind libg2o_hip.so (and through it /opt/rocm's HIP runtime + RCCL, the ROCm 7.2 it is built against) before any
+# test module imports torch: torch bundles its own libamdhip64 / librccl with the same sonames, and whichever is
+# loaded first is the one the product's calls resolve to (tests/test_host.py::test_runtime_binding checks this).
+try:
+    import g2o_amd as _g2o_amd
+
+    if os.path.exists(_g2o_amd.LIB_PATH):
+        _g2o_amd.lib()
+except Exception:  # the library is reported missing by the tests that need it
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; parity tests through the C ABI")

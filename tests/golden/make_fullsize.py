@@ -1,4 +1,7 @@
-"""Full-size BASELINE fixtures (C2, C3, C5) for the -m gpu parity tests.
+"""Full-size BASELINE fixtures (C2, C3, C4, C5) for the -m gpu parity tests.
+
+C4 covers the exact sequence bench.py times (iteration 0 with the structure, then 29 more: the driver runs
+--warmup 5 --steps 20, the default is 5 + 30 minus the untimed stage iterations), C2 / C3 / C5 at least 5 iterations.
 
 Run in the development container, where oracle/_ref (the reference's vendored CSparse compiled
 from /root/reference) is available.  Each fixture is data only: the synth recipe, the oracle's LM
@@ -6,7 +9,7 @@ trajectory (chi2 / lambda / trials per iteration, reference CSparse cs_amd block
 cs_chol) and the final minimal state (C2, C3: the whole state; C5: the cameras, a fixed stride of
 the points and per-chunk sums of all point coordinates, to keep the file small).
 
-    python tests/golden/make_fullsize.py C2 C3 C5
+    python tests/golden/make_fullsize.py C2 C3 C4 C5
 """
 import os
 import sys
@@ -23,7 +26,7 @@ import oracle_py  # noqa: E402
 from g2o_amd import synth  # noqa: E402
 
 # name -> LM iterations recorded
-ITERS = {"C2": 4, "C3": 2, "C5": 2}
+ITERS = {"C2": 6, "C3": 5, "C4": 30, "C5": 5}
 C5_POINT_STRIDE = 97      # every 97th point's coordinates stored exactly
 C5_CHUNK = 4096           # per-chunk sums of the point block of the minimal state
 
@@ -61,5 +64,5 @@ def make(name, threads):
 
 
 if __name__ == "__main__":
-    for nm in sys.argv[1:] or ["C2", "C3", "C5"]:
+    for nm in sys.argv[1:] or ["C2", "C3", "C4", "C5"]:
         make(nm, threads=int(os.environ.get("ORACLE_THREADS", "8")))

@@ -34,10 +34,13 @@ def _fixture(name):
 
 
 def _check_trajectory(fx, st, n):
+    """Per iteration: LM trial count (exact), chi2 and lambda (1e-6 relative: SURVEY.md §8d's chi2 and lambda
+    traces)."""
     assert n == int(fx["iterations"])
     for k, s in enumerate(st):
         assert s.levenbergIterations == int(fx["trials"][k]), (k, s.levenbergIterations, fx["trials"][k])
         assert abs(s.chi2 - fx["chi2"][k]) <= RTOL * abs(fx["chi2"][k]), (k, s.chi2, fx["chi2"][k])
+        assert abs(s.lambda_ - fx["lam"][k]) <= RTOL * abs(fx["lam"][k]), (k, s.lambda_, fx["lam"][k])
 
 
 def _staged_residual(g2o_amd_mod, prob, algo, lam):
@@ -84,6 +87,28 @@ def test_c3_full_trajectory(g2o_amd_mod):
     info = opt.factor_info()
     assert info["blocked_fronts"] > 0 and info["inplace_levels"] > 0 and info["bwd_rounds"] > 0, info
     assert info["syrk_launches"] > 0, info
+
+
+def test_c4_bench_sequence(g2o_amd_mod):
+    """C4 (the headline config) over exactly the iterations bench.py runs and times: optimize_step from iteration 0
+    (structure + lambda init), the warmup at full statistics, then the timed steps at stats level 1, every
+    iteration's chi2, lambda and trial count against the oracle + reference CSparse fixture, and the final state."""
+    fx = _fixture("C4")
+    prob = synth.by_name("C4")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm(ALG["C4"])
+    assert abs(opt.chi2() - float(fx["chi2_0"])) <= 1e-9 * float(fx["chi2_0"])
+    n = int(fx["iterations"])
+    st = []
+    for it in range(n):
+        if it == 5:  # bench.py: warmup done, the timed region runs at stats level 1
+            opt.set_stats_level(1)
+        r, s = opt.optimize_step(it)
+        st.append(s)
+        assert r == 0, (it, r)
+    _check_trajectory(fx, st, n)
+    x, xr = opt.minimal_state(), fx["state"]
+    assert np.linalg.norm(x - xr) <= RTOL * np.linalg.norm(xr)
 
 
 @pytest.mark.parametrize("name,lam", [("C2", 1e-3), ("C3", 1e-3), ("C4", 1e-2), ("C5", 1e-2)])

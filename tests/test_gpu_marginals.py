@@ -89,3 +89,31 @@ def test_marginals_many_batches(g2o_amd_mod, oracle):
     blocks = opt.compute_marginals(pat)
     _compare(blocks, _dense_inverse(oracle, prob), pd, 1e-9)
     assert opt.compute_marginals([]) == {}
+
+
+@pytest.mark.parametrize("knobs", [
+    {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
+    {"G2OHIP_CHOL_LAG": "2"},
+    {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_LAG": "1"},
+], ids=["blocked_fronts", "lagged_all_levels", "lagged_separate_contrib"])
+@pytest.mark.parametrize("name", ["C1", "C3"])
+def test_marginals_blocked_and_lagged_schedules(g2o_amd_mod, oracle, monkeypatch, knobs, name):
+    """The marginal solves read the factor's layout (L21 per front, L_kk^-1 per panel, no stored diagonal blocks).
+    The full-size schedules — blocked fronts with big-panel trailing updates and backward rounds, lagged rank-64 pair
+    steps — only appear on large systems; the schedule knobs force them on the small C1 / C3 pose graphs, so the
+    marginals are checked against the dense inverse on exactly those factor layouts."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    prob = synth.by_name(name, "small")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.initialize_optimization()
+    opt.build_structure()
+    opt.build_system()
+    info = opt.factor_info()
+    if "G2OHIP_CHOL_BLOCK_MIN" in knobs:
+        assert info["blocked_fronts"] > 0 and info["bwd_rounds"] > 0, info
+    pd, _, npose, _ = opt.block_dims()
+    pat = _pattern(npose)
+    blocks = opt.compute_marginals(pat)
+    assert blocks is not None
+    _compare(blocks, _dense_inverse(oracle, prob), pd, 1e-9)

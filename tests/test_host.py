@@ -150,3 +150,68 @@ def test_synth_c4_full_counts():
     assert p.num_edges == 1_000_000
     assert p.num_vertices == 101_000
     assert int(p.vertices[0].fixed.sum()) == 2
+
+
+def test_runtime_binding(g2o_amd_mod):
+    """The product's HIP runtime and RCCL calls resolve to /opt/rocm (ROCm 7.2, what libg2o_hip.so is built against),
+    not to the copies torch bundles under the same sonames: conftest.py binds the library before any test imports
+    torch, as bench.py does before its torch.distributed control plane."""
+    import torch  # noqa: F401  (loaded after the library: must not rebind it)
+    info = g2o_amd_mod.runtime_info()
+    assert info["libamdhip64"].startswith("/opt/rocm"), info
+    assert info["librccl"].startswith("/opt/rocm"), info
+    assert info["hip_runtime_version"] >= 70200000, info
+
+
+def _reduce_threads(g2o_amd_mod, key, sizes, is_max=False):
+    import threading
+    bufs = [np.arange(n, dtype=np.float64) + 10 * r for r, n in enumerate(sizes)]
+    errs = [None] * len(sizes)
+
+    def run(r):
+        try:
+            g2o_amd_mod.comm_local_reduce_host(key, r, len(sizes), bufs[r], is_max)
+        except g2o_amd_mod.G2OHipError as ex:
+            errs[r] = str(ex)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(len(sizes))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=30)
+    assert not any(t.is_alive() for t in th), "a rank hung in the collective"
+    return bufs, errs
+
+
+def test_local_comm_rank_ordered_sum(g2o_amd_mod):
+    bufs, errs = _reduce_threads(g2o_amd_mod, "sum-ok", [5, 5, 5])
+    assert errs == [None] * 3
+    want = sum(np.arange(5.0) + 10 * r for r in range(3))
+    for b in bufs:
+        np.testing.assert_array_equal(b, want)
+    bufs, errs = _reduce_threads(g2o_amd_mod, "max-ok", [4, 4], is_max=True)
+    assert errs == [None, None]
+    np.testing.assert_array_equal(bufs[0], np.arange(4.0) + 10)
+
+
+def test_local_comm_mismatch_raises(g2o_amd_mod):
+    """A rank-dependent collective sequence (the r02 segfault: ranks entering all-reduces of different lengths) is an
+    error on every rank, not a heap over-read or a hang."""
+    bufs, errs = _reduce_threads(g2o_amd_mod, "mismatch-n", [6, 3])
+    assert all(e and "collective mismatch" in e for e in errs), errs
+    np.testing.assert_array_equal(bufs[1], np.arange(3.0) + 10)  # untouched
+    # a different operation on one rank is a mismatch too
+    import threading
+    b = [np.ones(2), np.ones(2)]
+    errs = [None, None]
+
+    def run(r):
+        try:
+            g2o_amd_mod.comm_local_reduce_host("mismatch-op", r, 2, b[r], is_max=(r == 1))
+        except g2o_amd_mod.G2OHipError as ex:
+            errs[r] = str(ex)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    [t.start() for t in th]
+    [t.join(timeout=30) for t in th]
+    assert all(e and "collective mismatch" in e for e in errs), errs

@@ -4,9 +4,12 @@ Usage: python tools/pmc_traffic.py OUT.json FETCH_DIR WRITE_DIR
   FETCH_DIR: a `rocprofv3 --pmc FETCH_SIZE` pass, WRITE_DIR: a `rocprofv3 --pmc WRITE_SIZE` pass
   (separate passes: FETCH_SIZE needs 3 TCC counters, WRITE_SIZE 2, the TCC block holds 4).
 
-Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KB; on gfx950
-FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so it is doubled. Traffic
-per launch = mean over the kernel's dispatches of (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes.
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KB. On gfx950
+FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced streaming read; other access widths
+are uncalibrated. Both figures are therefore written per launch: `bytes_per_launch` = (FETCH_SIZE +
+WRITE_SIZE) * 1024 (raw, no correction: the lower bound, and the value bench.py reports as `traffic`)
+and `bytes_fetch_doubled` = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (the guide's correction, exact for
+16-B/lane streaming reads, an upper bound for narrower ones).
 Kernel names are mapped to the bench.py stage names below. The factorization ("chol_factor") is a
 chain of launches (scatter, extend-add, panel steps, trailing updates): its traffic is the sum over
 all of its dispatches divided by the number of factorizations (k_vec_init runs once per factorization).
@@ -80,11 +83,13 @@ def main():
         f = sum(fetch[stage]) / len(fetch[stage])
         w = sum(write[stage]) / len(write[stage])
         res[stage] = {
-            "bytes_per_launch": (2.0 * f + w) * 1024.0,
+            "bytes_per_launch": (f + w) * 1024.0,
+            "bytes_fetch_doubled": (2.0 * f + w) * 1024.0,
             "fetch_size_kb_raw": f,
             "write_size_kb": w,
             "launches": len(fetch[stage]),
-            "correction": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)",
+            "correction": "bytes_per_launch: (FETCH_SIZE + WRITE_SIZE) * 1024, raw; bytes_fetch_doubled: "
+                          "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 half-count of 16-B/lane streaming reads)",
         }
         if stage == "chol_factor":
             res[stage]["launches"] = "factorizations (sum over the factor's kernel chain)"

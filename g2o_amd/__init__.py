@@ -431,7 +431,7 @@ class SparseOptimizer:
         return {p: out[k * pd * pd:(k + 1) * pd * pd].reshape(pd, pd).T.copy() for k, p in enumerate(pairs)}
 
     FACTOR_INFO_KEYS = ("n", "nnzL", "flops", "supernodes", "levels", "max_front", "blocked_fronts",
-                        "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds")
+                        "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds", "dag_levels")
 
     def factor_info(self) -> dict:
         out = np.zeros(len(self.FACTOR_INFO_KEYS))

@@ -293,6 +293,7 @@ int g2ohip_linear_solve_ccs(int device, int n, const int* Ap, const int* Ai, con
       HIP_CHECK(hipMemcpyAsync(&f, df.get(), sizeof f, hipMemcpyDeviceToHost, s));
       dx.download(x, n, s);
       HIP_CHECK(hipStreamSynchronize(s));
+      if (f) ch.check_dag(s);
       ok = f ? 0 : 1;
     }
     (void)hipStreamDestroy(s);

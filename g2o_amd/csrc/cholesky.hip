@@ -381,6 +381,15 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
       }
     }
     PH(2)
+    if (t.a < 0) {  // level factored by k_dag: the assembled block and its right-hand side go into the front
+#pragma unroll
+      for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+        const int e = tid + 256 * u_, r = e & (NB - 1), c = e >> 5;
+        if (r < kb0 && c < kb0 && r >= c) F[c * m + r] = D[r * DS + c];
+      }
+      if (tid < kb0) v[tid] = vy[tid];
+      return;
+    }
     if (tid < 64) factor_block(D, kb0, vy, col, tid, fail, ysol + me.c0, PH_REC);
     __syncthreads();
     publish_inverse(D, kb0, tid, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns);
@@ -929,7 +938,528 @@ __global__ void __launch_bounds__(256) k_bwd_inner(const Task* __restrict__ task
   if (lane == 0) tsol[me.c0 + j] -= acc;
 }
 
+// ---------------------------------------------------------------------------- persistent tile DAG
+// Latency-bound levels (few fronts): the launch-per-panel schedule above pays a kernel boundary, a
+// reload of every tile and a reload of L_kk^-1 per 32 columns. Here one launch factors the whole level. Every 64 x 64
+// tile of every front of the level is owned by one workgroup (one per CU, all resident), which keeps the tile in
+// MFMA accumulators from the first panel to the last, and per panel k (32 columns, k0 = 32 k, in own tile column
+// Jp = k0 / 64, half h) plays one role:
+//   DIAG   (Jp, Jp): factor the diagonal block (its quadrant (h, h)) with chol32, y_k = L_kk^-1 (v_k - sum L_kq y_q);
+//          publish L_kk^-1 and y_k; for h = 0 also the L rows of quadrant (1, 0) (TRSM with the fresh inverse), then
+//          update quadrant (1, 1) locally: the next panel's diagonal block needs no hand-off;
+//   TRSM   (I, Jp), I > Jp: L_Ik = C_I,half L_kk^-T (the tile's own half-columns), publish it; for h = 0 update the
+//          tile's other half with L_Ik and the diagonal tile's quadrant-(1, 0) rows;
+//   UPDATE (I, J), J > Jp: C_IJ -= L_Ik L_Jk^T (diagonal tiles also fold L_Ik y_k into their right-hand side).
+// Hand-offs (MI355X_MICROARCH.md §visibility, the write-through form): every handed-off double is stored with an
+// sc1 (write-through) store, every storing wave drains (vmcnt 0), the workgroup barrier, then one lane stores the
+// flag = this call's epoch with an agent-scope atomic; the consumer's lane 0 polls the flag with agent-scope atomic
+// loads, the workgroup barrier, then every load of the handed-off bytes is an sc1 load. One workgroup per CU (the
+// launch reserves LDS for that). Within a workgroup the roles run per panel in the order DIAG, TRSM, UPDATE and every
+// dependency points to an earlier (panel, role): with all workgroups resident the DAG cannot deadlock. A poll that
+// spins too long (a bug, never expected) sets the timeout word and the fail flag and stops waiting.
+// Outputs are those of the panel-step schedule (lbuf L columns without the 32 x 32 diagonal blocks, linv per panel,
+// ysol, the contribution block in the front, the update vector in the front vector) except X = L11^-1: the backward
+// solve of these fronts is k_bwd_seq.
+using launch::DagFront;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ double ld_wt0(const double* p, long long idx, bool ok) {
+  const double v = ld_wt(p + (ok ? idx : 0));
+  return ok ? v : 0.0;
+}
+// every storing wave drains its write-through stores, then one lane raises the flag
+__device__ __forceinline__ void dag_signal(unsigned* flag, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr unsigned DAG_SPIN_MAX = 1u << 22;
+__device__ __forceinline__ void dag_poll(unsigned* flag, unsigned epoch, unsigned* tmo, int* fail) {
+  unsigned spins = 0;
+  while (__hip_atomic_load((gu32*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255u) == 0) {
+      if (__hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) return;
+      if (spins >= DAG_SPIN_MAX) {
+        __hip_atomic_store((gu32*)tmo, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *fail = 1;
+        return;
+      }
+    }
+  }
+}
+// lane 0 polls (one or two flags), then the workgroup barrier: every wave's loads come after the match
+__device__ __forceinline__ void dag_wait(unsigned* f1, unsigned* f2, unsigned epoch, unsigned* tmo, int* fail) {
+  if (threadIdx.x == 0) {
+    if (f1) dag_poll(f1, epoch, tmo, fail);
+    if (f2 && f2 != f1) dag_poll(f2, epoch, tmo, fail);
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ int dag_off(const DagFront& F, int I) { return I < F.nown ? 64 * I : F.ns + 64 * (I - F.nown); }
+__device__ __forceinline__ int dag_len(const DagFront& F, int I) {
+  return I < F.nown ? min(64, F.ns - 64 * I) : min(64, F.m - F.ns - 64 * (I - F.nown));
+}
+
+template <int TPW>
+struct DagLds {
+  double Li[NB * PS];   // L_kk^-1 row-major (li_tag: which front / panel it holds)
+  double Pa[TT * PS];   // staging: a tile's panel columns, or L rows loaded from another workgroup
+  double Pb[TT * PS];
+  double D[NB * DS];    // diagonal block / its inverse (factor_block)
+  __attribute__((aligned(16))) double col[4 * NB];
+  double vy[NB], yk[NB];
+  double vacc[TPW][TT];       // diagonal tiles: v_rows - sum_q L_rows,q y_q
+  double Lout[TPW][TT * PS];  // this panel's L rows produced by each tile slot (TRSM: 64 rows, DIAG: rows 32..63), read
+                              // in place by the slot's own later roles of the panel: no hand-off inside a workgroup
+};
+
+// acc (a tile's 64 x 64 in the MfmaTile layout of wave w) -> the wave's 32 x 32 quadrant into buf (row-major, stride S,
+// at row offset ro); called by the owning wave only
+__device__ __forceinline__ void dag_stage(const dx4 (&acc)[2][2], double* buf, int S, int ro, int lane) {
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) buf[(ro + 16 * x + lk + 4 * i) * S + 16 * y + lr] = acc[x][y][i];
+}
+// acc -= A B^T over K = 32: A rows ra.. (16 x 2 blocks), B rows rb.., both row-major stride PS
+__device__ __forceinline__ void dag_gemm_sub(dx4 (&acc)[2][2], const double* A, int ra, const double* B, int rb, int lane) {
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < NB / 4; ++kk) {
+    const int k = kk * 4 + lk;
+    const double a0 = -A[(ra + lr) * PS + k], a1 = -A[(ra + 16 + lr) * PS + k];
+    const double b0 = B[(rb + lr) * PS + k], b1 = B[(rb + 16 + lr) * PS + k];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+  }
+}
+// X = P L^-T for 16 rows (r0..r0+15) of P (in `in`) into the same rows of `out` (may alias); columns >= kb zeroed
+// (ragged last panel). One wave owns those rows of both buffers.
+__device__ __forceinline__ void dag_trsm16(const double* in, double* out, const double* Li, int r0, int kb, int lane) {
+  const int lr = lane & 15, lk = lane >> 4;
+  dx4 x0 = {0.0, 0.0, 0.0, 0.0}, x1 = x0;
+#pragma unroll
+  for (int kk = 0; kk < NB / 4; ++kk) {
+    const int k = kk * 4 + lk;
+    const double a = in[(r0 + lr) * PS + k];
+    x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Li[lr * PS + k], x0, 0, 0, 0);
+    x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Li[(16 + lr) * PS + k], x1, 0, 0, 0);
+  }
+  lds_fence();  // this wave's reads of its rows are done before it overwrites them
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + lk + 4 * i;
+    out[r * PS + lr] = lr < kb ? x0[i] : 0.0;
+    out[r * PS + 16 + lr] = 16 + lr < kb ? x1[i] : 0.0;
+  }
+}
+// slot of this workgroup holding tile (f, I, J), or -1
+template <int TPW>
+__device__ __forceinline__ int dag_slot(const int4 (&td)[TPW], int f, int I, int J) {
+  int s = -1;
+#pragma unroll
+  for (int q = 0; q < TPW; ++q)
+    if (td[q].x == f && td[q].y == I && td[q].z == J) s = q;
+  return s;
+}
+
+template <int TPW>
+__global__ void __launch_bounds__(256, 1) k_dag(const DagFront* __restrict__ frs, const int4* __restrict__ tiles,
+                                                double* __restrict__ fronts, double* lbuf, double* __restrict__ vecs,
+                                                double* ysol, double* linv, unsigned* flags, unsigned epoch, int* fail,
+                                                unsigned* tmo) {
+  __shared__ DagLds<TPW> S;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
+  int4 td[TPW];
+  dx4 acc[TPW][2][2];
+  int kmax = 0, li_tag = -1, yk_tag = -1;  // front * 65536 + panel whose L_kk^-1 / y_k S.Li / S.yk hold
+  // Signals: a role's write-through stores are drained and its flag raised at once; with `defer` (measured slower, DESIGN
+  // §5) the drain and flag wait until this workgroup is about to poll (it must never block while holding a signal: the
+  // DAG stays deadlock-free) or until a second diagonal factor has run behind them. pD..pDe / pT: panels of pending
+  // DIAG / TRSM signals of slot t, or -1.
+  constexpr bool defer = false;
+  int pD[TPW], pDe[TPW], pT[TPW];  // pending DIAG signals: panels pD .. pDe (a tile column's two panels)
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) pD[t] = pDe[t] = pT[t] = -1;
+  auto flush = [&]() {
+    bool any = false;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) any |= pD[t] >= 0 || pT[t] >= 0;
+    if (!any) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        if (pD[t] < 0 && pT[t] < 0) continue;
+        const DagFront F = frs[td[t].x];
+        for (int q = pD[t]; q >= 0 && q <= pDe[t]; ++q)
+          __hip_atomic_store((gu32*)(flags + F.flag_off + q), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pT[t] >= 0)
+          __hip_atomic_store((gu32*)(flags + F.flag_off + F.np + td[t].y * F.np + pT[t]), epoch, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) pD[t] = pDe[t] = pT[t] = -1;
+  };
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    td[t] = tiles[(size_t)blockIdx.x * TPW + t];
+    if (td[t].x < 0) continue;
+    const DagFront F = frs[td[t].x];
+    kmax = max(kmax, F.np);
+    const int I = td[t].y, J = td[t].z;
+    const int ro = dag_off(F, I), rl = dag_len(F, I), co = dag_off(F, J), cl = dag_len(F, J);
+    const double* Fp = fronts + F.f_off;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wr + 16 * x + lk + 4 * i, c = wc + 16 * y + lr;
+          acc[t][x][y][i] = ld0(Fp, (co + c) * F.m + ro + r, r < rl && c < cl && (I != J || r >= c));
+        }
+    if (I == J && tid < TT) S.vacc[t][tid] = ld0(vecs + F.v_off, ro + tid, tid < rl);
+  }
+  __syncthreads();
+
+  for (int k = 0; k < kmax; ++k) {
+    const int k0 = NB * k, Jp = k0 >> 6, h = (k0 >> 5) & 1;
+    // ---------------- DIAG
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (td[t].x < 0) continue;
+      const DagFront F = frs[td[t].x];
+      const int I = td[t].y, J = td[t].z;
+      if (k >= F.np || J != Jp || I != J) continue;
+      const int kb = min(NB, F.ns - k0), ro = dag_off(F, J), rl = dag_len(F, J);
+      if (w == 3 * h) {  // quadrant (h, h), lower triangle, row-major into D
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = 16 * x + lk + 4 * i, c = 16 * y + lr;
+              if (r >= c) S.D[r * DS + c] = acc[t][x][y][i];
+            }
+      }
+      if (tid < NB) S.vy[tid] = S.vacc[t][NB * h + tid];
+      __syncthreads();
+      if (tid < 64) factor_block(S.D, kb, S.vy, S.col, tid, fail, S.yk);
+      __syncthreads();
+      double* Lin = linv + (size_t)(F.c0 + k0) * (NB * NB);
+#pragma unroll
+      for (int u = 0; u < NB * NB / 256; ++u) {
+        const int e = tid + 256 * u, i = e >> 5, c = e & (NB - 1);
+        const double v = S.D[c * DS + i];  // L^-1(i, c), identity-padded past kb
+        S.Li[i * PS + c] = v;
+        st_wt(Lin + e, v);
+      }
+      li_tag = yk_tag = td[t].x * 65536 + k;
+      if (tid < kb) st_wt(ysol + F.c0 + k0 + tid, S.yk[tid]);
+      if (h == 0 && rl > NB) {
+        // quadrant (1, 0): X1 = C10 L_kk^-T (wave 1 holds C10; waves 2 and 3 solve 16 rows each) -> Lout rows 32..
+        double* X1 = S.Lout[t];
+        if (w == 1) dag_stage(acc[t], S.Pa, PS, NB, lane);
+        __syncthreads();
+        if (w >= 2) dag_trsm16(S.Pa, X1, S.Li, NB + 16 * (w - 2), kb, lane);
+        __syncthreads();
+        double* Lf = lbuf + F.l_off;
+#pragma unroll
+        for (int u = 0; u < NB * NB / 256; ++u) {
+          const int e = tid + 256 * u, r = e & (NB - 1), q = e >> 5;
+          if (r < rl - NB && q < kb) st_wt(Lf + (size_t)(k0 + q) * F.m + ro + NB + r, X1[(NB + r) * PS + q]);
+        }
+        if (pD[t] < 0) pD[t] = k;
+        pDe[t] = k;
+        if (!defer) flush();
+        // rows 32.. of the right-hand side, and quadrant (1, 1) of this tile, by panel k (the next panel's diagonal)
+        if (tid < NB) {
+          double s2 = 0.0;
+#pragma unroll
+          for (int q = 0; q < NB; ++q) s2 += X1[(NB + tid) * PS + q] * S.yk[q];
+          S.vacc[t][NB + tid] -= s2;
+        }
+        if (w == 3) dag_gemm_sub(acc[t], X1, NB, X1, NB, lane);
+        __syncthreads();
+        if (k + 1 >= F.np) flush();
+      } else {
+        if (pD[t] < 0) pD[t] = k;
+        pDe[t] = k;
+        flush();  // the second factor of the tile column: its drain also covers the first's
+      }
+    }
+    // ---------------- TRSM
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (td[t].x < 0) continue;
+      const DagFront F = frs[td[t].x];
+      const int I = td[t].y, J = td[t].z;
+      if (k >= F.np || J != Jp || I == J) continue;
+      const int kb = min(NB, F.ns - k0), ro = dag_off(F, I), rl = dag_len(F, I);
+      const int sd = dag_slot(td, td[t].x, Jp, Jp);  // this workgroup factored panel k itself
+      const bool li_here = li_tag == td[t].x * 65536 + k;
+      if ((w >> 1) == h) dag_stage(acc[t], S.Pa, PS, wr, lane);  // this tile's half-h columns (its panel k)
+      if (li_here && yk_tag == li_tag && (sd >= 0 || h == 1)) {
+        __syncthreads();
+      } else {
+        flush();
+        dag_wait(flags + F.flag_off + k, nullptr, epoch, tmo, fail);
+        const double* Lin = linv + (size_t)(F.c0 + k0) * (NB * NB);
+        const double* Lf = lbuf + F.l_off;
+        const int dro = dag_off(F, Jp) + NB, drl = dag_len(F, Jp) - NB;  // diagonal tile's quadrant-(1, 0) rows (h = 0)
+        double lv[NB * NB / 256], xv[NB * NB / 256];
+#pragma unroll
+        for (int u = 0; u < NB * NB / 256; ++u) {
+          const int e = tid + 256 * u, r = e & (NB - 1), q = e >> 5;
+          lv[u] = ld_wt0(Lin, e, !li_here);
+          xv[u] = ld_wt0(Lf, (long long)(k0 + q) * F.m + dro + r, h == 0 && sd < 0 && r < drl && q < kb);
+        }
+        const double yv = ld_wt0(ysol, F.c0 + k0 + tid, tid < kb);  // y_k rides with L_kk^-1 (the diagonal update)
+#pragma unroll
+        for (int u = 0; u < NB * NB / 256; ++u) {
+          const int e = tid + 256 * u, r = e & (NB - 1), q = e >> 5;
+          if (!li_here) S.Li[(e >> 5) * PS + (e & (NB - 1))] = lv[u];
+          S.Pb[(NB + r) * PS + q] = xv[u];
+        }
+        if (tid < NB) S.yk[tid] = yv;
+        li_tag = yk_tag = td[t].x * 65536 + k;
+        __syncthreads();
+      }
+      double* X = S.Lout[t];
+      dag_trsm16(S.Pa, X, S.Li, 16 * w, kb, lane);
+      __syncthreads();
+      double* Lw = lbuf + F.l_off;
+#pragma unroll
+      for (int u = 0; u < TT * NB / 256; ++u) {
+        const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+        if (r < rl && q < kb) st_wt(Lw + (size_t)(k0 + q) * F.m + ro + r, X[r * PS + q]);
+      }
+      pT[t] = k;
+      if (!defer) flush();
+      if (h == 0 && (w >> 1) == 1)  // the other half: -= L_Ik X1^T
+        dag_gemm_sub(acc[t], X, wr, sd >= 0 ? S.Lout[sd] : S.Pb, NB, lane);
+      __syncthreads();
+    }
+    // ---------------- UPDATE
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (td[t].x < 0) continue;
+      const DagFront F = frs[td[t].x];
+      const int I = td[t].y, J = td[t].z;
+      if (k >= F.np || J <= Jp) continue;
+      const int kb = min(NB, F.ns - k0);
+      const int roI = dag_off(F, I), rlI = dag_len(F, I), roJ = dag_off(F, J), rlJ = dag_len(F, J);
+      const int sI = dag_slot(td, td[t].x, I, Jp), sJ = I == J ? sI : dag_slot(td, td[t].x, J, Jp);
+      unsigned* pf = flags + F.flag_off + F.np;
+      const bool remote = sI < 0 || (sJ < 0 && I != J);
+      const bool yk_here = yk_tag == td[t].x * 65536 + k;
+      if (remote) {
+        flush();
+        dag_wait(sI < 0 ? pf + I * F.np + k : nullptr, sJ < 0 ? pf + J * F.np + k : nullptr, epoch, tmo, fail);
+      }
+      const double* Lf = lbuf + F.l_off;
+      double av[TT * NB / 256], bv[TT * NB / 256];
+#pragma unroll
+      for (int u = 0; u < TT * NB / 256; ++u) {
+        const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+        av[u] = ld_wt0(Lf, (long long)(k0 + q) * F.m + roI + r, sI < 0 && r < rlI && q < kb);
+        bv[u] = ld_wt0(Lf, (long long)(k0 + q) * F.m + roJ + r, sJ < 0 && I != J && r < rlJ && q < kb);
+      }
+      // y_k: from the TRSM / DIAG of this panel on this workgroup, else loaded (published before any flag this
+      // tile's operands depend on; a diagonal tile with local operands always has it here)
+      const bool yload = I == J && !yk_here;
+      const double ykv = ld_wt0(ysol, F.c0 + k0 + tid, yload && tid < kb);
+      if (remote) {
+#pragma unroll
+        for (int u = 0; u < TT * NB / 256; ++u) {
+          const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+          if (sI < 0) S.Pa[r * PS + q] = av[u];
+          if (sJ < 0 && I != J) S.Pb[r * PS + q] = bv[u];
+        }
+      }
+      if (yload) {
+        if (tid < NB) S.yk[tid] = ykv;
+        yk_tag = td[t].x * 65536 + k;
+      }
+      __syncthreads();
+      const double* A = sI >= 0 ? S.Lout[sI] : S.Pa;
+      const double* B = I == J ? A : (sJ >= 0 ? S.Lout[sJ] : S.Pb);
+      if (I == J && tid < TT) {
+        double s2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) s2 += A[tid * PS + q] * S.yk[q];
+        S.vacc[t][tid] -= s2;
+      }
+      dag_gemm_sub(acc[t], A, wr, B, wc, lane);
+      __syncthreads();
+    }
+    bool dcont = false;  // a diagonal tile factors its second panel next: keep that signal behind its factor
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) dcont |= pD[t] >= 0;
+    if (!dcont) flush();
+  }
+  flush();
+  // ---------------- contribution block and update vector (read by the parent's assembly in the next launch)
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    if (td[t].x < 0) continue;
+    const DagFront F = frs[td[t].x];
+    const int I = td[t].y, J = td[t].z;
+    if (J < F.nown) continue;
+    const int ro = dag_off(F, I), rl = dag_len(F, I), co = dag_off(F, J), cl = dag_len(F, J);
+    double* Fp = fronts + F.f_off;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wr + 16 * x + lk + 4 * i, c = wc + 16 * y + lr;
+          if (r < rl && c < cl && (I != J || r >= c)) Fp[(size_t)(co + c) * F.m + ro + r] = acc[t][x][y][i];
+        }
+    if (I == J && tid < rl) vecs[F.v_off + ro + tid] = S.vacc[t][tid];
+  }
+}
+
+// Backward solve of a k_dag front (no explicit X = L11^-1), right-looking: t (= y - L21^T x_rows from k_bwd_gemv) is
+// reduced in LDS; from the last block, x_b = L_bb^-T t_b, then t_c -= sum_r L(b0 + r, c) x_b[r] for every column c < b0
+// (row block b of L11, 4 threads per column). The sequential chain per block is one 32 x 32 product and one update
+// pass over registers; block b-1's rows of L and its L^-1 are loaded while block b is solved.
+constexpr int BSQ_C = 6;                 // column passes of 64: ns <= 64 * BSQ_C + 32
+constexpr int BSQ_N = 64 * BSQ_C + NB;   // largest ns
+__global__ void __launch_bounds__(256) k_bwd_seq(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                                 const double* __restrict__ lbuf, const double* __restrict__ linv,
+                                                 const double* __restrict__ tsol, double* __restrict__ xsol,
+                                                 const int* __restrict__ perm, double* __restrict__ xout) {
+  __shared__ double ts[BSQ_N];
+  __shared__ double Lis[2][NB * (NB + 1)];
+  __shared__ double xb[NB];
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int m = me.ns + me.nr, ns = me.ns;
+  const int tid = threadIdx.x, cq = tid >> 2, rq = tid & 3;
+  const double* L = lbuf + me.l_off;
+  const int np = (ns + NB - 1) / NB;
+  double cur[BSQ_C][8], nxt[BSQ_C][8], li[NB * NB / 256];
+  auto load_rows = [&](int b, double (&dst)[BSQ_C][8], double (&lv)[NB * NB / 256]) {
+    const int b0 = NB * b;
+#pragma unroll
+    for (int p = 0; p < BSQ_C; ++p)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int c = 64 * p + cq, i = b0 + 8 * rq + r;
+        dst[p][r] = ld0(L, c * m + i, c < b0 && i < ns);
+      }
+    const double* Li = linv + (size_t)(me.c0 + b0) * (NB * NB);
+#pragma unroll
+    for (int u = 0; u < NB * NB / 256; ++u) lv[u] = Li[tid + 256 * u];
+  };
+  for (int i = tid; i < ns; i += 256) ts[i] = tsol[me.c0 + i];
+  load_rows(np - 1, cur, li);
+  int cb = 0;
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = tid + 256 * u;
+    Lis[0][(e >> 5) * (NB + 1) + (e & (NB - 1))] = li[u];
+  }
+  __syncthreads();
+  for (int b = np - 1; b >= 0; --b) {
+    const int b0 = NB * b, kb = min(NB, ns - b0);
+    if (b > 0) load_rows(b - 1, nxt, li);
+    if (tid < NB) {  // x_b = L_bb^-T t_b: x[j] = sum_i L^-1(i, j) t[i]
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int i = 0; i < NB; ++i) a4[i & 3] += (i < kb ? Lis[cb][i * (NB + 1) + tid] * ts[b0 + min(i, kb - 1)] : 0.0);
+      const double x = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      xb[tid] = tid < kb ? x : 0.0;
+      if (tid < kb) {
+        xsol[me.c0 + b0 + tid] = x;
+        xout[perm[me.c0 + b0 + tid]] = x;
+      }
+    }
+    __syncthreads();
+    if (b > 0) {
+#pragma unroll
+      for (int p = 0; p < BSQ_C; ++p) {
+        const int c = 64 * p + cq;
+        double part = 0.0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) part += cur[p][r] * xb[8 * rq + r];
+        part += __shfl_xor(part, 1, 64);
+        part += __shfl_xor(part, 2, 64);
+        if (rq == 0 && c < b0) ts[c] -= part;
+      }
+      cb ^= 1;
+#pragma unroll
+      for (int u = 0; u < NB * NB / 256; ++u) {
+        const int e = tid + 256 * u;
+        Lis[cb][(e >> 5) * (NB + 1) + (e & (NB - 1))] = li[u];
+      }
+#pragma unroll
+      for (int p = 0; p < BSQ_C; ++p)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[p][r] = nxt[p][r];
+    }
+    __syncthreads();
+  }
+}
+
 namespace launch {
+
+// one workgroup per CU (the validated form of the write-through hand-offs): dynamic LDS tops each instance up to more
+// than half of the CU's 160 KB
+template <int TPW>
+static int dag_reserve() {
+  static int r = -1;
+  if (r < 0) {
+    hipFuncAttributes a;
+    HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_dag<TPW>)));
+    r = std::max(0, 82 * 1024 - (int)a.sharedSizeBytes);
+  }
+  return r;
+}
+void chol_dag(int nworkers, int tpw, const DagFront* fr, const int4* tiles, double* fronts, double* lbuf, double* vecs,
+              double* ysol, double* linv, unsigned* flags, unsigned epoch, int* fail, unsigned* tmo, hipStream_t s) {
+  if (nworkers <= 0) return;
+  if (tpw == 2)
+    hipLaunchKernelGGL(k_dag<2>, nworkers, 256, dag_reserve<2>(), s, fr, tiles, fronts, lbuf, vecs, ysol, linv, flags, epoch, fail, tmo);
+  else
+    hipLaunchKernelGGL(k_dag<4>, nworkers, 256, dag_reserve<4>(), s, fr, tiles, fronts, lbuf, vecs, ysol, linv, flags, epoch, fail, tmo);
+  KERNEL_CHECK();
+}
+int chol_dag_max_workers(int device) {
+  hipDeviceProp_t p;
+  HIP_CHECK(hipGetDeviceProperties(&p, device));
+  int per2 = 0, per4 = 0;
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_dag<2>, 256, dag_reserve<2>()));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, k_dag<4>, 256, dag_reserve<4>()));
+  return per2 >= 1 && per4 >= 1 ? p.multiProcessorCount : 0;
+}
+void chol_bwd_seq(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* linv,
+                  const double* tsol, double* xsol, const int* perm, double* xout, hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_bwd_seq, ntasks, 256, 0, s, tasks, fd, lbuf, linv, tsol, xsol, perm, xout);
+  KERNEL_CHECK();
+}
 
 int debug_phases(unsigned long long* out, int maxrec) {
 #ifdef G2OHIP_PHASES

@@ -404,6 +404,23 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const long long lag_fused_min = lag_mode >= 2 ? 0 : (lfm ? atoll(lfm) : 256);
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
     const long long pre_max = pm ? atoll(pm) : (256LL << 20);
+    // persistent tile DAG (k_dag): 0 (default) off, 1 latency-bound levels (those whose panel steps would fuse the
+    // contribution block), 2 every level whose tiles fit the resident workgroups. Off by default: at C4 its levels take
+    // 135-155 us against 121-161 us for the panel-step launches (the hand-off payload reads dominate)
+    const char* dm = getenv("G2OHIP_CHOL_DAG");
+    const int dag_mode = dm ? atoi(dm) : 0;
+    int dag_cap = 0;
+    if (dag_mode) {
+      int dev = 0;
+      HIP_CHECK(hipGetDevice(&dev));
+      dag_cap = launch::chol_dag_max_workers(dev);
+    }
+    std::vector<launch::DagFront> hdf;
+    std::vector<int4> hdt;
+    std::vector<char> level_dag(sym.levels.size(), 0);
+    int dag_flag_total = 0;
+    op_front_off.clear();
+    n_dag_levels = 0;
     std::vector<long long> zr, pdst;
     std::vector<int> psrc;
     for (size_t l = 0; l < sym.levels.size(); ++l) {
@@ -416,6 +433,22 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         tiles0 += (long long)T * (T + 1) / 2;
       }
       const bool fused_contrib = tiles0 <= fused_max;
+      // the tile DAG: every 64 x 64 tile of the level's fronts (own and contribution parts tiled separately) owned by
+      // one resident workgroup, at most CHOL_DAG_TPW tiles each
+      long long dtiles = 0;
+      bool dag_fit = dag_mode != 0 && dag_cap > 0;
+      for (int sn : lv) {
+        const Supernode& q = sym.sn[sn];
+        const long long nt = (q.ns + TT - 1) / TT + (q.nr + TT - 1) / TT;
+        dtiles += nt * (nt + 1) / 2;
+        if (q.ns > 6 * 64 + NB) dag_fit = false;  // k_bwd_seq holds a block row of at most 6 x 64 columns
+      }
+      long long dpairs = 0;  // diagonal-pair workgroups (see the tile ownership below)
+      for (int sn : lv) dpairs += (sym.sn[sn].ns + TT - 1) / TT + (sym.sn[sn].nr + TT - 1) / TT;
+      const long long drest = dtiles - (2 * dpairs - (long long)lv.size());
+      const bool dag = dag_fit && (fused_contrib || dag_mode >= 2) && dpairs <= dag_cap &&
+                       dpairs + (std::max(0LL, drest - 2 * dpairs) + 3) / 4 <= dag_cap;
+      level_dag[l] = dag;
       // k_extend_add: every front's first-diagonal-block task first, then the slabs
       // small levels (all fronts <= pre_max bytes together) are zeroed + scattered before the first level
       // (two massively parallel passes off the critical chain); large ones are assembled in place
@@ -450,7 +483,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       int lmaxm = 0;
       for (int sn : lv) lmaxm = std::max(lmaxm, sym.sn[sn].ns + sym.sn[sn].nr);
       Op ea{pre ? 0 : (lmaxm <= 512 ? 5 : 4), (int)tk.size(), 0};
-      for (int sn : lv) tk.push_back(Task{sn, 0, 0, 1});
+      // first diagonal blocks: assembled and factored beside the slabs, or (DAG levels, a = -1) assembled into the front
+      for (int sn : lv) tk.push_back(Task{sn, dag ? -1 : 0, 0, 1});
       // every front is assembled here (input entries, zeros, children); slabs of EA columns where the level
       // has enough of them to fill the chip several times over, else 4 (latency-bound upper levels)
       const int slab = level_slab[l];
@@ -462,6 +496,63 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       }
       ea.count = (int)tk.size() - ea.off;
       ops.push_back(ea);
+      op_front_off.push_back(0);
+      if (dag) {
+        const int f0 = (int)hdf.size();
+        std::vector<int> ntr_of;
+        for (int sn : lv) {
+          const Supernode& q = sym.sn[sn];
+          const int m = q.ns + q.nr, nown = (q.ns + TT - 1) / TT, ntr = nown + (q.nr + TT - 1) / TT;
+          const int np = (q.ns + NB - 1) / NB;
+          hdf.push_back(launch::DagFront{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0, nown, ntr, np,
+                                         dag_flag_total, 0});
+          dag_flag_total += np + ntr * np;
+          ntr_of.push_back(ntr);
+        }
+        // ownership: the diagonal tile (J, J) and its left neighbour (J, J-1) share a workgroup, so the panel chain
+        // crosses workgroups once per 64 columns (the factor of panel 2j+1 -> the next diagonal's owner, which solves
+        // its own row's panel and updates its diagonal tile from LDS); the other tiles, column by column with the
+        // fronts interleaved, are dealt round-robin (a panel's TRSM / update tiles land on different workgroups)
+        std::vector<std::vector<int4>> bins;
+        std::vector<int4> rest;
+        int maxntr = 0;
+        for (int n : ntr_of) maxntr = std::max(maxntr, n);
+        for (size_t f = 0; f < ntr_of.size(); ++f)
+          for (int J = 0; J < ntr_of[f]; ++J) {
+            bins.push_back({int4{(int)f, J, J, 0}});
+            if (J > 0) bins.back().push_back(int4{(int)f, J, J - 1, 0});
+          }
+        for (int J = 0; J < maxntr; ++J)
+          for (size_t f = 0; f < ntr_of.size(); ++f)
+            for (int I = J + 2; I < ntr_of[f]; ++I) rest.push_back(int4{(int)f, I, J, 0});
+        const int npair = (int)bins.size(), nrest = (int)rest.size();
+        int tpw = 2;
+        if (npair + (nrest + 1) / 2 > dag_cap) tpw = 4;
+        const int extra = tpw == 4 ? std::max(0, nrest - 2 * npair) : nrest;  // tiles beyond the pair bins' spare slots
+        const int nnew = (extra + tpw - 1) / tpw;
+        if (npair + nnew > dag_cap) throw DeviceError("tile DAG: level does not fit the resident workgroups");
+        bins.resize(npair + nnew);
+        // spread: round-robin over the bins that still have room (pair bins first take up to tpw - 2 more)
+        size_t bi = tpw == 4 ? 0 : (size_t)npair;
+        for (const int4& tl : rest) {
+          for (size_t tries = 0; tries < bins.size(); ++tries) {
+            if ((int)bins[bi].size() < tpw) break;
+            bi = (bi + 1) % bins.size();
+          }
+          bins[bi].push_back(tl);
+          bi = (bi + 1) % bins.size();
+          if (tpw == 2 && bi < (size_t)npair) bi = npair;
+        }
+        const int nw = (int)bins.size();
+        Op dg{7, (int)hdt.size(), nw, tpw};
+        hdt.resize(hdt.size() + (size_t)nw * tpw, int4{-1, 0, 0, 0});
+        for (int b = 0; b < nw; ++b)
+          for (size_t q = 0; q < bins[b].size(); ++q) hdt[dg.off + (size_t)b * tpw + q] = bins[b][q];
+        ops.push_back(dg);
+        op_front_off.push_back(f0);
+        ++n_dag_levels;
+        continue;
+      }
       int maxp = 0;
       for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
       // blocked fronts (wide supernodes on levels with a separate contribution pass): the rank-32 tile
@@ -522,7 +613,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         st.count = (int)stk.size() - st.off;
         for (int k = st.off; k < st.off + st.count; ++k)
           if (stk[k].flags & 64) st.kind = 6;
-        if (st.count) ops.push_back(st);
+        if (st.count) { ops.push_back(st); op_front_off.push_back(0); }
         if ((p + 1) * NB % lpb) continue;
         // end of a big panel: trailing update of the blocked fronts, then their next first blocks
         Op gm{3, (int)tk.size(), 0};
@@ -539,8 +630,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         }
         gm.count = (int)tk.size() - gm.off;
         d0.count = (int)stk.size() - d0.off;
-        if (gm.count) { ops.push_back(gm); ++n_syrk_ops; }
-        if (d0.count) ops.push_back(d0);
+        if (gm.count) { ops.push_back(gm); op_front_off.push_back(0); ++n_syrk_ops; }
+        if (d0.count) { ops.push_back(d0); op_front_off.push_back(0); }
       }
       Op sy{3, (int)tk.size(), 0};
       for (int sn : lv) {
@@ -551,9 +642,16 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, 0, ti | (tj << 16), 0});
       }
       sy.count = (int)tk.size() - sy.off;
-      if (sy.count) { ops.push_back(sy); ++n_syrk_ops; }
+      if (sy.count) { ops.push_back(sy); op_front_off.push_back(0); ++n_syrk_ops; }
       for (int sn : lv) n_blocked += blocked(sym.sn[sn]) ? 1 : 0;
     }
+    dag_fronts.upload(hdf.empty() ? std::vector<launch::DagFront>(1) : hdf, s);
+    dag_tiles.upload(hdt.empty() ? std::vector<int4>{int4{-1, 0, 0, 0}} : hdt, s);
+    dag_flags.resize(std::max(dag_flag_total, 1));
+    dag_flags.zero(s);
+    dag_tmo.resize(1);
+    dag_tmo.zero(s);
+    dag_epoch = 0;
     nzero = (int)(zr.size() / 2);
     npre = (long long)pdst.size();
     zero_rng.upload(zr.empty() ? std::vector<long long>{0, 0} : zr, s);
@@ -577,6 +675,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       bl.gemv.second = (int)tk.size() - bl.gemv.first;
       bl.xall = {(int)tk.size(), 0};
       int rounds = 0;
+      if (level_dag[l]) {  // no explicit X = L11^-1: one sequential block solve per front
+        bl.seq = {(int)tk.size(), (int)lv.size()};
+        for (int sn : lv) tk.push_back(Task{sn, 0, 0, 0});
+        bwd_ops.push_back(bl);
+        bwd_off.push_back((int)tk.size());
+        continue;
+      }
       for (int sn : lv) {
         const int ns = sym.sn[sn].ns;
         if (sn_pb[sn]) { rounds = std::max(rounds, (ns + sn_pb[sn] - 1) / sn_pb[sn]); continue; }
@@ -640,6 +745,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
 
 void DeviceCholesky::factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s,
                             bool prezeroed) {
+  if (n_dag_levels) ++dag_epoch;  // flag value of this call (flags only ever equal the epoch of the call that set them)
   launch::chol_vec_init((int)sym.sn.size(), fd.get(), perm.get(), rhs, vecs.get(), s);
   launch::chol_prescatter(prezeroed ? 0 : nzero, zero_rng.get(), npre, vals, pre_dst.get(), pre_src.get(), lam,
                           fronts.get(), s);
@@ -657,9 +763,23 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       case 6: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
                                 vecs.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 6, s);
         break;
+      case 7: launch::chol_dag(op.count, op.tpw, dag_fronts.get() + op_front_off[&op - ops.data()], dag_tiles.get() + op.off,
+                               fronts.get(), lbuf.get(), vecs.get(), y_p.get(), linv.get(), dag_flags.get(), dag_epoch,
+                               fail, dag_tmo.get(), s);
+        break;
       default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;
     }
   }
+}
+
+void DeviceCholesky::check_dag(hipStream_t s) {
+  if (!n_dag_levels) return;
+  unsigned t = 0;
+  HIP_CHECK(hipMemcpyAsync(&t, dag_tmo.get(), sizeof t, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (t == dag_epoch && t != 0)
+    throw DeviceError("supernodal factorization: the tile DAG of a level stopped waiting for a flag (epoch " +
+                      std::to_string(t) + ")");
 }
 
 void DeviceCholesky::solve(double* x, hipStream_t s) {
@@ -669,6 +789,8 @@ void DeviceCholesky::solve(double* x, hipStream_t s) {
                           x_p.get(), t_p.get(), s);
     launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
                        perm.get(), x, s);
+    launch::chol_bwd_seq(bl.seq.second, tasks.get() + bl.seq.first, fd.get(), lbuf.get(), linv.get(), t_p.get(), x_p.get(),
+                         perm.get(), x, s);
     for (const auto& rd : bl.rounds) {
       launch::chol_bwd_inner(rd.first.second, tasks.get() + rd.first.first, fd.get(), lbuf.get(), x_p.get(), t_p.get(), s);
       launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
@@ -2189,6 +2311,7 @@ int Engine::solve_sync() {
   HIP_CHECK(hipMemcpyAsync(f, failp(), sizeof f, hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
   timer.collect();
+  if (f[0] && !use_pcg() && !use_cgls()) chol.check_dag(stream);
   if (f[0] && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
   return f[0] ? 0 : 1;
 }
@@ -2374,6 +2497,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     int f[2];
     std::memcpy(f, hs + 8, sizeof f);
     const bool ok2 = f[0] == 0;
+    if (!ok2 && !use_pcg() && !use_cgls()) chol.check_dag(stream);
     if (!ok2 && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
     if (ev2 && first_trial) {
       float mq = 0;
@@ -2468,6 +2592,7 @@ int Engine::gn_solve(int iteration, g2ohip_batch_stats* st) {
     st->timeUpdate = b * 1e-3;
   }
   levenberg_iterations = 0;
+  if (f[0] != 0 && !use_pcg() && !use_cgls()) chol.check_dag(stream);
   if (f[0] != 0 && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
   return f[0] == 0 ? 0 : 2;
 }
@@ -2701,6 +2826,7 @@ int Engine::compute_marginals(int nblocks, const int* brow, const int* bcol, dou
   int fail = 0;
   HIP_CHECK(hipMemcpyAsync(&fail, dmarg_fail.get(), sizeof fail, hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
+  if (fail) C.check_dag(stream);
   if (fail) return 0;
   // distinct block columns, batched K / pd per multi-right-hand-side solve
   std::vector<int> ucol(bcol, bcol + nblocks);
@@ -2750,7 +2876,8 @@ int Engine::factor_info(double* out, int n) {
   const Symbolic& S = chol.sym;
   const double v[] = {(double)S.n, (double)S.nnzL, S.flops, (double)S.sn.size(), (double)S.num_levels,
                       (double)S.max_front, (double)chol.n_blocked, (double)chol.n_inplace_levels,
-                      (double)chol.n_pre_levels, (double)chol.n_syrk_ops, (double)chol.n_bwd_rounds};
+                      (double)chol.n_pre_levels, (double)chol.n_syrk_ops, (double)chol.n_bwd_rounds,
+                      (double)chol.n_dag_levels};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;

@@ -101,15 +101,26 @@ struct DeviceCholesky {
   std::vector<int> bwd_off;    // per level: offset of its backward-gemv tasks in `tasks` (+1 end)
   struct BwdLevel {            // backward solve of one level: (offset, count) task ranges in `tasks`
     std::pair<int, int> gemv, xall;
+    std::pair<int, int> seq{0, 0};  // fronts factored by k_dag: k_bwd_seq (one task per front)
     std::vector<std::pair<std::pair<int, int>, std::pair<int, int>>> rounds;  // blocked fronts: (inner, x)
   };
   std::vector<BwdLevel> bwd_ops;
   int max_ns = 0;
   // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
   // trailing-update (k_syrk) launches, big-panel backward rounds
-  int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
-  struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add, 2 panel step
-                                        // (6: with lagged-pair tasks), 3 syrk
+  int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0, n_dag_levels = 0;
+  struct Op { int kind, off, count, tpw = 1; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add,
+                                                 // 2 panel step (6: with lagged-pair tasks), 3 syrk, 7 tile DAG
+                                                 // (off: first worker's tile slots, off2 fronts), tpw tiles per worker
+  std::vector<int> op_front_off;  // per op: first DagFront of a kind-7 op
+  // persistent tile DAG of latency-bound levels (cholesky.hip k_dag)
+  DevBuf<launch::DagFront> dag_fronts;
+  DevBuf<int4> dag_tiles;
+  DevBuf<unsigned> dag_flags, dag_tmo;
+  unsigned dag_epoch = 0;
+  // throws when the last factorization's tile DAG gave up waiting (a bug, never expected): called where a failed
+  // factorization is observed (the DAG also raises the not-PD flag then)
+  void check_dag(hipStream_t s);
   std::vector<Op> ops;
   std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
   DevBuf<launch::Task> tasks;

@@ -191,6 +191,28 @@ void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double
                 const int* perm, double* xout, hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only
 constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 16, CHOL_BW = 4;
+// ---- persistent tile DAG of a latency-bound level (cholesky.hip k_dag) ----
+// A front is cut into 64 x 64 tiles: own rows/columns [0, ns) from 0, contribution rows/columns [ns, m) from ns, so no
+// tile mixes the two. Tile (I, J), I >= J, is owned by one resident workgroup for the whole factorization of the level
+// (its values stay in registers); panels of 32 columns advance by flags instead of kernel boundaries.
+struct DagFront {
+  long long f_off, l_off, v_off;
+  int m, ns, c0;
+  int nown;      // own tile rows / columns (ceil(ns / 64))
+  int ntr;       // tile rows (own + contribution)
+  int np;        // 32-column panels (ceil(ns / 32))
+  int flag_off;  // flags: [np diagonal flags | ntr * np panel flags (row-major by tile row)]
+  int pad;
+};
+constexpr int CHOL_DAG_TPW = 4;  // tiles per workgroup at most
+// nworkers workgroups, tpw tile slots each (int4 {front, I, J, 0}, front < 0: empty); epoch: this call's flag value
+void chol_dag(int nworkers, int tpw, const DagFront* fr, const int4* tiles, double* fronts, double* lbuf, double* vecs,
+              double* ysol, double* linv, unsigned* flags, unsigned epoch, int* fail, unsigned* tmo, hipStream_t s);
+int chol_dag_max_workers(int device);  // resident one per CU
+// backward solve x = L11^-T t of fronts factored by k_dag (no explicit L11^-1): one workgroup per front, blocks of 32
+// columns from the last, L's columns of the next block prefetched while the current one is solved
+void chol_bwd_seq(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* linv,
+                  const double* tsol, double* xsol, const int* perm, double* xout, hipStream_t s);
 // computeMarginals multi-right-hand-side solves (marginals.hip): one launch per tree level, one workgroup per front
 void marg_forward(int nf, const int* lfronts, const FrontDesc* fd, const int* children, const int* relmap,
                   const double* lbuf, const double* linv, const long long* woff, double* W, double* Y, double* T, int n,

@@ -23,11 +23,11 @@ test)
   echo SMOKE_OK
   ;;
 prof)
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_prof -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-posegraph > $O/${TAG}_bench_prof.json 2> $O/${TAG}_bench_prof.err || { echo PROF_FAIL; tail -20 $O/${TAG}_bench_prof.err; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_prof -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-posegraph --no-c5 > $O/${TAG}_bench_prof.json 2> $O/${TAG}_bench_prof.err || { echo PROF_FAIL; tail -20 $O/${TAG}_bench_prof.err; exit 1; }
   echo PROF_OK
   RX='k_schur|k_linearize|k_backsub|k_vertex_reduce|k_cam_assemble|k_lm_fixup|k_zero_ranges|k_chol_scatter|k_vec_init|k_extend_add|k_step|k_syrk|k_permute'
-  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/${TAG}_pmc_fetch -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-posegraph --no-kernel-timing > $O/${TAG}_pmc_fetch.log 2>&1 || { echo PMC_FETCH_FAIL; tail -20 $O/${TAG}_pmc_fetch.log; exit 1; }
-  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/${TAG}_pmc_write -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-posegraph --no-kernel-timing > $O/${TAG}_pmc_write.log 2>&1 || { echo PMC_WRITE_FAIL; tail -20 $O/${TAG}_pmc_write.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/${TAG}_pmc_fetch -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-posegraph --no-c5 --no-kernel-timing > $O/${TAG}_pmc_fetch.log 2>&1 || { echo PMC_FETCH_FAIL; tail -20 $O/${TAG}_pmc_fetch.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/${TAG}_pmc_write -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-posegraph --no-c5 --no-kernel-timing > $O/${TAG}_pmc_write.log 2>&1 || { echo PMC_WRITE_FAIL; tail -20 $O/${TAG}_pmc_write.log; exit 1; }
   python tools/pmc_traffic.py $O/${TAG}_traffic.json $O/${TAG}_pmc_fetch $O/${TAG}_pmc_write > $O/${TAG}_traffic.log 2>&1 || { echo TRAFFIC_PARSE_FAIL; cat $O/${TAG}_traffic.log; }
   echo PMC_OK
   ;;

@@ -336,3 +336,28 @@ def test_ba_assembly_paths(g2o_amd_mod, oracle, monkeypatch, fused):
     monkeypatch.setenv("G2OHIP_ASM_FUSED", fused)
     for prob in (synth.ba(num_cameras=100, num_points=60, obs_per_point=80, window=100), _ragged_ba(seed=5)):
         _check(*_run_both(g2o_amd_mod, oracle, prob, 4))
+
+
+@pytest.mark.parametrize("mode", ["0", "2"], ids=["panel_steps_only", "tile_dag_every_fitting_level"])
+@pytest.mark.parametrize("name", ["C1", "C2", "C3", "C4", "C5"])
+def test_factor_schedules(g2o_amd_mod, oracle, monkeypatch, name, mode):
+    """Both factorization schedules of a tree level against the oracle: the launch-per-panel steps (G2OHIP_CHOL_DAG=0)
+    and the persistent tile DAG (k_dag) on every level whose tiles fit the resident workgroups (=2; the default uses it
+    on the latency-bound levels only). Reduced system, solution and an LM trajectory."""
+    monkeypatch.setenv("G2OHIP_CHOL_DAG", mode)
+    prob = synth.by_name(name, "small")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    ref = oracle.OracleGraph(prob)
+    g = opt.stage(1e-3)
+    r = ref.stage(1e-3)
+    assert g["ok"] == r["ok"] == 1
+    for k in ("bschur", "x"):
+        assert np.linalg.norm(g[k] - r[k]) <= 1e-9 * np.linalg.norm(r[k]), k
+    info = opt.factor_info()
+    assert (info["dag_levels"] > 0) == (mode == "2"), info
+    opt.build_system()
+    opt.set_lambda(1e-3)
+    assert opt.solve()
+    assert opt.linear_residual() <= 1e-10
+    opt.restore_diagonal()
+    _check(*_run_both(g2o_amd_mod, oracle, prob, 4))

@@ -191,8 +191,10 @@ def test_load_without_final_newline_and_truncated(g2o_amd_mod, oracle, tmp_path)
 
 @pytest.mark.parametrize("name", ["C2", "C4"])
 def test_save_load_round_trip(g2o_amd_mod, tmp_path, name):
-    """The parallel writer after LM iterations: reloading its file gives the same state bit for bit (shortest
-    round-trip decimals) and the same chi2."""
+    """The parallel writer after LM iterations: reloading its file gives the same state and chi2. The decimals are
+    shortest round-trip, so every stored double reads back bit for bit; VERTEX_SE3:EXPMAP is written as the
+    camera-to-world pose (types_six_dof_expmap.cpp:93-101, the inverse of the estimate) and inverted again on load,
+    which leaves the cameras within a few ulps (SE2 poses: exact)."""
     prob = synth.by_name(name, "small")
     opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
     opt.optimize(2)
@@ -201,5 +203,10 @@ def test_save_load_round_trip(g2o_amd_mod, tmp_path, name):
     o2 = g2o_amd_mod.SparseOptimizer(0)
     o2.load(path)
     assert o2.num_vertices() == prob.num_vertices and o2.num_edges() == prob.num_edges
-    np.testing.assert_array_equal(o2.minimal_state(), opt.minimal_state())
-    assert o2.chi2() == opt.chi2()
+    x1, x2 = opt.minimal_state(), o2.minimal_state()
+    if name == "C2":
+        np.testing.assert_array_equal(x2, x1)
+        assert o2.chi2() == opt.chi2()
+    else:
+        assert np.abs(x2 - x1).max() <= 1e-14 * np.abs(x1).max()
+        assert abs(o2.chi2() - opt.chi2()) <= 1e-12 * opt.chi2()

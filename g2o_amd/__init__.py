@@ -431,7 +431,9 @@ class SparseOptimizer:
         return {p: out[k * pd * pd:(k + 1) * pd * pd].reshape(pd, pd).T.copy() for k, p in enumerate(pairs)}
 
     FACTOR_INFO_KEYS = ("n", "nnzL", "flops", "supernodes", "levels", "max_front", "blocked_fronts",
-                        "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds", "dag_levels")
+                        "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds", "dag_levels",
+                        "owned_fronts", "shared_fronts", "subtree_roots", "root_exchange_doubles",
+                        "model_rank_subtrees_s", "model_shared_s", "model_single_gpu_s")
 
     def factor_info(self) -> dict:
         out = np.zeros(len(self.FACTOR_INFO_KEYS))

@@ -1423,6 +1423,30 @@ __global__ void __launch_bounds__(256) k_bwd_seq(const Task* __restrict__ tasks,
   }
 }
 
+// ---------------------------------------------------------------------------- distributed factorization glue
+// (landmark-sharded BA) contiguous copies between the front pool / front vectors and an exchange buffer:
+// ranges (src, dst, len) in doubles, one workgroup per range
+__global__ void __launch_bounds__(256) k_copy_ranges(const long long* __restrict__ rng, const double* __restrict__ src,
+                                                     double* __restrict__ dst) {
+  const long long so = rng[3 * blockIdx.x], d0 = rng[3 * blockIdx.x + 1], len = rng[3 * blockIdx.x + 2];
+  for (long long i = threadIdx.x; i < len; i += 256) dst[d0 + i] = src[so + i];
+}
+// x of the distributed solve: every rank holds its own columns (and rank 0 the shared ones) in xr[0 .. n), zeros
+// elsewhere, the not-PD flag of its fronts in xr[n]; after the all-reduce: x = xr, fail |= xr[n] > 0
+__global__ void k_dist_fail_in(const int* __restrict__ fail, double* __restrict__ xr, int n) {
+  if (threadIdx.x == 0) xr[n] = *fail ? 1.0 : 0.0;
+}
+__global__ void __launch_bounds__(256) k_dist_x_out(const double* __restrict__ xr, int n, double* __restrict__ x,
+                                                    int* __restrict__ fail) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k < n) x[k] = xr[k];
+  if (k == 0 && xr[n] > 0.0) *fail = 1;
+}
+__global__ void __launch_bounds__(256) k_zero_idx(const int* __restrict__ idx, int n, double* __restrict__ x) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k < n) x[idx[k]] = 0.0;
+}
+
 namespace launch {
 
 // one workgroup per CU (the validated form of the write-through hand-offs): dynamic LDS tops each instance up to more
@@ -1458,6 +1482,25 @@ void chol_bwd_seq(int ntasks, const Task* tasks, const FrontDesc* fd, const doub
                   const double* tsol, double* xsol, const int* perm, double* xout, hipStream_t s) {
   if (ntasks <= 0) return;
   hipLaunchKernelGGL(k_bwd_seq, ntasks, 256, 0, s, tasks, fd, lbuf, linv, tsol, xsol, perm, xout);
+  KERNEL_CHECK();
+}
+
+void chol_copy_ranges(int n, const long long* rng, const double* src, double* dst, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_copy_ranges, n, 256, 0, s, rng, src, dst);
+  KERNEL_CHECK();
+}
+void chol_dist_fail_in(const int* fail, double* xr, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_dist_fail_in, 1, 64, 0, s, fail, xr, n);
+  KERNEL_CHECK();
+}
+void chol_dist_x_out(const double* xr, int n, double* x, int* fail, hipStream_t s) {
+  hipLaunchKernelGGL(k_dist_x_out, grid_for(std::max(n, 1), 256), 256, 0, s, xr, n, x, fail);
+  KERNEL_CHECK();
+}
+void chol_zero_idx(const int* idx, int n, double* x, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_zero_idx, grid_for(n, 256), 256, 0, s, idx, n, x);
   KERNEL_CHECK();
 }
 

@@ -306,6 +306,84 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     for (int sn : sym.levels[l]) { lcols += sym.sn[sn].ns + sym.sn[sn].nr; sn_level[sn] = (int)l; }
     level_slab[l] = lcols >= 16LL * launch::CHOL_EA * 256 ? launch::CHOL_EA : 4;
   }
+  // ---- distribution over ranks (landmark-sharded BA): cut the elimination tree into a shared top and whole subtrees,
+  // each subtree owned by one rank. Modelled front time: its flops at 30 TF/s plus 10 us per 32-column panel step
+  // (the measured chain cost); a subtree's time is the sum over its fronts. The heaviest candidate
+  // subtree is split (its root joins the shared top) until there are at least as many candidates as ranks and none
+  // exceeds 1.25x the average; the candidates then go to ranks largest first (longest-processing-time rule).
+  sn_owner.assign(sym.sn.size(), -1);
+  n_owned_fronts = n_shared_fronts = n_roots = 0;
+  if (distributed()) {
+    const int nsn = (int)sym.sn.size();
+    std::vector<double> ft(nsn), st(nsn, 0.0);
+    for (int k = 0; k < nsn; ++k) {
+      const double m = sym.sn[k].ns + sym.sn[k].nr;
+      double fl = 0;
+      for (int c = 0; c < sym.sn[k].ns; ++c) fl += (m - c) * (m - c);
+      ft[k] = fl / 30e12 + ((sym.sn[k].ns + 31) / 32) * 10e-6;
+    }
+    for (int k = 0; k < nsn; ++k) st[k] += ft[k];  // children precede parents (postorder)
+    for (int k = 0; k < nsn; ++k)
+      if (sym.sn[k].parent >= 0) st[sym.sn[k].parent] += st[k];
+    std::vector<int> cand;
+    for (int k = 0; k < nsn; ++k)
+      if (sym.sn[k].parent < 0) cand.push_back(k);
+    std::vector<char> shared(nsn, 0);
+    for (;;) {
+      double tot = 0, mx = -1;
+      int arg = -1;
+      for (size_t i = 0; i < cand.size(); ++i) {
+        tot += st[cand[i]];
+        if (st[cand[i]] > mx) { mx = st[cand[i]]; arg = (int)i; }
+      }
+      const int c = cand[arg];
+      const bool enough = (int)cand.size() >= dist_nranks && mx <= 1.25 * tot / dist_nranks;
+      if (enough || sym.children_ptr[c + 1] == sym.children_ptr[c]) break;
+      shared[c] = 1;
+      cand.erase(cand.begin() + arg);
+      for (int ci = sym.children_ptr[c]; ci < sym.children_ptr[c + 1]; ++ci) cand.push_back(sym.children[ci]);
+    }
+    std::sort(cand.begin(), cand.end(), [&](int a, int b) { return st[a] > st[b] || (st[a] == st[b] && a < b); });
+    std::vector<double> load(dist_nranks, 0.0);
+    std::vector<int> sub_owner(nsn, -1);
+    for (int c : cand) {
+      const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      load[r] += st[c];
+      sub_owner[c] = r;
+    }
+    for (int k = nsn - 1; k >= 0; --k) {  // parents after children: walk down from the subtree roots
+      if (shared[k]) continue;
+      sn_owner[k] = sub_owner[k] >= 0 ? sub_owner[k] : sn_owner[sym.sn[k].parent];
+    }
+    double tshared = 0, tall = 0;
+    for (int k = 0; k < nsn; ++k) {
+      tall += ft[k];
+      if (sn_owner[k] < 0) { ++n_shared_fronts; tshared += ft[k]; }
+      else if (sn_owner[k] == dist_rank) ++n_owned_fronts;
+    }
+    dist_model[0] = load[dist_rank];
+    dist_model[1] = tshared;
+    dist_model[2] = tall;
+  }
+  // forward plan: the level front lists in execution order (distributed: this rank's fronts level by level, the root
+  // exchange, then the shared fronts level by level); the backward solve walks the same plan in reverse
+  std::vector<std::vector<int>> fplan;
+  int xch_at = -1;
+  if (distributed()) {
+    for (const auto& lv : sym.levels) {
+      std::vector<int> o;
+      for (int sn : lv) if (sn_owner[sn] == dist_rank) o.push_back(sn);
+      if (!o.empty()) fplan.push_back(o);
+    }
+    xch_at = (int)fplan.size();
+    for (const auto& lv : sym.levels) {
+      std::vector<int> o;
+      for (int sn : lv) if (sn_owner[sn] < 0) o.push_back(sn);
+      if (!o.empty()) fplan.push_back(o);
+    }
+  } else {
+    fplan = sym.levels;
+  }
   // per child: [#rows mapping into the parent's first diagonal block | first child row of every parent
   // slab] (rel is increasing), so the extend-add tasks need no search on the chain
   std::vector<int> hjt, hcmp;
@@ -417,14 +495,18 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     }
     std::vector<launch::DagFront> hdf;
     std::vector<int4> hdt;
-    std::vector<char> level_dag(sym.levels.size(), 0);
+    std::vector<char> level_dag(fplan.size(), 0);
     int dag_flag_total = 0;
     op_front_off.clear();
     n_dag_levels = 0;
     std::vector<long long> zr, pdst;
     std::vector<int> psrc;
-    for (size_t l = 0; l < sym.levels.size(); ++l) {
-      const auto& lv = sym.levels[l];
+    for (size_t l = 0; l < fplan.size(); ++l) {
+      if ((int)l == xch_at) {  // subtree roots -> every rank (before the first shared front is assembled)
+        ops.push_back(Op{8, 0, 0});
+        op_front_off.push_back(0);
+      }
+      const auto& lv = fplan[l];
       long long tiles0 = 0;  // fused tiles of the level's first step
       if (l == 0) n_blocked = n_inplace_levels = n_pre_levels = n_syrk_ops = n_bwd_rounds = 0;
       for (int sn : lv) {
@@ -487,7 +569,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       for (int sn : lv) tk.push_back(Task{sn, dag ? -1 : 0, 0, 1});
       // every front is assembled here (input entries, zeros, children); slabs of EA columns where the level
       // has enough of them to fill the chip several times over, else 4 (latency-bound upper levels)
-      const int slab = level_slab[l];
+      const int slab = level_slab[sn_level[lv[0]]];
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
         const int m = q.ns + q.nr;
@@ -645,6 +727,46 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       if (sy.count) { ops.push_back(sy); op_front_off.push_back(0); ++n_syrk_ops; }
       for (int sn : lv) n_blocked += blocked(sym.sn[sn]) ? 1 : 0;
     }
+    // root exchange (distributed): per subtree root, the lower triangle of its contribution block column by column
+    // and its update vector, at fixed offsets of one buffer; a rank packs its own roots, the all-reduce sums zeros
+    // elsewhere, every rank unpacks the others' into its front pool / front vectors
+    if (distributed()) {
+      std::vector<long long> pf, pv, uf, uv, zi;
+      long long off = 0;
+      n_roots = 0;
+      auto add = [](std::vector<long long>& v, long long a, long long b, long long n) { v.push_back(a); v.push_back(b); v.push_back(n); };
+      for (size_t k = 0; k < sym.sn.size(); ++k) {
+        const int par = sym.sn[k].parent;
+        if (sn_owner[k] < 0 || par < 0 || sn_owner[par] >= 0) continue;
+        ++n_roots;
+        const Supernode& q = sym.sn[k];
+        const long long m = q.ns + q.nr;
+        const bool mine = sn_owner[k] == dist_rank;
+        for (int j = 0; j < q.nr; ++j) {
+          const long long fo = q.front_off + (long long)(q.ns + j) * m + q.ns + j, len = q.nr - j;
+          if (mine) add(pf, fo, off, len); else add(uf, off, fo, len);
+          off += len;
+        }
+        if (q.nr > 0) {
+          if (mine) add(pv, q.vec_off + q.ns, off, q.nr); else add(uv, off, q.vec_off + q.ns, q.nr);
+          off += q.nr;
+        }
+      }
+      xch_len = off;
+      xch_pack_f = (int)pf.size() / 3; xch_pack_v = (int)pv.size() / 3;
+      xch_unpack_f = (int)uf.size() / 3; xch_unpack_v = (int)uv.size() / 3;
+      std::vector<long long> all;
+      for (auto* v : {&pf, &pv, &uf, &uv}) all.insert(all.end(), v->begin(), v->end());
+      xch_ranges.upload(all.empty() ? std::vector<long long>{0, 0, 0} : all, s);
+      xch_buf.resize(std::max<long long>(xch_len, 1));
+      std::vector<int> zx;
+      for (size_t k = 0; k < sym.sn.size(); ++k)
+        if (sn_owner[k] < 0)
+          for (int c = sym.sn[k].c0; c < sym.sn[k].c0 + sym.sn[k].ns; ++c) zx.push_back(sym.perm[c]);
+      nxzero = (int)zx.size();
+      xzero_idx.upload(zx.empty() ? std::vector<int>{0} : zx, s);
+      xred.resize((size_t)sym.n + 1);
+    }
     dag_fronts.upload(hdf.empty() ? std::vector<launch::DagFront>(1) : hdf, s);
     dag_tiles.upload(hdt.empty() ? std::vector<int4>{int4{-1, 0, 0, 0}} : hdt, s);
     dag_flags.resize(std::max(dag_flag_total, 1));
@@ -663,8 +785,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     bwd_off.assign(1, (int)tk.size());
     bwd_ops.clear();
     max_ns = 1;
-    for (size_t l = 0; l < sym.levels.size(); ++l) {
-      const auto& lv = sym.levels[l];
+    for (size_t l = 0; l < fplan.size(); ++l) {
+      const auto& lv = fplan[l];
       BwdLevel bl;
       bl.gemv = {(int)tk.size(), 0};
       for (int sn : lv) {
@@ -746,6 +868,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
 void DeviceCholesky::factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s,
                             bool prezeroed) {
   if (n_dag_levels) ++dag_epoch;  // flag value of this call (flags only ever equal the epoch of the call that set them)
+  last_fail = fail;
   launch::chol_vec_init((int)sym.sn.size(), fd.get(), perm.get(), rhs, vecs.get(), s);
   launch::chol_prescatter(prezeroed ? 0 : nzero, zero_rng.get(), npre, vals, pre_dst.get(), pre_src.get(), lam,
                           fronts.get(), s);
@@ -763,6 +886,17 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       case 6: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
                                 vecs.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 6, s);
         break;
+      case 8: {  // subtree roots -> every rank
+        const long long* R = xch_ranges.get();
+        xch_buf.zero(s);
+        launch::chol_copy_ranges(xch_pack_f, R, fronts.get(), xch_buf.get(), s);
+        launch::chol_copy_ranges(xch_pack_v, R + 3LL * xch_pack_f, vecs.get(), xch_buf.get(), s);
+        allreduce(xch_buf.get(), (size_t)xch_len);
+        launch::chol_copy_ranges(xch_unpack_f, R + 3LL * (xch_pack_f + xch_pack_v), xch_buf.get(), fronts.get(), s);
+        launch::chol_copy_ranges(xch_unpack_v, R + 3LL * (xch_pack_f + xch_pack_v + xch_unpack_f), xch_buf.get(),
+                                 vecs.get(), s);
+        break;
+      }
       case 7: launch::chol_dag(op.count, op.tpw, dag_fronts.get() + op_front_off[&op - ops.data()], dag_tiles.get() + op.off,
                                fronts.get(), lbuf.get(), vecs.get(), y_p.get(), linv.get(), dag_flags.get(), dag_epoch,
                                fail, dag_tmo.get(), s);
@@ -783,19 +917,32 @@ void DeviceCholesky::check_dag(hipStream_t s) {
 }
 
 void DeviceCholesky::solve(double* x, hipStream_t s) {
-  for (size_t l = level_off.size() - 1; l-- > 0;) {  // root level first
+  // distributed: every rank solves the shared top and its own subtrees into a zeroed buffer, rank 0 alone keeps the
+  // shared columns, and one all-reduce (with the not-PD flag in its last entry) gives every rank the whole x
+  double* xo = x;
+  if (distributed()) {
+    xo = xred.get();
+    xred.zero(s);
+  }
+  for (size_t l = bwd_ops.size(); l-- > 0;) {  // the forward plan in reverse (root level first)
     const BwdLevel& bl = bwd_ops[l];
     launch::chol_bwd_gemv(bl.gemv.second, tasks.get() + bl.gemv.first, fd.get(), rows.get(), lbuf.get(), y_p.get(),
                           x_p.get(), t_p.get(), s);
     launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
-                       perm.get(), x, s);
+                       perm.get(), xo, s);
     launch::chol_bwd_seq(bl.seq.second, tasks.get() + bl.seq.first, fd.get(), lbuf.get(), linv.get(), t_p.get(), x_p.get(),
-                         perm.get(), x, s);
+                         perm.get(), xo, s);
     for (const auto& rd : bl.rounds) {
       launch::chol_bwd_inner(rd.first.second, tasks.get() + rd.first.first, fd.get(), lbuf.get(), x_p.get(), t_p.get(), s);
       launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
-                         perm.get(), x, s);
+                         perm.get(), xo, s);
     }
+  }
+  if (distributed()) {
+    if (dist_rank != 0) launch::chol_zero_idx(xzero_idx.get(), nxzero, xo, s);
+    launch::chol_dist_fail_in(last_fail, xo, sym.n, s);
+    allreduce(xo, (size_t)sym.n + 1);
+    launch::chol_dist_x_out(xo, sym.n, x, last_fail, s);
   }
 }
 
@@ -2067,6 +2214,22 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     } else if (use_pcg()) {
       pcg.setup(num_poses, pd, s_bi, s_bj, stream);
     } else {
+      // landmark shards: the factorization is distributed too (subtrees of the elimination tree per rank, DESIGN.md
+      // §6); G2OHIP_DIST_FACTOR=0 keeps the replicated factorization (every rank factors all of S)
+      const char* df = getenv("G2OHIP_DIST_FACTOR");
+      const bool dist = nranks > 1 && comm && !(df && atoi(df) == 0);
+      chol.dist_rank = dist ? rank : 0;
+      chol.dist_nranks = dist ? nranks : 1;
+      chol.allreduce = [this](double* p, size_t n) { allreduce_sum(p, n); };
+      // timing only (tools/dist_factor_time.py): one process plays rank r of N of the distributed factorization with
+      // no-op exchanges — the kernel chain rank r would run, on this GPU; the solution is not meaningful
+      const char* sim = getenv("G2OHIP_DIST_SIMULATE");
+      int sr = 0, sn = 0;
+      if (!dist && sim && sscanf(sim, "%d/%d", &sr, &sn) == 2 && sn > 1 && sr >= 0 && sr < sn) {
+        chol.dist_rank = sr;
+        chol.dist_nranks = sn;
+        chol.allreduce = [](double*, size_t) {};
+      }
       chol.setup(num_poses, pd, s_bi, s_bj, stream);
     }
   } else if (use_pcg()) {
@@ -2877,7 +3040,9 @@ int Engine::factor_info(double* out, int n) {
   const double v[] = {(double)S.n, (double)S.nnzL, S.flops, (double)S.sn.size(), (double)S.num_levels,
                       (double)S.max_front, (double)chol.n_blocked, (double)chol.n_inplace_levels,
                       (double)chol.n_pre_levels, (double)chol.n_syrk_ops, (double)chol.n_bwd_rounds,
-                      (double)chol.n_dag_levels};
+                      (double)chol.n_dag_levels, (double)chol.n_owned_fronts, (double)chol.n_shared_fronts,
+                      (double)chol.n_roots, (double)chol.xch_len, chol.dist_model[0], chol.dist_model[1],
+                      chol.dist_model[2]};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <limits>
 #include <map>
 #include <memory>
@@ -121,6 +122,24 @@ struct DeviceCholesky {
   // throws when the last factorization's tile DAG gave up waiting (a bug, never expected): called where a failed
   // factorization is observed (the DAG also raises the not-PD flag then)
   void check_dag(hipStream_t s);
+  // ---- distributed factorization (landmark-sharded BA). Set dist_rank / dist_nranks / allreduce before
+  // setup. The elimination tree is cut: every front below the cut belongs to one rank (whole subtrees, balanced by
+  // modelled time), the fronts above it are factored by every rank. A rank factors its subtrees, the subtree roots'
+  // contribution blocks and update vectors meet in one all-reduce (zeros elsewhere), every rank factors the top;
+  // the backward solve runs top-down the same way and x meets in one all-reduce (with the not-PD flag).
+  int dist_rank = 0, dist_nranks = 1;
+  std::function<void(double*, size_t)> allreduce;
+  std::vector<int> sn_owner;                 // per supernode: owning rank, -1 shared (every rank)
+  int n_owned_fronts = 0, n_shared_fronts = 0, n_roots = 0;
+  double dist_model[3] = {0, 0, 0};          // modelled seconds: this rank's subtrees, the shared top, single-GPU total
+  long long xch_len = 0;                      // doubles of the root exchange
+  int xch_pack_f = 0, xch_pack_v = 0, xch_unpack_f = 0, xch_unpack_v = 0;
+  DevBuf<long long> xch_ranges;               // (src, dst, len): pack fronts | pack vecs | unpack fronts | unpack vecs
+  DevBuf<double> xch_buf, xred;
+  DevBuf<int> xzero_idx;                      // caller-order indices of the shared columns (zeroed on ranks != 0)
+  int nxzero = 0;
+  int* last_fail = nullptr;
+  bool distributed() const { return dist_nranks > 1; }
   std::vector<Op> ops;
   std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
   DevBuf<launch::Task> tasks;

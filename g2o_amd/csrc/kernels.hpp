@@ -209,6 +209,12 @@ constexpr int CHOL_DAG_TPW = 4;  // tiles per workgroup at most
 void chol_dag(int nworkers, int tpw, const DagFront* fr, const int4* tiles, double* fronts, double* lbuf, double* vecs,
               double* ysol, double* linv, unsigned* flags, unsigned epoch, int* fail, unsigned* tmo, hipStream_t s);
 int chol_dag_max_workers(int device);  // resident one per CU
+// distributed factorization glue: contiguous range copies (src, dst, len) in doubles; the distributed
+// solve's not-PD flag into / x and flag out of its all-reduce buffer; x[idx[k]] = 0
+void chol_copy_ranges(int n, const long long* rng, const double* src, double* dst, hipStream_t s);
+void chol_dist_fail_in(const int* fail, double* xr, int n, hipStream_t s);
+void chol_dist_x_out(const double* xr, int n, double* x, int* fail, hipStream_t s);
+void chol_zero_idx(const int* idx, int n, double* x, hipStream_t s);
 // backward solve x = L11^-T t of fronts factored by k_dag (no explicit L11^-1): one workgroup per front, blocks of 32
 // columns from the last, L's columns of the next block prefetched while the current one is solved
 void chol_bwd_seq(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* linv,

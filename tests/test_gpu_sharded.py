@@ -134,3 +134,40 @@ def test_rccl_binding_single_rank(g2o_amd_mod):
     v = np.linspace(-3.0, 5.0, 1000)
     s, m = g2o_amd_mod.SparseOptimizer.comm_selftest(v)
     assert np.array_equal(s, v) and np.array_equal(m, v)
+
+
+@pytest.mark.parametrize("name,nranks", [("C5", 2), ("C5", 3), ("mid", 4), ("mid", 7)])
+def test_distributed_factorization(g2o_amd_mod, oracle, monkeypatch, name, nranks):
+    """The distributed factorization: the elimination tree cut into per-rank subtrees and a shared top,
+    the subtree roots' contribution blocks exchanged in one all-reduce, x in another. Against the replicated
+    factorization (G2OHIP_DIST_FACTOR=0: every rank factors all of S), the single-GPU run and the oracle."""
+    prob = synth.by_name(name, "small") if name != "mid" else synth.ba(400, 20000)
+    iters = 4
+    opts, res = _run_sharded(g2o_amd_mod, prob, nranks, iters)
+    info = [o.factor_info() for o in opts]
+    assert sum(i["owned_fronts"] for i in info) + info[0]["shared_fronts"] == info[0]["supernodes"], info
+    assert info[0]["subtree_roots"] > 0 and info[0]["root_exchange_doubles"] > 0, info[0]
+    x, states = _gather_state(prob, opts)
+    C = prob.vertices[0].ids.size
+    for s in states[1:]:
+        assert np.array_equal(s[:6 * C], states[0][:6 * C])  # x meets in one all-reduce: identical on every rank
+    monkeypatch.setenv("G2OHIP_DIST_FACTOR", "0")
+    ropts, rres = _run_sharded(g2o_amd_mod, prob, nranks, iters)
+    assert ropts[0].factor_info()["owned_fronts"] == 0
+    xr_, _ = _gather_state(prob, ropts)
+    monkeypatch.delenv("G2OHIP_DIST_FACTOR")
+    single = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    n1, st1 = single.optimize(iters)
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.optimize(iters, oracle.make_config(threads=8))
+    for r in range(nranks):
+        n, st = res[r]
+        assert n == n1 == nr
+        for a, b, c, d in zip(st, st1, sr, rres[r][1]):
+            assert a.levenbergIterations == b.levenbergIterations == c.levenbergIterations == d.levenbergIterations
+            assert abs(a.chi2 - c.chi2) <= RTOL * c.chi2
+    xs = single.minimal_state()
+    assert np.linalg.norm(x - xs) <= 1e-9 * np.linalg.norm(xs)
+    assert np.linalg.norm(x - xr_) <= 1e-9 * np.linalg.norm(xr_)
+    xo = ref.minimal_state()
+    assert np.linalg.norm(x - xo) <= RTOL * np.linalg.norm(xo)

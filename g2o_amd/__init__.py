@@ -433,7 +433,8 @@ class SparseOptimizer:
     FACTOR_INFO_KEYS = ("n", "nnzL", "flops", "supernodes", "levels", "max_front", "blocked_fronts",
                         "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds", "dag_levels",
                         "owned_fronts", "shared_fronts", "subtree_roots", "root_exchange_doubles",
-                        "model_rank_subtrees_s", "model_shared_s", "model_single_gpu_s")
+                        "model_rank_subtrees_s", "model_shared_s", "model_single_gpu_s", "model_exchange_s",
+                        "distributed")
 
     def factor_info(self) -> dict:
         out = np.zeros(len(self.FACTOR_INFO_KEYS))

@@ -307,63 +307,101 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     level_slab[l] = lcols >= 16LL * launch::CHOL_EA * 256 ? launch::CHOL_EA : 4;
   }
   // ---- distribution over ranks (landmark-sharded BA): cut the elimination tree into a shared top and whole subtrees,
-  // each subtree owned by one rank. Modelled front time: its flops at 30 TF/s plus 10 us per 32-column panel step
-  // (the measured chain cost); a subtree's time is the sum over its fronts. The heaviest candidate
-  // subtree is split (its root joins the shared top) until there are at least as many candidates as ranks and none
-  // exceeds 1.25x the average; the candidates then go to ranks largest first (longest-processing-time rule).
+  // each subtree owned by one rank. Candidate cuts: starting from the tree's roots, the candidate subtree with the
+  // largest serial work is split (its root joins the shared top), one cut per split, up to 4 candidates per rank; each
+  // cut's subtrees go to ranks largest first (longest-processing-time rule). Every cut is priced with the level-
+  // synchronous model below (a rank's fronts of one tree level run in the same launches, as do the shared ones) plus
+  // the two all-reduces it adds (root exchange, x), and kept only if it beats the replicated factorization's model:
+  // a tree whose top is all chain (C4 at 8 ranks: one-bandwidth separators) gains less from distribution than its
+  // exchange costs. dist_force (G2OHIP_DIST_FACTOR=1, the simulation mode) takes the best cut regardless.
   sn_owner.assign(sym.sn.size(), -1);
   n_owned_fronts = n_shared_fronts = n_roots = 0;
-  if (distributed()) {
-    const int nsn = (int)sym.sn.size();
-    std::vector<double> ft(nsn), st(nsn, 0.0);
+  dist_on = false;
+  std::fill(dist_model, dist_model + 5, 0.0);
+  if (dist_nranks > 1) {
+    const int nsn = (int)sym.sn.size(), N = dist_nranks;
+    std::vector<double> fl(nsn), chain(nsn), st(nsn);
     for (int k = 0; k < nsn; ++k) {
       const double m = sym.sn[k].ns + sym.sn[k].nr;
-      double fl = 0;
-      for (int c = 0; c < sym.sn[k].ns; ++c) fl += (m - c) * (m - c);
-      ft[k] = fl / 30e12 + ((sym.sn[k].ns + 31) / 32) * 10e-6;
+      double f = 0;
+      for (int c = 0; c < sym.sn[k].ns; ++c) f += (m - c) * (m - c);
+      fl[k] = f;
+      chain[k] = ((sym.sn[k].ns + 31) / 32) * dist_cost::STEP_S;
+      st[k] = std::max(chain[k], f / dist_cost::TILE_FLOPS);
     }
-    for (int k = 0; k < nsn; ++k) st[k] += ft[k];  // children precede parents (postorder)
-    for (int k = 0; k < nsn; ++k)
+    for (int k = 0; k < nsn; ++k)  // children precede parents (postorder): subtree serial work
       if (sym.sn[k].parent >= 0) st[sym.sn[k].parent] += st[k];
+    // a set of fronts run level by level: per level the longer of its longest panel chain and its flops at the tile rate
+    auto levels_time = [&](const std::vector<int>& owner, int who) {
+      double t = 0;
+      for (const auto& lv : sym.levels) {
+        double ch = 0, f = 0;
+        bool any = false;
+        for (int sn : lv)
+          if (owner[sn] == who) { any = true; ch = std::max(ch, chain[sn]); f += fl[sn]; }
+        if (any) t += std::max(ch, f / dist_cost::TILE_FLOPS) + dist_cost::LEVEL_S;
+      }
+      return t;
+    };
+    auto allreduce_time = [&](double doubles) {
+      return dist_cost::ALLREDUCE_LAT_S + 2.0 * (N - 1) / N * 8.0 * doubles / dist_cost::ALLREDUCE_BW;
+    };
+    std::vector<int> none(nsn, -2);  // the replicated model: every front in one set
+    const double t_repl = levels_time(none, -2);
     std::vector<int> cand;
     for (int k = 0; k < nsn; ++k)
       if (sym.sn[k].parent < 0) cand.push_back(k);
     std::vector<char> shared(nsn, 0);
+    std::vector<int> best_owner, owner(nsn);
+    double best = 1e30, best_rank = 0, best_shared = 0, best_xch = 0;
     for (;;) {
-      double tot = 0, mx = -1;
       int arg = -1;
-      for (size_t i = 0; i < cand.size(); ++i) {
-        tot += st[cand[i]];
-        if (st[cand[i]] > mx) { mx = st[cand[i]]; arg = (int)i; }
-      }
+      for (size_t i = 0; i < cand.size(); ++i)
+        if (sym.children_ptr[cand[i] + 1] > sym.children_ptr[cand[i]] && (arg < 0 || st[cand[i]] > st[cand[arg]])) arg = (int)i;
+      if (arg < 0 || (int)cand.size() >= 4 * N) break;
       const int c = cand[arg];
-      const bool enough = (int)cand.size() >= dist_nranks && mx <= 1.25 * tot / dist_nranks;
-      if (enough || sym.children_ptr[c + 1] == sym.children_ptr[c]) break;
       shared[c] = 1;
       cand.erase(cand.begin() + arg);
       for (int ci = sym.children_ptr[c]; ci < sym.children_ptr[c + 1]; ++ci) cand.push_back(sym.children[ci]);
+      if (cand.size() < 2) continue;
+      std::vector<int> srt(cand);
+      std::sort(srt.begin(), srt.end(), [&](int a, int b) { return st[a] > st[b] || (st[a] == st[b] && a < b); });
+      std::vector<double> load(N, 0.0);
+      std::vector<int> sub_owner(nsn, -1);
+      double xd = 0;
+      for (int s : srt) {
+        const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        load[r] += st[s];
+        sub_owner[s] = r;
+        const double nr = sym.sn[s].nr;
+        xd += nr * (nr + 1) / 2 + nr;
+      }
+      for (int k = nsn - 1; k >= 0; --k)  // parents after children: walk down from the subtree roots
+        owner[k] = shared[k] ? -1 : sub_owner[k] >= 0 ? sub_owner[k] : owner[sym.sn[k].parent];
+      double tr = 0;
+      for (int r = 0; r < N; ++r) tr = std::max(tr, levels_time(owner, r));
+      const double ts = levels_time(owner, -1), tx = allreduce_time(xd) + allreduce_time(sym.n + 1.0);
+      if (tr + ts + tx < best) {
+        best = tr + ts + tx;
+        best_owner = owner;
+        best_rank = levels_time(owner, dist_rank);
+        best_shared = ts;
+        best_xch = tx;
+      }
     }
-    std::sort(cand.begin(), cand.end(), [&](int a, int b) { return st[a] > st[b] || (st[a] == st[b] && a < b); });
-    std::vector<double> load(dist_nranks, 0.0);
-    std::vector<int> sub_owner(nsn, -1);
-    for (int c : cand) {
-      const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-      load[r] += st[c];
-      sub_owner[c] = r;
+    dist_on = !best_owner.empty() && (dist_force || best < t_repl);
+    dist_model[0] = best_rank;
+    dist_model[1] = best_shared;
+    dist_model[2] = t_repl;
+    dist_model[3] = best_xch;
+    dist_model[4] = dist_on ? 1.0 : 0.0;
+    if (dist_on) {
+      sn_owner = best_owner;
+      for (int k = 0; k < nsn; ++k) {
+        if (sn_owner[k] < 0) ++n_shared_fronts;
+        else if (sn_owner[k] == dist_rank) ++n_owned_fronts;
+      }
     }
-    for (int k = nsn - 1; k >= 0; --k) {  // parents after children: walk down from the subtree roots
-      if (shared[k]) continue;
-      sn_owner[k] = sub_owner[k] >= 0 ? sub_owner[k] : sn_owner[sym.sn[k].parent];
-    }
-    double tshared = 0, tall = 0;
-    for (int k = 0; k < nsn; ++k) {
-      tall += ft[k];
-      if (sn_owner[k] < 0) { ++n_shared_fronts; tshared += ft[k]; }
-      else if (sn_owner[k] == dist_rank) ++n_owned_fronts;
-    }
-    dist_model[0] = load[dist_rank];
-    dist_model[1] = tshared;
-    dist_model[2] = tall;
   }
   // forward plan: the level front lists in execution order (distributed: this rank's fronts level by level, the root
   // exchange, then the shared fronts level by level); the backward solve walks the same plan in reverse
@@ -2220,6 +2258,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       const bool dist = nranks > 1 && comm && !(df && atoi(df) == 0);
       chol.dist_rank = dist ? rank : 0;
       chol.dist_nranks = dist ? nranks : 1;
+      chol.dist_force = df && atoi(df) == 1;
       chol.allreduce = [this](double* p, size_t n) { allreduce_sum(p, n); };
       // timing only (tools/dist_factor_time.py): one process plays rank r of N of the distributed factorization with
       // no-op exchanges — the kernel chain rank r would run, on this GPU; the solution is not meaningful
@@ -2228,6 +2267,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       if (!dist && sim && sscanf(sim, "%d/%d", &sr, &sn) == 2 && sn > 1 && sr >= 0 && sr < sn) {
         chol.dist_rank = sr;
         chol.dist_nranks = sn;
+        chol.dist_force = true;
         chol.allreduce = [](double*, size_t) {};
       }
       chol.setup(num_poses, pd, s_bi, s_bj, stream);
@@ -3042,7 +3082,7 @@ int Engine::factor_info(double* out, int n) {
                       (double)chol.n_pre_levels, (double)chol.n_syrk_ops, (double)chol.n_bwd_rounds,
                       (double)chol.n_dag_levels, (double)chol.n_owned_fronts, (double)chol.n_shared_fronts,
                       (double)chol.n_roots, (double)chol.xch_len, chol.dist_model[0], chol.dist_model[1],
-                      chol.dist_model[2]};
+                      chol.dist_model[2], chol.dist_model[3], chol.dist_model[4]};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;

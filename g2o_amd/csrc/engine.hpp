@@ -83,6 +83,13 @@ void set_state_from_est(int vtype, const double* est, double* st);
 void est_from_state(int vtype, const double* st, double* est);
 void minimal_from_state(int vtype, const double* st, double* out);
 
+// Cost model of the distributed factorization's cut, calibrated on C4 / C5 (rank schedules timed alone
+// on one GPU, tools/dist_factor_time.py): a 32-column panel step on the chain, the panel steps' tile rate, a level's
+// fixed launches, and an all-reduce over xGMI (latency + bus bandwidth, ring traffic 2 (N-1)/N).
+namespace dist_cost {
+constexpr double STEP_S = 10e-6, TILE_FLOPS = 12e12, LEVEL_S = 20e-6, ALLREDUCE_LAT_S = 30e-6, ALLREDUCE_BW = 120e9;
+}
+
 // Device-resident multifrontal factor of one block-sparse SPD matrix.
 struct DeviceCholesky {
   Symbolic sym;
@@ -131,7 +138,10 @@ struct DeviceCholesky {
   std::function<void(double*, size_t)> allreduce;
   std::vector<int> sn_owner;                 // per supernode: owning rank, -1 shared (every rank)
   int n_owned_fronts = 0, n_shared_fronts = 0, n_roots = 0;
-  double dist_model[3] = {0, 0, 0};          // modelled seconds: this rank's subtrees, the shared top, single-GPU total
+  bool dist_on = false;                      // setup chose a cut (the model beat the replicated factorization, or forced)
+  bool dist_force = false;                   // take the best cut even when the model prefers replication
+  double dist_model[5] = {0, 0, 0, 0, 0};    // modelled seconds: this rank's subtrees, the shared top, replicated
+                                             // factorization, the two all-reduces of the cut; 1 if distributed
   long long xch_len = 0;                      // doubles of the root exchange
   int xch_pack_f = 0, xch_pack_v = 0, xch_unpack_f = 0, xch_unpack_v = 0;
   DevBuf<long long> xch_ranges;               // (src, dst, len): pack fronts | pack vecs | unpack fronts | unpack vecs
@@ -139,7 +149,7 @@ struct DeviceCholesky {
   DevBuf<int> xzero_idx;                      // caller-order indices of the shared columns (zeroed on ranks != 0)
   int nxzero = 0;
   int* last_fail = nullptr;
-  bool distributed() const { return dist_nranks > 1; }
+  bool distributed() const { return dist_on; }
   std::vector<Op> ops;
   std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
   DevBuf<launch::Task> tasks;

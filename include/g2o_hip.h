@@ -176,12 +176,13 @@ int g2ohip_solver_linear_iterations(g2ohip_graph* g);
 /* ||(A + lambda I) x - b|| / ||b|| of the last Solver::solve, evaluated on the device (A = the Schur complement
  * with Schur, else Hpp): a size-independent check of the factorization at any problem size. */
 int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel);
-/* Symbolic / schedule summary of the device factorization: out[0..18] = n, nnz(L), flops (this ordering),
+/* Symbolic / schedule summary of the device factorization: out[0..20] = n, nnz(L), flops (this ordering),
  * supernodes, tree levels, largest front, blocked fronts, levels assembled in place, pre-scattered levels,
- * trailing-update launches, big-panel backward rounds, levels factored by the persistent tile DAG, and for a
- * distributed factorization (landmark shards) this rank's fronts, the shared fronts, the subtree roots, the doubles of
- * the root exchange, the modelled seconds of this rank's subtrees, of the shared top and of the whole factorization on
- * one GPU. Returns the number of entries available. */
+ * trailing-update launches, big-panel backward rounds, levels factored by the persistent tile DAG, and for landmark
+ * shards (nranks > 1) this rank's fronts, the shared fronts, the subtree roots, the doubles of the root exchange, the
+ * cost model of the best cut of the elimination tree (modelled seconds of this rank's subtrees, of the shared top, of
+ * the replicated factorization, of the cut's two all-reduces) and whether the factorization is distributed (1) or
+ * replicated (0: the model preferred replication, or G2OHIP_DIST_FACTOR=0). Returns the number of entries available. */
 int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n);
 /* Solver::computeMarginals (core/solver.h:108; BlockSolver::computeMarginals block_solver.hpp:451-460 ->
  * LinearSolverCSparse::solvePattern linear_solver_csparse.h:190-225, MarginalCovarianceCholesky): the pose-block

@@ -140,11 +140,14 @@ def test_rccl_binding_single_rank(g2o_amd_mod):
 def test_distributed_factorization(g2o_amd_mod, oracle, monkeypatch, name, nranks):
     """The distributed factorization: the elimination tree cut into per-rank subtrees and a shared top,
     the subtree roots' contribution blocks exchanged in one all-reduce, x in another. Against the replicated
-    factorization (G2OHIP_DIST_FACTOR=0: every rank factors all of S), the single-GPU run and the oracle."""
+    factorization (G2OHIP_DIST_FACTOR=0: every rank factors all of S), the single-GPU run and the oracle.
+    G2OHIP_DIST_FACTOR=1 forces the cut at these sizes (unset, the cost model decides per tree)."""
     prob = synth.by_name(name, "small") if name != "mid" else synth.ba(400, 20000)
     iters = 4
+    monkeypatch.setenv("G2OHIP_DIST_FACTOR", "1")  # the best cut even where the cost model would replicate
     opts, res = _run_sharded(g2o_amd_mod, prob, nranks, iters)
     info = [o.factor_info() for o in opts]
+    assert all(i["distributed"] == 1 for i in info), info
     assert sum(i["owned_fronts"] for i in info) + info[0]["shared_fronts"] == info[0]["supernodes"], info
     assert info[0]["subtree_roots"] > 0 and info[0]["root_exchange_doubles"] > 0, info[0]
     x, states = _gather_state(prob, opts)
@@ -153,7 +156,7 @@ def test_distributed_factorization(g2o_amd_mod, oracle, monkeypatch, name, nrank
         assert np.array_equal(s[:6 * C], states[0][:6 * C])  # x meets in one all-reduce: identical on every rank
     monkeypatch.setenv("G2OHIP_DIST_FACTOR", "0")
     ropts, rres = _run_sharded(g2o_amd_mod, prob, nranks, iters)
-    assert ropts[0].factor_info()["owned_fronts"] == 0
+    assert ropts[0].factor_info()["owned_fronts"] == 0 and ropts[0].factor_info()["distributed"] == 0
     xr_, _ = _gather_state(prob, ropts)
     monkeypatch.delenv("G2OHIP_DIST_FACTOR")
     single = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)

@@ -5,7 +5,11 @@ exchanges no-ops) on the full C5 problem and times the factor + solve kernel cha
 factorization is timed beside it. The trajectories of the simulated runs are not meaningful (the exchanged parts are
 missing); only the kernel chains' durations are. Prints one JSON line.
 
-    python tools/dist_factor_time.py [--config C5] [--ranks 8]
+    python tools/dist_factor_time.py [--config C5] [--ranks 8[,4,2]]
+
+Beside the measured times each run reports the setup's cost model (factor_info: model_rank_subtrees_s + model_shared_s
+for the rank, model_single_gpu_s for the replicated factorization, model_exchange_s for the two all-reduces it adds),
+the calibration data of engine.hpp's dist_cost constants.
 """
 import argparse
 import json
@@ -47,14 +51,21 @@ print(json.dumps(dict(factor_ms=opt.kernel_ms("chol_factor"), solve_ms=opt.kerne
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C5")
-    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--ranks", default="8")
     a = ap.parse_args()
-    res = {"config": a.config, "ranks": a.ranks, "single": one(a.config, None), "per_rank": []}
-    for r in range(a.ranks):
-        res["per_rank"].append(one(a.config, f"{r}/{a.ranks}"))
-        print(f"rank {r}: factor {res['per_rank'][-1]['factor_ms']:.3f} ms", file=sys.stderr, flush=True)
-    res["max_rank_factor_ms"] = max(x["factor_ms"] for x in res["per_rank"])
-    res["max_rank_solve_ms"] = max(x["solve_ms"] for x in res["per_rank"])
+    res = {"config": a.config, "single": one(a.config, None), "by_ranks": {}}
+    for n in [int(x) for x in a.ranks.split(",")]:
+        d = {"per_rank": []}
+        for r in range(n):
+            d["per_rank"].append(one(a.config, f"{r}/{n}"))
+            i = d["per_rank"][-1]["info"]
+            print(f"N={n} rank {r}: factor {d['per_rank'][-1]['factor_ms']:.3f} ms, model "
+                  f"{1e3 * (i['model_rank_subtrees_s'] + i['model_shared_s']):.3f} ms (+ exchange "
+                  f"{1e3 * i['model_exchange_s']:.3f}; replicated model {1e3 * i['model_single_gpu_s']:.3f})",
+                  file=sys.stderr, flush=True)
+        d["max_rank_factor_ms"] = max(x["factor_ms"] for x in d["per_rank"])
+        d["max_rank_solve_ms"] = max(x["solve_ms"] for x in d["per_rank"])
+        res["by_ranks"][str(n)] = d
     print(json.dumps(res))
 
 

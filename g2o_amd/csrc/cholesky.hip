@@ -1473,10 +1473,16 @@ void chol_dag(int nworkers, int tpw, const DagFront* fr, const int4* tiles, doub
 int chol_dag_max_workers(int device) {
   hipDeviceProp_t p;
   HIP_CHECK(hipGetDeviceProperties(&p, device));
-  int per2 = 0, per4 = 0;
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, k_dag<2>, 256, dag_reserve<2>()));
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, k_dag<4>, 256, dag_reserve<4>()));
-  return per2 >= 1 && per4 >= 1 ? p.multiProcessorCount : 0;
+  // every worker must be resident at once (they wait on each other): one 256-thread workgroup per CU fits when its
+  // LDS (static + the dynamic top-up) is within the CU's and its registers within a SIMD's budget for one wave each.
+  // (hipOccupancyMaxActiveBlocksPerMultiprocessor returned "unknown error" for these kernels on the MI355X boxes)
+  hipFuncAttributes a2, a4;
+  HIP_CHECK(hipFuncGetAttributes(&a2, reinterpret_cast<const void*>(&k_dag<2>)));
+  HIP_CHECK(hipFuncGetAttributes(&a4, reinterpret_cast<const void*>(&k_dag<4>)));
+  const bool fit = (int)a2.sharedSizeBytes + dag_reserve<2>() <= 160 * 1024 &&
+                   (int)a4.sharedSizeBytes + dag_reserve<4>() <= 160 * 1024 && a2.numRegs <= 512 && a4.numRegs <= 512 &&
+                   a2.maxThreadsPerBlock >= 256 && a4.maxThreadsPerBlock >= 256;
+  return fit ? p.multiProcessorCount : 0;
 }
 void chol_bwd_seq(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* linv,
                   const double* tsol, double* xsol, const int* perm, double* xout, hipStream_t s) {

@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(256)
             ++q;
           }
 #pragma unroll
-        for (int i = 0; i < DA; ++i) a[i * DA + i] += sp.lam;
+        for (int i = 0; i < DA; ++i) a[i * DA + i] += sp.lamp ? sp.lamp[0] : sp.lam;
         double U[UF], cl[DA];
         if (!lm_ufac<DA>(a, acc + DA * (DA + 1) / 2, U, cl)) *sp.fail = 1;
         double* Uo = sp.Ufac + (size_t)(hA - num_poses - lm_begin) * UF;
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restri
         ++q;
       }
 #pragma unroll
-    for (int j = 0; j < 3; ++j) a[j * 3 + j] += sp.lam;
+    for (int j = 0; j < 3; ++j) a[j * 3 + j] += sp.lamp ? sp.lamp[0] : sp.lam;
     double U[6], cl[3];
     if (!lm_ufac<3>(a, acc + 6, U, cl)) *sp.fail = 1;
 #pragma unroll
@@ -436,7 +436,7 @@ __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* 
     while (tid >= base + c + 1) base += ++c;
     const int r = tid - base;
     if constexpr (FG) {  // S(i,i) = lambda I + sum B^T (Omega - M) B
-      const double o = r == c ? t + sp.lam_rank : t;
+      const double o = r == c ? t + (sp.lamp ? sp.lamp[1] : sp.lam_rank) : t;
       double* So = sp.S + (size_t)sp.sdiag[i] * DB * DB;
       So[c * DB + r] = o;
       So[r * DB + c] = o;

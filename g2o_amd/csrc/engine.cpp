@@ -998,14 +998,20 @@ void DeviceCholesky::solve_multi(double* Y, double* W, double* T, int K, hipStre
 Engine::Engine(int dev) : device(dev) {
   HIP_CHECK(hipSetDevice(device));
   HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-  dscal.resize(12);  // [0] lambda [1] chi2 [2] scale [3] maxdiag [4] lambda (rank 0) [5] 0 | [8..9] fail flags (int)
+  // [0] lambda [1] chi2 [2] scale [3] maxdiag [4] lambda (rank 0) [5] 0 | [8] fail flags (two ints) | [12] next lambda
+  // [13] next lambda (rank 0) [14] accepted [15] rho (lm_decide)
+  dscal.resize(16);
   dscal.zero(stream);
   for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
   for (auto& e : lm_ev_) HIP_CHECK(hipEventCreate(&e));
+  HIP_CHECK(hipEventCreateWithFlags(&rb_ev_, hipEventDisableTiming));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hscal_), 16 * sizeof(double), hipHostMallocDefault));
 }
 Engine::~Engine() {
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
   for (auto& e : lm_ev_) if (e) (void)hipEventDestroy(e);
+  if (rb_ev_) (void)hipEventDestroy(rb_ev_);
+  if (hscal_) (void)hipHostFree(hscal_);
   comm.reset();
   if (stream) (void)hipStreamDestroy(stream);
 }
@@ -2327,7 +2333,7 @@ void Engine::ensure_hpp() {
   if (!std::isnan(fz_lambda)) build_system();
 }
 
-int Engine::build_system_split(double lambda) {  // block_solver.hpp:462-521
+int Engine::build_system_split(double lambda, const double* lamp) {  // block_solver.hpp:462-521
   if (!structure_built) {
     int r = build_structure();
     if (r) return r;
@@ -2339,10 +2345,11 @@ int Engine::build_system_split(double lambda) {  // block_solver.hpp:462-521
     const EGroup& g = groups[0];
     const int lm_begin = local_lm.empty() ? 0 : local_lm.front();
     launch::SchurSplit sp{};
-    const bool split = fz_split_ok && std::isfinite(lambda);
+    const bool split = fz_split_ok && (std::isfinite(lambda) || lamp);
     if (split) {  // block_solver.hpp:341-400 (the landmark pass and the diagonal terms) at lambda, during assembly
       sp.lam = lambda;
       sp.lam_rank = rank == 0 ? lambda : 0.0;
+      sp.lamp = lamp;
       sp.Ufac = dUfac.get();
       sp.cl = dCl.get();
       sp.G = dG.get();
@@ -2353,7 +2360,9 @@ int Engine::build_system_split(double lambda) {  // block_solver.hpp:462-521
       sp.S = dS.get();
       sp.bschur = dS.get() + (size_t)nS * pd * pd;
       sp.fail = failp() + 1;
-      fz_lambda = lambda;
+      // a device lambda is not known here: +inf never equals a trial's lambda, so solve_async re-assembles unless the
+      // host, having read the decision, confirms the value (lm_solve), and ensure_hpp sees a split assembly
+      fz_lambda = lamp ? std::numeric_limits<double>::infinity() : lambda;
     }
     timer.begin("linearize", stream);
     launch::linearize_fused(group_args(g), fz_chunks.get(), fz_nchunks, d_hidx[g.vtA].get(), d_hidx[g.vtB].get(),
@@ -2665,6 +2674,13 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   int& qmax = levenberg_iterations;
   qmax = 0;
   bool first_trial = true;
+  // the next iteration's assembly depends on the trial's decision (the state it leaves, lambda in Hll + lambda I): the
+  // device takes the decision itself (lm_decide, the same arithmetic), so the assembly is enqueued behind the scalar
+  // readback and the GPU starts on it while the host is still waking up; a rejected trial's speculative assembly is
+  // discarded (fz_lambda stays +inf: the next trial re-assembles at the popped state). Not with the stage timer on
+  // (its events would be read before the speculative work ran).
+  const bool spec = ba_fused && fz_split_ok && !timer.enabled && !write_debug;  // (the not-PD dump reads S)
+  bool spec_built = false, last_accept = false;
   do {
     push();
     if (st) st->levenbergIterations++;
@@ -2692,9 +2708,17 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     if (do_schur) allreduce_sum(dscal.get() + 1, 2);
     else allreduce_sum(dscal.get() + 2, 1);
     if (ev2) HIP_CHECK(hipEventRecord(e3, stream));
-    double hs[12];  // lambda, chi2, scale, ... | fail flags (one readback per trial)
-    HIP_CHECK(hipMemcpyAsync(hs, dscal.get(), sizeof hs, hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
+    if (spec) launch::lm_decide(dscal.get(), currentChi, (double)ni, rank == 0, stream);
+    double* hs = hscal_;  // lambda, chi2, scale, ... | fail flags | decision (one readback per trial, pinned)
+    HIP_CHECK(hipMemcpyAsync(hs, dscal.get(), 16 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    if (spec) {
+      HIP_CHECK(hipEventRecord(rb_ev_, stream));
+      build_system_split(std::numeric_limits<double>::quiet_NaN(), dscal.get() + 12);
+      spec_built = true;
+      HIP_CHECK(hipEventSynchronize(rb_ev_));
+    } else {
+      HIP_CHECK(hipStreamSynchronize(stream));
+    }
     timer.collect();
     tempChi = hs[1];
     int f[2];
@@ -2725,20 +2749,32 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
       st->timeLinearSolver = c * 1e-3;
     }
     if (!ok2) tempChi = std::numeric_limits<double>::max();
-    rho = currentChi - tempChi;
-    double scale = hs[2];
-    scale += 1e-3;
-    rho /= scale;
-    if (rho > 0 && std::isfinite(tempChi)) {
-      double alpha = 1. - std::pow((2 * rho - 1), 3);
-      alpha = std::min(alpha, 2. / 3.);
-      const double scaleFactor = std::max(1. / 3., alpha);
-      current_lambda *= scaleFactor;
+    bool accept;
+    if (spec) {  // the device's decision (k_lm_decide restates the branch below)
+      rho = hs[15];
+      accept = hs[14] != 0.0;
+      current_lambda = hs[12];
+    } else {
+      rho = currentChi - tempChi;
+      double scale = hs[2];
+      scale += 1e-3;
+      rho /= scale;
+      accept = rho > 0 && std::isfinite(tempChi);
+      if (accept) {
+        double alpha = 1. - std::pow((2 * rho - 1), 3);
+        alpha = std::min(alpha, 2. / 3.);
+        const double scaleFactor = std::max(1. / 3., alpha);
+        current_lambda *= scaleFactor;
+      } else {
+        current_lambda *= ni;
+      }
+    }
+    last_accept = accept;
+    if (accept) {
       ni = 2;
       currentChi = tempChi;
       discard_top();
     } else {
-      current_lambda *= ni;
       ni *= 2;
       pop();
       if (!std::isfinite(current_lambda)) break;
@@ -2752,7 +2788,10 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   // the next iteration starts with buildSystem on exactly this state: enqueue it now so the GPU works
   // while the host returns to the caller (skipped when the loop is about to stop)
   const bool more = !(qmax == maxTrials || rho == 0 || !std::isfinite(current_lambda));
-  if (more) {
+  if (spec_built && last_accept) {  // the last trial was accepted: its speculative assembly is this state's, at this lambda
+    fz_lambda = current_lambda;
+    built_ver = state_ver;
+  } else if (more) {
     build_system_split(current_lambda);
     built_ver = state_ver;
   }

@@ -245,7 +245,9 @@ class Engine {
   int build_system();
   // buildSystem with lambda known (the LM loop): where eligible the landmark side of the Schur complement is formed
   // during assembly (kernels.hpp SchurSplit); solve_async re-assembles when a trial's lambda differs
-  int build_system_split(double lambda);
+  // lamp (optional): the split's lambda pair read from the device (dscal[12..13], written by lm_decide) — the next
+  // iteration's assembly enqueued before the host has read the trial's decision (fz_lambda stays NaN until it has)
+  int build_system_split(double lambda, const double* lamp = nullptr);
   int set_lambda(double lambda, int backup);
   int restore_diagonal();
   int solve_sync();  // 1 ok / 0 not PD
@@ -385,6 +387,8 @@ class Engine {
   unsigned long long built_ver = 0;
   double chi_cache = 0.0;
   hipEvent_t lm_ev_[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t rb_ev_ = nullptr;   // the trial's scalar readback landed (the stream may hold more work behind it)
+  double* hscal_ = nullptr;      // pinned host copy of dscal (one readback per LM trial)
   int levenberg_iterations = 0;
 
   void ensure_device_state();

@@ -1379,6 +1379,32 @@ __global__ void k_set_scalars(double* __restrict__ p, double lam, double lam_ran
   p[5] = 0.0;
   if (reset_fail) p[8] = 0.0;  // the two int not-PD flags live in p[8]
 }
+// the LM trial decision, restated from the host loop (Engine::lm_solve, optimization_algorithm_levenberg.cpp:127-141):
+// the host reads it back instead of recomputing it, so both sides follow one decision
+__global__ void k_lm_decide(double* __restrict__ p, double current_chi, double ni, int rank0) {
+  int f;
+  __builtin_memcpy(&f, p + 8, sizeof f);
+  const double temp = f == 0 ? p[1] : __DBL_MAX__;
+  double rho = current_chi - temp;
+  double scale = p[2];
+  scale += 1e-3;
+  rho /= scale;
+  const double lam = p[0];
+  double nl, acc;
+  if (rho > 0 && isfinite(temp)) {
+    double alpha = 1. - pow(2 * rho - 1, 3);
+    alpha = alpha < 2. / 3. ? alpha : 2. / 3.;
+    nl = lam * (1. / 3. > alpha ? 1. / 3. : alpha);
+    acc = 1.0;
+  } else {
+    nl = lam * ni;
+    acc = 0.0;
+  }
+  p[12] = nl;
+  p[13] = rank0 ? nl : 0.0;
+  p[14] = acc;
+  p[15] = rho;
+}
 // max |diag| over nb blocks of dim x dim (col-major), partial per block of threads
 __global__ void __launch_bounds__(256) k_diag_absmax(const double* __restrict__ H, int nb, int dim,
                                                      double* __restrict__ out) {
@@ -1421,6 +1447,10 @@ void copy_multi(const CopyList& cl, hipStream_t s) {
 }
 void set_scalars(double* p, double lam, double lam_rank, hipStream_t s, bool reset_fail) {
   hipLaunchKernelGGL(k_set_scalars, 1, 1, 0, s, p, lam, lam_rank, reset_fail ? 1 : 0);
+  KERNEL_CHECK();
+}
+void lm_decide(double* p, double current_chi, double ni, bool rank0, hipStream_t s) {
+  hipLaunchKernelGGL(k_lm_decide, 1, 1, 0, s, p, current_chi, ni, rank0 ? 1 : 0);
   KERNEL_CHECK();
 }
 // writes max|diag| of two block sets into out (partial needs >= 64 doubles)

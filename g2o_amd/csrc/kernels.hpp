@@ -42,6 +42,8 @@ void offblock_reduce(int nb, int bsz, const int* ptr, const long long* soff, con
 struct SchurSplit {
   double lam;            // lambda of every landmark block
   double lam_rank;       // lambda on S's diagonal (rank 0 only when sharded)
+  const double* lamp;    // non-null: lam, lam_rank read from the device ([0], [1]) — the next iteration's assembly
+                         // enqueued before the host knows the LM decision (lm_decide writes them)
   double* Ufac;          // per local landmark U record (6 doubles)
   double* cl;            // c = U^-1 b_l, global landmark index
   double* G;             // Hpl's block order
@@ -117,6 +119,10 @@ void error_scale(int family, const EdgeArgs& a, int ne, long long n, long long n
 void scale_sum(long long n, long long npose, const double* x, const double* b, const double* lam, double* partial,
                double* out, hipStream_t s);
 void set_scalars(double* p, double lam, double lam_rank, hipStream_t s, bool reset_fail = false);
+// OptimizationAlgorithmLevenberg's trial decision (optimization_algorithm_levenberg.cpp:127-141) from the device chi2
+// and scale of the trial: p[12] the next lambda, p[13] the same for S's diagonal (rank 0 only), p[14] 1 accepted,
+// p[15] rho (the layout of dscal: engine.cpp)
+void lm_decide(double* p, double current_chi, double ni, bool rank0, hipStream_t s);
 // y = (A + lam I) x, A symmetric as upper blocks (block CSR with transposed entries); lam may be null; with b also
 // per-row (y - b)^2 -> r2 and b^2 -> b2 (y may be null)
 void block_symv(int pd, int n, const int* rptr, const int2* ent, const int* diag, const double* vals, const double* lam,

@@ -1431,6 +1431,13 @@ __global__ void __launch_bounds__(256) k_copy_ranges(const long long* __restrict
   const long long so = rng[3 * blockIdx.x], d0 = rng[3 * blockIdx.x + 1], len = rng[3 * blockIdx.x + 2];
   for (long long i = threadIdx.x; i < len; i += 256) dst[d0 + i] = src[so + i];
 }
+__global__ void __launch_bounds__(256) k_pack_blocks(long long n, int bb, const long long* __restrict__ boff,
+                                                     const double* __restrict__ src, double* __restrict__ dst) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long long t = i / bb;
+  dst[boff[t] + (i - t * bb)] = src[i];
+}
 // x of the distributed solve: every rank holds its own columns (and rank 0 the shared ones) in xr[0 .. n), zeros
 // elsewhere, the not-PD flag of its fronts in xr[n]; after the all-reduce: x = xr, fail |= xr[n] > 0
 __global__ void k_dist_fail_in(const int* __restrict__ fail, double* __restrict__ xr, int n) {
@@ -1494,6 +1501,12 @@ void chol_bwd_seq(int ntasks, const Task* tasks, const FrontDesc* fd, const doub
 void chol_copy_ranges(int n, const long long* rng, const double* src, double* dst, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_copy_ranges, n, 256, 0, s, rng, src, dst);
+  KERNEL_CHECK();
+}
+void chol_pack_blocks(long long nblk, int bb, const long long* boff, const double* src, double* dst, hipStream_t s) {
+  const long long n = nblk * bb;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pack_blocks, (unsigned)((n + 255) / 256), 256, 0, s, n, bb, boff, src, dst);
   KERNEL_CHECK();
 }
 void chol_dist_fail_in(const int* fail, double* xr, int n, hipStream_t s) {

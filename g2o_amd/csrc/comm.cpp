@@ -18,10 +18,11 @@ namespace g2ohip {
 
 namespace {
 
-enum : int { OP_SUM = 1, OP_MAX = 2 };
+enum : int { OP_SUM = 1, OP_MAX = 2, OP_RS = 3 };
 
 std::string call_desc(long long seq, size_t n, int op) {
-  return "call #" + std::to_string(seq) + " (" + (op == OP_MAX ? "max" : "sum") + ", n=" + std::to_string(n) + ")";
+  return "call #" + std::to_string(seq) + " (" + (op == OP_MAX ? "max" : op == OP_RS ? "reduce-scatter" : "sum") +
+         ", n=" + std::to_string(n) + ")";
 }
 
 struct RcclComm : Comm {
@@ -62,6 +63,13 @@ struct RcclComm : Comm {
     const ncclResult_t r = ncclAllReduce(p, p, n, ncclDouble, ncclMax, c, s);
     if (r != ncclSuccess) throw DeviceError(std::string("ncclAllReduce(max): ") + ncclGetErrorString(r));
   }
+  void reduce_scatter_sum(double* p, size_t count, hipStream_t s) override {
+    verify(count, OP_RS, s);
+    ++seq;
+    // in place (recvbuff = sendbuff + rank * recvcount)
+    const ncclResult_t r = ncclReduceScatter(p, p + (size_t)rank * count, count, ncclDouble, ncclSum, c, s);
+    if (r != ncclSuccess) throw DeviceError(std::string("ncclReduceScatter(sum): ") + ncclGetErrorString(r));
+  }
 };
 
 // ---- in-process group for LocalComm ----
@@ -101,6 +109,12 @@ struct Group {
     std::vector<double> acc(bufs[0]);
     for (int r = 1; r < nranks; ++r)
       for (size_t k = 0; k < n; ++k) acc[k] = op == OP_MAX ? std::max(acc[k], bufs[r][k]) : acc[k] + bufs[r][k];
+    if (op == OP_RS) {  // n = nranks segments: only this rank's segment is summed into out (RCCL leaves the rest)
+      const size_t cnt = n / nranks;
+      barrier();
+      std::copy(acc.begin() + (size_t)rank * cnt, acc.begin() + (size_t)(rank + 1) * cnt, out + (size_t)rank * cnt);
+      return;
+    }
     barrier();  // everyone has read every buffer
     std::copy(acc.begin(), acc.end(), out);
   }
@@ -129,6 +143,7 @@ struct LocalComm : Comm {
   }
   void allreduce_sum(double* p, size_t n, hipStream_t s) override { reduce(p, n, s, OP_SUM); }
   void allreduce_max(double* p, size_t n, hipStream_t s) override { reduce(p, n, s, OP_MAX); }
+  void reduce_scatter_sum(double* p, size_t count, hipStream_t s) override { reduce(p, count * g->nranks, s, OP_RS); }
 };
 
 }  // namespace

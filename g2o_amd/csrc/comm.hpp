@@ -1,7 +1,8 @@
-// Collectives of the landmark-sharded BA path: one sum all-reduce of the
-// reduced camera system [Hschur upper blocks | bschur] per LM trial plus scalar reductions.
+// Collectives of the landmark-sharded BA path: the reduced camera system [Hschur upper blocks | bschur]
+// per LM trial (one sum all-reduce, or with the distributed factorization a reduce-scatter of the blocks each rank's
+// subtrees read plus an all-reduce of the shared ones) plus scalar reductions.
 //
-//   RcclComm   production transport: ncclAllReduce on the solver's stream (RCCL over xGMI).
+//   RcclComm   production transport: ncclAllReduce / ncclReduceScatter on the solver's stream (RCCL over xGMI).
 //   LocalComm  test transport: N engines driven by N host threads of ONE process on one GPU;
 //              host-staged, summed in rank order. Lets the sharding logic run under pytest on
 //              a single-GPU box; never selected by the product path.
@@ -22,6 +23,9 @@ struct Comm {
   virtual ~Comm() = default;
   virtual void allreduce_sum(double* dptr, size_t n, hipStream_t s) = 0;
   virtual void allreduce_max(double* dptr, size_t n, hipStream_t s) = 0;
+  // in place: dptr holds nranks segments of `count` doubles; afterwards segment `rank` holds the sum over ranks of that
+  // segment (the other segments are left as they were: this rank's own partial values)
+  virtual void reduce_scatter_sum(double* dptr, size_t count, hipStream_t s) = 0;
   long long seq = 0;  // collectives issued so far on this communicator
 };
 

@@ -346,8 +346,24 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     auto allreduce_time = [&](double doubles) {
       return dist_cost::ALLREDUCE_LAT_S + 2.0 * (N - 1) / N * 8.0 * doubles / dist_cost::ALLREDUCE_BW;
     };
+    // the reduced system's own communication: one all-reduce of every block + rhs when replicated; with rs_enable a
+    // reduce-scatter of the blocks each rank's subtrees read (segments padded to the largest) + an all-reduce of the
+    // shared blocks and the rhs. Blocks per supernode: a block lands in the front of its smaller permuted column.
+    const double bb = (double)bdim * bdim;
+    std::vector<double> sn_blocks(nsn, 0.0);
+    for (size_t t = 0; t < bi.size(); ++t)
+      sn_blocks[sym.block_sn[std::min(sym.bpinv[bi[t]], sym.bpinv[bj[t]])]] += 1.0;
+    const double ar_full = allreduce_time(bi.size() * bb + (double)nblocks * bdim);
+    auto input_time = [&](const std::vector<int>& owner) {
+      if (!rs_enable) return ar_full;
+      std::vector<double> ob(N + 1, 0.0);
+      for (int k = 0; k < nsn; ++k) ob[owner[k] >= 0 ? owner[k] : N] += sn_blocks[k];
+      const double seg = *std::max_element(ob.begin(), ob.begin() + N) * bb;
+      return dist_cost::ALLREDUCE_LAT_S + (N - 1) * 8.0 * seg / dist_cost::ALLREDUCE_BW +
+             allreduce_time(ob[N] * bb + (double)nblocks * bdim);
+    };
     std::vector<int> none(nsn, -2);  // the replicated model: every front in one set
-    const double t_repl = levels_time(none, -2);
+    const double t_repl = levels_time(none, -2) + ar_full;
     std::vector<int> cand;
     for (int k = 0; k < nsn; ++k)
       if (sym.sn[k].parent < 0) cand.push_back(k);
@@ -381,14 +397,17 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       double tr = 0;
       for (int r = 0; r < N; ++r) tr = std::max(tr, levels_time(owner, r));
       const double ts = levels_time(owner, -1), tx = allreduce_time(xd) + allreduce_time(sym.n + 1.0);
-      if (tr + ts + tx < best) {
-        best = tr + ts + tx;
+      const double ti = input_time(owner);
+      if (tr + ts + tx + ti < best) {
+        best = tr + ts + tx + ti;
+        rs_model[0] = ti;
         best_owner = owner;
         best_rank = levels_time(owner, dist_rank);
         best_shared = ts;
         best_xch = tx;
       }
     }
+    rs_model[1] = ar_full;
     dist_on = !best_owner.empty() && (dist_force || best < t_repl);
     dist_model[0] = best_rank;
     dist_model[1] = best_shared;
@@ -402,6 +421,36 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         else if (sn_owner[k] == dist_rank) ++n_owned_fronts;
       }
     }
+  }
+  // reduce-scatter layout of the input (see engine.hpp): block t -> rs_buf offset; the entry sources remapped into it
+  rs_on = dist_on && rs_enable && reduce_scatter;
+  rs_seg = rs_tail_len = rs_rhs_off = 0;
+  rs_nblk = (long long)bi.size();
+  if (rs_on) {
+    const int N = dist_nranks, B = bdim * bdim;
+    std::vector<long long> cnt(N + 1, 0), boff(bi.size());
+    std::vector<int> own(bi.size());
+    for (size_t t = 0; t < bi.size(); ++t) {
+      const int o = sn_owner[sym.block_sn[std::min(sym.bpinv[bi[t]], sym.bpinv[bj[t]])]];
+      own[t] = o >= 0 ? o : N;
+      cnt[own[t]]++;
+    }
+    rs_seg = *std::max_element(cnt.begin(), cnt.begin() + N) * B;
+    std::vector<long long> fillc(N + 1, 0);
+    for (size_t t = 0; t < bi.size(); ++t) {
+      const int o = own[t];
+      boff[t] = (o < N ? (long long)o * rs_seg : (long long)N * rs_seg) + fillc[o]++ * B;
+    }
+    rs_rhs_off = (long long)N * rs_seg + cnt[N] * B;
+    rs_tail_len = cnt[N] * B + (long long)nblocks * bdim;
+    if (rs_rhs_off + (long long)nblocks * bdim >= (1LL << 31))
+      throw DeviceError("reduce-scatter layout too large for 32-bit entry indexing");
+    for (int& k : ent_srcv) k = (int)(boff[k / B] + k % B);
+    ent_src.upload(ent_srcv.empty() ? std::vector<int>{0} : ent_srcv, s);
+    rs_bmap.upload(boff.empty() ? std::vector<long long>{0} : boff, s);
+    rs_rhs_rng.upload(std::vector<long long>{(long long)bi.size() * B, rs_rhs_off, (long long)nblocks * bdim}, s);
+    rs_buf.resize(std::max<long long>(rs_rhs_off + (long long)nblocks * bdim, 1));
+    rs_buf.zero(s);  // segment padding is never written: zeros go into the reduce-scatter
   }
   // forward plan: the level front lists in execution order (distributed: this rank's fronts level by level, the root
   // exchange, then the shared fronts level by level); the backward solve walks the same plan in reverse
@@ -944,6 +993,13 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
   }
 }
 
+void DeviceCholesky::reduce_input(const double* vals, hipStream_t s) {
+  launch::chol_pack_blocks(rs_nblk, pd * pd, rs_bmap.get(), vals, rs_buf.get(), s);
+  launch::chol_copy_ranges(1, rs_rhs_rng.get(), vals, rs_buf.get(), s);
+  reduce_scatter(rs_buf.get(), (size_t)rs_seg);
+  allreduce(rs_buf.get() + (size_t)dist_nranks * rs_seg, (size_t)rs_tail_len);
+}
+
 void DeviceCholesky::check_dag(hipStream_t s) {
   if (!n_dag_levels) return;
   unsigned t = 0;
@@ -1477,7 +1533,8 @@ void Engine::write_debug_dump() {
   if (do_schur) dS.download(blocks.data(), blocks.size(), stream);
   else dH.download(blocks.data(), blocks.size(), stream);
   HIP_CHECK(hipStreamSynchronize(stream));
-  fprintf(stderr, "Cholesky failure, writing %s (Hessian loadable by Octave)\n", debug_path.c_str());
+  fprintf(stderr, "Cholesky failure, writing %s (Hessian loadable by Octave)%s\n", debug_path.c_str(),
+          chol.rs_on ? " — rank 0's partial sums (reduce-scattered S; set writeDebug before initializeOptimization)" : "");
   write_octave_blocks(debug_path.c_str(), bi, bj, pd, blocks.data(), num_poses, do_schur ? 0.0 : lambda_host, true,
                       false);
 }
@@ -2266,6 +2323,11 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       chol.dist_nranks = dist ? nranks : 1;
       chol.dist_force = df && atoi(df) == 1;
       chol.allreduce = [this](double* p, size_t n) { allreduce_sum(p, n); };
+      // the reduced system itself reduce-scattered by subtree ownership (G2OHIP_DIST_RS=0: all-reduced whole, A/B);
+      // not with the not-PD dump, which writes the whole S from rank 0
+      const char* drs = getenv("G2OHIP_DIST_RS");
+      chol.rs_enable = dist && !write_debug && !(drs && atoi(drs) == 0);
+      chol.reduce_scatter = [this](double* p, size_t n) { comm->reduce_scatter_sum(p, n, stream); };
       // timing only (tools/dist_factor_time.py): one process plays rank r of N of the distributed factorization with
       // no-op exchanges — the kernel chain rank r would run, on this GPU; the solution is not meaningful
       const char* sim = getenv("G2OHIP_DIST_SIMULATE");
@@ -2275,6 +2337,8 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         chol.dist_nranks = sn;
         chol.dist_force = true;
         chol.allreduce = [](double*, size_t) {};
+        chol.reduce_scatter = [](double*, size_t) {};
+        chol.rs_enable = !(drs && atoi(drs) == 0);
       }
       chol.setup(num_poses, pd, s_bi, s_bj, stream);
     }
@@ -2489,7 +2553,9 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
                      ds_hpp.get(), dH.get(), S, zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(),
                      stream);
   timer.end(stream);
-  allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
+  const bool rs = !use_pcg() && chol.rs_on;  // distributed factorization: each rank's blocks reduce-scattered to it
+  if (rs) chol.reduce_input(dS.get(), stream);
+  else allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
   if (sev) HIP_CHECK(hipEventRecord(ev_[1], stream));
   if (use_pcg()) {
     timer.begin("pcg", stream);
@@ -2498,7 +2564,8 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
     if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
   } else {
     timer.begin("chol_factor", stream);
-    chol.factor(S, dscal.get() + 5, bschur, failp(), stream, zero_here);
+    if (rs) chol.factor(chol.rs_buf.get(), dscal.get() + 5, chol.rs_buf.get() + chol.rs_rhs_off, failp(), stream, zero_here);
+    else chol.factor(S, dscal.get() + 5, bschur, failp(), stream, zero_here);
     timer.end(stream);
     if (sev) HIP_CHECK(hipEventRecord(ev_[2], stream));
     timer.begin("chol_solve", stream);
@@ -2911,6 +2978,9 @@ int Engine::stage(double lambda, double* b, double* x, double* Hs, double* bs, l
   }
   set_lambda(lambda, 1);
   const int ok = solve_sync();
+  // the distributed factorization reduce-scatters S (dS keeps this rank's partial sums): the whole reduced system
+  // for the caller takes one more all-reduce (every rank calls stage, as it calls every other collective step)
+  if ((Hs || bs) && do_schur && chol.rs_on) allreduce_sum(dS.get(), (size_t)nS * pd * pd + size_poses);
   if (b) db.download(b, n, stream);
   if (x) dx.download(x, n, stream);
   if (Hs || bs) {
@@ -3121,7 +3191,8 @@ int Engine::factor_info(double* out, int n) {
                       (double)chol.n_pre_levels, (double)chol.n_syrk_ops, (double)chol.n_bwd_rounds,
                       (double)chol.n_dag_levels, (double)chol.n_owned_fronts, (double)chol.n_shared_fronts,
                       (double)chol.n_roots, (double)chol.xch_len, chol.dist_model[0], chol.dist_model[1],
-                      chol.dist_model[2], chol.dist_model[3], chol.dist_model[4]};
+                      chol.dist_model[2], chol.dist_model[3], chol.dist_model[4], chol.rs_on ? 1.0 : 0.0,
+                      (double)chol.rs_seg, (double)chol.rs_tail_len, chol.rs_model[0], chol.rs_model[1]};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;

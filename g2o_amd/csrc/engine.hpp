@@ -150,6 +150,19 @@ struct DeviceCholesky {
   int nxzero = 0;
   int* last_fail = nullptr;
   bool distributed() const { return dist_on; }
+  // reduce-scatter of the input (distributed only, rs_enable set by the caller before setup): the reduced system's
+  // blocks are packed by the rank whose subtrees read them — [rank 0's blocks | ... | rank N-1's (each segment padded to
+  // rs_seg doubles) | shared blocks + rhs] — one reduce-scatter sums each rank's own segment, one all-reduce the tail;
+  // the factor reads its entries from rs_buf (ent_src remapped), never another rank's segment
+  bool rs_enable = false, rs_on = false;
+  std::function<void(double*, size_t)> reduce_scatter;  // in place, `count` doubles per rank
+  long long rs_seg = 0, rs_tail_len = 0, rs_rhs_off = 0, rs_nblk = 0;
+  double rs_model[2] = {0, 0};                // modelled seconds: reduce-scatter + tail all-reduce, full all-reduce
+  DevBuf<long long> rs_bmap;                  // per input block: its offset in rs_buf
+  DevBuf<long long> rs_rhs_rng;               // (src, dst, len) of the rhs
+  DevBuf<double> rs_buf;
+  // pack this rank's partial [blocks | rhs] (the caller's layout) and reduce; factor(rs_buf, ..., rs_buf + rs_rhs_off)
+  void reduce_input(const double* vals, hipStream_t s);
   std::vector<Op> ops;
   std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
   DevBuf<launch::Task> tasks;

@@ -218,6 +218,8 @@ int chol_dag_max_workers(int device);  // resident one per CU
 // distributed factorization glue: contiguous range copies (src, dst, len) in doubles; the distributed
 // solve's not-PD flag into / x and flag out of its all-reduce buffer; x[idx[k]] = 0
 void chol_copy_ranges(int n, const long long* rng, const double* src, double* dst, hipStream_t s);
+// dst[boff[t] + i] = src[t bb + i], i < bb, for nblk blocks of bb doubles (the reduce-scatter pack)
+void chol_pack_blocks(long long nblk, int bb, const long long* boff, const double* src, double* dst, hipStream_t s);
 void chol_dist_fail_in(const int* fail, double* xr, int n, hipStream_t s);
 void chol_dist_x_out(const double* xr, int n, double* x, int* fail, hipStream_t s);
 void chol_zero_idx(const int* idx, int n, double* x, hipStream_t s);

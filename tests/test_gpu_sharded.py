@@ -150,6 +150,8 @@ def test_distributed_factorization(g2o_amd_mod, oracle, monkeypatch, name, nrank
     assert all(i["distributed"] == 1 for i in info), info
     assert sum(i["owned_fronts"] for i in info) + info[0]["shared_fronts"] == info[0]["supernodes"], info
     assert info[0]["subtree_roots"] > 0 and info[0]["root_exchange_doubles"] > 0, info[0]
+    # the reduced system reaches each rank as a reduce-scatter of the blocks its subtrees read + the shared tail
+    assert all(i["reduce_scatter"] == 1 and i["rs_segment_doubles"] > 0 and i["rs_tail_doubles"] > 0 for i in info), info
     x, states = _gather_state(prob, opts)
     C = prob.vertices[0].ids.size
     for s in states[1:]:
@@ -174,3 +176,21 @@ def test_distributed_factorization(g2o_amd_mod, oracle, monkeypatch, name, nrank
     assert np.linalg.norm(x - xr_) <= 1e-9 * np.linalg.norm(xr_)
     xo = ref.minimal_state()
     assert np.linalg.norm(x - xo) <= RTOL * np.linalg.norm(xo)
+
+
+def test_distributed_reduce_scatter_equals_allreduce(g2o_amd_mod, monkeypatch):
+    """The reduce-scatter of S by subtree ownership (each rank receives only the blocks its fronts read, plus the shared
+    tail) against the same distributed factorization fed by the plain all-reduce of the whole S (G2OHIP_DIST_RS=0): the
+    LocalComm sums are rank-ordered in both, so the trajectories agree bitwise."""
+    prob = synth.by_name("C5", "small")
+    monkeypatch.setenv("G2OHIP_DIST_FACTOR", "1")
+    opts, res = _run_sharded(g2o_amd_mod, prob, 3, 3)
+    assert all(o.factor_info()["reduce_scatter"] == 1 for o in opts)
+    monkeypatch.setenv("G2OHIP_DIST_RS", "0")
+    aopts, ares = _run_sharded(g2o_amd_mod, prob, 3, 3)
+    assert all(o.factor_info()["reduce_scatter"] == 0 for o in aopts)
+    x, _ = _gather_state(prob, opts)
+    xa, _ = _gather_state(prob, aopts)
+    assert np.array_equal(x, xa)
+    for r in range(3):
+        assert [s.chi2 for s in res[r][1]] == [s.chi2 for s in ares[r][1]]

@@ -435,7 +435,7 @@ class SparseOptimizer:
                         "owned_fronts", "shared_fronts", "subtree_roots", "root_exchange_doubles",
                         "model_rank_subtrees_s", "model_shared_s", "model_single_gpu_s", "model_exchange_s",
                         "distributed", "reduce_scatter", "rs_segment_doubles", "rs_tail_doubles", "model_input_s",
-                        "model_input_allreduce_s")
+                        "model_input_allreduce_s", "w64_levels")
 
     def factor_info(self) -> dict:
         out = np.zeros(len(self.FACTOR_INFO_KEYS))

@@ -227,7 +227,7 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col)
 // The diagonal block of L itself is not stored: every consumer of the factor (tile TRSM, next-diagonal
 // update, inverse tasks, backward and multi-right-hand-side solves) uses L^-1 for diagonal blocks.
 __device__ __forceinline__ void factor_block(double* D, int kb, const double* vy, double* col, int lane, int* fail,
-                                             double* ysol, unsigned long long* ph = nullptr) {
+                                             double* ysol, unsigned long long* ph = nullptr, double* ylds = nullptr) {
   double row[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
@@ -255,7 +255,9 @@ __device__ __forceinline__ void factor_block(double* D, int kb, const double* vy
 #pragma unroll
       for (int c = 0; c < 8; ++c) y4[c & 3] += (c0 + c <= lane ? dv[c] : 0.0) * (c0 + c < kb ? vv[c] : 0.0);
     }
-    if (lane < kb) ysol[lane] = (y4[0] + y4[1]) + (y4[2] + y4[3]);
+    const double yv = (y4[0] + y4[1]) + (y4[2] + y4[3]);
+    if (lane < kb) ysol[lane] = yv;
+    if (ylds) ylds[lane] = lane < kb ? yv : 0.0;  // (same wave: in-order LDS traffic for its later readers)
   }
 }
 // After factor_block and a workgroup barrier: L_kk^-1 row-major to linv and the diagonal block of
@@ -270,6 +272,182 @@ __device__ __forceinline__ void publish_inverse(const double* D, int kb, int tid
   for (int u = 0; u < NB * NB / 256; ++u) {
     const int e = tid + 256 * u, c = e >> 5, i = e & (NB - 1);
     if (c < kb && i < kb) X[(size_t)c * ldx + i] = D[c * DS + i];
+  }
+}
+
+// ---------------------------------------------------------------------------- 64-column panel steps
+// The launch-per-panel schedule with 64-column panels (DeviceCholesky::setup chooses it per level): half the kernel
+// boundaries on the diagonal chain — each boundary costs ~3 us of drain + dispatch and ~2.4 us of reloads at the next
+// diagonal task's start (tools/phase_probe.py) against ~4 us for a chol32 — and every trailing update is rank 64 (the
+// lagged pairs' traffic without their strip steps). The current panel's inverse L_p^-1 = [A 0; N B] is kept as the two
+// per-32-panel inverses A = L_a^-1, B = L_b^-1 (linv, as the 32-column schedule: the backward solve and
+// computeMarginals read them) and N = -L_b^-1 L_ba L_a^-1 (linvn, one per 64-panel). Tasks (StepTask, k0kb = k0 | kb << 16,
+// kb <= 64):
+//   tile (flags & 1 update)  TRSM of the tile's panel rows as X = P L_p^-T in two 32-column halves (X_a = P_a A^T,
+//                            X_b = P_a N^T + P_b B^T), then C_IJ -= X_I X_J^T half by half (rank 64); writers store
+//                            L rows and update the front vector with X_I y_p;
+//   diagonal (flags & 4)     the next 64 x 64 block: D' = D - X X^T with its own X rows, then chol64 (below);
+//   inverse (flags & 16)     X = L11^-1 for the backward solve, block row by block row (32-row blocks p, 32-column
+//                            blocks j): W_pj += L_pa X_aj + L_pb X_bj for the previous 64-panel (a, b); the two rows of
+//                            the current 64-panel finalised as X = -L_p^-1 W.
+constexpr int W64_LI = 3 * NB * PS;           // A | N | B of the current panel, row-major, stride PS
+constexpr int W64_R = W64_LI;                 // role region
+constexpr int W64_COL = W64_R + TT * PS + 3 * NB * DS;
+constexpr int W64_VN = W64_COL + 4 * NB, W64_YL = W64_VN + TT, W64_YK = W64_YL + TT;
+constexpr int W64_LDS = W64_YK + TT;
+static_assert(W64_R + 2 * TT * PS <= W64_COL && TT * (TT + 1) <= 2 * TT * PS, "tile role region");
+static_assert(W64_R + TT * PS + NB * PS + TT * (NB + 1) <= W64_LDS, "inverse role region");
+static_assert(W64_COL % 2 == 0, "col buffer: 16-byte aligned");
+
+struct Chol64Lds {
+  double *Qaa, *Qba, *Qbb;  // quadrants of the block, 32 x DS each (row-major; lower parts valid)
+  double *S, *Nb;           // scratch: 64 x PS and 32 x PS
+  double *col, *vn, *yl;    // chol32 column buffers, right-hand side (64), y (64)
+};
+// publish_inverse over threads [t0, t0 + nt) of the workgroup (the others are busy)
+__device__ __forceinline__ void publish_inv_part(const double* D, int kb, int t, int nt, double* linv, double* X, int ldx) {
+  for (int e = t; e < NB * NB; e += nt) linv[e] = D[(e & (NB - 1)) * DS + (e >> 5)];
+  for (int e = t; e < NB * NB; e += nt) {
+    const int c = e >> 5, i = e & (NB - 1);
+    if (c < kb && i < kb) X[(size_t)c * ldx + i] = D[c * DS + i];
+  }
+}
+struct NoSide {
+  __device__ void operator()() const {}
+};
+// Factor the kbn x kbn (kbn <= 64) block in q.Q* with right-hand side q.vn: L_a = chol(Qaa), L_ba = Qba L_a^-T,
+// L_b = chol(Qbb - L_ba L_ba^T), N = -L_b^-1 L_ba L_a^-1, y = L^-1 vn. Publishes L_a^-1, L_b^-1 (linv rows), N (linvn),
+// the block's part of X = L11^-1 (X, leading dimension ldx) and y (ysol); L_ba goes to the factor (Lba, leading dimension
+// ldl: the only part of L this block owns in lbuf, diagonal 32 x 32 blocks are never stored). Whole workgroup; while
+// wave 0 runs each chol32 the other three waves work beside it: side_a() during the first (the caller's updates of Qba,
+// Qbb and vn_b), M = L_ba L_a^-1 and the a half's publishing during the second.
+template <class SideA>
+__device__ __forceinline__ void chol64(const Chol64Lds& q, int kbn, int tid, int* fail, double* ysol, double* linv_a,
+                                       double* linv_b, double* linvn, double* X, int ldx, double* Lba, int ldl,
+                                       unsigned long long* ph, SideA side_a) {
+  const int lane = tid & 63, w = tid >> 6, lr = lane & 15, lk = lane >> 4;
+  const int kna = min(NB, kbn), knb = kbn - NB;
+  if (tid < 64) factor_block(q.Qaa, kna, q.vn, q.col, tid, fail, ysol, ph, q.yl);
+  else side_a();
+  __syncthreads();
+  if (knb <= 0) {
+    publish_inv_part(q.Qaa, kna, tid, 256, linv_a, X, ldx);
+    return;
+  }
+  const int tr = w & 1, tc = w >> 1;
+  {  // L_ba = Qba L_a^-T (L_a^-1(c, k) = Qaa[k DS + c]); rows past knb zeroed (N and the tiles rely on it)
+    dx4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < NB / 4; ++kk) {
+      const int k = kk * 4 + lk;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q.Qba[(16 * tr + lr) * DS + k], q.Qaa[k * DS + 16 * tc + lr], acc, 0, 0, 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * tr + lk + 4 * i, c = 16 * tc + lr;
+      const double v = r < knb ? acc[i] : 0.0;
+      q.Qba[r * DS + c] = v;
+      if (r < knb) Lba[(size_t)c * ldl + r] = v;
+    }
+  }
+  __syncthreads();
+  if (w < 3) {  // Qbb -= L_ba L_ba^T on the lower 16 x 16 tiles (0,0), (1,0), (1,1)
+    const int ur = (w + 1) >> 1, uc = w >> 1;
+    dx4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < NB / 4; ++kk) {
+      const int k = kk * 4 + lk;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q.Qba[(16 * ur + lr) * DS + k], q.Qba[(16 * uc + lr) * DS + k], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q.Qbb[(16 * ur + lk + 4 * i) * DS + 16 * uc + lr] -= acc[i];
+  } else if (lane < NB) {  // the b rows' right-hand side: vn_b -= L_ba y_a
+    double s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) s2 += q.Qba[lane * DS + k] * q.yl[k];
+    q.vn[NB + lane] -= s2;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    factor_block(q.Qbb, knb, q.vn + NB, q.col, tid, fail, ysol + NB, nullptr, q.yl + NB);
+  } else {  // beside it: M = L_ba L_a^-1 (row-major into S; tiles over waves 1..3), the a half published
+    for (int tl = w - 1; tl < 4; tl += 3) {
+      const int ur = tl & 1, uc = tl >> 1;
+      dx4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q.Qba[(16 * ur + lr) * DS + k], q.Qaa[(16 * uc + lr) * DS + k], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) q.S[(16 * ur + lk + 4 * i) * PS + 16 * uc + lr] = acc[i];
+    }
+    publish_inv_part(q.Qaa, kna, tid - 64, 192, linv_a, X, ldx);
+  }
+  __syncthreads();
+  {  // N = -L_b^-1 M
+    dx4 an = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < NB / 4; ++kk) {
+      const int k = kk * 4 + lk;
+      an = __builtin_amdgcn_mfma_f64_16x16x4f64(q.Qbb[k * DS + 16 * tr + lr], q.S[k * PS + 16 * tc + lr], an, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q.Nb[(16 * tr + lk + 4 * i) * PS + 16 * tc + lr] = -an[i];
+  }
+  __syncthreads();
+  publish_inv_part(q.Qbb, knb, tid, 256, linv_b, X + (size_t)NB * ldx + NB, ldx);
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = tid + 256 * u;
+    linvn[e] = q.Nb[(e >> 5) * PS + (e & (NB - 1))];
+  }
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = tid + 256 * u, c = e >> 5, i = e & (NB - 1);
+    if (i < knb) X[(size_t)c * ldx + NB + i] = q.Nb[i * PS + c];
+  }
+}
+
+// stage the current panel's inverses A | N | B (row-major, as in linv / linvn) into Li3; B and N only with a b half
+__device__ __forceinline__ void load_li3(const double* la, const double* ln, const double* lb, bool bh, int tid,
+                                         double (&v)[3][NB * NB / 256]) {
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    v[0][u] = la[tid + 256 * u];
+    v[1][u] = ld0(ln, tid + 256 * u, bh);
+    v[2][u] = ld0(lb, tid + 256 * u, bh);
+  }
+}
+__device__ __forceinline__ void store_li3(double* Li3, int tid, const double (&v)[3][NB * NB / 256]) {
+#pragma unroll
+  for (int h = 0; h < 3; ++h)
+#pragma unroll
+    for (int u = 0; u < NB * NB / 256; ++u) {
+      const int e = tid + 256 * u;
+      Li3[h * NB * PS + (e >> 5) * PS + (e & (NB - 1))] = v[h][u];
+    }
+}
+// X rows of a 64-row panel slab (rows 16 w .. 16 w + 15 of this wave), cols [16 h, 16 h + 16) of a 32-column half:
+// x[h] += P(rows, 0:32) Lq^T with Lq row-major (stride PS) in LDS
+__device__ __forceinline__ void trsm_half(const double* P, const double* Lq, int lane, int w, dx4 (&x)[2]) {
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < NB / 4; ++kk) {
+    const int k = kk * 4 + lk;
+    const double a = P[(16 * w + lr) * PS + k];
+    x[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Lq[lr * PS + k], x[0], 0, 0, 0);
+    x[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Lq[(16 + lr) * PS + k], x[1], 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void store_xhalf(double* P, int lane, int w, const dx4 (&x)[2]) {
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 16 * w + lk + 4 * i;
+    P[r * PS + lr] = x[0][i];
+    P[r * PS + 16 + lr] = x[1][i];
   }
 }
 
@@ -295,7 +473,9 @@ __device__ __forceinline__ double input_entry(const double* vals, const int* ent
 }
 // ASM: the level's fronts are assembled here (EAC: rows per LDS column chunk); else they were pre-zeroed and
 // scattered
-template <bool ASM, int EAC>
+// W64: the level runs 64-column panel steps (k_step64): its first-block tasks assemble and factor the first 64 columns
+// (chol64), and the slabs leave those 64 x 64 entries to them
+template <bool ASM, int EAC, bool W64>
 __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                     const int* __restrict__ children, const int* __restrict__ relmap,
                                                     const int* __restrict__ jtab, const int* __restrict__ cmptr,
@@ -304,13 +484,106 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
                                                     const double* __restrict__ lam, double* __restrict__ fronts,
                                                     double* __restrict__ vecs, double* __restrict__ lbuf,
                                                     double* __restrict__ ysol, double* __restrict__ linv,
-                                                    double* __restrict__ xinv, int* __restrict__ fail) {
+                                                    double* __restrict__ linvn, double* __restrict__ xinv,
+                                                    int* __restrict__ fail) {
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr, kb0 = min(NB, me.ns);
+  const int m = me.ns + me.nr, kb0 = min(W64 ? TT : NB, me.ns);
   double* F = fronts + me.front_off;
   double* v = vecs + me.vec_off;
   const int tid = threadIdx.x;
+  // W64: one buffer for both roles (the 64-wide first block, the slabs' column buffers)
+  constexpr int SMU = !W64 ? 1 : (W64_LDS > 4 * EAC ? W64_LDS : 4 * EAC);
+  __shared__ __attribute__((aligned(16))) double smu[SMU];
+  if constexpr (W64) {
+    if (t.c == 1) {
+      // ---- first 64 x 64 block: assembled (input entries, children), factored with chol64, published
+      Chol64Lds q;
+      q.S = smu + W64_R;
+      q.Qaa = q.S + TT * PS;
+      q.Qba = q.Qaa + NB * DS;
+      q.Qbb = q.Qba + NB * DS;
+      q.Nb = smu + NB * PS;
+      q.col = smu + W64_COL;
+      q.vn = smu + W64_VN;
+      q.yl = smu + W64_YL;
+      int* cp = reinterpret_cast<int*>(smu + W64_YK);  // kb0 + 1 column pointers (64 doubles hold 128 ints)
+      auto qp = [&](int r, int c) -> double* {
+        return r < NB ? q.Qaa + r * DS + c : (c < NB ? q.Qba + (r - NB) * DS + c : q.Qbb + (r - NB) * DS + c - NB);
+      };
+      PH_BEGIN(1)
+      if constexpr (!ASM) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+          const bool ok = r < kb0 && c <= r;
+          const double x = ld0(F, c * m + r, ok);
+          if (c <= r) *qp(r, c) = x;
+        }
+        if (tid < TT) q.vn[tid] = ld0(v, tid, tid < kb0);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+          if (c <= r) *qp(r, c) = 0.0;
+        }
+        if (tid <= kb0) cp[tid] = colptr[me.c0 + tid];
+        if (tid < TT) q.vn[tid] = ld0(v, tid, tid < kb0);
+        __syncthreads();
+        for (int e = cp[0] + tid; e < cp[kb0]; e += 256) {
+          int lo = 0, hi = kb0;
+          while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cp[mid] <= e) lo = mid; else hi = mid; }
+          int r;
+          const double x = input_entry(vals, ent_src, ent_row, e, lam, r);
+          if (r < kb0) *qp(r, lo) = x;
+        }
+      }
+      __syncthreads();
+      // children two at a time: every load of a pair in flight before the first add, adds in fixed child order
+      constexpr int B0C = 2;
+      for (int kc = me.child_begin; kc < me.child_end; kc += B0C) {
+        double val[B0C][16], vv[B0C];
+        int dst[B0C][16], vdst[B0C];
+#pragma unroll
+        for (int c = 0; c < B0C; ++c) {
+          const bool has = kc + c < me.child_end;
+          const FrontDesc cd = fd[children[has ? kc + c : kc]];
+          const int mc = cd.ns + cd.nr, nrc = cd.nr;
+          const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;
+          const int* rel = relmap + cd.rows_off;
+          const int n0 = has ? jtab[cd.jt_off] : 0;  // child rows mapping into the first 64 x 64 block
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int e = tid + 256 * u;
+            const int i = e & (TT - 1), j = e >> 6;
+            const bool in = i < nrc && j <= i;
+            val[c][u] = ld0(U, j * mc + i, in);
+            const int ri = ld0(rel, i, in), rj = ld0(rel, j, in);
+            dst[c][u] = (in && i < n0) ? (ri | (rj << 8)) : -1;
+          }
+          vv[c] = ld0(vecs + cd.vec_off + cd.ns, tid, tid < nrc && tid < TT);
+          const int rt = ld0(rel, tid, tid < nrc && tid < TT);
+          vdst[c] = tid < n0 && tid < TT ? rt : -1;
+        }
+#pragma unroll
+        for (int c = 0; c < B0C; ++c) {
+          if (kc + c >= me.child_end) break;
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (dst[c][u] >= 0) *qp(dst[c][u] & 0xff, dst[c][u] >> 8) += val[c][u];
+          if (vdst[c] >= 0) q.vn[vdst[c]] += vv[c];
+          __syncthreads();
+        }
+      }
+      PH(2)
+      chol64(q, kb0, tid, fail, ysol + me.c0, linv + (size_t)me.c0 * (NB * NB), linv + (size_t)(me.c0 + NB) * (NB * NB),
+             linvn + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns, lbuf + me.l_off + NB, m, PH_REC, NoSide{});
+      PH(3)
+      PH(4)
+      return;
+    }
+  }
+  if constexpr (!W64) {
   if (t.c == 1) {
     __shared__ double D[NB * DS];
     __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
@@ -397,13 +670,15 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     PH(4)
     return;
   }
+  }
   const int a = t.a, b = t.b;
   const int lane = tid & 63, w = tid >> 6;
   if constexpr (ASM) {
     // In-place assembly: each wave builds its columns in an LDS column buffer (zero, the column's input
     // entries, then every (child, child column) pair mapping to it in child order) and writes each entry
     // of the front once; rows in chunks of EAC. The children's update vectors follow below.
-    __shared__ double cbuf[4][EAC];
+    __shared__ double cbuf_[W64 ? 1 : 4][W64 ? 1 : EAC];
+    double(*cbuf)[EAC] = W64 ? reinterpret_cast<double(*)[EAC]>(smu) : reinterpret_cast<double(*)[EAC]>(&cbuf_[0][0]);
     for (int j = a + w; j < b; j += 4) {
       const int rlo = j < kb0 ? kb0 : j;  // rows of the first diagonal block: block-0 task
       double* Fj = F + (size_t)j * m;
@@ -830,6 +1105,344 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
     const int gi = I0 + r, gj = J0 + c;
     const bool dblk = gi < r0 + kbn && gj < r0 + kbn;
     if (gi < m && gj < climit && gi >= gj && !dblk) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
+  }
+  PH1(4)
+  PH1R(7)
+}
+
+// ---------------------------------------------------------------------------- 64-column panel steps (kernel)
+// (see the 64-column helpers above k_extend_add)
+__global__ void __launch_bounds__(256, 2) k_step64(const StepTask* __restrict__ tasks, const launch::StepHead head,
+                                                   double* __restrict__ fronts, double* __restrict__ lbuf,
+                                                   double* __restrict__ vecs, double* __restrict__ ysol,
+                                                   double* __restrict__ linv, double* __restrict__ linvn,
+                                                   double* __restrict__ xinv, int* __restrict__ fail) {
+  __shared__ __attribute__((aligned(16))) double sm[W64_LDS];
+  PH_BEGIN(2)
+  PH1_BEGIN(3)
+  const StepTask t = (int)blockIdx.x < head.n ? head.t[blockIdx.x] : tasks[blockIdx.x];
+  const int m = t.m, ns = t.ns;
+  double* F = fronts + t.f_off;
+  double* L = lbuf + t.l_off;
+  double* v = vecs + t.v_off;
+  const int k0 = t.k0kb & 0xffff, kb = t.k0kb >> 16;  // current panel [k0, k0 + kb), kb <= 64
+  const int kbb = kb - NB;                             // columns of its b half (<= 0: none)
+  const bool bh = kbb > 0;
+  const int r0 = k0 + kb;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double* Li3 = sm;
+  const double* la = linv + (size_t)(t.c0 + k0) * (NB * NB);
+  const double* lb = linv + (size_t)(t.c0 + k0 + (bh ? NB : 0)) * (NB * NB);
+  const double* ln = linvn + (size_t)(t.c0 + k0) * (NB * NB);
+
+  if (t.flags & 4) {
+    // ---- next-diagonal task: the 64 x 64 block at r0 with this panel's update applied, then chol64
+    const int kbn = min(TT, ns - r0);
+    Chol64Lds q;
+    q.S = sm + W64_R;
+    q.Qaa = q.S + TT * PS;
+    q.Qba = q.Qaa + NB * DS;
+    q.Qbb = q.Qba + NB * DS;
+    q.Nb = Li3 + NB * PS;
+    q.col = sm + W64_COL;
+    q.vn = sm + W64_VN;
+    q.yl = sm + W64_YL;
+    double* yk = sm + W64_YK;
+    double lv[3][NB * NB / 256], pa[8], pb[8], dq[16];
+    load_li3(la, ln, lb, bh, tid, lv);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+      pa[u] = ld0(F, (k0 + c) * m + r0 + r, r < kbn && c < kb);
+      pb[u] = ld0(F, (k0 + NB + c) * m + r0 + r, r < kbn && c < kbb);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+      dq[u] = ld0(F, (r0 + c) * m + r0 + r, r < kbn && c <= r);
+    }
+    const double vo = ld0(v, r0 + tid, tid < kbn);
+    const double ykv = ld0(ysol, t.c0 + k0 + tid, tid < kb);
+    store_li3(Li3, tid, lv);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+      q.S[r * PS + c] = pa[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+      if (c <= r) {
+        double* Qp = r < NB ? q.Qaa + r * DS + c : (c < NB ? q.Qba + (r - NB) * DS + c : q.Qbb + (r - NB) * DS + c - NB);
+        *Qp = dq[u];
+      }
+    }
+    if (tid < TT) { q.vn[tid] = vo; yk[tid] = ykv; }
+    __syncthreads();
+    PH(2)
+    // X = P L_p^-T: X_a = P_a A^T (S afterwards), X_b = P_a N^T + P_b B^T (X2 = the Li3 region afterwards)
+    dx4 xa[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}}, xb[2] = {xa[0], xa[0]};
+    trsm_half(q.S, Li3, lane, w, xa);
+    trsm_half(q.S, Li3 + NB * PS, lane, w, xb);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+      q.S[r * PS + c] = pb[u];
+    }
+    __syncthreads();
+    trsm_half(q.S, Li3 + 2 * NB * PS, lane, w, xb);
+    __syncthreads();
+    double* X2 = Li3;  // 64 x PS (A | N | B are dead)
+    store_xhalf(q.S, lane, w, xa);
+    store_xhalf(X2, lane, w, xb);
+    __syncthreads();
+    const int lr = lane & 15, lk = lane >> 4;
+    // tile (ur, uc) of the 64 x 64 block: Q -= X(rows) X(cols)^T over K = 64 (both halves)
+    auto dtile = [&](int ur, int uc) {
+      dx4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q.S[(16 * ur + lr) * PS + k], q.S[(16 * uc + lr) * PS + k], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X2[(16 * ur + lr) * PS + k], X2[(16 * uc + lr) * PS + k], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * ur + lk + 4 * i, c = 16 * uc + lr;
+        double* Qp = r < NB ? q.Qaa + r * DS + c : (c < NB ? q.Qba + (r - NB) * DS + c : q.Qbb + (r - NB) * DS + c - NB);
+        *Qp -= acc[i];
+      }
+    };
+    auto vrow = [&](int r) {  // vn_r -= X_r y_p
+      double s2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) s2 += q.S[r * PS + k] * yk[k] + X2[r * PS + k] * yk[NB + k];
+      q.vn[r] -= s2;
+    };
+    // the a quadrant and vn_a first (the first chol32 needs them); the b rows beside that chol32 (chol64's side work)
+    if (w < 3) dtile((w + 1) >> 1, w >> 1);
+    else if (lane < NB) vrow(lane);
+    __syncthreads();
+    PH(2)
+    chol64(q, kbn, tid, fail, ysol + t.c0 + r0, linv + (size_t)(t.c0 + r0) * (NB * NB),
+           linv + (size_t)(t.c0 + r0 + NB) * (NB * NB), linvn + (size_t)(t.c0 + r0) * (NB * NB),
+           xinv + t.x_off + (size_t)r0 * ns + r0, ns, L + (size_t)r0 * m + r0 + NB, m, PH_REC, [&] {
+             // waves 1..3: the ba quadrant's tiles (2,0) (2,1) (3,0) (3,1), the bb quadrant's (2,2) (3,2) (3,3), vn_b
+             const int sw = w - 1;
+             for (int tl = sw; tl < 7; tl += 3) {
+               const int ur = tl < 4 ? 2 + (tl >> 1) : (tl == 4 ? 2 : 3), uc = tl < 4 ? (tl & 1) : (tl == 6 ? 3 : 2);
+               dtile(ur, uc);
+             }
+             if (sw == 2 && lane < NB) vrow(NB + lane);
+           });
+    PH(3)
+    PH(4)
+    return;
+  }
+
+  if (t.flags & 16) {
+    // ---- inverse task: block column j, block row p (32-blocks) of X = L11^-1. The previous 64-panel is (a, b) =
+    // (k0 / 32 - 2, k0 / 32 - 1); W_pj += L_pa X_aj + L_pb X_bj; the current panel's rows (p = k0 / 32, with p + 1)
+    // are finalised: X_pj = -A W_pj, X_p+1,j = -(N W_pj + B W_p+1,j).
+    const int j = t.tile & 0xffff, p = t.tile >> 16, qa = k0 / NB - 2, qb = qa + 1;
+    const bool fin = p * NB == k0;
+    const int rows = min(fin ? TT : NB, ns - NB * p);  // output rows (64 when finalising both rows of the panel)
+    double* Xf = xinv + t.x_off;
+    double* Ls = sm + W64_R;            // 64 x PS: L(rows, q)
+    double* Xs = Ls + TT * PS;          // 32 x PS: X_qj (row k, column c)
+    double* Wl = Xs + NB * PS;          // 64 x (NB + 1)
+    const int lr = lane & 15, lk = lane >> 4;
+    // wave w: output rows 16 w .. 16 w + 15 (rows < 64), two 16-column tiles
+    dx4 acc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+    double wv[2][4];  // W so far (the earlier panels' terms), in the MFMA output layout
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * w + lk + 4 * i, c = 16 * h + lr;
+        wv[h][i] = ld0(Xf, (NB * j + c) * ns + NB * p + r, j < qa && r < rows);
+      }
+#pragma unroll
+    for (int term = 0; term < 2; ++term) {
+      const int qq = term == 0 ? qa : qb;
+      if (qq < j) continue;  // X_qj = 0 above the diagonal (uniform)
+      double lq[8], xq[4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+        lq[u] = ld0(L, (NB * qq + c) * m + NB * p + r, r < rows);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = tid + 256 * u, k = e & (NB - 1), c = e >> 5;
+        xq[u] = Xf[(NB * j + c) * ns + NB * qq + k];
+      }
+      __syncthreads();  // the previous term's reads of Ls / Xs are done
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+        Ls[r * PS + c] = lq[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = tid + 256 * u, k = e & (NB - 1), c = e >> 5;
+        Xs[k * PS + c] = xq[u];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        const double a = Ls[(16 * w + lr) * PS + k];
+        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Xs[k * PS + lr], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Xs[k * PS + 16 + lr], acc[1], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[h][i] += wv[h][i];
+    if (!fin) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * w + lk + 4 * i, c = 16 * h + lr;
+          if (r < rows) Xf[(size_t)(NB * j + c) * ns + NB * p + r] = acc[h][i];
+        }
+      return;
+    }
+    double lv[3][NB * NB / 256];
+    load_li3(la, ln, lb, bh, tid, lv);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Wl[(16 * w + lk + 4 * i) * (NB + 1) + 16 * h + lr] = acc[h][i];
+    store_li3(Li3, tid, lv);
+    __syncthreads();
+    // wave w: rows 16 w .. of X_p (w < 2: -A W_top) or X_p+1 (w >= 2: -(N W_top + B W_bot))
+    dx4 xo[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+    const int wr = 16 * (w & 1);
+    const double* L1 = w < 2 ? Li3 : Li3 + NB * PS;
+#pragma unroll
+    for (int kk = 0; kk < NB / 4; ++kk) {
+      const int k = kk * 4 + lk;
+      const double a = L1[(wr + lr) * PS + k];
+      xo[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[k * (NB + 1) + lr], xo[0], 0, 0, 0);
+      xo[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[k * (NB + 1) + 16 + lr], xo[1], 0, 0, 0);
+    }
+    if (w >= 2) {
+#pragma unroll
+      for (int kk = 0; kk < NB / 4; ++kk) {
+        const int k = kk * 4 + lk;
+        const double a = Li3[2 * NB * PS + (wr + lr) * PS + k];
+        xo[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[(NB + k) * (NB + 1) + lr], xo[0], 0, 0, 0);
+        xo[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[(NB + k) * (NB + 1) + 16 + lr], xo[1], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * w + lk + 4 * i, c = 16 * h + lr;
+        if (r < rows) Xf[(size_t)(NB * j + c) * ns + NB * p + r] = -xo[h][i];
+      }
+    return;
+  }
+
+  // ---- tile task (I, J): rows I0 = r0 + 64 ti, columns J0 = r0 + 64 tj
+  const int ti = t.tile & 0xffff, tj = t.tile >> 16;
+  const bool upd = t.flags & 1, writer = tj == 0;
+  const int I0 = r0 + ti * TT, J0 = r0 + tj * TT;
+  double* Pa = sm + W64_R;
+  double* Pb = Pa + TT * PS;
+  double* yk = sm + W64_YK;
+  const int climit = t.clim;
+  double lv[3][NB * NB / 256], pa0[8], pb0[8], pa1[8], pb1[8], cv[16];
+  load_li3(la, ln, lb, bh, tid, lv);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+    pa0[u] = ld0(F, (k0 + c) * m + I0 + r, c < kb && I0 + r < m);
+    pb0[u] = ld0(F, (k0 + c) * m + J0 + r, upd && c < kb && J0 + r < m);
+    pa1[u] = ld0(F, (k0 + NB + c) * m + I0 + r, c < kbb && I0 + r < m);
+    pb1[u] = ld0(F, (k0 + NB + c) * m + J0 + r, upd && c < kbb && J0 + r < m);
+  }
+  const double ykv = ld0(ysol, t.c0 + k0 + tid, tid < kb);
+  store_li3(Li3, tid, lv);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+    Pa[r * PS + c] = pa0[u];
+    Pb[r * PS + c] = pb0[u];
+  }
+  if (tid < TT) yk[tid] = ykv;
+  if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
+  __syncthreads();
+  // X_a = P_a A^T and P_a N^T for the rows of I and J (wave w: rows 16 w ..)
+  dx4 xia[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}}, xja[2] = {xia[0], xia[0]}, xib[2] = {xia[0], xia[0]},
+      xjb[2] = {xia[0], xia[0]};
+  trsm_half(Pa, Li3, lane, w, xia);
+  if (upd) trsm_half(Pb, Li3, lane, w, xja);
+  if (bh) {
+    trsm_half(Pa, Li3 + NB * PS, lane, w, xib);
+    if (upd) trsm_half(Pb, Li3 + NB * PS, lane, w, xjb);
+  }
+  __syncthreads();
+  if (bh) {  // X_b = P_a N^T + P_b B^T
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
+      Pa[r * PS + c] = pa1[u];
+      Pb[r * PS + c] = pb1[u];
+    }
+    __syncthreads();
+    trsm_half(Pa, Li3 + 2 * NB * PS, lane, w, xib);
+    if (upd) trsm_half(Pb, Li3 + 2 * NB * PS, lane, w, xjb);
+    __syncthreads();
+  }
+  PH1(2)
+  // rows / columns of the next diagonal block [r0, r0 + kbn): its diagonal task applies this panel itself
+  const int kbn = max(0, min(TT, ns - r0));
+  MfmaTile T;
+  T.zero();
+  double s2 = 0.0;  // writers: X_I y_p
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 1 && !bh) break;
+    store_xhalf(Pa, lane, w, h == 0 ? xia : xib);
+    if (upd) store_xhalf(Pb, lane, w, h == 0 ? xja : xjb);
+    __syncthreads();
+    if (writer) {
+      if (tid < TT) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) s2 += Pa[tid * PS + q] * yk[NB * h + q];
+      }
+      const int qn = h == 0 ? min(NB, kb) : kbb;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
+        if (q < qn && I0 + r < m) L[(size_t)(k0 + NB * h + q) * m + I0 + r] = Pa[r * PS + q];
+      }
+    }
+    if (upd) T.step(Pa, Pb, lane, w);
+    __syncthreads();
+  }
+  if (writer && tid < TT && I0 + tid < m && I0 + tid >= r0 + kbn) v[I0 + tid] -= s2;
+  PH1(3)
+  if (!upd) { PH1R(7) return; }
+  T.store(Pa, lane, w);
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
+    const int gi = I0 + r, gj = J0 + c;
+    const bool dblk = gi < r0 + kbn && gj < r0 + kbn;
+    if (gi < m && gj < climit && gi >= gj && !dblk) F[(size_t)gj * m + gi] = cv[u] - Pa[r * CS + c];
   }
   PH1(4)
   PH1R(7)
@@ -1558,18 +2171,17 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const int* perm, const doub
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
-                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
-                     int assemble, hipStream_t s) {
+                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* linvn, double* xinv,
+                     int* fail, int assemble, bool w64, hipStream_t s) {
   if (ntasks <= 0) return;
-  if (assemble == 2)  // fronts up to 512 rows: a small column buffer keeps more workgroups per CU
-    hipLaunchKernelGGL((k_extend_add<true, 512>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment,
-                       colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
-  else if (assemble)
-    hipLaunchKernelGGL((k_extend_add<true, 2048>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, colptr, ent_row, ent_src, vals,
-                       lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
-  else
-    hipLaunchKernelGGL((k_extend_add<false, 1>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, colptr, ent_row, ent_src, vals,
-                       lam, fronts, vecs, lbuf, ysol, linv, xinv, fail);
+#define G2OHIP_EA(A_, E_, W_)                                                                                        \
+  hipLaunchKernelGGL((k_extend_add<A_, E_, W_>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, \
+                     colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, linvn, xinv, fail)
+  // assemble 2: fronts up to 512 rows (a small column buffer keeps more workgroups per CU)
+  if (assemble == 2) { if (w64) G2OHIP_EA(true, 512, true); else G2OHIP_EA(true, 512, false); }
+  else if (assemble) { if (w64) G2OHIP_EA(true, 2048, true); else G2OHIP_EA(true, 2048, false); }
+  else { if (w64) G2OHIP_EA(false, 1, true); else G2OHIP_EA(false, 1, false); }
+#undef G2OHIP_EA
   KERNEL_CHECK();
 }
 void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs,
@@ -1579,6 +2191,12 @@ void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* 
     hipLaunchKernelGGL(k_step<true>, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   else
     hipLaunchKernelGGL(k_step<false>, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
+  KERNEL_CHECK();
+}
+void chol_step64(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs,
+                 double* ysol, double* linv, double* linvn, double* xinv, int* fail, hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_step64, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, linvn, xinv, fail);
   KERNEL_CHECK();
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {

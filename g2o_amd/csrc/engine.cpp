@@ -306,6 +306,29 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     for (int sn : sym.levels[l]) { lcols += sym.sn[sn].ns + sym.sn[sn].nr; sn_level[sn] = (int)l; }
     level_slab[l] = lcols >= 16LL * launch::CHOL_EA * 256 ? launch::CHOL_EA : 4;
   }
+  // 64-column panel steps (k_step64, G2OHIP_CHOL_W64=1) on every level none of whose fronts would be blocked (the wide /
+  // big-panel rules below)
+  sn_w64.assign(sym.sn.size(), 0);
+  n_w64_levels = 0;
+  {
+    const char* ew = getenv("G2OHIP_CHOL_W64");
+    // off by default: at C4 the 64-column steps measured break-even on the chain-bound levels (18.8 us per 64 columns
+    // against 2 x 9.2) and slower on the throughput-bound ones
+    const bool w64_on = ew && atoi(ew) != 0 && !(getenv("G2OHIP_CHOL_DAG") && atoi(getenv("G2OHIP_CHOL_DAG")) != 0);
+    const char* bm = getenv("G2OHIP_CHOL_BLOCK_MIN");
+    const int block_min = bm ? atoi(bm) : 512;
+    const char* wf = getenv("G2OHIP_CHOL_WIDE_FRONTS");
+    const int wide_fronts = wf ? atoi(wf) : 64;
+    const char* wp = getenv("G2OHIP_CHOL_WIDE_PB");
+    const int wide_pb = wp ? std::max(64, atoi(wp) / 64 * 64) : 128;
+    for (const auto& lv : sym.levels) {
+      int mx = 0;
+      for (int sn : lv) mx = std::max(mx, sym.sn[sn].ns);
+      const bool ok = w64_on && mx <= ((int)lv.size() >= wide_fronts ? wide_pb : block_min);
+      for (int sn : lv) sn_w64[sn] = ok;
+      n_w64_levels += ok;
+    }
+  }
   // ---- distribution over ranks (landmark-sharded BA): cut the elimination tree into a shared top and whole subtrees,
   // each subtree owned by one rank. Candidate cuts: starting from the tree's roots, the candidate subtree with the
   // largest serial work is split (its root joins the shared top), one cut per split, up to 4 candidates per rank; each
@@ -482,7 +505,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     int jt = 0;
     if (q.parent >= 0) {
       const Supernode& pq = sym.sn[q.parent];
-      const int mp = pq.ns + pq.nr, slab = level_slab[sn_level[q.parent]], kb0 = std::min(launch::CHOL_NB, pq.ns);
+      const int mp = pq.ns + pq.nr, slab = level_slab[sn_level[q.parent]];
+      const int kb0 = std::min(sn_w64[q.parent] ? launch::CHOL_TT : launch::CHOL_NB, pq.ns);
       const int* rel = sym.relmap.data() + q.rows_off;
       jt = (int)hjt.size();
       hjt.push_back((int)(std::lower_bound(rel, rel + q.nr, kb0) - rel));
@@ -664,6 +688,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         for (int a = 0; a < m; a += slab) tk.push_back(Task{sn, a, std::min(a + slab, m), 2 + a / slab});
       }
       ea.count = (int)tk.size() - ea.off;
+      ea.w64 = sn_w64[lv[0]];
       ops.push_back(ea);
       op_front_off.push_back(0);
       if (dag) {
@@ -720,6 +745,55 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         ops.push_back(dg);
         op_front_off.push_back(f0);
         ++n_dag_levels;
+        continue;
+      }
+      if (sn_w64[lv[0]]) {
+        // 64-column panel steps (cholesky.hip k_step64): per launch the next 64 x 64 diagonal block, the rank-64 tiles
+        // of the current panel (into the contribution block when fused) and X = L11^-1 for the previous panel
+        int maxq = 0;
+        for (int sn : lv) maxq = std::max(maxq, (sym.sn[sn].ns + TT - 1) / TT);
+        for (int p = 0; p < maxq; ++p) {
+          Op st{9, (int)stk.size(), 0};
+          std::vector<launch::StepTask> diag_t, tile_t, inv_t;
+          for (int sn : lv) {
+            const Supernode& q = sym.sn[sn];
+            const int k0 = p * TT;
+            if (k0 >= q.ns) continue;
+            const int kb = std::min(TT, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
+            const int clim = fused_contrib ? m : q.ns;
+            const int T = (m - r0 + TT - 1) / TT, TJ = (clim - r0 + TT - 1) / TT;
+            auto mk = [&](int tile, int flags) {
+              return launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns, q.c0,
+                                      k0 | (kb << 16), tile, flags, clim};
+            };
+            if (r0 < q.ns) diag_t.push_back(mk(0, 4));
+            for (int tj = 0; tj < std::max(TJ, 1); ++tj)
+              for (int ti = tj; ti < T; ++ti) tile_t.push_back(mk(ti | (tj << 16), (tj < TJ ? 1 : 0) | (fused_contrib ? 8 : 0)));
+            // X = L11^-1: the previous panel's 32-blocks (2p - 2, 2p - 1) into every pending block row >= 2p + 2, and
+            // block rows 2p, 2p + 1 (this panel) final
+            const int nblk = (q.ns + NB - 1) / NB;
+            if (p >= 1 && !dev_noinv)
+              for (int bp = 2 * p; bp < nblk; ++bp) {
+                if (bp == 2 * p + 1) continue;  // finalised with row 2p
+                for (int j = 0; j < 2 * p; ++j) inv_t.push_back(mk(j | (bp << 16), 16));
+              }
+          }
+          stk.insert(stk.end(), diag_t.begin(), diag_t.end());
+          if (!dev_diagonly) stk.insert(stk.end(), tile_t.begin(), tile_t.end());
+          if (!dev_diagonly) stk.insert(stk.end(), inv_t.begin(), inv_t.end());
+          st.count = (int)stk.size() - st.off;
+          if (st.count) { ops.push_back(st); op_front_off.push_back(0); }
+        }
+        Op sy{3, (int)tk.size(), 0};
+        for (int sn : lv) {
+          if (fused_contrib) break;
+          const Supernode& q = sym.sn[sn];
+          const int T = (q.nr + TT - 1) / TT;
+          for (int tj = 0; tj < T; ++tj)
+            for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, 0, ti | (tj << 16), 0});
+        }
+        sy.count = (int)tk.size() - sy.off;
+        if (sy.count) { ops.push_back(sy); op_front_off.push_back(0); ++n_syrk_ops; }
         continue;
       }
       int maxp = 0;
@@ -928,7 +1002,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
     heads.assign(ops.size(), launch::StepHead{});
     for (size_t k = 0; k < ops.size(); ++k) {
-      if (ops[k].kind != 2 && ops[k].kind != 6) continue;
+      if (ops[k].kind != 2 && ops[k].kind != 6 && ops[k].kind != 9) continue;
       launch::StepHead& h = heads[k];
       h.n = 0;
       while (h.n < launch::CHOL_HEAD && h.n < ops[k].count) {  // the first workgroups (diagonal tasks among them)
@@ -947,6 +1021,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   y_p.resize(std::max(sym.n, 1));
   lbuf.resize(std::max<long long>(lpool, 1));
   linv.resize((size_t)(sym.n + launch::CHOL_NB) * launch::CHOL_NB * launch::CHOL_NB);  // one 32x32 L_kk^-1 per panel start
+  linvn.resize(n_w64_levels ? (size_t)(sym.n + launch::CHOL_NB) * launch::CHOL_NB * launch::CHOL_NB : 1);
   xinv.resize(std::max<long long>(xoff, 1));
   t_p.resize(std::max(sym.n, 1));
   x_p.resize(std::max(sym.n, 1));
@@ -968,7 +1043,11 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
                                       cment.get(), colptr.get(),
                                       ent_row.get(),
                                       ent_src.get(), vals, lam, fronts.get(), vecs.get(),
-                                      lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 0 ? 0 : (op.kind == 5 ? 2 : 1), s); break;
+                                      lbuf.get(), y_p.get(), linv.get(), linvn.get(), xinv.get(), fail,
+                                      op.kind == 0 ? 0 : (op.kind == 5 ? 2 : 1), op.w64 != 0, s); break;
+      case 9: launch::chol_step64(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
+                                  vecs.get(), y_p.get(), linv.get(), linvn.get(), xinv.get(), fail, s);
+        break;
       case 2:
       case 6: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
                                 vecs.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 6, s);
@@ -3192,7 +3271,8 @@ int Engine::factor_info(double* out, int n) {
                       (double)chol.n_dag_levels, (double)chol.n_owned_fronts, (double)chol.n_shared_fronts,
                       (double)chol.n_roots, (double)chol.xch_len, chol.dist_model[0], chol.dist_model[1],
                       chol.dist_model[2], chol.dist_model[3], chol.dist_model[4], chol.rs_on ? 1.0 : 0.0,
-                      (double)chol.rs_seg, (double)chol.rs_tail_len, chol.rs_model[0], chol.rs_model[1]};
+                      (double)chol.rs_seg, (double)chol.rs_tail_len, chol.rs_model[0], chol.rs_model[1],
+                      (double)chol.n_w64_levels};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;

@@ -117,8 +117,9 @@ struct DeviceCholesky {
   // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
   // trailing-update (k_syrk) launches, big-panel backward rounds
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0, n_dag_levels = 0;
-  struct Op { int kind, off, count, tpw = 1; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add,
-                                                 // 2 panel step (6: with lagged-pair tasks), 3 syrk, 7 tile DAG
+  struct Op { int kind, off, count, tpw = 1, w64 = 0; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add,
+                                                 // 2 panel step (6: with lagged-pair tasks), 3 syrk, 7 tile DAG,
+                                                 // 9 64-column panel step; w64: extend-add of a 64-column level
                                                  // (off: first worker's tile slots, off2 fronts), tpw tiles per worker
   std::vector<int> op_front_off;  // per op: first DagFront of a kind-7 op
   // persistent tile DAG of latency-bound levels (cholesky.hip k_dag)
@@ -168,6 +169,9 @@ struct DeviceCholesky {
   DevBuf<launch::Task> tasks;
   DevBuf<launch::StepTask> step_tasks;
   DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, t_p, lbuf, linv, xinv;
+  DevBuf<double> linvn;              // 64-column levels: N = -L_b^-1 L_ba L_a^-1 per 64-panel start (32 x 32, row-major)
+  std::vector<char> sn_w64;          // per supernode: its level runs 64-column panel steps (k_step64)
+  int n_w64_levels = 0;
   long long lpool = 0;
   void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
   // numeric LL^T fused with the forward solve of rhs (y = L^-1 P rhs)

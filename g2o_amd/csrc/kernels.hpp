@@ -179,8 +179,12 @@ void chol_vec_init(int nfronts, const FrontDesc* fd, const int* perm, const doub
 // column c (permuted): ent_row/ent_src[colptr[c] .. colptr[c+1]) = row in the front | diag << 30, index in vals
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
-                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv, int* fail,
-                     int assemble, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place, 2 in place (m <= 512)
+                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* linvn, double* xinv,
+                     int* fail, int assemble, bool w64, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place,
+                                                                         // 2 in place (m <= 512); w64: 64-column level
+// 64-column panel steps (cholesky.hip k_step64): linvn holds N = -L_b^-1 L_ba L_a^-1 per 64-panel start
+void chol_step64(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs,
+                 double* ysol, double* linv, double* linvn, double* xinv, int* fail, hipStream_t s);
 void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs, double* ysol,
                double* linv, double* xinv, int* fail, bool pairs, hipStream_t s);  // pairs: lagged-pair tasks present
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is

@@ -338,13 +338,15 @@ def test_ba_assembly_paths(g2o_amd_mod, oracle, monkeypatch, fused):
         _check(*_run_both(g2o_amd_mod, oracle, prob, 4))
 
 
-@pytest.mark.parametrize("mode", ["0", "2"], ids=["panel_steps_only", "tile_dag_every_fitting_level"])
+@pytest.mark.parametrize("mode", ["0", "2", "w64"], ids=["panel_steps_only", "tile_dag_every_fitting_level", "w64_steps"])
 @pytest.mark.parametrize("name", ["C1", "C2", "C3", "C4", "C5"])
 def test_factor_schedules(g2o_amd_mod, oracle, monkeypatch, name, mode):
-    """Both factorization schedules of a tree level against the oracle: the launch-per-panel steps (G2OHIP_CHOL_DAG=0)
-    and the persistent tile DAG (k_dag) on every level whose tiles fit the resident workgroups (=2; the default uses it
-    on the latency-bound levels only). Reduced system, solution and an LM trajectory."""
-    monkeypatch.setenv("G2OHIP_CHOL_DAG", mode)
+    """The factorization schedules of a tree level against the oracle: the launch-per-panel 32-column steps
+    (G2OHIP_CHOL_DAG=0), the persistent tile DAG (k_dag) on every level whose tiles fit the resident workgroups (=2) and
+    the 64-column panel steps (k_step64, G2OHIP_CHOL_W64=1, every unblocked level). Reduced system, solution and an LM
+    trajectory."""
+    monkeypatch.setenv("G2OHIP_CHOL_DAG", "0" if mode == "w64" else mode)
+    monkeypatch.setenv("G2OHIP_CHOL_W64", "1" if mode == "w64" else "0")
     prob = synth.by_name(name, "small")
     opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
     ref = oracle.OracleGraph(prob)
@@ -355,6 +357,7 @@ def test_factor_schedules(g2o_amd_mod, oracle, monkeypatch, name, mode):
         assert np.linalg.norm(g[k] - r[k]) <= 1e-9 * np.linalg.norm(r[k]), k
     info = opt.factor_info()
     assert (info["dag_levels"] > 0) == (mode == "2"), info
+    assert (info["w64_levels"] > 0) == (mode == "w64"), info
     opt.build_system()
     opt.set_lambda(1e-3)
     assert opt.solve()

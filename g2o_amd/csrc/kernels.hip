@@ -519,6 +519,75 @@ __global__ void __launch_bounds__(256)
   So[r * PD + cc] = o;
 }
 
+// The pairs of one staged batch into a Schur row task's accumulators: thread (slot ls, q) owns columns c0 .. c0 + CW - 1
+// (c0 = (q & 1) CW) of the slot's block over the slot's pairs of parity q >> 1 (landmark order): acc(j, r) +=
+// G_a(r, :) . G_b(c0 + j, :). Gs: the batch's blocks (PD x LD col-major each), sp: pairs (posA | posB << 16) slot-sorted,
+// spp: the slot CSR.
+template <int PD, int LD>
+__device__ __forceinline__ void schur_pairs(const double* Gs, const int* sp, const int* spp, int noff, int ls, int q,
+                                            double (&acc)[((PD + 1) / 2) * PD]) {
+  constexpr int GB = PD * LD, CW = (PD + 1) / 2;
+  const int c0 = (q & 1) * CW, par = q >> 1;
+  if (ls >= noff) return;
+  const int p1 = spp[ls + 1];
+  for (int p = spp[ls] + par; p < p1; p += 2) {
+    const int pr = sp[p];
+    const double* ga = &Gs[(pr & 0xffff) * GB];
+    const double* gb = &Gs[(pr >> 16) * GB + c0];
+#pragma unroll
+    for (int kk = 0; kk < LD; ++kk) {  // one column of G_a and CW entries of G_b at a time
+      double A[PD], Bm[CW];
+      if constexpr (PD % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < PD / 2; ++k) {
+          const double2 x = *reinterpret_cast<const double2*>(ga + kk * PD + 2 * k);
+          A[2 * k] = x.x; A[2 * k + 1] = x.y;
+        }
+#pragma unroll
+        for (int j = 0; j < CW; ++j) Bm[j] = gb[kk * PD + j];
+      } else {  // odd PD: the second half has CW - 1 columns (the spare one reads column c0 and is zeroed)
+#pragma unroll
+        for (int r = 0; r < PD; ++r) A[r] = ga[kk * PD + r];
+#pragma unroll
+        for (int j = 0; j < CW; ++j) {
+          const bool in = c0 + j < PD;
+          const double v = gb[kk * PD + (in ? j : 0)];
+          Bm[j] = in ? v : 0.0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < CW; ++j)
+#pragma unroll
+        for (int r = 0; r < PD; ++r) acc[j * PD + r] += A[r] * Bm[j];
+    }
+  }
+}
+// Even + odd pairs (fixed order) and the S block store: thread (h, par) stores rows [0, CW) (par 0) or [CW, PD) (par 1)
+// of its columns; S(i, j) = Hpp(i, j) - sum
+template <int PD>
+__device__ __forceinline__ void schur_row_store(double (&acc)[((PD + 1) / 2) * PD], int ls, int q, int noff, int soff,
+                                                const int* s_hpp, const double* Hpp, double* S) {
+  constexpr int CW = (PD + 1) / 2;
+  const int c0 = (q & 1) * CW, par = q >> 1;
+#pragma unroll
+  for (int k = 0; k < CW * PD; ++k) acc[k] += __shfl_xor(acc[k], 2, 4);
+  if (ls < noff) {
+    const int sidx = soff + ls;
+    const int hp = s_hpp[sidx];
+    const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * PD * PD;
+    double* So = S + (size_t)sidx * PD * PD;
+#pragma unroll
+    for (int j = 0; j < CW; ++j)
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        if ((r >= CW) != (par == 1)) continue;
+        if (PD % 2 != 0 && c0 + j >= PD) continue;
+        const int k = (c0 + j) * PD + r;
+        So[k] = (hp >= 0 ? Hh[k] : 0.0) - acc[j * PD + r];
+      }
+  }
+}
+
 // Off-diagonal blocks, row-stationary (block_solver.hpp:361-391, j > i): one workgroup per (camera
 // row i, chunk of up to 64 off-diagonal slots of the row's Schur pattern). The row's landmarks are
 // walked in landmark order in batches; a batch stages the G blocks (G = Hpl U^-T, written once per
@@ -597,43 +666,7 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
       }
     }
   };
-  // thread q of a slot: columns c0 .. c0 + CW - 1 of the block (h = q & 1) over the pairs of parity q >> 1
-  const int c0 = (q & 1) * CW, par = q >> 1;
-  auto compute = [&](int buf) {
-    if (ls >= t.noff) return;
-    const int p1 = spp[buf][ls + 1];
-    for (int p = spp[buf][ls] + par; p < p1; p += 2) {
-      const int pr = sp[buf][p];
-      const double* ga = &Gs[buf][(pr & 0xffff) * GB];
-      const double* gb = &Gs[buf][(pr >> 16) * GB + c0];
-#pragma unroll
-      for (int kk = 0; kk < LD; ++kk) {  // one column of G_a and CW entries of G_b at a time
-        double A[PD], Bm[CW];
-        if constexpr (PD % 2 == 0) {
-#pragma unroll
-          for (int k = 0; k < PD / 2; ++k) {
-            const double2 x = *reinterpret_cast<const double2*>(ga + kk * PD + 2 * k);
-            A[2 * k] = x.x; A[2 * k + 1] = x.y;
-          }
-#pragma unroll
-          for (int j = 0; j < CW; ++j) Bm[j] = gb[kk * PD + j];
-        } else {  // odd PD: the second half has CW - 1 columns (the spare one reads column c0 and is zeroed)
-#pragma unroll
-          for (int r = 0; r < PD; ++r) A[r] = ga[kk * PD + r];
-#pragma unroll
-          for (int j = 0; j < CW; ++j) {
-            const bool in = c0 + j < PD;
-            const double v = gb[kk * PD + (in ? j : 0)];
-            Bm[j] = in ? v : 0.0;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < CW; ++j)
-#pragma unroll
-          for (int r = 0; r < PD; ++r) acc[j * PD + r] += A[r] * Bm[j];
-      }
-    }
-  };
+  auto compute = [&](int buf) { schur_pairs<PD, LD>(Gs[buf], sp[buf], spp[buf], t.noff, ls, q, acc); };
 
   // Invariant at the top of iteration k: Gs[k&1] holds batch k (landed), so/sp/spp[k&1] its indices
   // and pair list, so/sp/spp[(k+1)&1] those of batch k+1; B1, B2 = records k+1, k+2 (already landed:
@@ -662,24 +695,7 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     B1 = B2;
     B2 = B3;
   }
-  // even + odd pairs (fixed order); thread (h, par) stores rows [0, CW) (par 0) or [CW, PD) (par 1) of its columns
-#pragma unroll
-  for (int k = 0; k < CW * PD; ++k) acc[k] += __shfl_xor(acc[k], 2, 4);
-  if (ls < t.noff) {
-    const int sidx = t.soff + ls;
-    const int hp = s_hpp[sidx];
-    const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * PD * PD;
-    double* So = S + (size_t)sidx * PD * PD;
-#pragma unroll
-    for (int j = 0; j < CW; ++j)
-#pragma unroll
-      for (int r = 0; r < PD; ++r) {
-        if ((r >= CW) != (par == 1)) continue;
-        if (PD % 2 != 0 && c0 + j >= PD) continue;
-        const int k = (c0 + j) * PD + r;
-        So[k] = (hp >= 0 ? Hh[k] : 0.0) - acc[j * PD + r];
-      }
-  }
+  schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S);
 }
 
 // back-substitution: x_l = Dinv_l (b_l - sum_a Hpl_a^T x_pose(a)); LANES lanes per landmark stride over

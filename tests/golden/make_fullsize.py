@@ -1,4 +1,5 @@
-"""Full-size BASELINE fixtures (C2, C3, C4, C5) for the -m gpu parity tests.
+"""Full-size BASELINE fixtures (C2, C3, C4, C5, and C4R: C4 with random covisibility, a dense reduced camera system)
+for the -m gpu parity tests.
 
 C4 covers the exact sequence bench.py times (iteration 0 with the structure, then 29 more: the driver runs
 --warmup 5 --steps 20, the default is 5 + 30 minus the untimed stage iterations), C2 / C3 / C5 at least 5 iterations.
@@ -9,7 +10,7 @@ trajectory (chi2 / lambda / trials per iteration, reference CSparse cs_amd block
 cs_chol) and the final minimal state (C2, C3: the whole state; C5: the cameras, a fixed stride of
 the points and per-chunk sums of all point coordinates, to keep the file small).
 
-    python tests/golden/make_fullsize.py C2 C3 C4 C5
+    python tests/golden/make_fullsize.py C2 C3 C4 C5 C4R
 """
 import os
 import sys
@@ -26,7 +27,7 @@ import oracle_py  # noqa: E402
 from g2o_amd import synth  # noqa: E402
 
 # name -> LM iterations recorded
-ITERS = {"C2": 6, "C3": 5, "C4": 30, "C5": 5}
+ITERS = {"C2": 6, "C3": 5, "C4": 30, "C5": 5, "C4R": 3}
 C5_POINT_STRIDE = 97      # every 97th point's coordinates stored exactly
 C5_CHUNK = 4096           # per-chunk sums of the point block of the minimal state
 

@@ -1,4 +1,4 @@
-"""BASELINE configs C2, C3 and C5 at their full sizes on the GPU.
+"""BASELINE configs C2, C3, C4, C5 and C4's random-covisibility variant at their full sizes on the GPU.
 
 Trajectories are compared with committed fixtures of the oracle run with the reference's own CSparse
 (cs_amd block ordering + cs_chol), generated in the development container by
@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 RTOL = 1e-6
-ALG = {"C2": "lm_hip_fix3_3", "C3": "lm_hip_fix6_6", "C4": "lm_hip_fix6_3", "C5": "lm_hip_fix6_3"}
+ALG = {"C2": "lm_hip_fix3_3", "C3": "lm_hip_fix6_6", "C4": "lm_hip_fix6_3", "C5": "lm_hip_fix6_3", "C4R": "lm_hip_fix6_3"}
 
 
 def _fixture(name):
@@ -129,6 +129,25 @@ def test_c4_bench_sequence(g2o_amd_mod):
     _check_trajectory(fx, st, n, chi0)
     x, xr = opt.minimal_state(), fx["state"]
     assert np.linalg.norm(x - xr) <= RTOL * np.linalg.norm(xr)
+
+
+def test_c4r_full_random_covisibility(g2o_amd_mod):
+    """SURVEY.md §8d's C4 variant covis=random at full size (1k cameras x 100k points x 1M observations, every point
+    seen by 10 of ALL 1000 cameras): the reduced camera system is dense (6000 x 6000, 72 GFLOP per factorization), one
+    front takes the blocked dense-front schedule (big panels, rank-256 k_syrk trailing updates). Trajectory (chi2,
+    lambda, trial counts) and final state against the oracle + reference CSparse fixture."""
+    fx = _fixture("C4R")
+    prob = synth.by_name("C4R")
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm(ALG["C4R"])
+    chi0 = opt.chi2()
+    assert abs(chi0 - float(fx["chi2_0"])) <= 1e-9 * float(fx["chi2_0"])
+    n, st = opt.optimize(int(fx["iterations"]))
+    _check_trajectory(fx, st, n, chi0)
+    x, xr = opt.minimal_state(), fx["state"]
+    assert np.linalg.norm(x - xr) <= RTOL * np.linalg.norm(xr)
+    info = opt.factor_info()
+    assert info["blocked_fronts"] >= 1 and info["max_front"] >= 5000, info
 
 
 @pytest.mark.parametrize("name,lam", [("C2", 1e-3), ("C3", 1e-3), ("C4", 1e-2), ("C5", 1e-2)])

@@ -459,12 +459,13 @@ class SparseOptimizer:
 
     @staticmethod
     def comm_selftest(values, device: int = 0):
-        """RCCL binding smoke test on one device (one-rank communicator): [allreduce sum | allreduce max]."""
+        """RCCL binding smoke test on one device (one-rank communicator): allreduce sum, allreduce max and the
+        in-place reduce-scatter sum (rank 0's segment), each over `values`."""
         v = np.ascontiguousarray(values, np.float64)
-        out = np.zeros(2 * v.size)
+        out = np.zeros(3 * v.size)
         uid = (C.c_ubyte * 128).from_buffer_copy(SparseOptimizer.comm_unique_id())
         _check(lib().g2ohip_comm_selftest(device, uid, v.size, _p(v), _p(out)), "comm_selftest")
-        return out[: v.size], out[v.size:]
+        return out[: v.size], out[v.size: 2 * v.size], out[2 * v.size:]
 
     def set_comm(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_ubyte * 128).from_buffer_copy(uid)

@@ -322,12 +322,12 @@ int g2ohip_comm_selftest(int device, const unsigned char uid[128], int n, const 
     hipStream_t s = nullptr;
     HIP_CHECK(hipStreamCreate(&s));
     double* d = nullptr;
-    HIP_CHECK(hipMalloc(&d, sizeof(double) * 2 * (size_t)n));
-    HIP_CHECK(hipMemcpyAsync(d, in, sizeof(double) * n, hipMemcpyHostToDevice, s));
-    HIP_CHECK(hipMemcpyAsync(d + n, in, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMalloc(&d, sizeof(double) * 3 * (size_t)n));
+    for (int k = 0; k < 3; ++k) HIP_CHECK(hipMemcpyAsync(d + (size_t)k * n, in, sizeof(double) * n, hipMemcpyHostToDevice, s));
     c->allreduce_sum(d, (size_t)n, s);
     c->allreduce_max(d + n, (size_t)n, s);
-    HIP_CHECK(hipMemcpyAsync(out, d, sizeof(double) * 2 * (size_t)n, hipMemcpyDeviceToHost, s));
+    c->reduce_scatter_sum(d + 2 * (size_t)n, (size_t)n, s);  // in place: rank r's segment is [r n, (r + 1) n)
+    HIP_CHECK(hipMemcpyAsync(out, d, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     HIP_CHECK(hipFree(d));
     HIP_CHECK(hipStreamDestroy(s));

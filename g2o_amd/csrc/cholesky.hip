@@ -102,23 +102,34 @@ __global__ void __launch_bounds__(256) k_zero_ranges(const long long* __restrict
   const long long off = rng[2 * blockIdx.x], len = rng[2 * blockIdx.x + 1];
   for (long long i = threadIdx.x; i < len; i += 256) fronts[off + i] = 0.0;
 }
-__global__ void __launch_bounds__(256) k_chol_scatter(long long nent, const double* __restrict__ vals,
+// front vectors: v_s = [P rhs (own columns); 0], the permutation applied on the fly (one workgroup per front)
+__device__ __forceinline__ void vec_init_front(const FrontDesc* __restrict__ fd, int f, const int* __restrict__ perm,
+                                               const double* __restrict__ rhs, double* __restrict__ vecs) {
+  const FrontDesc me = fd[f];
+  const int m = me.ns + me.nr;
+  double* v = vecs + me.vec_off;
+  for (int i = threadIdx.x; i < m; i += 256) v[i] = i < me.ns ? rhs[perm[me.c0 + i]] : 0.0;
+}
+__global__ void __launch_bounds__(256) k_vec_init(const FrontDesc* __restrict__ fd, const int* __restrict__ perm,
+                                                  const double* __restrict__ rhs, double* __restrict__ vecs) {
+  vec_init_front(fd, blockIdx.x, perm, rhs, vecs);
+}
+// the input entries of the prescattered levels; the workgroups past the entries' own (nsb) initialise the front
+// vectors, one per front (disjoint data, one launch instead of two at the start of every factorization)
+__global__ void __launch_bounds__(256) k_chol_scatter(long long nent, int nsb, const double* __restrict__ vals,
                                                       const long long* __restrict__ dst, const int* __restrict__ src,
-                                                      const double* __restrict__ lam, double* __restrict__ fronts) {
+                                                      const double* __restrict__ lam, double* __restrict__ fronts,
+                                                      const FrontDesc* __restrict__ fd, const int* __restrict__ perm,
+                                                      const double* __restrict__ rhs, double* __restrict__ vecs) {
+  if ((int)blockIdx.x >= nsb) {
+    vec_init_front(fd, (int)blockIdx.x - nsb, perm, rhs, vecs);
+    return;
+  }
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nent) return;
   const int sr = src[k];
   const double v = vals[sr & 0x7fffffff];
   fronts[dst[k]] = sr < 0 ? v + *lam : v;
-}
-
-// front vectors: v_s = [P rhs (own columns); 0], the permutation applied on the fly
-__global__ void __launch_bounds__(256) k_vec_init(const FrontDesc* __restrict__ fd, const int* __restrict__ perm,
-                                                  const double* __restrict__ rhs, double* __restrict__ vecs) {
-  const FrontDesc me = fd[blockIdx.x];
-  const int m = me.ns + me.nr;
-  double* v = vecs + me.vec_off;
-  for (int i = threadIdx.x; i < m; i += 256) v[i] = i < me.ns ? rhs[perm[me.c0 + i]] : 0.0;
 }
 
 // ---------------------------------------------------------------------------- wave helpers
@@ -833,7 +844,8 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   __shared__ double vn[NB];
   PH_BEGIN(2)
   PH1_BEGIN(3)
-  const StepTask t = (int)blockIdx.x < head.n ? head.t[blockIdx.x] : tasks[blockIdx.x];
+  const int bid = (int)blockIdx.x < head.xcd_from ? (int)blockIdx.x : xcd_item_from(blockIdx.x, head.xcd_from, gridDim.x);
+  const StepTask t = bid < head.n ? head.t[bid] : tasks[bid];
   const int m = t.m, ns = t.ns;
   double* F = fronts + t.f_off;
   double* L = lbuf + t.l_off;
@@ -1455,9 +1467,9 @@ __global__ void __launch_bounds__(256, 2) k_step64(const StepTask* __restrict__ 
 // [kb, ns), K = the big panel's columns [ka, kb) of the finished factor.
 using SyrkTile = GemmNT<TT, TT>;
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                              double* __restrict__ fronts, const double* __restrict__ lbuf) {
+                                              double* __restrict__ fronts, const double* __restrict__ lbuf, int xcd) {
   __shared__ double sh[SyrkTile::LDS_DOUBLES];
-  const Task t = tasks[blockIdx.x];
+  const Task t = tasks[xcd ? xcd_item(blockIdx.x, gridDim.x) : (int)blockIdx.x];  // xcd: a front's tiles behind one L2
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, ns = me.ns;
   const int ti = t.b & 0xffff, tj = t.b >> 16;
@@ -2154,20 +2166,21 @@ int debug_phases(unsigned long long* out, int maxrec) {
 }
 
 void chol_prescatter(int nzero, const long long* zr, long long nent, const double* vals, const long long* dst,
-                     const int* src, const double* lam, double* fronts, hipStream_t s) {
+                     const int* src, const double* lam, double* fronts, int nfronts, const FrontDesc* fd,
+                     const int* perm, const double* rhs, double* vecs, hipStream_t s) {
   if (nzero > 0) {
     hipLaunchKernelGGL(k_zero_ranges, nzero, 256, 0, s, zr, fronts);
     KERNEL_CHECK();
   }
   if (nent > 0) {
-    hipLaunchKernelGGL(k_chol_scatter, grid_for(nent, 256), 256, 0, s, nent, vals, dst, src, lam, fronts);
+    const int nsb = grid_for(nent, 256);
+    hipLaunchKernelGGL(k_chol_scatter, nsb + std::max(nfronts, 0), 256, 0, s, nent, nsb, vals, dst, src, lam, fronts,
+                       fd, perm, rhs, vecs);
+    KERNEL_CHECK();
+  } else if (nfronts > 0) {
+    hipLaunchKernelGGL(k_vec_init, nfronts, 256, 0, s, fd, perm, rhs, vecs);
     KERNEL_CHECK();
   }
-}
-void chol_vec_init(int nfronts, const FrontDesc* fd, const int* perm, const double* rhs, double* vecs, hipStream_t s) {
-  if (nfronts <= 0) return;
-  hipLaunchKernelGGL(k_vec_init, nfronts, 256, 0, s, fd, perm, rhs, vecs);
-  KERNEL_CHECK();
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
@@ -2199,9 +2212,13 @@ void chol_step64(int ntasks, const StepTask* tasks, const StepHead& head, double
   hipLaunchKernelGGL(k_step64, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, linvn, xinv, fail);
   KERNEL_CHECK();
 }
+bool chol_syrk_xcd() {
+  static const bool on = getenv("G2OHIP_SYRK_XCD") && atoi(getenv("G2OHIP_SYRK_XCD")) != 0;
+  return on;
+}
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
+  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf, chol_syrk_xcd() ? 1 : 0);
   KERNEL_CHECK();
 }
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s) {

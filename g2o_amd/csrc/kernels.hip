@@ -824,6 +824,27 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// an edge's chi2 from its error: e^T Omega e, robustified to rho[0] (activeRobustChi2, sparse_optimizer.cpp:102-116)
+template <class F>
+__device__ __forceinline__ double edge_chi(const EdgeData& d, int e, const double* err) {
+  double Om[F::D * F::D];
+  load_info<F::D>(info_rec(d, e, F::INFO), Om);
+  double c = 0;
+#pragma unroll
+  for (int i = 0; i < F::D; ++i) {
+    double r = 0;
+#pragma unroll
+    for (int j = 0; j < F::D; ++j) r += Om[i * F::D + j] * err[j];
+    c += err[i] * r;
+  }
+  if (d.rk) {
+    double r0, r1;
+    robustify(d.rk, d.rk_delta, c, r0, r1);
+    c = r0;
+  }
+  return c;
+}
+
 // ------------------------------------------------------------------------------ oplus
 __device__ __forceinline__ void d_oplus_se3expmap(int v, const int* __restrict__ xoff, const double* __restrict__ x,
                                             double* __restrict__ st, int* __restrict__ nopl) {
@@ -980,22 +1001,7 @@ __global__ void __launch_bounds__(RED_BLOCK) k_error_partial(EdgeData d, int ne,
     if (e < ne) {
       double err[F::D];
       F::error(d, (int)e, err);
-      double Om[F::D * F::D];
-      load_info<F::D>(info_rec(d, (int)e, F::INFO), Om);
-      double c = 0;
-#pragma unroll
-      for (int i = 0; i < F::D; ++i) {
-        double r = 0;
-#pragma unroll
-        for (int j = 0; j < F::D; ++j) r += Om[i * F::D + j] * err[j];
-        c += err[i] * r;
-      }
-      if (d.rk) {  // activeRobustChi2: rho[0] (sparse_optimizer.cpp:102-116)
-        double r0, r1;
-        robustify(d.rk, d.rk_delta, c, r0, r1);
-        c = r0;
-      }
-      s += c;
+      s += edge_chi<F>(d, (int)e, err);
     }
   }
   sh[threadIdx.x] = s;
@@ -1024,22 +1030,7 @@ __global__ void __launch_bounds__(RED_BLOCK) k_error_scale_partial(EdgeData d, i
       if (e < ne) {
         double err[F::D];
         F::error(d, (int)e, err);
-        double Om[F::D * F::D];
-        load_info<F::D>(info_rec(d, (int)e, F::INFO), Om);
-        double c = 0;
-#pragma unroll
-        for (int i = 0; i < F::D; ++i) {
-          double r = 0;
-#pragma unroll
-          for (int j = 0; j < F::D; ++j) r += Om[i * F::D + j] * err[j];
-          c += err[i] * r;
-        }
-        if (d.rk) {
-          double r0, r1;
-          robustify(d.rk, d.rk_delta, c, r0, r1);
-          c = r0;
-        }
-        s += c;
+        s += edge_chi<F>(d, (int)e, err);
       }
     }
   } else {

@@ -232,7 +232,8 @@ int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int
  * call sequence as g2ohip_set_comm; used to test the sharded path on a single-GPU box. */
 int g2ohip_set_comm_local(g2ohip_graph* g, const char* group_key, int rank, int nranks);
 /* RCCL transport self-test on one device (a one-rank communicator from `uid`): the product's allreduce sum and max
- * (the calls g2ohip_set_comm's ranks make) over n doubles of `in` on a stream of `device`; out = [sum | max].
+ * and its in-place reduce-scatter sum (the calls g2ohip_set_comm's ranks make) over n doubles of `in` on a stream of
+ * `device`; out (3n doubles) = [sum | max | reduce-scatter segment].
  * A one-GPU box cannot host two ranks of one RCCL communicator, so this is the binding's smoke test there. */
 int g2ohip_comm_selftest(int device, const unsigned char uid[128], int n, const double* in, double* out);
 /* The test transport's rank-ordered host reduction alone (no GPU): `nranks` host threads that share `group_key` each

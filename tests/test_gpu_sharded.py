@@ -128,12 +128,12 @@ def test_sharded_pcg_matches_single(g2o_amd_mod):
 
 
 def test_rccl_binding_single_rank(g2o_amd_mod):
-    """The RCCL transport itself (RcclComm: ncclGetUniqueId, ncclCommInitRank, ncclAllReduce sum / max on a HIP
-    stream, ncclCommDestroy) on a one-rank communicator: a one-GPU box cannot host two ranks of one RCCL
+    """The RCCL transport itself (RcclComm: ncclGetUniqueId, ncclCommInitRank, ncclAllReduce sum / max and the in-place
+    ncclReduceScatter on a HIP stream, ncclCommDestroy) on a one-rank communicator: a one-GPU box cannot host two ranks of one RCCL
     communicator (RCCL refuses duplicate GPUs), so the multi-rank path is covered by the LocalComm tests above."""
     v = np.linspace(-3.0, 5.0, 1000)
-    s, m = g2o_amd_mod.SparseOptimizer.comm_selftest(v)
-    assert np.array_equal(s, v) and np.array_equal(m, v)
+    s, m, r = g2o_amd_mod.SparseOptimizer.comm_selftest(v)
+    assert np.array_equal(s, v) and np.array_equal(m, v) and np.array_equal(r, v)
 
 
 @pytest.mark.parametrize("name,nranks", [("C5", 2), ("C5", 3), ("mid", 4), ("mid", 7)])

@@ -844,8 +844,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   __shared__ double vn[NB];
   PH_BEGIN(2)
   PH1_BEGIN(3)
-  const int bid = (int)blockIdx.x < head.xcd_from ? (int)blockIdx.x : xcd_item_from(blockIdx.x, head.xcd_from, gridDim.x);
-  const StepTask t = bid < head.n ? head.t[bid] : tasks[bid];
+  const StepTask t = (int)blockIdx.x < head.n ? head.t[blockIdx.x] : tasks[blockIdx.x];
   const int m = t.m, ns = t.ns;
   double* F = fronts + t.f_off;
   double* L = lbuf + t.l_off;
@@ -1467,9 +1466,9 @@ __global__ void __launch_bounds__(256, 2) k_step64(const StepTask* __restrict__ 
 // [kb, ns), K = the big panel's columns [ka, kb) of the finished factor.
 using SyrkTile = GemmNT<TT, TT>;
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                              double* __restrict__ fronts, const double* __restrict__ lbuf, int xcd) {
+                                              double* __restrict__ fronts, const double* __restrict__ lbuf) {
   __shared__ double sh[SyrkTile::LDS_DOUBLES];
-  const Task t = tasks[xcd ? xcd_item(blockIdx.x, gridDim.x) : (int)blockIdx.x];  // xcd: a front's tiles behind one L2
+  const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, ns = me.ns;
   const int ti = t.b & 0xffff, tj = t.b >> 16;
@@ -2212,13 +2211,9 @@ void chol_step64(int ntasks, const StepTask* tasks, const StepHead& head, double
   hipLaunchKernelGGL(k_step64, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, linvn, xinv, fail);
   KERNEL_CHECK();
 }
-bool chol_syrk_xcd() {
-  static const bool on = getenv("G2OHIP_SYRK_XCD") && atoi(getenv("G2OHIP_SYRK_XCD")) != 0;
-  return on;
-}
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf, chol_syrk_xcd() ? 1 : 0);
+  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
   KERNEL_CHECK();
 }
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s) {

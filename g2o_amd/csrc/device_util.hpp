@@ -20,19 +20,6 @@ __device__ __forceinline__ int xcd_item(int bid, int n) {
   const int xcd = bid & 7, q = n >> 3, r = n & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
-// the same over the items [b0, n) only (the first b0 keep their own workgroups, in dispatch order): the workgroups
-// bid >= b0 of XCD x (bid & 7 == x) take one contiguous range of those items
-__device__ __forceinline__ int xcd_item_from(int bid, int b0, int n) {
-  const int x = bid & 7;
-  int start = 0;
-#pragma unroll
-  for (int y = 0; y < 7; ++y) {
-    const int f = b0 + ((y - b0) & 7);  // XCD y's first workgroup at or after b0
-    if (y < x && f < n) start += (n - 1 - f) / 8 + 1;
-  }
-  const int fx = b0 + ((x - b0) & 7);
-  return b0 + start + (bid - fx) / 8;
-}
 
 // Landmark block of the Schur complement (block_solver.hpp:341-360), split symmetrically:
 //   Hll + lambda I = U U^T,  c = U^-1 b_l,  G_a = Hpl_a U^-T   =>   Hpl Dinv Hpl^T = G G^T,  Hpl Dinv b_l = G c_l.

@@ -854,7 +854,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         if (!dev_diagonly) stk.insert(stk.end(), tile_t.begin(), tile_t.end());
         if (!dev_diagonly) stk.insert(stk.end(), inv_t.begin(), inv_t.end());
         st.count = (int)stk.size() - st.off;
-        st.nd = (int)diag_t.size();
         for (int k = st.off; k < st.off + st.count; ++k)
           if (stk[k].flags & 64) st.kind = 6;
         if (st.count) { ops.push_back(st); op_front_off.push_back(0); }
@@ -874,7 +873,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         }
         gm.count = (int)tk.size() - gm.off;
         d0.count = (int)stk.size() - d0.off;
-        d0.nd = d0.count;  // next-diagonal tasks only
         if (gm.count) { ops.push_back(gm); op_front_off.push_back(0); ++n_syrk_ops; }
         if (d0.count) { ops.push_back(d0); op_front_off.push_back(0); }
       }
@@ -1003,13 +1001,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
     heads.assign(ops.size(), launch::StepHead{});
-    // the tile and inverse tasks of a panel step dealt XCD-contiguously (a front's tiles share its L panel rows through
-    // one L2); the next-diagonal tasks keep the first workgroups (G2OHIP_STEP_XCD=1; default: plain order)
-    const bool step_xcd = getenv("G2OHIP_STEP_XCD") && atoi(getenv("G2OHIP_STEP_XCD")) != 0;
     for (size_t k = 0; k < ops.size(); ++k) {
       if (ops[k].kind != 2 && ops[k].kind != 6 && ops[k].kind != 9) continue;
       launch::StepHead& h = heads[k];
-      h.xcd_from = step_xcd && ops[k].kind != 9 ? ops[k].nd : std::numeric_limits<int>::max();
       h.n = 0;
       while (h.n < launch::CHOL_HEAD && h.n < ops[k].count) {  // the first workgroups (diagonal tasks among them)
         h.t[h.n] = stk[ops[k].off + h.n];

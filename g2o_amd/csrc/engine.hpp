@@ -117,10 +117,9 @@ struct DeviceCholesky {
   // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
   // trailing-update (k_syrk) launches, big-panel backward rounds
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0, n_dag_levels = 0;
-  struct Op { int kind, off, count, tpw = 1, w64 = 0, nd = 0; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add,
+  struct Op { int kind, off, count, tpw = 1, w64 = 0; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add,
                                                  // 2 panel step (6: with lagged-pair tasks), 3 syrk, 7 tile DAG,
-                                                 // 9 64-column panel step; w64: extend-add of a 64-column level;
-                                                 // nd: leading next-diagonal tasks of a panel step (dispatch order kept)
+                                                 // 9 64-column panel step; w64: extend-add of a 64-column level
                                                  // (off: first worker's tile slots, off2 fronts), tpw tiles per worker
   std::vector<int> op_front_off;  // per op: first DagFront of a kind-7 op
   // persistent tile DAG of latency-bound levels (cholesky.hip k_dag)

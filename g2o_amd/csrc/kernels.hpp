@@ -167,7 +167,6 @@ constexpr int CHOL_HEAD = 8;
 struct StepHead {
   StepTask t[CHOL_HEAD];
   int n;
-  int xcd_from;  // tasks from this index on are dealt XCD-contiguously (a front's tiles behind one L2); >= count: off
 };
 // zero ranges (offset, length pairs) of the front pool, then scatter input entries: fronts[dst[k]] =
 // vals[src[k] & 0x7fffffff] (+ lambda when src[k] < 0), and the front vectors v_s = [rhs(perm[c0 ..]) (own
@@ -191,7 +190,6 @@ void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* 
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
 // the contribution block, K = [0, ns)); columns stop at ns unless kb = ns (then m)
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s);
-bool chol_syrk_xcd();  // k_syrk deals its tiles XCD-contiguously (G2OHIP_SYRK_XCD)
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]
 void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]
 void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int* rows, const double* lbuf,

@@ -12,7 +12,8 @@ and `bytes_fetch_doubled` = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (the guide's co
 16-B/lane streaming reads, an upper bound for narrower ones).
 Kernel names are mapped to the bench.py stage names below. The factorization ("chol_factor") is a
 chain of launches (scatter, extend-add, panel steps, trailing updates): its traffic is the sum over
-all of its dispatches divided by the number of factorizations (k_vec_init runs once per factorization).
+all of its dispatches divided by the number of factorizations (k_chol_scatter, which also initialises the front
+vectors, runs once per factorization; k_vec_init counts where no level is pre-scattered).
 """
 import csv
 import glob
@@ -46,7 +47,7 @@ def _split_variant(name):
 
 def read_counter(d, counter):
     per = defaultdict(list)
-    fsum, nfac = 0.0, 0
+    fsum, nscat, nvec = 0.0, 0, 0
     rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         rows += [r for r in csv.DictReader(open(f)) if r.get("Counter_Name") == counter]
@@ -62,11 +63,13 @@ def read_counter(d, counter):
                 per[sub].append(float(r["Counter_Value"]))
         if any("::" + k + "(" in name or "::" + k + "<" in name for k in FACTOR):
             fsum += float(r["Counter_Value"])
-            nfac += "::k_vec_init(" in name
+            nscat += "::k_chol_scatter(" in name
+            nvec += "::k_vec_init(" in name
     st = defaultdict(list)
     for sub, vals in per.items():  # per stage: sum of its kernels' per-dispatch means, one entry per dispatch
         st[STAGES[sub]].append((sum(vals) / len(vals), len(vals)))
     out = {k: [sum(m for m, _ in v)] * max(n for _, n in v) for k, v in st.items()}
+    nfac = nscat or nvec
     if nfac:
         out["chol_factor"] = [fsum / nfac] * nfac
     return out

@@ -405,6 +405,15 @@ class Engine {
   double chi_cache = 0.0;
   hipEvent_t lm_ev_[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t rb_ev_ = nullptr;   // the trial's scalar readback landed (the stream may hold more work behind it)
+  // Schur rows beside the camera pass: with the split formed at assembly, k_schur_rows (off-diagonal blocks, from G)
+  // does not depend on k_cam_assemble (diagonal blocks, bschur), so it runs on side_stream_ from the end of the
+  // landmark pass while the camera pass runs on `stream`; rows_ahead_: this assembly's rows are launched (solve_async
+  // joins instead of launching); rows_side_: side work the main stream has not joined yet
+  hipStream_t side_stream_ = nullptr;
+  hipEvent_t rows_fork_ev_ = nullptr, rows_done_ev_ = nullptr;
+  bool rows_ahead_ = false, rows_side_ = false;
+  void rows_join();
+  void launch_schur_rows(bool split, bool zero_here, hipStream_t s);
   double* hscal_ = nullptr;      // pinned host copy of dscal (one readback per LM trial)
   int levenberg_iterations = 0;
 

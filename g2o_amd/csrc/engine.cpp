@@ -1139,19 +1139,12 @@ Engine::Engine(int dev) : device(dev) {
   for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
   for (auto& e : lm_ev_) HIP_CHECK(hipEventCreate(&e));
   HIP_CHECK(hipEventCreateWithFlags(&rb_ev_, hipEventDisableTiming));
-  HIP_CHECK(hipStreamCreateWithFlags(&side_stream_, hipStreamNonBlocking));
-  HIP_CHECK(hipEventCreateWithFlags(&rows_fork_ev_, hipEventDisableTiming));
-  HIP_CHECK(hipEventCreateWithFlags(&rows_done_ev_, hipEventDisableTiming));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hscal_), 16 * sizeof(double), hipHostMallocDefault));
 }
 Engine::~Engine() {
-  if (side_stream_) (void)hipStreamSynchronize(side_stream_);
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
   for (auto& e : lm_ev_) if (e) (void)hipEventDestroy(e);
   if (rb_ev_) (void)hipEventDestroy(rb_ev_);
-  if (rows_fork_ev_) (void)hipEventDestroy(rows_fork_ev_);
-  if (rows_done_ev_) (void)hipEventDestroy(rows_done_ev_);
-  if (side_stream_) (void)hipStreamDestroy(side_stream_);
   if (hscal_) (void)hipHostFree(hscal_);
   comm.reset();
   if (stream) (void)hipStreamDestroy(stream);
@@ -2017,8 +2010,6 @@ void Engine::setup_edges_device() {
 }
 
 int Engine::build_structure() {  // block_solver.hpp:102-256
-  if (side_stream_) HIP_CHECK(hipStreamSynchronize(side_stream_));  // no Schur rows still reading the old buffers
-  rows_side_ = rows_ahead_ = false;
   if (!initialized) {
     int r = initialize();
     if (r) return r;
@@ -2491,8 +2482,6 @@ int Engine::build_system_split(double lambda, const double* lamp) {  // block_so
   }
   ensure_device_state();
   refresh_host_payload(true);
-  rows_join();  // a previous assembly's Schur rows may still read G / write S
-  rows_ahead_ = false;
   fz_lambda = std::numeric_limits<double>::quiet_NaN();
   if (ba_fused) {  // assembly.hip: landmark side reduced inside the linearize waves, camera side recomputed per camera
     const EGroup& g = groups[0];
@@ -2528,20 +2517,6 @@ int Engine::build_system_split(double lambda, const double* lamp) {  // block_so
     // split landmarks first: the camera pass reads every landmark's U and c
     launch::lm_fixup(fz_nfix, fz_fix.get(), fz_lpart.get(), dHll.get(), db.get(), num_poses, size_poses, lm_begin,
                      split ? &sp : nullptr, stream);
-    // every G block is final here: the Schur rows run beside the camera pass where that pass (one workgroup per
-    // camera) leaves the chip short of work: C4's 1000 cameras 839.8 -> 843.8 LM it/s, C5's 4000 202.9 -> 197.2 (the
-    // two passes contend). Timed runs and the debug dump keep the one-stream order. G2OHIP_ROWS_OVERLAP=0 / 1: off /
-    // on regardless of the camera count (A/B)
-    const char* ov = getenv("G2OHIP_ROWS_OVERLAP");
-    const int overlap_env = ov ? atoi(ov) : -1;
-    const bool overlap = overlap_env == 1 || (overlap_env == -1 && num_poses <= 2048);
-    if (split && overlap && !timer.enabled && !write_debug) {
-      HIP_CHECK(hipEventRecord(rows_fork_ev_, stream));
-      HIP_CHECK(hipStreamWaitEvent(side_stream_, rows_fork_ev_, 0));
-      launch_schur_rows(true, !use_pcg() && chol.nzero > 0, side_stream_);
-      HIP_CHECK(hipEventRecord(rows_done_ev_, side_stream_));
-      rows_side_ = rows_ahead_ = true;
-    }
     EdgeArgs ca = group_args(g);
     ca.v0 = cm_v0.get();
     ca.v1 = cm_v1.get();
@@ -2650,15 +2625,12 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   // the Cholesky's pre-scattered fronts are cleared by extra workgroups of the Schur pass (they are dead since the
   // last factorization), off the factorization's own chain
   const bool zero_here = !use_pcg() && chol.nzero > 0;
-  if (split && rows_ahead_) {  // launched beside this assembly's camera pass
-    rows_join();
-  } else {
-    rows_join();
-    timer.begin("schur_rows", stream);
-    launch_schur_rows(split, zero_here, stream);
-    timer.end(stream);
-  }
-  rows_ahead_ = false;
+  timer.begin("schur_rows", stream);
+  launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(),
+                     split ? sch_st_obs_h.get() : sch_st_obs.get(), sch_pairs.get(), sch_pp.get(), dG.get(),
+                     ds_hpp.get(), dH.get(), S, zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(),
+                     stream);
+  timer.end(stream);
   const bool rs = !use_pcg() && chol.rs_on;  // distributed factorization: each rank's blocks reduce-scattered to it
   if (rs) chol.reduce_input(dS.get(), stream);
   else allreduce_sum(S, (size_t)nS * pd * pd + size_poses);
@@ -2687,18 +2659,6 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
     launch::backsub(pd, ld, nLloc, d_lm_ptr.get(), d_blk_pose.get(), Hpl, dDinv.get(), db.get(), size_poses, lm_begin,
                     dx.get(), stream);
   timer.end(stream);
-}
-
-void Engine::launch_schur_rows(bool split, bool zero_here, hipStream_t s) {
-  launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(),
-                     split ? sch_st_obs_h.get() : sch_st_obs.get(), sch_pairs.get(), sch_pp.get(), dG.get(),
-                     ds_hpp.get(), dH.get(), dS.get(), zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(),
-                     s);
-}
-void Engine::rows_join() {
-  if (!rows_side_) return;
-  HIP_CHECK(hipStreamWaitEvent(stream, rows_done_ev_, 0));
-  rows_side_ = false;
 }
 
 int Engine::solve_sync() {
@@ -2864,7 +2824,8 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   // readback and the GPU starts on it while the host is still waking up; a rejected trial's speculative assembly is
   // discarded (fz_lambda stays +inf: the next trial re-assembles at the popped state). Not with the stage timer on
   // (its events would be read before the speculative work ran).
-  const bool spec = ba_fused && fz_split_ok && !timer.enabled && !write_debug;  // (the not-PD dump reads S)
+  // (the not-PD dump reads S; stage timers of the assembly would be collected while the next assembly is queued)
+  const bool spec = ba_fused && fz_split_ok && !timer_times_build() && !write_debug;
   bool spec_built = false, last_accept = false;
   do {
     push();
@@ -2878,11 +2839,14 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     if (ev2) HIP_CHECK(hipEventRecord(e2, stream));
     // computeScale (:177-184) on the device, sum x (lambda x + b), while lambda is still set; the
     // restoreDiagonal that follows (:113) is the next setLambda (lambda is virtual, never in H)
+    // one rank, device decision: the finals and k_lm_decide in one launch (no all-reduce between them)
+    const bool decide_fused = spec && nranks <= 1 && groups.size() == 1 && groups[0].family != FAM_HOSTJ;
     if (groups.size() == 1 && groups[0].family != FAM_HOSTJ) {  // chi2 and the scale sum in one pass + one final
       timer.begin("error", stream);
       const EGroup& g = groups[0];
+      const launch::LmDecide dec{currentChi, (double)ni, rank == 0};
       launch::error_scale(g.family, group_args(g), g.ne, vector_size(), size_poses, dx.get(), db.get(), dscal.get(),
-                          dpartial.get(), dscal.get() + 1, dscal.get() + 2, stream);
+                          dpartial.get(), dscal.get() + 1, dscal.get() + 2, stream, decide_fused ? &dec : nullptr);
       timer.end(stream);
     } else {
       launch::scale_sum(vector_size(), size_poses, dx.get(), db.get(), dscal.get(), dpartial.get(), dscal.get() + 2,
@@ -2893,7 +2857,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     if (do_schur) allreduce_sum(dscal.get() + 1, 2);
     else allreduce_sum(dscal.get() + 2, 1);
     if (ev2) HIP_CHECK(hipEventRecord(e3, stream));
-    if (spec) launch::lm_decide(dscal.get(), currentChi, (double)ni, rank == 0, stream);
+    if (spec && !decide_fused) launch::lm_decide(dscal.get(), currentChi, (double)ni, rank == 0, stream);
     double* hs = hscal_;  // lambda, chi2, scale, ... | fail flags | decision (one readback per trial, pinned)
     HIP_CHECK(hipMemcpyAsync(hs, dscal.get(), 16 * sizeof(double), hipMemcpyDeviceToHost, stream));
     if (spec) {

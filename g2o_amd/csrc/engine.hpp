@@ -405,15 +405,12 @@ class Engine {
   double chi_cache = 0.0;
   hipEvent_t lm_ev_[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t rb_ev_ = nullptr;   // the trial's scalar readback landed (the stream may hold more work behind it)
-  // Schur rows beside the camera pass: with the split formed at assembly, k_schur_rows (off-diagonal blocks, from G)
-  // does not depend on k_cam_assemble (diagonal blocks, bschur), so it runs on side_stream_ from the end of the
-  // landmark pass while the camera pass runs on `stream`; rows_ahead_: this assembly's rows are launched (solve_async
-  // joins instead of launching); rows_side_: side work the main stream has not joined yet
-  hipStream_t side_stream_ = nullptr;
-  hipEvent_t rows_fork_ev_ = nullptr, rows_done_ev_ = nullptr;
-  bool rows_ahead_ = false, rows_side_ = false;
-  void rows_join();
-  void launch_schur_rows(bool split, bool zero_here, hipStream_t s);
+  // the kernel timer records events in the assembly (all classes, or one of the assembly's): the speculative next
+  // assembly is off then (a timer on chol_factor alone, bench.py's, leaves it on)
+  bool timer_times_build() const {
+    return timer.enabled && (timer.only.empty() || timer.only == "linearize" || timer.only == "vreduce" ||
+                             timer.only == "schur_rows");
+  }
   double* hscal_ = nullptr;      // pinned host copy of dscal (one readback per LM trial)
   int levenberg_iterations = 0;
 

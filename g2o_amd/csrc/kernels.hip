@@ -1069,6 +1069,55 @@ __global__ void __launch_bounds__(RED_BLOCK) k_sum_final2(const double* __restri
   }
   if (threadIdx.x == 0) *(blockIdx.x == 0 ? out0 : out1) = sh[0];
 }
+__device__ __forceinline__ void lm_decide_body(double* __restrict__ p, double current_chi, double ni, int rank0) {
+  int f;
+  __builtin_memcpy(&f, p + 8, sizeof f);
+  const double temp = f == 0 ? p[1] : __DBL_MAX__;
+  double rho = current_chi - temp;
+  double scale = p[2];
+  scale += 1e-3;
+  rho /= scale;
+  const double lam = p[0];
+  double nl, acc;
+  if (rho > 0 && isfinite(temp)) {
+    double alpha = 1. - pow(2 * rho - 1, 3);
+    alpha = alpha < 2. / 3. ? alpha : 2. / 3.;
+    nl = lam * (1. / 3. > alpha ? 1. / 3. : alpha);
+    acc = 1.0;
+  } else {
+    nl = lam * ni;
+    acc = 0.0;
+  }
+  p[12] = nl;
+  p[13] = rank0 ? nl : 0.0;
+  p[14] = acc;
+  p[15] = rho;
+}
+__global__ void k_lm_decide(double* __restrict__ p, double current_chi, double ni, int rank0) {
+  lm_decide_body(p, current_chi, ni, rank0);
+}
+// one rank: k_sum_final2's two sums (the same order, one after the other in one workgroup) into p[1] (chi2) and p[2]
+// (scale), then the trial decision on them (one launch less per LM trial)
+__global__ void __launch_bounds__(RED_BLOCK) k_sum_final2_decide(const double* __restrict__ partial, int n0, int n1,
+                                                                 double* __restrict__ p, double current_chi, double ni,
+                                                                 int rank0) {
+  __shared__ double sh[RED_BLOCK];
+  for (int q = 0; q < 2; ++q) {
+    const double* pp = q == 0 ? partial : partial + n0;
+    const int np = q == 0 ? n0 : n1;
+    double s = 0;
+    for (int i = threadIdx.x; i < np; i += RED_BLOCK) s += pp[i];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int m = RED_BLOCK / 2; m > 0; m >>= 1) {
+      if ((int)threadIdx.x < m) sh[threadIdx.x] += sh[threadIdx.x + m];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) p[1 + q] = sh[0];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) lm_decide_body(p, current_chi, ni, rank0);
+}
 
 // computeScale (optimization_algorithm_levenberg.cpp:177-184) fused with the first sum pass:
 // x (lambda x + b), lambda = lam[4] (rank-0 share) on the pose part, lam[0] on the landmark part
@@ -1338,7 +1387,8 @@ int error_partials(int family, const EdgeArgs& a, int ne, double* partial, hipSt
   return np;
 }
 void error_scale(int family, const EdgeArgs& a, int ne, long long n, long long npose, const double* x, const double* b,
-                 const double* lam, double* partial, double* out_chi, double* out_scale, hipStream_t s) {
+                 const double* lam, double* partial, double* out_chi, double* out_scale, hipStream_t s,
+                 const LmDecide* dec) {
   const int npe = (int)sum_partials(ne), nps = (int)sum_partials(n);
   if (npe + nps > 0)
     family_dispatch(family, a, [&](auto fam) {
@@ -1346,7 +1396,11 @@ void error_scale(int family, const EdgeArgs& a, int ne, long long n, long long n
       hipLaunchKernelGGL(k_error_scale_partial<F>, npe + nps, RED_BLOCK, 0, s, mk(a), ne, npe, n, npose, x, b, lam,
                          partial);
     });
-  hipLaunchKernelGGL(k_sum_final2, 2, RED_BLOCK, 0, s, partial, npe, nps, out_chi, out_scale);
+  if (dec)  // out_chi, out_scale = p + 1, p + 2
+    hipLaunchKernelGGL(k_sum_final2_decide, 1, RED_BLOCK, 0, s, partial, npe, nps, out_chi - 1, dec->current_chi,
+                       dec->ni, dec->rank0 ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_sum_final2, 2, RED_BLOCK, 0, s, partial, npe, nps, out_chi, out_scale);
   KERNEL_CHECK();
 }
 void sum_final(const double* partial, int np, double* out, hipStream_t s) {
@@ -1388,30 +1442,6 @@ __global__ void k_set_scalars(double* __restrict__ p, double lam, double lam_ran
 }
 // the LM trial decision, restated from the host loop (Engine::lm_solve, optimization_algorithm_levenberg.cpp:127-141):
 // the host reads it back instead of recomputing it, so both sides follow one decision
-__global__ void k_lm_decide(double* __restrict__ p, double current_chi, double ni, int rank0) {
-  int f;
-  __builtin_memcpy(&f, p + 8, sizeof f);
-  const double temp = f == 0 ? p[1] : __DBL_MAX__;
-  double rho = current_chi - temp;
-  double scale = p[2];
-  scale += 1e-3;
-  rho /= scale;
-  const double lam = p[0];
-  double nl, acc;
-  if (rho > 0 && isfinite(temp)) {
-    double alpha = 1. - pow(2 * rho - 1, 3);
-    alpha = alpha < 2. / 3. ? alpha : 2. / 3.;
-    nl = lam * (1. / 3. > alpha ? 1. / 3. : alpha);
-    acc = 1.0;
-  } else {
-    nl = lam * ni;
-    acc = 0.0;
-  }
-  p[12] = nl;
-  p[13] = rank0 ? nl : 0.0;
-  p[14] = acc;
-  p[15] = rho;
-}
 // max |diag| over nb blocks of dim x dim (col-major), partial per block of threads
 __global__ void __launch_bounds__(256) k_diag_absmax(const double* __restrict__ H, int nb, int dim,
                                                      double* __restrict__ out) {

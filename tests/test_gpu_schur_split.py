@@ -92,20 +92,3 @@ def test_split_hpp_consumers_after_optimize(g2o_amd_mod, oracle):
     r = ref.stage(0.0)  # buildSystem at the optimized state
     Hpp, _, _ = ref.hessian_dense(r["np"], r["nl"])
     assert np.linalg.norm(y - Hpp @ v) <= 1e-8 * np.linalg.norm(Hpp @ v)
-
-
-@pytest.mark.parametrize("name", ["C4", "C5"])
-def test_rows_beside_camera_pass_bitwise(g2o_amd_mod, monkeypatch, name):
-    """k_schur_rows on the side stream beside the camera pass (engine.hpp rows_ahead_) against the one-stream order
-    (G2OHIP_ROWS_OVERLAP=0): the same kernels on the same inputs, so the trajectories agree bit for bit. Forced on
-    (=1) as well, for the camera counts the default leaves on one stream."""
-    prob = synth.by_name(name, "small")
-    runs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("G2OHIP_ROWS_OVERLAP", flag)
-        opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
-        n, st = opt.optimize(5)
-        runs.append((n, [s.chi2 for s in st], [s.levenbergIterations for s in st], opt.minimal_state()))
-    (n1, c1, t1, x1), (n0, c0, t0, x0) = runs
-    assert n1 == n0 and t1 == t0 and c1 == c0
-    assert np.array_equal(x1, x0)

@@ -2715,7 +2715,10 @@ int Engine::get_b(double* b) {
   return G2OHIP_OK;
 }
 
-int Engine::push() {  // base_vertex.h:93-95 for all active vertices (stream-ordered device copy)
+int Engine::push() { return push_set_lambda(false, 0.0); }
+// push (base_vertex.h:93-95 for all active vertices, a stream-ordered device copy); with_lambda: the trial's
+// setLambda (set_lambda_device(lam, true)) rides in the same launch
+int Engine::push_set_lambda(bool with_lambda, double lam) {
   ensure_device_state();
   if ((int)stack_.size() <= stack_depth_) stack_.emplace_back(NVT);
   auto& lvl = stack_[stack_depth_++];
@@ -2726,6 +2729,12 @@ int Engine::push() {  // base_vertex.h:93-95 for all active vertices (stream-ord
     cl.src[cl.n] = dstate[t].get();
     cl.dst[cl.n] = lvl[t].get();
     cl.len[cl.n++] = (long long)dstate[t].size();
+  }
+  if (with_lambda) {
+    lambda_host = lam;
+    cl.sp = dscal.get();
+    cl.lam = lam;
+    cl.lam_rank = rank == 0 ? lam : 0.0;
   }
   launch::copy_multi(cl, stream);  // one launch for every vertex type
   return G2OHIP_OK;
@@ -2828,10 +2837,9 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   const bool spec = ba_fused && fz_split_ok && !timer_times_build() && !write_debug;
   bool spec_built = false, last_accept = false;
   do {
-    push();
+    push_set_lambda(true, current_lambda);  // + setLambda, which also clears the not-PD flags, in the same launch
     if (st) st->levenbergIterations++;
     const bool ev1 = st && stats_level >= 1, ev2 = st && stats_level >= 2;
-    set_lambda_device(current_lambda, true);  // also clears the not-PD flags
     if (ev1) HIP_CHECK(hipEventRecord(e0, stream));
     solve_async(false);
     if (ev1) HIP_CHECK(hipEventRecord(e1, stream));

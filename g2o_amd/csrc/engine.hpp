@@ -273,6 +273,7 @@ class Engine {
   int get_b(double* b);
   int update_from(const double* xh);
   int push();
+  int push_set_lambda(bool with_lambda, double lam);
   int pop();
   int discard_top();
   int stage(double lambda, double* b, double* x, double* Hs, double* bs, long long* dims);

@@ -1465,6 +1465,12 @@ __global__ void k_max_final(const double* __restrict__ partial, int np, double* 
   *out = m;
 }
 __global__ void __launch_bounds__(256) k_copy_multi(launch::CopyList cl) {
+  if (cl.sp && blockIdx.x == 0 && threadIdx.x == 0) {  // k_set_scalars(sp, lam, lam_rank, reset_fail = 1)
+    cl.sp[0] = cl.lam;
+    cl.sp[4] = cl.lam_rank;
+    cl.sp[5] = 0.0;
+    cl.sp[8] = 0.0;
+  }
   for (int k = 0; k < cl.n; ++k) {  // uniform loop; grid-stride over each buffer
     const double2* src = reinterpret_cast<const double2*>(cl.src[k]);
     double2* dst = reinterpret_cast<double2*>(cl.dst[k]);
@@ -1475,7 +1481,7 @@ __global__ void __launch_bounds__(256) k_copy_multi(launch::CopyList cl) {
 }
 namespace launch {
 void copy_multi(const CopyList& cl, hipStream_t s) {
-  if (cl.n <= 0) return;
+  if (cl.n <= 0 && !cl.sp) return;
   long long mx = 0;
   for (int k = 0; k < cl.n; ++k) mx = std::max(mx, cl.len[k]);
   const unsigned g = (unsigned)std::min<long long>(std::max<long long>((mx / 2 + 255) / 256, 1), 1024);

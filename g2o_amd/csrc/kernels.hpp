@@ -135,6 +135,10 @@ struct CopyList {  // up to 4 device-to-device copies of doubles in one launch (
   double* dst[4];
   long long len[4];
   int n;
+  // optional: set_scalars in the same launch (the LM trial's push + setLambda): sp[0] = lam, sp[4] = lam_rank,
+  // sp[5] = 0, the not-PD flags cleared
+  double* sp = nullptr;
+  double lam = 0.0, lam_rank = 0.0;
 };
 void copy_multi(const CopyList& cl, hipStream_t s);
 void diag_absmax(const double* H1, int nb1, int d1, const double* H2, int nb2, int d2, double* partial, double* out,

@@ -2835,7 +2835,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
   // (its events would be read before the speculative work ran).
   // (the not-PD dump reads S; stage timers of the assembly would be collected while the next assembly is queued)
   const bool spec = ba_fused && fz_split_ok && !timer_times_build() && !write_debug;
-  bool spec_built = false, last_accept = false;
+  bool spec_built = false, last_accept = false, last_decide_fused = false;
   do {
     push_set_lambda(true, current_lambda);  // + setLambda, which also clears the not-PD flags, in the same launch
     if (st) st->levenbergIterations++;
@@ -2849,6 +2849,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     // restoreDiagonal that follows (:113) is the next setLambda (lambda is virtual, never in H)
     // one rank, device decision: the finals and k_lm_decide in one launch (no all-reduce between them)
     const bool decide_fused = spec && nranks <= 1 && groups.size() == 1 && groups[0].family != FAM_HOSTJ;
+    last_decide_fused = decide_fused;
     if (groups.size() == 1 && groups[0].family != FAM_HOSTJ) {  // chi2 and the scale sum in one pass + one final
       timer.begin("error", stream);
       const EGroup& g = groups[0];
@@ -2938,7 +2939,10 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     }
     qmax++;
   } while (rho < 0 && qmax < maxTrials);
-  set_lambda_device(0.0);  // restoreDiagonal of the last trial (block_solver.hpp:552-565)
+  // restoreDiagonal of the last trial (block_solver.hpp:552-565); after an accepted trial whose decision ran in
+  // k_sum_final2_decide the device has done it already
+  if (last_decide_fused && last_accept) lambda_host = 0.0;
+  else set_lambda_device(0.0);
   // the state left behind has chi2 currentChi (accepted: the last tempChi; rejected: popped back)
   chi_cache = currentChi;
   chi_ver = state_ver;

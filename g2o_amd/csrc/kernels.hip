@@ -1097,7 +1097,8 @@ __global__ void k_lm_decide(double* __restrict__ p, double current_chi, double n
   lm_decide_body(p, current_chi, ni, rank0);
 }
 // one rank: k_sum_final2's two sums (the same order, one after the other in one workgroup) into p[1] (chi2) and p[2]
-// (scale), then the trial decision on them (one launch less per LM trial)
+// (scale), then the trial decision on them (one launch less per LM trial); an accepted trial also gets the loop's
+// closing restoreDiagonal (lambda 0), which the host then skips
 __global__ void __launch_bounds__(RED_BLOCK) k_sum_final2_decide(const double* __restrict__ partial, int n0, int n1,
                                                                  double* __restrict__ p, double current_chi, double ni,
                                                                  int rank0) {
@@ -1116,7 +1117,14 @@ __global__ void __launch_bounds__(RED_BLOCK) k_sum_final2_decide(const double* _
     if (threadIdx.x == 0) p[1 + q] = sh[0];
     __syncthreads();
   }
-  if (threadIdx.x == 0) lm_decide_body(p, current_chi, ni, rank0);
+  if (threadIdx.x == 0) {
+    lm_decide_body(p, current_chi, ni, rank0);
+    if (p[14] != 0.0) {  // accepted: the trial loop ends here, with restoreDiagonal (the host's set_lambda(0))
+      p[0] = 0.0;
+      p[4] = 0.0;
+      p[5] = 0.0;
+    }
+  }
 }
 
 // computeScale (optimization_algorithm_levenberg.cpp:177-184) fused with the first sum pass:

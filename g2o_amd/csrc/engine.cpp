@@ -1140,12 +1140,16 @@ Engine::Engine(int dev) : device(dev) {
   for (auto& e : lm_ev_) HIP_CHECK(hipEventCreate(&e));
   HIP_CHECK(hipEventCreateWithFlags(&rb_ev_, hipEventDisableTiming));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hscal_), 16 * sizeof(double), hipHostMallocDefault));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hdec_), 16 * sizeof(double),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hdec_dev_), hdec_, 0));
 }
 Engine::~Engine() {
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
   for (auto& e : lm_ev_) if (e) (void)hipEventDestroy(e);
   if (rb_ev_) (void)hipEventDestroy(rb_ev_);
   if (hscal_) (void)hipHostFree(hscal_);
+  if (hdec_) (void)hipHostFree(hdec_);
   comm.reset();
   if (stream) (void)hipStreamDestroy(stream);
 }
@@ -2853,7 +2857,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     if (groups.size() == 1 && groups[0].family != FAM_HOSTJ) {  // chi2 and the scale sum in one pass + one final
       timer.begin("error", stream);
       const EGroup& g = groups[0];
-      const launch::LmDecide dec{currentChi, (double)ni, rank == 0};
+      const launch::LmDecide dec{currentChi, (double)ni, rank == 0, hdec_dev_};
       launch::error_scale(g.family, group_args(g), g.ne, vector_size(), size_poses, dx.get(), db.get(), dscal.get(),
                           dpartial.get(), dscal.get() + 1, dscal.get() + 2, stream, decide_fused ? &dec : nullptr);
       timer.end(stream);
@@ -2867,8 +2871,10 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     else allreduce_sum(dscal.get() + 2, 1);
     if (ev2) HIP_CHECK(hipEventRecord(e3, stream));
     if (spec && !decide_fused) launch::lm_decide(dscal.get(), currentChi, (double)ni, rank == 0, stream);
-    double* hs = hscal_;  // lambda, chi2, scale, ... | fail flags | decision (one readback per trial, pinned)
-    HIP_CHECK(hipMemcpyAsync(hs, dscal.get(), 16 * sizeof(double), hipMemcpyDeviceToHost, stream));
+    // lambda, chi2, scale, ... | fail flags | decision: one readback per trial into pinned memory, or (one rank) written
+    // to mapped host memory by the decision kernel itself
+    double* hs = decide_fused ? hdec_ : hscal_;
+    if (!decide_fused) HIP_CHECK(hipMemcpyAsync(hs, dscal.get(), 16 * sizeof(double), hipMemcpyDeviceToHost, stream));
     if (spec) {
       HIP_CHECK(hipEventRecord(rb_ev_, stream));
       build_system_split(std::numeric_limits<double>::quiet_NaN(), dscal.get() + 12);

@@ -413,6 +413,8 @@ class Engine {
                              timer.only == "schur_rows");
   }
   double* hscal_ = nullptr;      // pinned host copy of dscal (one readback per LM trial)
+  double* hdec_ = nullptr;       // mapped coherent host memory the one-rank decision kernel writes the scalars to
+  double* hdec_dev_ = nullptr;   // its device address
   int levenberg_iterations = 0;
 
   void ensure_device_state();

@@ -1101,7 +1101,7 @@ __global__ void k_lm_decide(double* __restrict__ p, double current_chi, double n
 // closing restoreDiagonal (lambda 0), which the host then skips
 __global__ void __launch_bounds__(RED_BLOCK) k_sum_final2_decide(const double* __restrict__ partial, int n0, int n1,
                                                                  double* __restrict__ p, double current_chi, double ni,
-                                                                 int rank0) {
+                                                                 int rank0, double* host_out) {
   __shared__ double sh[RED_BLOCK];
   for (int q = 0; q < 2; ++q) {
     const double* pp = q == 0 ? partial : partial + n0;
@@ -1124,6 +1124,8 @@ __global__ void __launch_bounds__(RED_BLOCK) k_sum_final2_decide(const double* _
       p[4] = 0.0;
       p[5] = 0.0;
     }
+    if (host_out)
+      for (int k = 0; k < 16; ++k) host_out[k] = p[k];
   }
 }
 
@@ -1406,7 +1408,7 @@ void error_scale(int family, const EdgeArgs& a, int ne, long long n, long long n
     });
   if (dec)  // out_chi, out_scale = p + 1, p + 2
     hipLaunchKernelGGL(k_sum_final2_decide, 1, RED_BLOCK, 0, s, partial, npe, nps, out_chi - 1, dec->current_chi,
-                       dec->ni, dec->rank0 ? 1 : 0);
+                       dec->ni, dec->rank0 ? 1 : 0, dec->host_out);
   else
     hipLaunchKernelGGL(k_sum_final2, 2, RED_BLOCK, 0, s, partial, npe, nps, out_chi, out_scale);
   KERNEL_CHECK();

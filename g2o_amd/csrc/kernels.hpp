@@ -114,7 +114,11 @@ void sum_final(const double* partial, int np, double* out, hipStream_t s);
 // error_partials (one edge group) + scale_sum in one launch and both finals in a second: chi2 -> out_chi, the
 // computeScale sum -> out_scale (the same sums bit for bit). dec (one rank, out_chi = p + 1, out_scale = p + 2): the
 // finals and lm_decide in one launch
-struct LmDecide { double current_chi, ni; bool rank0; };
+struct LmDecide {
+  double current_chi, ni;
+  bool rank0;
+  double* host_out;  // mapped, coherent host memory: the 16 scalars after the decision (replaces the readback copy)
+};
 void error_scale(int family, const EdgeArgs& a, int ne, long long n, long long npose, const double* x, const double* b,
                  const double* lam, double* partial, double* out_chi, double* out_scale, hipStream_t s,
                  const LmDecide* dec = nullptr);

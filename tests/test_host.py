@@ -215,3 +215,33 @@ def test_local_comm_mismatch_raises(g2o_amd_mod):
     [t.start() for t in th]
     [t.join(timeout=30) for t in th]
     assert all(e and "collective mismatch" in e for e in errs), errs
+
+
+def test_pmc_traffic_factor_per_factorization(tmp_path):
+    """tools/pmc_traffic.py: the factorization's traffic is the sum over its kernel chain divided by the number of
+    factorizations, counted by the scatter launch (which also initialises the front vectors; k_vec_init only where no
+    level is pre-scattered). Two factorizations of scatter + two panel steps + a contribution pass."""
+    import csv
+    import json
+    import subprocess
+    import sys
+    names = ["g2ohip::k_chol_scatter(long long)", "void g2ohip::k_step<false>(int)", "void g2ohip::k_step<true>(int)",
+             "g2ohip::k_syrk(int)", "void g2ohip::k_schur_rows<6, 3>(int)"]
+    vals = {"FETCH_SIZE": [10.0, 20.0, 30.0, 40.0, 7.0], "WRITE_SIZE": [1.0, 2.0, 3.0, 4.0, 5.0]}
+    dirs = {}
+    for counter, v in vals.items():
+        d = tmp_path / counter
+        d.mkdir()
+        with open(d / "run_counter_collection.csv", "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Counter_Name", "Counter_Value"])
+            w.writeheader()
+            for _ in range(2):  # two factorizations
+                for n, x in zip(names, v):
+                    w.writerow({"Kernel_Name": n, "Counter_Name": counter, "Counter_Value": x})
+        dirs[counter] = str(d)
+    out = tmp_path / "traffic.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), str(out), dirs["FETCH_SIZE"],
+                    dirs["WRITE_SIZE"]], check=True, capture_output=True)
+    res = json.load(open(out))
+    assert res["chol_factor"]["bytes_per_launch"] == (100.0 + 10.0) * 1024  # one factorization's chain
+    assert res["schur_rows"]["bytes_per_launch"] == (7.0 + 5.0) * 1024

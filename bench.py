@@ -119,13 +119,34 @@ def _oracle_run(prob, iters, nthreads):
             "chi2": timed[-1].chi2}, oracle_py
 
 
+def cpu_grant():
+    """The CPUs this process is granted (the baseline runs on all of them): the affinity mask, capped by a
+    cgroup CPU quota (the GPU box grants a share of a larger host, so os.cpu_count() counts CPUs this job cannot use)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            parts = open(path).read().split()
+            if path.endswith("cpu.max") and parts[0] != "max":
+                quota = int(parts[0]) / int(parts[1])
+            elif path.endswith("cfs_quota_us") and int(parts[0]) > 0:
+                per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                quota = int(parts[0]) / per
+            if quota:
+                break
+        except (OSError, ValueError, IndexError):
+            continue
+    cpus = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"cpus": cpus, "affinity": aff, "cgroup_quota": quota, "os_cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(prob, iters, threads, iters_1t=2):
     """The oracle (C++ restatement of BlockSolver + LM) with the reference's own CSparse (oracle/_ref,
     cs_amd block ordering + up-looking LL^T) timed on this host: OpenMP assembly/Schur on all granted
     cores (the reference forces OpenMP, CMakeLists.txt:146) and a 1-thread run; the factorization is
     single-threaded in both, as CSparse is."""
-    nthreads = threads or os.cpu_count() or 1
-    nthreads = min(nthreads, 16)  # the GPU box grants a 16-CPU share
+    grant = cpu_grant()
+    nthreads = threads or grant["cpus"]
     multi, oracle_py = _oracle_run(prob, iters, nthreads)
     if multi is None:
         return None
@@ -134,6 +155,7 @@ def cpu_baseline(prob, iters, threads, iters_1t=2):
         "value": multi["value"],
         "unit": "LM it/s",
         "cores": nthreads,
+        "cpu_grant": grant,
         "kind": "port",
         "ms_per_linear_solve": multi["ms_per_linear_solve"],
         "one_thread": one,
@@ -190,13 +212,13 @@ def posegraph_leg(local, steps=5, warmup=1):
         "ms_per_linear_solve": float(np.median(lin)),
         "steps": steps,
         "final_chi2": timed[-1].chi2,
-        "factor": {"bound": "mfma", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+        "factor": with_peaks({"bound": "mfma", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                    "frac": tf / PEAK_FP64_TFLOPS, "flops_per_launch": flops,
                    "flops_convention": "reference cs_amd sum c_k^2" if ref else "backend ordering",
                    "backend_ordering_flops": own,
                    "backend_ordering_achieved": own / (fms * 1e-3) / 1e12 if fms > 0 else 0.0,
                    "backend_ordering_frac": own / (fms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if fms > 0 else 0.0,
-                   "avg_launch_ms": fms},
+                   "avg_launch_ms": fms, "traffic": traffic_lookup("C3")("chol_factor")}),
     }
 
 
@@ -229,6 +251,8 @@ def c5_leg(local, steps=10, warmup=2):
         opt.optimize_step(it)
         it += 1
     kt = {k: opt.kernel_ms(k) for k in names}
+    rows_bytes = opt.kernel_bytes("schur_rows")
+    tr = traffic_lookup("C5")
     cf = load_json("chol_flops.json").get("C5", {}).get("ref_cs_amd", {}).get("flops")
     own = opt.kernel_flops("chol_factor")
     fms = kt["chol_factor"]
@@ -240,12 +264,20 @@ def c5_leg(local, steps=10, warmup=2):
         "ms_per_step": 1e3 * dt / steps, "ms_per_linear_solve": float(np.median(lin)),
         "levenberg_trials": sum(s.levenbergIterations for s in timed), "final_chi2": timed[-1].chi2,
         "stages_ms_avg": kt,
-        "factor": {"bound": "mfma", "avg_launch_ms": fms, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                   "ref_order_flops": cf, "backend_ordering_flops": own,
-                   "achieved": (cf or own) / (fms * 1e-3) / 1e12 if fms > 0 else 0.0,
-                   "backend_ordering_achieved": own / (fms * 1e-3) / 1e12 if fms > 0 else 0.0},
+        "factor": with_peaks({"bound": "mfma", "avg_launch_ms": fms, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                              "ref_order_flops": cf, "backend_ordering_flops": own,
+                              "achieved": (cf or own) / (fms * 1e-3) / 1e12 if fms > 0 else 0.0,
+                              "frac": (cf or own) / (fms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if fms > 0 else 0.0,
+                              "backend_ordering_achieved": own / (fms * 1e-3) / 1e12 if fms > 0 else 0.0,
+                              "traffic": tr("chol_factor"), "traffic_fetch_doubled": tr("chol_factor", "bytes_fetch_doubled")}),
         "generate_s": gen,
     }
+    if kt["schur_rows"] > 0:
+        a = rows_bytes / (kt["schur_rows"] * 1e-3) / 1e9
+        out["schur_rows"] = with_peaks({"bound": "hbm", "achieved": a, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                        "frac": a / PEAK_HBM_GBS, "algorithmic_bytes_per_launch": rows_bytes,
+                                        "avg_launch_ms": kt["schur_rows"], "traffic": tr("schur_rows"),
+                                        "traffic_fetch_doubled": tr("schur_rows", "bytes_fetch_doubled")})
     opt.close()
     return out
 
@@ -256,6 +288,52 @@ def load_json(name):
         return json.load(open(path)) if os.path.exists(path) else {}
     except Exception:
         return {}
+
+
+def traffic_lookup(config):
+    """PMC traffic per launch (tools/pmc_traffic.py output) for `config`: G2OHIP_TRAFFIC_JSON_<CONFIG>, else
+    G2OHIP_TRAFFIC_JSON, else profiles/traffic_<config>.json, else profiles/traffic.json, whichever exists first and
+    was measured on that workload (its _meta.config); null otherwise.
+    traffic: the raw PMC bytes (FETCH_SIZE + WRITE_SIZE); traffic_fetch_doubled: with the guide's gfx950 half-count
+    correction of FETCH_SIZE, which is exact only for 16-B/lane streaming reads."""
+    data = {}
+    for path in (os.environ.get(f"G2OHIP_TRAFFIC_JSON_{config}"), os.environ.get("G2OHIP_TRAFFIC_JSON"),
+                 os.path.join(HERE, "profiles", f"traffic_{config.lower()}.json"),
+                 os.path.join(HERE, "profiles", "traffic.json")):
+        if not path or not os.path.exists(path):
+            continue
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("_meta", {}).get("config", "C4") == config:
+            data = d
+            break
+
+    def traffic(k, key="bytes_per_launch"):
+        rec = data.get(k)
+        if not isinstance(rec, dict):
+            return None
+        if key == "bytes_per_launch" and "bytes_fetch_doubled" not in rec:  # older file: only the doubled figure
+            return (rec["fetch_size_kb_raw"] + rec["write_size_kb"]) * 1024.0
+        if key == "bytes_fetch_doubled" and key not in rec:
+            return rec.get("bytes_per_launch")
+        return rec.get(key)
+    return traffic
+
+
+PEAKS_MEASURED = {}
+
+
+def with_peaks(d):
+    """Every roofline line against both peaks: the spec one (`peak`, `frac`) and the one measured on this GPU in this run
+    (g2ohip_measure_peaks: HBM streaming copy, FP64 MFMA issue loop)."""
+    if not PEAKS_MEASURED or not isinstance(d, dict):
+        return d
+    pm = PEAKS_MEASURED["hbm_copy_GBps"] if d.get("unit") == "GB/s" else PEAKS_MEASURED["fp64_mfma_TFps"]
+    d["peak_measured"] = pm
+    d["frac_measured"] = d["achieved"] / pm if pm > 0 else None
+    return d
 
 
 def stage_bytes(prob):
@@ -344,6 +422,10 @@ def main():
         it += 1
     kt = {k: {"avg_ms": opt.kernel_ms(k), "count": opt.kernel_count(k)} for k in names}
     finfo = opt.factor_info()
+    try:  # after the timed region: ~1 s of streaming copy and MFMA / VALU issue loops
+        PEAKS_MEASURED.update(g2o_amd.measure_peaks(local))
+    except Exception as ex:  # reported, not fatal
+        PEAKS_MEASURED["error"] = repr(ex)
 
     # algorithmic flops of the factorization: sum_k c_k^2 under the REFERENCE ordering (cs_amd on the block
     # pattern), from tools/chol_flops.py (oracle/_ref, committed JSON); the backend's own
@@ -351,27 +433,7 @@ def main():
     cf = load_json("chol_flops.json").get(args.config, {})
     ref_flops = cf.get("ref_cs_amd", {}).get("flops")
     own_flops = finfo["flops"]
-    traffic_all = load_json("traffic.json")
-    tf = os.environ.get("G2OHIP_TRAFFIC_JSON")
-    if tf and os.path.exists(tf):
-        traffic_all = json.load(open(tf))
-
-    # PMC traffic is measured on one workload (its _meta.config): other configs report null
-    traffic_cfg = traffic_all.get("_meta", {}).get("config", "C4")
-
-    # traffic: the raw PMC bytes (FETCH_SIZE + WRITE_SIZE); traffic_fetch_doubled: with the guide's gfx950 half-count
-    # correction of FETCH_SIZE, which is exact only for 16-B/lane streaming reads (tools/pmc_traffic.py)
-    def traffic(k, key="bytes_per_launch"):
-        if traffic_cfg != args.config:
-            return None
-        rec = traffic_all.get(k)
-        if not isinstance(rec, dict):
-            return None
-        if key == "bytes_per_launch" and "bytes_fetch_doubled" not in rec:  # older file: only the doubled figure
-            return (rec["fetch_size_kb_raw"] + rec["write_size_kb"]) * 1024.0
-        if key == "bytes_fetch_doubled" and key not in rec:
-            return rec.get("bytes_per_launch")
-        return rec.get(key)
+    traffic = traffic_lookup(args.config)
 
     flops = ref_flops if ref_flops else own_flops
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
@@ -467,8 +529,11 @@ def main():
             "parallelism": f"landmark-shard{world}" if world > 1 else "single",
         },
         "stages_ms_avg": {k: v["avg_ms"] for k, v in kt.items()},  # 2 extra untimed iterations
-        "roofline": roofline,
-        "roofline_secondary": secondary,
+        "roofline": with_peaks(roofline),
+        "roofline_secondary": [with_peaks(d) for d in secondary],
+        "peaks": {"spec": {"hbm_GBps": PEAK_HBM_GBS, "fp64_TFps": PEAK_FP64_TFLOPS,
+                           "source": "MI355X_MICROARCH.md (spec)"},
+                  "measured": dict(PEAKS_MEASURED, source="g2ohip_measure_peaks on this GPU, this run")},
         "factor": finfo,
         "setup_s": {"generate": gen_s, "warmup_incl_structure": warm_s},
         "runtime": runtime,

@@ -62,11 +62,12 @@ EXPORTS = [
     "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_solver_multiply_hessian",
     "g2ohip_solver_linear_residual", "g2ohip_solver_factor_info", "g2ohip_solver_compute_marginals", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
     "g2ohip_discard_top", "g2ohip_stage", "g2ohip_linear_solve_ccs", "g2ohip_comm_unique_id",
-    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_comm_selftest", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
+    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_comm_selftest", "g2ohip_comm_selftest_rs", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
     "g2ohip_kernel_timing_only", "g2ohip_set_stats_level", "g2ohip_kernel_ms",
     "g2ohip_kernel_count", "g2ohip_kernel_bytes", "g2ohip_kernel_flops", "g2ohip_last_error",
     "g2ohip_version", "g2ohip_host_payload_len", "g2ohip_solver_save_hessian", "g2ohip_solver_set_write_debug",
-    "g2ohip_comm_local_reduce_host", "g2ohip_runtime_info", "g2ohip_device_synchronize",
+    "g2ohip_comm_local_reduce_host", "g2ohip_runtime_info", "g2ohip_device_synchronize", "g2ohip_lm_scale_factor",
+    "g2ohip_measure_peaks",
 ]
 
 
@@ -132,6 +133,7 @@ def lib() -> C.CDLL:
         "g2ohip_set_comm": ([P, P, I, I], I),
         "g2ohip_set_comm_local": ([P, C.c_char_p, I, I], I),
         "g2ohip_comm_selftest": ([I, P, I, P, P], I),
+        "g2ohip_comm_selftest_rs": ([I, P, I, P, P, P], I),
         "g2ohip_debug_phases": ([P, I], I),
         "g2ohip_symbolic_analyze": ([I, I, I, P, P, P, P], I),
         "g2ohip_enable_kernel_timing": ([P, I], None),
@@ -143,6 +145,8 @@ def lib() -> C.CDLL:
         "g2ohip_kernel_flops": ([P, C.c_char_p], D),
         "g2ohip_last_error": ([], C.c_char_p),
         "g2ohip_version": ([], C.c_char_p),
+        "g2ohip_lm_scale_factor": ([D], D),
+        "g2ohip_measure_peaks": ([I, P, I], I),
         "g2ohip_host_payload_len": ([P, I], LL),
         "g2ohip_solver_save_hessian": ([P, C.c_char_p], I),
         "g2ohip_solver_set_write_debug": ([P, I], I),
@@ -168,6 +172,14 @@ def runtime_info() -> dict:
 
 def device_synchronize(device: int = 0) -> None:
     _check(lib().g2ohip_device_synchronize(device), "device_synchronize")
+
+
+def measure_peaks(device: int = 0) -> dict:
+    """Measured roofline peaks of the device (g2ohip_measure_peaks): HBM streaming copy, FP64 MFMA and VALU issue rates."""
+    out = np.zeros(4)
+    _check(lib().g2ohip_measure_peaks(device, _p(out), 4), "measure_peaks")
+    return {"hbm_copy_GBps": float(out[0]), "fp64_mfma_TFps": float(out[1]), "fp64_valu_TFps": float(out[2]),
+            "cus": int(out[3])}
 
 
 def comm_local_reduce_host(group_key: str, rank: int, nranks: int, buf, is_max: bool = False):
@@ -431,16 +443,16 @@ class SparseOptimizer:
         return {p: out[k * pd * pd:(k + 1) * pd * pd].reshape(pd, pd).T.copy() for k, p in enumerate(pairs)}
 
     FACTOR_INFO_KEYS = ("n", "nnzL", "flops", "supernodes", "levels", "max_front", "blocked_fronts",
-                        "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds", "dag_levels",
+                        "inplace_levels", "prescatter_levels", "syrk_launches", "bwd_rounds", None,
                         "owned_fronts", "shared_fronts", "subtree_roots", "root_exchange_doubles",
                         "model_rank_subtrees_s", "model_shared_s", "model_single_gpu_s", "model_exchange_s",
                         "distributed", "reduce_scatter", "rs_segment_doubles", "rs_tail_doubles", "model_input_s",
-                        "model_input_allreduce_s", "w64_levels")
+                        "model_input_allreduce_s", None)  # None: retired slots (always 0), kept for the ABI layout
 
     def factor_info(self) -> dict:
         out = np.zeros(len(self.FACTOR_INFO_KEYS))
         _check(lib().g2ohip_solver_factor_info(self.h, _p(out), len(out)), "factor_info")
-        return dict(zip(self.FACTOR_INFO_KEYS, out.tolist()))
+        return {k: v for k, v in zip(self.FACTOR_INFO_KEYS, out.tolist()) if k is not None}
 
     def stage(self, lam: float):
         dims = np.zeros(3, np.int64)
@@ -462,10 +474,11 @@ class SparseOptimizer:
         """RCCL binding smoke test on one device (one-rank communicator): allreduce sum, allreduce max and the
         in-place reduce-scatter sum (rank 0's segment), each over `values`."""
         v = np.ascontiguousarray(values, np.float64)
-        out = np.zeros(3 * v.size)
+        out = np.zeros(2 * v.size)
+        rs = np.zeros(v.size)
         uid = (C.c_ubyte * 128).from_buffer_copy(SparseOptimizer.comm_unique_id())
-        _check(lib().g2ohip_comm_selftest(device, uid, v.size, _p(v), _p(out)), "comm_selftest")
-        return out[: v.size], out[v.size: 2 * v.size], out[2 * v.size:]
+        _check(lib().g2ohip_comm_selftest_rs(device, uid, v.size, _p(v), _p(out), _p(rs)), "comm_selftest")
+        return out[: v.size], out[v.size:], rs
 
     def set_comm(self, uid: bytes, rank: int, nranks: int):
         buf = (C.c_ubyte * 128).from_buffer_copy(uid)

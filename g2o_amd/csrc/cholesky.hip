@@ -286,182 +286,6 @@ __device__ __forceinline__ void publish_inverse(const double* D, int kb, int tid
   }
 }
 
-// ---------------------------------------------------------------------------- 64-column panel steps
-// The launch-per-panel schedule with 64-column panels (DeviceCholesky::setup chooses it per level): half the kernel
-// boundaries on the diagonal chain — each boundary costs ~3 us of drain + dispatch and ~2.4 us of reloads at the next
-// diagonal task's start (tools/phase_probe.py) against ~4 us for a chol32 — and every trailing update is rank 64 (the
-// lagged pairs' traffic without their strip steps). The current panel's inverse L_p^-1 = [A 0; N B] is kept as the two
-// per-32-panel inverses A = L_a^-1, B = L_b^-1 (linv, as the 32-column schedule: the backward solve and
-// computeMarginals read them) and N = -L_b^-1 L_ba L_a^-1 (linvn, one per 64-panel). Tasks (StepTask, k0kb = k0 | kb << 16,
-// kb <= 64):
-//   tile (flags & 1 update)  TRSM of the tile's panel rows as X = P L_p^-T in two 32-column halves (X_a = P_a A^T,
-//                            X_b = P_a N^T + P_b B^T), then C_IJ -= X_I X_J^T half by half (rank 64); writers store
-//                            L rows and update the front vector with X_I y_p;
-//   diagonal (flags & 4)     the next 64 x 64 block: D' = D - X X^T with its own X rows, then chol64 (below);
-//   inverse (flags & 16)     X = L11^-1 for the backward solve, block row by block row (32-row blocks p, 32-column
-//                            blocks j): W_pj += L_pa X_aj + L_pb X_bj for the previous 64-panel (a, b); the two rows of
-//                            the current 64-panel finalised as X = -L_p^-1 W.
-constexpr int W64_LI = 3 * NB * PS;           // A | N | B of the current panel, row-major, stride PS
-constexpr int W64_R = W64_LI;                 // role region
-constexpr int W64_COL = W64_R + TT * PS + 3 * NB * DS;
-constexpr int W64_VN = W64_COL + 4 * NB, W64_YL = W64_VN + TT, W64_YK = W64_YL + TT;
-constexpr int W64_LDS = W64_YK + TT;
-static_assert(W64_R + 2 * TT * PS <= W64_COL && TT * (TT + 1) <= 2 * TT * PS, "tile role region");
-static_assert(W64_R + TT * PS + NB * PS + TT * (NB + 1) <= W64_LDS, "inverse role region");
-static_assert(W64_COL % 2 == 0, "col buffer: 16-byte aligned");
-
-struct Chol64Lds {
-  double *Qaa, *Qba, *Qbb;  // quadrants of the block, 32 x DS each (row-major; lower parts valid)
-  double *S, *Nb;           // scratch: 64 x PS and 32 x PS
-  double *col, *vn, *yl;    // chol32 column buffers, right-hand side (64), y (64)
-};
-// publish_inverse over threads [t0, t0 + nt) of the workgroup (the others are busy)
-__device__ __forceinline__ void publish_inv_part(const double* D, int kb, int t, int nt, double* linv, double* X, int ldx) {
-  for (int e = t; e < NB * NB; e += nt) linv[e] = D[(e & (NB - 1)) * DS + (e >> 5)];
-  for (int e = t; e < NB * NB; e += nt) {
-    const int c = e >> 5, i = e & (NB - 1);
-    if (c < kb && i < kb) X[(size_t)c * ldx + i] = D[c * DS + i];
-  }
-}
-struct NoSide {
-  __device__ void operator()() const {}
-};
-// Factor the kbn x kbn (kbn <= 64) block in q.Q* with right-hand side q.vn: L_a = chol(Qaa), L_ba = Qba L_a^-T,
-// L_b = chol(Qbb - L_ba L_ba^T), N = -L_b^-1 L_ba L_a^-1, y = L^-1 vn. Publishes L_a^-1, L_b^-1 (linv rows), N (linvn),
-// the block's part of X = L11^-1 (X, leading dimension ldx) and y (ysol); L_ba goes to the factor (Lba, leading dimension
-// ldl: the only part of L this block owns in lbuf, diagonal 32 x 32 blocks are never stored). Whole workgroup; while
-// wave 0 runs each chol32 the other three waves work beside it: side_a() during the first (the caller's updates of Qba,
-// Qbb and vn_b), M = L_ba L_a^-1 and the a half's publishing during the second.
-template <class SideA>
-__device__ __forceinline__ void chol64(const Chol64Lds& q, int kbn, int tid, int* fail, double* ysol, double* linv_a,
-                                       double* linv_b, double* linvn, double* X, int ldx, double* Lba, int ldl,
-                                       unsigned long long* ph, SideA side_a) {
-  const int lane = tid & 63, w = tid >> 6, lr = lane & 15, lk = lane >> 4;
-  const int kna = min(NB, kbn), knb = kbn - NB;
-  if (tid < 64) factor_block(q.Qaa, kna, q.vn, q.col, tid, fail, ysol, ph, q.yl);
-  else side_a();
-  __syncthreads();
-  if (knb <= 0) {
-    publish_inv_part(q.Qaa, kna, tid, 256, linv_a, X, ldx);
-    return;
-  }
-  const int tr = w & 1, tc = w >> 1;
-  {  // L_ba = Qba L_a^-T (L_a^-1(c, k) = Qaa[k DS + c]); rows past knb zeroed (N and the tiles rely on it)
-    dx4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < NB / 4; ++kk) {
-      const int k = kk * 4 + lk;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q.Qba[(16 * tr + lr) * DS + k], q.Qaa[k * DS + 16 * tc + lr], acc, 0, 0, 0);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 16 * tr + lk + 4 * i, c = 16 * tc + lr;
-      const double v = r < knb ? acc[i] : 0.0;
-      q.Qba[r * DS + c] = v;
-      if (r < knb) Lba[(size_t)c * ldl + r] = v;
-    }
-  }
-  __syncthreads();
-  if (w < 3) {  // Qbb -= L_ba L_ba^T on the lower 16 x 16 tiles (0,0), (1,0), (1,1)
-    const int ur = (w + 1) >> 1, uc = w >> 1;
-    dx4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < NB / 4; ++kk) {
-      const int k = kk * 4 + lk;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q.Qba[(16 * ur + lr) * DS + k], q.Qba[(16 * uc + lr) * DS + k], acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) q.Qbb[(16 * ur + lk + 4 * i) * DS + 16 * uc + lr] -= acc[i];
-  } else if (lane < NB) {  // the b rows' right-hand side: vn_b -= L_ba y_a
-    double s2 = 0.0;
-#pragma unroll
-    for (int k = 0; k < NB; ++k) s2 += q.Qba[lane * DS + k] * q.yl[k];
-    q.vn[NB + lane] -= s2;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    factor_block(q.Qbb, knb, q.vn + NB, q.col, tid, fail, ysol + NB, nullptr, q.yl + NB);
-  } else {  // beside it: M = L_ba L_a^-1 (row-major into S; tiles over waves 1..3), the a half published
-    for (int tl = w - 1; tl < 4; tl += 3) {
-      const int ur = tl & 1, uc = tl >> 1;
-      dx4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < NB / 4; ++kk) {
-        const int k = kk * 4 + lk;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q.Qba[(16 * ur + lr) * DS + k], q.Qaa[(16 * uc + lr) * DS + k], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) q.S[(16 * ur + lk + 4 * i) * PS + 16 * uc + lr] = acc[i];
-    }
-    publish_inv_part(q.Qaa, kna, tid - 64, 192, linv_a, X, ldx);
-  }
-  __syncthreads();
-  {  // N = -L_b^-1 M
-    dx4 an = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < NB / 4; ++kk) {
-      const int k = kk * 4 + lk;
-      an = __builtin_amdgcn_mfma_f64_16x16x4f64(q.Qbb[k * DS + 16 * tr + lr], q.S[k * PS + 16 * tc + lr], an, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) q.Nb[(16 * tr + lk + 4 * i) * PS + 16 * tc + lr] = -an[i];
-  }
-  __syncthreads();
-  publish_inv_part(q.Qbb, knb, tid, 256, linv_b, X + (size_t)NB * ldx + NB, ldx);
-#pragma unroll
-  for (int u = 0; u < NB * NB / 256; ++u) {
-    const int e = tid + 256 * u;
-    linvn[e] = q.Nb[(e >> 5) * PS + (e & (NB - 1))];
-  }
-#pragma unroll
-  for (int u = 0; u < NB * NB / 256; ++u) {
-    const int e = tid + 256 * u, c = e >> 5, i = e & (NB - 1);
-    if (i < knb) X[(size_t)c * ldx + NB + i] = q.Nb[i * PS + c];
-  }
-}
-
-// stage the current panel's inverses A | N | B (row-major, as in linv / linvn) into Li3; B and N only with a b half
-__device__ __forceinline__ void load_li3(const double* la, const double* ln, const double* lb, bool bh, int tid,
-                                         double (&v)[3][NB * NB / 256]) {
-#pragma unroll
-  for (int u = 0; u < NB * NB / 256; ++u) {
-    v[0][u] = la[tid + 256 * u];
-    v[1][u] = ld0(ln, tid + 256 * u, bh);
-    v[2][u] = ld0(lb, tid + 256 * u, bh);
-  }
-}
-__device__ __forceinline__ void store_li3(double* Li3, int tid, const double (&v)[3][NB * NB / 256]) {
-#pragma unroll
-  for (int h = 0; h < 3; ++h)
-#pragma unroll
-    for (int u = 0; u < NB * NB / 256; ++u) {
-      const int e = tid + 256 * u;
-      Li3[h * NB * PS + (e >> 5) * PS + (e & (NB - 1))] = v[h][u];
-    }
-}
-// X rows of a 64-row panel slab (rows 16 w .. 16 w + 15 of this wave), cols [16 h, 16 h + 16) of a 32-column half:
-// x[h] += P(rows, 0:32) Lq^T with Lq row-major (stride PS) in LDS
-__device__ __forceinline__ void trsm_half(const double* P, const double* Lq, int lane, int w, dx4 (&x)[2]) {
-  const int lr = lane & 15, lk = lane >> 4;
-#pragma unroll
-  for (int kk = 0; kk < NB / 4; ++kk) {
-    const int k = kk * 4 + lk;
-    const double a = P[(16 * w + lr) * PS + k];
-    x[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Lq[lr * PS + k], x[0], 0, 0, 0);
-    x[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Lq[(16 + lr) * PS + k], x[1], 0, 0, 0);
-  }
-}
-__device__ __forceinline__ void store_xhalf(double* P, int lane, int w, const dx4 (&x)[2]) {
-  const int lr = lane & 15, lk = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 16 * w + lk + 4 * i;
-    P[r * PS + lr] = x[0][i];
-    P[r * PS + 16 + lr] = x[1][i];
-  }
-}
-
 // ---------------------------------------------------------------------------- assembly + extend-add
 // One launch per level assembles every front of the level from scratch (no front-pool memset, no
 // separate scatter pass), with two kinds of workgroup:
@@ -484,9 +308,7 @@ __device__ __forceinline__ double input_entry(const double* vals, const int* ent
 }
 // ASM: the level's fronts are assembled here (EAC: rows per LDS column chunk); else they were pre-zeroed and
 // scattered
-// W64: the level runs 64-column panel steps (k_step64): its first-block tasks assemble and factor the first 64 columns
-// (chol64), and the slabs leave those 64 x 64 entries to them
-template <bool ASM, int EAC, bool W64>
+template <bool ASM, int EAC>
 __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                     const int* __restrict__ children, const int* __restrict__ relmap,
                                                     const int* __restrict__ jtab, const int* __restrict__ cmptr,
@@ -495,106 +317,13 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
                                                     const double* __restrict__ lam, double* __restrict__ fronts,
                                                     double* __restrict__ vecs, double* __restrict__ lbuf,
                                                     double* __restrict__ ysol, double* __restrict__ linv,
-                                                    double* __restrict__ linvn, double* __restrict__ xinv,
-                                                    int* __restrict__ fail) {
+                                                    double* __restrict__ xinv, int* __restrict__ fail) {
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr, kb0 = min(W64 ? TT : NB, me.ns);
+  const int m = me.ns + me.nr, kb0 = min(NB, me.ns);
   double* F = fronts + me.front_off;
   double* v = vecs + me.vec_off;
   const int tid = threadIdx.x;
-  // W64: one buffer for both roles (the 64-wide first block, the slabs' column buffers)
-  constexpr int SMU = !W64 ? 1 : (W64_LDS > 4 * EAC ? W64_LDS : 4 * EAC);
-  __shared__ __attribute__((aligned(16))) double smu[SMU];
-  if constexpr (W64) {
-    if (t.c == 1) {
-      // ---- first 64 x 64 block: assembled (input entries, children), factored with chol64, published
-      Chol64Lds q;
-      q.S = smu + W64_R;
-      q.Qaa = q.S + TT * PS;
-      q.Qba = q.Qaa + NB * DS;
-      q.Qbb = q.Qba + NB * DS;
-      q.Nb = smu + NB * PS;
-      q.col = smu + W64_COL;
-      q.vn = smu + W64_VN;
-      q.yl = smu + W64_YL;
-      int* cp = reinterpret_cast<int*>(smu + W64_YK);  // kb0 + 1 column pointers (64 doubles hold 128 ints)
-      auto qp = [&](int r, int c) -> double* {
-        return r < NB ? q.Qaa + r * DS + c : (c < NB ? q.Qba + (r - NB) * DS + c : q.Qbb + (r - NB) * DS + c - NB);
-      };
-      PH_BEGIN(1)
-      if constexpr (!ASM) {
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-          const bool ok = r < kb0 && c <= r;
-          const double x = ld0(F, c * m + r, ok);
-          if (c <= r) *qp(r, c) = x;
-        }
-        if (tid < TT) q.vn[tid] = ld0(v, tid, tid < kb0);
-      } else {
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-          if (c <= r) *qp(r, c) = 0.0;
-        }
-        if (tid <= kb0) cp[tid] = colptr[me.c0 + tid];
-        if (tid < TT) q.vn[tid] = ld0(v, tid, tid < kb0);
-        __syncthreads();
-        for (int e = cp[0] + tid; e < cp[kb0]; e += 256) {
-          int lo = 0, hi = kb0;
-          while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (cp[mid] <= e) lo = mid; else hi = mid; }
-          int r;
-          const double x = input_entry(vals, ent_src, ent_row, e, lam, r);
-          if (r < kb0) *qp(r, lo) = x;
-        }
-      }
-      __syncthreads();
-      // children two at a time: every load of a pair in flight before the first add, adds in fixed child order
-      constexpr int B0C = 2;
-      for (int kc = me.child_begin; kc < me.child_end; kc += B0C) {
-        double val[B0C][16], vv[B0C];
-        int dst[B0C][16], vdst[B0C];
-#pragma unroll
-        for (int c = 0; c < B0C; ++c) {
-          const bool has = kc + c < me.child_end;
-          const FrontDesc cd = fd[children[has ? kc + c : kc]];
-          const int mc = cd.ns + cd.nr, nrc = cd.nr;
-          const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;
-          const int* rel = relmap + cd.rows_off;
-          const int n0 = has ? jtab[cd.jt_off] : 0;  // child rows mapping into the first 64 x 64 block
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int e = tid + 256 * u;
-            const int i = e & (TT - 1), j = e >> 6;
-            const bool in = i < nrc && j <= i;
-            val[c][u] = ld0(U, j * mc + i, in);
-            const int ri = ld0(rel, i, in), rj = ld0(rel, j, in);
-            dst[c][u] = (in && i < n0) ? (ri | (rj << 8)) : -1;
-          }
-          vv[c] = ld0(vecs + cd.vec_off + cd.ns, tid, tid < nrc && tid < TT);
-          const int rt = ld0(rel, tid, tid < nrc && tid < TT);
-          vdst[c] = tid < n0 && tid < TT ? rt : -1;
-        }
-#pragma unroll
-        for (int c = 0; c < B0C; ++c) {
-          if (kc + c >= me.child_end) break;
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            if (dst[c][u] >= 0) *qp(dst[c][u] & 0xff, dst[c][u] >> 8) += val[c][u];
-          if (vdst[c] >= 0) q.vn[vdst[c]] += vv[c];
-          __syncthreads();
-        }
-      }
-      PH(2)
-      chol64(q, kb0, tid, fail, ysol + me.c0, linv + (size_t)me.c0 * (NB * NB), linv + (size_t)(me.c0 + NB) * (NB * NB),
-             linvn + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns, lbuf + me.l_off + NB, m, PH_REC, NoSide{});
-      PH(3)
-      PH(4)
-      return;
-    }
-  }
-  if constexpr (!W64) {
   if (t.c == 1) {
     __shared__ double D[NB * DS];
     __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
@@ -665,15 +394,6 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
       }
     }
     PH(2)
-    if (t.a < 0) {  // level factored by k_dag: the assembled block and its right-hand side go into the front
-#pragma unroll
-      for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
-        const int e = tid + 256 * u_, r = e & (NB - 1), c = e >> 5;
-        if (r < kb0 && c < kb0 && r >= c) F[c * m + r] = D[r * DS + c];
-      }
-      if (tid < kb0) v[tid] = vy[tid];
-      return;
-    }
     if (tid < 64) factor_block(D, kb0, vy, col, tid, fail, ysol + me.c0, PH_REC);
     __syncthreads();
     publish_inverse(D, kb0, tid, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns);
@@ -681,15 +401,13 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     PH(4)
     return;
   }
-  }
   const int a = t.a, b = t.b;
   const int lane = tid & 63, w = tid >> 6;
   if constexpr (ASM) {
     // In-place assembly: each wave builds its columns in an LDS column buffer (zero, the column's input
     // entries, then every (child, child column) pair mapping to it in child order) and writes each entry
     // of the front once; rows in chunks of EAC. The children's update vectors follow below.
-    __shared__ double cbuf_[W64 ? 1 : 4][W64 ? 1 : EAC];
-    double(*cbuf)[EAC] = W64 ? reinterpret_cast<double(*)[EAC]>(smu) : reinterpret_cast<double(*)[EAC]>(&cbuf_[0][0]);
+    __shared__ double cbuf[4][EAC];
     for (int j = a + w; j < b; j += 4) {
       const int rlo = j < kb0 ? kb0 : j;  // rows of the first diagonal block: block-0 task
       double* Fj = F + (size_t)j * m;
@@ -1121,344 +839,6 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   PH1R(7)
 }
 
-// ---------------------------------------------------------------------------- 64-column panel steps (kernel)
-// (see the 64-column helpers above k_extend_add)
-__global__ void __launch_bounds__(256, 2) k_step64(const StepTask* __restrict__ tasks, const launch::StepHead head,
-                                                   double* __restrict__ fronts, double* __restrict__ lbuf,
-                                                   double* __restrict__ vecs, double* __restrict__ ysol,
-                                                   double* __restrict__ linv, double* __restrict__ linvn,
-                                                   double* __restrict__ xinv, int* __restrict__ fail) {
-  __shared__ __attribute__((aligned(16))) double sm[W64_LDS];
-  PH_BEGIN(2)
-  PH1_BEGIN(3)
-  const StepTask t = (int)blockIdx.x < head.n ? head.t[blockIdx.x] : tasks[blockIdx.x];
-  const int m = t.m, ns = t.ns;
-  double* F = fronts + t.f_off;
-  double* L = lbuf + t.l_off;
-  double* v = vecs + t.v_off;
-  const int k0 = t.k0kb & 0xffff, kb = t.k0kb >> 16;  // current panel [k0, k0 + kb), kb <= 64
-  const int kbb = kb - NB;                             // columns of its b half (<= 0: none)
-  const bool bh = kbb > 0;
-  const int r0 = k0 + kb;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double* Li3 = sm;
-  const double* la = linv + (size_t)(t.c0 + k0) * (NB * NB);
-  const double* lb = linv + (size_t)(t.c0 + k0 + (bh ? NB : 0)) * (NB * NB);
-  const double* ln = linvn + (size_t)(t.c0 + k0) * (NB * NB);
-
-  if (t.flags & 4) {
-    // ---- next-diagonal task: the 64 x 64 block at r0 with this panel's update applied, then chol64
-    const int kbn = min(TT, ns - r0);
-    Chol64Lds q;
-    q.S = sm + W64_R;
-    q.Qaa = q.S + TT * PS;
-    q.Qba = q.Qaa + NB * DS;
-    q.Qbb = q.Qba + NB * DS;
-    q.Nb = Li3 + NB * PS;
-    q.col = sm + W64_COL;
-    q.vn = sm + W64_VN;
-    q.yl = sm + W64_YL;
-    double* yk = sm + W64_YK;
-    double lv[3][NB * NB / 256], pa[8], pb[8], dq[16];
-    load_li3(la, ln, lb, bh, tid, lv);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-      pa[u] = ld0(F, (k0 + c) * m + r0 + r, r < kbn && c < kb);
-      pb[u] = ld0(F, (k0 + NB + c) * m + r0 + r, r < kbn && c < kbb);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-      dq[u] = ld0(F, (r0 + c) * m + r0 + r, r < kbn && c <= r);
-    }
-    const double vo = ld0(v, r0 + tid, tid < kbn);
-    const double ykv = ld0(ysol, t.c0 + k0 + tid, tid < kb);
-    store_li3(Li3, tid, lv);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-      q.S[r * PS + c] = pa[u];
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-      if (c <= r) {
-        double* Qp = r < NB ? q.Qaa + r * DS + c : (c < NB ? q.Qba + (r - NB) * DS + c : q.Qbb + (r - NB) * DS + c - NB);
-        *Qp = dq[u];
-      }
-    }
-    if (tid < TT) { q.vn[tid] = vo; yk[tid] = ykv; }
-    __syncthreads();
-    PH(2)
-    // X = P L_p^-T: X_a = P_a A^T (S afterwards), X_b = P_a N^T + P_b B^T (X2 = the Li3 region afterwards)
-    dx4 xa[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}}, xb[2] = {xa[0], xa[0]};
-    trsm_half(q.S, Li3, lane, w, xa);
-    trsm_half(q.S, Li3 + NB * PS, lane, w, xb);
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-      q.S[r * PS + c] = pb[u];
-    }
-    __syncthreads();
-    trsm_half(q.S, Li3 + 2 * NB * PS, lane, w, xb);
-    __syncthreads();
-    double* X2 = Li3;  // 64 x PS (A | N | B are dead)
-    store_xhalf(q.S, lane, w, xa);
-    store_xhalf(X2, lane, w, xb);
-    __syncthreads();
-    const int lr = lane & 15, lk = lane >> 4;
-    // tile (ur, uc) of the 64 x 64 block: Q -= X(rows) X(cols)^T over K = 64 (both halves)
-    auto dtile = [&](int ur, int uc) {
-      dx4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < NB / 4; ++kk) {
-        const int k = kk * 4 + lk;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(q.S[(16 * ur + lr) * PS + k], q.S[(16 * uc + lr) * PS + k], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int kk = 0; kk < NB / 4; ++kk) {
-        const int k = kk * 4 + lk;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X2[(16 * ur + lr) * PS + k], X2[(16 * uc + lr) * PS + k], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * ur + lk + 4 * i, c = 16 * uc + lr;
-        double* Qp = r < NB ? q.Qaa + r * DS + c : (c < NB ? q.Qba + (r - NB) * DS + c : q.Qbb + (r - NB) * DS + c - NB);
-        *Qp -= acc[i];
-      }
-    };
-    auto vrow = [&](int r) {  // vn_r -= X_r y_p
-      double s2 = 0.0;
-#pragma unroll
-      for (int k = 0; k < NB; ++k) s2 += q.S[r * PS + k] * yk[k] + X2[r * PS + k] * yk[NB + k];
-      q.vn[r] -= s2;
-    };
-    // the a quadrant and vn_a first (the first chol32 needs them); the b rows beside that chol32 (chol64's side work)
-    if (w < 3) dtile((w + 1) >> 1, w >> 1);
-    else if (lane < NB) vrow(lane);
-    __syncthreads();
-    PH(2)
-    chol64(q, kbn, tid, fail, ysol + t.c0 + r0, linv + (size_t)(t.c0 + r0) * (NB * NB),
-           linv + (size_t)(t.c0 + r0 + NB) * (NB * NB), linvn + (size_t)(t.c0 + r0) * (NB * NB),
-           xinv + t.x_off + (size_t)r0 * ns + r0, ns, L + (size_t)r0 * m + r0 + NB, m, PH_REC, [&] {
-             // waves 1..3: the ba quadrant's tiles (2,0) (2,1) (3,0) (3,1), the bb quadrant's (2,2) (3,2) (3,3), vn_b
-             const int sw = w - 1;
-             for (int tl = sw; tl < 7; tl += 3) {
-               const int ur = tl < 4 ? 2 + (tl >> 1) : (tl == 4 ? 2 : 3), uc = tl < 4 ? (tl & 1) : (tl == 6 ? 3 : 2);
-               dtile(ur, uc);
-             }
-             if (sw == 2 && lane < NB) vrow(NB + lane);
-           });
-    PH(3)
-    PH(4)
-    return;
-  }
-
-  if (t.flags & 16) {
-    // ---- inverse task: block column j, block row p (32-blocks) of X = L11^-1. The previous 64-panel is (a, b) =
-    // (k0 / 32 - 2, k0 / 32 - 1); W_pj += L_pa X_aj + L_pb X_bj; the current panel's rows (p = k0 / 32, with p + 1)
-    // are finalised: X_pj = -A W_pj, X_p+1,j = -(N W_pj + B W_p+1,j).
-    const int j = t.tile & 0xffff, p = t.tile >> 16, qa = k0 / NB - 2, qb = qa + 1;
-    const bool fin = p * NB == k0;
-    const int rows = min(fin ? TT : NB, ns - NB * p);  // output rows (64 when finalising both rows of the panel)
-    double* Xf = xinv + t.x_off;
-    double* Ls = sm + W64_R;            // 64 x PS: L(rows, q)
-    double* Xs = Ls + TT * PS;          // 32 x PS: X_qj (row k, column c)
-    double* Wl = Xs + NB * PS;          // 64 x (NB + 1)
-    const int lr = lane & 15, lk = lane >> 4;
-    // wave w: output rows 16 w .. 16 w + 15 (rows < 64), two 16-column tiles
-    dx4 acc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-    double wv[2][4];  // W so far (the earlier panels' terms), in the MFMA output layout
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * w + lk + 4 * i, c = 16 * h + lr;
-        wv[h][i] = ld0(Xf, (NB * j + c) * ns + NB * p + r, j < qa && r < rows);
-      }
-#pragma unroll
-    for (int term = 0; term < 2; ++term) {
-      const int qq = term == 0 ? qa : qb;
-      if (qq < j) continue;  // X_qj = 0 above the diagonal (uniform)
-      double lq[8], xq[4];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-        lq[u] = ld0(L, (NB * qq + c) * m + NB * p + r, r < rows);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = tid + 256 * u, k = e & (NB - 1), c = e >> 5;
-        xq[u] = Xf[(NB * j + c) * ns + NB * qq + k];
-      }
-      __syncthreads();  // the previous term's reads of Ls / Xs are done
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-        Ls[r * PS + c] = lq[u];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = tid + 256 * u, k = e & (NB - 1), c = e >> 5;
-        Xs[k * PS + c] = xq[u];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < NB / 4; ++kk) {
-        const int k = kk * 4 + lk;
-        const double a = Ls[(16 * w + lr) * PS + k];
-        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Xs[k * PS + lr], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Xs[k * PS + 16 + lr], acc[1], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[h][i] += wv[h][i];
-    if (!fin) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 16 * w + lk + 4 * i, c = 16 * h + lr;
-          if (r < rows) Xf[(size_t)(NB * j + c) * ns + NB * p + r] = acc[h][i];
-        }
-      return;
-    }
-    double lv[3][NB * NB / 256];
-    load_li3(la, ln, lb, bh, tid, lv);
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Wl[(16 * w + lk + 4 * i) * (NB + 1) + 16 * h + lr] = acc[h][i];
-    store_li3(Li3, tid, lv);
-    __syncthreads();
-    // wave w: rows 16 w .. of X_p (w < 2: -A W_top) or X_p+1 (w >= 2: -(N W_top + B W_bot))
-    dx4 xo[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-    const int wr = 16 * (w & 1);
-    const double* L1 = w < 2 ? Li3 : Li3 + NB * PS;
-#pragma unroll
-    for (int kk = 0; kk < NB / 4; ++kk) {
-      const int k = kk * 4 + lk;
-      const double a = L1[(wr + lr) * PS + k];
-      xo[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[k * (NB + 1) + lr], xo[0], 0, 0, 0);
-      xo[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[k * (NB + 1) + 16 + lr], xo[1], 0, 0, 0);
-    }
-    if (w >= 2) {
-#pragma unroll
-      for (int kk = 0; kk < NB / 4; ++kk) {
-        const int k = kk * 4 + lk;
-        const double a = Li3[2 * NB * PS + (wr + lr) * PS + k];
-        xo[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[(NB + k) * (NB + 1) + lr], xo[0], 0, 0, 0);
-        xo[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Wl[(NB + k) * (NB + 1) + 16 + lr], xo[1], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * w + lk + 4 * i, c = 16 * h + lr;
-        if (r < rows) Xf[(size_t)(NB * j + c) * ns + NB * p + r] = -xo[h][i];
-      }
-    return;
-  }
-
-  // ---- tile task (I, J): rows I0 = r0 + 64 ti, columns J0 = r0 + 64 tj
-  const int ti = t.tile & 0xffff, tj = t.tile >> 16;
-  const bool upd = t.flags & 1, writer = tj == 0;
-  const int I0 = r0 + ti * TT, J0 = r0 + tj * TT;
-  double* Pa = sm + W64_R;
-  double* Pb = Pa + TT * PS;
-  double* yk = sm + W64_YK;
-  const int climit = t.clim;
-  double lv[3][NB * NB / 256], pa0[8], pb0[8], pa1[8], pb1[8], cv[16];
-  load_li3(la, ln, lb, bh, tid, lv);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-    pa0[u] = ld0(F, (k0 + c) * m + I0 + r, c < kb && I0 + r < m);
-    pb0[u] = ld0(F, (k0 + c) * m + J0 + r, upd && c < kb && J0 + r < m);
-    pa1[u] = ld0(F, (k0 + NB + c) * m + I0 + r, c < kbb && I0 + r < m);
-    pb1[u] = ld0(F, (k0 + NB + c) * m + J0 + r, upd && c < kbb && J0 + r < m);
-  }
-  const double ykv = ld0(ysol, t.c0 + k0 + tid, tid < kb);
-  store_li3(Li3, tid, lv);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-    Pa[r * PS + c] = pa0[u];
-    Pb[r * PS + c] = pb0[u];
-  }
-  if (tid < TT) yk[tid] = ykv;
-  if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
-  __syncthreads();
-  // X_a = P_a A^T and P_a N^T for the rows of I and J (wave w: rows 16 w ..)
-  dx4 xia[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}}, xja[2] = {xia[0], xia[0]}, xib[2] = {xia[0], xia[0]},
-      xjb[2] = {xia[0], xia[0]};
-  trsm_half(Pa, Li3, lane, w, xia);
-  if (upd) trsm_half(Pb, Li3, lane, w, xja);
-  if (bh) {
-    trsm_half(Pa, Li3 + NB * PS, lane, w, xib);
-    if (upd) trsm_half(Pb, Li3 + NB * PS, lane, w, xjb);
-  }
-  __syncthreads();
-  if (bh) {  // X_b = P_a N^T + P_b B^T
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u, r = e & (TT - 1), c = e >> 6;
-      Pa[r * PS + c] = pa1[u];
-      Pb[r * PS + c] = pb1[u];
-    }
-    __syncthreads();
-    trsm_half(Pa, Li3 + 2 * NB * PS, lane, w, xib);
-    if (upd) trsm_half(Pb, Li3 + 2 * NB * PS, lane, w, xjb);
-    __syncthreads();
-  }
-  PH1(2)
-  // rows / columns of the next diagonal block [r0, r0 + kbn): its diagonal task applies this panel itself
-  const int kbn = max(0, min(TT, ns - r0));
-  MfmaTile T;
-  T.zero();
-  double s2 = 0.0;  // writers: X_I y_p
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (h == 1 && !bh) break;
-    store_xhalf(Pa, lane, w, h == 0 ? xia : xib);
-    if (upd) store_xhalf(Pb, lane, w, h == 0 ? xja : xjb);
-    __syncthreads();
-    if (writer) {
-      if (tid < TT) {
-#pragma unroll
-        for (int q = 0; q < NB; ++q) s2 += Pa[tid * PS + q] * yk[NB * h + q];
-      }
-      const int qn = h == 0 ? min(NB, kb) : kbb;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-        if (q < qn && I0 + r < m) L[(size_t)(k0 + NB * h + q) * m + I0 + r] = Pa[r * PS + q];
-      }
-    }
-    if (upd) T.step(Pa, Pb, lane, w);
-    __syncthreads();
-  }
-  if (writer && tid < TT && I0 + tid < m && I0 + tid >= r0 + kbn) v[I0 + tid] -= s2;
-  PH1(3)
-  if (!upd) { PH1R(7) return; }
-  T.store(Pa, lane, w);
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
-    const int gi = I0 + r, gj = J0 + c;
-    const bool dblk = gi < r0 + kbn && gj < r0 + kbn;
-    if (gi < m && gj < climit && gi >= gj && !dblk) F[(size_t)gj * m + gi] = cv[u] - Pa[r * CS + c];
-  }
-  PH1(4)
-  PH1R(7)
-}
-
 // ---------------------------------------------------------------------------- contribution block
 // U = A22 - L21 L21^T (rows/columns ns..m-1) in one pass with K = ns (gemm_nt.hpp: 64x64 tiles, K in
 // double-buffered 16-column LDS chunks). Task: s, b = ti | tj << 16, K = [a, c) (c = 0: [0, ns)).
@@ -1562,491 +942,6 @@ __global__ void __launch_bounds__(256) k_bwd_inner(const Task* __restrict__ task
   if (lane == 0) tsol[me.c0 + j] -= acc;
 }
 
-// ---------------------------------------------------------------------------- persistent tile DAG
-// Latency-bound levels (few fronts): the launch-per-panel schedule above pays a kernel boundary, a
-// reload of every tile and a reload of L_kk^-1 per 32 columns. Here one launch factors the whole level. Every 64 x 64
-// tile of every front of the level is owned by one workgroup (one per CU, all resident), which keeps the tile in
-// MFMA accumulators from the first panel to the last, and per panel k (32 columns, k0 = 32 k, in own tile column
-// Jp = k0 / 64, half h) plays one role:
-//   DIAG   (Jp, Jp): factor the diagonal block (its quadrant (h, h)) with chol32, y_k = L_kk^-1 (v_k - sum L_kq y_q);
-//          publish L_kk^-1 and y_k; for h = 0 also the L rows of quadrant (1, 0) (TRSM with the fresh inverse), then
-//          update quadrant (1, 1) locally: the next panel's diagonal block needs no hand-off;
-//   TRSM   (I, Jp), I > Jp: L_Ik = C_I,half L_kk^-T (the tile's own half-columns), publish it; for h = 0 update the
-//          tile's other half with L_Ik and the diagonal tile's quadrant-(1, 0) rows;
-//   UPDATE (I, J), J > Jp: C_IJ -= L_Ik L_Jk^T (diagonal tiles also fold L_Ik y_k into their right-hand side).
-// Hand-offs (MI355X_MICROARCH.md §visibility, the write-through form): every handed-off double is stored with an
-// sc1 (write-through) store, every storing wave drains (vmcnt 0), the workgroup barrier, then one lane stores the
-// flag = this call's epoch with an agent-scope atomic; the consumer's lane 0 polls the flag with agent-scope atomic
-// loads, the workgroup barrier, then every load of the handed-off bytes is an sc1 load. One workgroup per CU (the
-// launch reserves LDS for that). Within a workgroup the roles run per panel in the order DIAG, TRSM, UPDATE and every
-// dependency points to an earlier (panel, role): with all workgroups resident the DAG cannot deadlock. A poll that
-// spins too long (a bug, never expected) sets the timeout word and the fail flag and stops waiting.
-// Outputs are those of the panel-step schedule (lbuf L columns without the 32 x 32 diagonal blocks, linv per panel,
-// ysol, the contribution block in the front, the update vector in the front vector) except X = L11^-1: the backward
-// solve of these fronts is k_bwd_seq.
-using launch::DagFront;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned int gu32;
-
-__device__ __forceinline__ void st_wt(double* p, double v) {
-  __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_wt(const double* p) {
-  return __builtin_bit_cast(double, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ double ld_wt0(const double* p, long long idx, bool ok) {
-  const double v = ld_wt(p + (ok ? idx : 0));
-  return ok ? v : 0.0;
-}
-// every storing wave drains its write-through stores, then one lane raises the flag
-__device__ __forceinline__ void dag_signal(unsigned* flag, unsigned epoch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-constexpr unsigned DAG_SPIN_MAX = 1u << 22;
-__device__ __forceinline__ void dag_poll(unsigned* flag, unsigned epoch, unsigned* tmo, int* fail) {
-  unsigned spins = 0;
-  while (__hip_atomic_load((gu32*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-    __builtin_amdgcn_s_sleep(1);
-    if ((++spins & 255u) == 0) {
-      if (__hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) return;
-      if (spins >= DAG_SPIN_MAX) {
-        __hip_atomic_store((gu32*)tmo, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *fail = 1;
-        return;
-      }
-    }
-  }
-}
-// lane 0 polls (one or two flags), then the workgroup barrier: every wave's loads come after the match
-__device__ __forceinline__ void dag_wait(unsigned* f1, unsigned* f2, unsigned epoch, unsigned* tmo, int* fail) {
-  if (threadIdx.x == 0) {
-    if (f1) dag_poll(f1, epoch, tmo, fail);
-    if (f2 && f2 != f1) dag_poll(f2, epoch, tmo, fail);
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ int dag_off(const DagFront& F, int I) { return I < F.nown ? 64 * I : F.ns + 64 * (I - F.nown); }
-__device__ __forceinline__ int dag_len(const DagFront& F, int I) {
-  return I < F.nown ? min(64, F.ns - 64 * I) : min(64, F.m - F.ns - 64 * (I - F.nown));
-}
-
-template <int TPW>
-struct DagLds {
-  double Li[NB * PS];   // L_kk^-1 row-major (li_tag: which front / panel it holds)
-  double Pa[TT * PS];   // staging: a tile's panel columns, or L rows loaded from another workgroup
-  double Pb[TT * PS];
-  double D[NB * DS];    // diagonal block / its inverse (factor_block)
-  __attribute__((aligned(16))) double col[4 * NB];
-  double vy[NB], yk[NB];
-  double vacc[TPW][TT];       // diagonal tiles: v_rows - sum_q L_rows,q y_q
-  double Lout[TPW][TT * PS];  // this panel's L rows produced by each tile slot (TRSM: 64 rows, DIAG: rows 32..63), read
-                              // in place by the slot's own later roles of the panel: no hand-off inside a workgroup
-};
-
-// acc (a tile's 64 x 64 in the MfmaTile layout of wave w) -> the wave's 32 x 32 quadrant into buf (row-major, stride S,
-// at row offset ro); called by the owning wave only
-__device__ __forceinline__ void dag_stage(const dx4 (&acc)[2][2], double* buf, int S, int ro, int lane) {
-  const int lr = lane & 15, lk = lane >> 4;
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) buf[(ro + 16 * x + lk + 4 * i) * S + 16 * y + lr] = acc[x][y][i];
-}
-// acc -= A B^T over K = 32: A rows ra.. (16 x 2 blocks), B rows rb.., both row-major stride PS
-__device__ __forceinline__ void dag_gemm_sub(dx4 (&acc)[2][2], const double* A, int ra, const double* B, int rb, int lane) {
-  const int lr = lane & 15, lk = lane >> 4;
-#pragma unroll
-  for (int kk = 0; kk < NB / 4; ++kk) {
-    const int k = kk * 4 + lk;
-    const double a0 = -A[(ra + lr) * PS + k], a1 = -A[(ra + 16 + lr) * PS + k];
-    const double b0 = B[(rb + lr) * PS + k], b1 = B[(rb + 16 + lr) * PS + k];
-    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
-  }
-}
-// X = P L^-T for 16 rows (r0..r0+15) of P (in `in`) into the same rows of `out` (may alias); columns >= kb zeroed
-// (ragged last panel). One wave owns those rows of both buffers.
-__device__ __forceinline__ void dag_trsm16(const double* in, double* out, const double* Li, int r0, int kb, int lane) {
-  const int lr = lane & 15, lk = lane >> 4;
-  dx4 x0 = {0.0, 0.0, 0.0, 0.0}, x1 = x0;
-#pragma unroll
-  for (int kk = 0; kk < NB / 4; ++kk) {
-    const int k = kk * 4 + lk;
-    const double a = in[(r0 + lr) * PS + k];
-    x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Li[lr * PS + k], x0, 0, 0, 0);
-    x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Li[(16 + lr) * PS + k], x1, 0, 0, 0);
-  }
-  lds_fence();  // this wave's reads of its rows are done before it overwrites them
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = r0 + lk + 4 * i;
-    out[r * PS + lr] = lr < kb ? x0[i] : 0.0;
-    out[r * PS + 16 + lr] = 16 + lr < kb ? x1[i] : 0.0;
-  }
-}
-// slot of this workgroup holding tile (f, I, J), or -1
-template <int TPW>
-__device__ __forceinline__ int dag_slot(const int4 (&td)[TPW], int f, int I, int J) {
-  int s = -1;
-#pragma unroll
-  for (int q = 0; q < TPW; ++q)
-    if (td[q].x == f && td[q].y == I && td[q].z == J) s = q;
-  return s;
-}
-
-template <int TPW>
-__global__ void __launch_bounds__(256, 1) k_dag(const DagFront* __restrict__ frs, const int4* __restrict__ tiles,
-                                                double* __restrict__ fronts, double* lbuf, double* __restrict__ vecs,
-                                                double* ysol, double* linv, unsigned* flags, unsigned epoch, int* fail,
-                                                unsigned* tmo) {
-  __shared__ DagLds<TPW> S;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int lr = lane & 15, lk = lane >> 4;
-  const int wr = (w & 1) * 32, wc = (w >> 1) * 32;
-  int4 td[TPW];
-  dx4 acc[TPW][2][2];
-  int kmax = 0, li_tag = -1, yk_tag = -1;  // front * 65536 + panel whose L_kk^-1 / y_k S.Li / S.yk hold
-  // Signals: a role's write-through stores are drained and its flag raised at once; with `defer` (measured slower, DESIGN
-  // §5) the drain and flag wait until this workgroup is about to poll (it must never block while holding a signal: the
-  // DAG stays deadlock-free) or until a second diagonal factor has run behind them. pD..pDe / pT: panels of pending
-  // DIAG / TRSM signals of slot t, or -1.
-  constexpr bool defer = false;
-  int pD[TPW], pDe[TPW], pT[TPW];  // pending DIAG signals: panels pD .. pDe (a tile column's two panels)
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) pD[t] = pDe[t] = pT[t] = -1;
-  auto flush = [&]() {
-    bool any = false;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) any |= pD[t] >= 0 || pT[t] >= 0;
-    if (!any) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
-    __syncthreads();
-    if (tid == 0) {
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        if (pD[t] < 0 && pT[t] < 0) continue;
-        const DagFront F = frs[td[t].x];
-        for (int q = pD[t]; q >= 0 && q <= pDe[t]; ++q)
-          __hip_atomic_store((gu32*)(flags + F.flag_off + q), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (pT[t] >= 0)
-          __hip_atomic_store((gu32*)(flags + F.flag_off + F.np + td[t].y * F.np + pT[t]), epoch, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) pD[t] = pDe[t] = pT[t] = -1;
-  };
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    td[t] = tiles[(size_t)blockIdx.x * TPW + t];
-    if (td[t].x < 0) continue;
-    const DagFront F = frs[td[t].x];
-    kmax = max(kmax, F.np);
-    const int I = td[t].y, J = td[t].z;
-    const int ro = dag_off(F, I), rl = dag_len(F, I), co = dag_off(F, J), cl = dag_len(F, J);
-    const double* Fp = fronts + F.f_off;
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = wr + 16 * x + lk + 4 * i, c = wc + 16 * y + lr;
-          acc[t][x][y][i] = ld0(Fp, (co + c) * F.m + ro + r, r < rl && c < cl && (I != J || r >= c));
-        }
-    if (I == J && tid < TT) S.vacc[t][tid] = ld0(vecs + F.v_off, ro + tid, tid < rl);
-  }
-  __syncthreads();
-
-  for (int k = 0; k < kmax; ++k) {
-    const int k0 = NB * k, Jp = k0 >> 6, h = (k0 >> 5) & 1;
-    // ---------------- DIAG
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      if (td[t].x < 0) continue;
-      const DagFront F = frs[td[t].x];
-      const int I = td[t].y, J = td[t].z;
-      if (k >= F.np || J != Jp || I != J) continue;
-      const int kb = min(NB, F.ns - k0), ro = dag_off(F, J), rl = dag_len(F, J);
-      if (w == 3 * h) {  // quadrant (h, h), lower triangle, row-major into D
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-          for (int y = 0; y < 2; ++y)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int r = 16 * x + lk + 4 * i, c = 16 * y + lr;
-              if (r >= c) S.D[r * DS + c] = acc[t][x][y][i];
-            }
-      }
-      if (tid < NB) S.vy[tid] = S.vacc[t][NB * h + tid];
-      __syncthreads();
-      if (tid < 64) factor_block(S.D, kb, S.vy, S.col, tid, fail, S.yk);
-      __syncthreads();
-      double* Lin = linv + (size_t)(F.c0 + k0) * (NB * NB);
-#pragma unroll
-      for (int u = 0; u < NB * NB / 256; ++u) {
-        const int e = tid + 256 * u, i = e >> 5, c = e & (NB - 1);
-        const double v = S.D[c * DS + i];  // L^-1(i, c), identity-padded past kb
-        S.Li[i * PS + c] = v;
-        st_wt(Lin + e, v);
-      }
-      li_tag = yk_tag = td[t].x * 65536 + k;
-      if (tid < kb) st_wt(ysol + F.c0 + k0 + tid, S.yk[tid]);
-      if (h == 0 && rl > NB) {
-        // quadrant (1, 0): X1 = C10 L_kk^-T (wave 1 holds C10; waves 2 and 3 solve 16 rows each) -> Lout rows 32..
-        double* X1 = S.Lout[t];
-        if (w == 1) dag_stage(acc[t], S.Pa, PS, NB, lane);
-        __syncthreads();
-        if (w >= 2) dag_trsm16(S.Pa, X1, S.Li, NB + 16 * (w - 2), kb, lane);
-        __syncthreads();
-        double* Lf = lbuf + F.l_off;
-#pragma unroll
-        for (int u = 0; u < NB * NB / 256; ++u) {
-          const int e = tid + 256 * u, r = e & (NB - 1), q = e >> 5;
-          if (r < rl - NB && q < kb) st_wt(Lf + (size_t)(k0 + q) * F.m + ro + NB + r, X1[(NB + r) * PS + q]);
-        }
-        if (pD[t] < 0) pD[t] = k;
-        pDe[t] = k;
-        if (!defer) flush();
-        // rows 32.. of the right-hand side, and quadrant (1, 1) of this tile, by panel k (the next panel's diagonal)
-        if (tid < NB) {
-          double s2 = 0.0;
-#pragma unroll
-          for (int q = 0; q < NB; ++q) s2 += X1[(NB + tid) * PS + q] * S.yk[q];
-          S.vacc[t][NB + tid] -= s2;
-        }
-        if (w == 3) dag_gemm_sub(acc[t], X1, NB, X1, NB, lane);
-        __syncthreads();
-        if (k + 1 >= F.np) flush();
-      } else {
-        if (pD[t] < 0) pD[t] = k;
-        pDe[t] = k;
-        flush();  // the second factor of the tile column: its drain also covers the first's
-      }
-    }
-    // ---------------- TRSM
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      if (td[t].x < 0) continue;
-      const DagFront F = frs[td[t].x];
-      const int I = td[t].y, J = td[t].z;
-      if (k >= F.np || J != Jp || I == J) continue;
-      const int kb = min(NB, F.ns - k0), ro = dag_off(F, I), rl = dag_len(F, I);
-      const int sd = dag_slot(td, td[t].x, Jp, Jp);  // this workgroup factored panel k itself
-      const bool li_here = li_tag == td[t].x * 65536 + k;
-      if ((w >> 1) == h) dag_stage(acc[t], S.Pa, PS, wr, lane);  // this tile's half-h columns (its panel k)
-      if (li_here && yk_tag == li_tag && (sd >= 0 || h == 1)) {
-        __syncthreads();
-      } else {
-        flush();
-        dag_wait(flags + F.flag_off + k, nullptr, epoch, tmo, fail);
-        const double* Lin = linv + (size_t)(F.c0 + k0) * (NB * NB);
-        const double* Lf = lbuf + F.l_off;
-        const int dro = dag_off(F, Jp) + NB, drl = dag_len(F, Jp) - NB;  // diagonal tile's quadrant-(1, 0) rows (h = 0)
-        double lv[NB * NB / 256], xv[NB * NB / 256];
-#pragma unroll
-        for (int u = 0; u < NB * NB / 256; ++u) {
-          const int e = tid + 256 * u, r = e & (NB - 1), q = e >> 5;
-          lv[u] = ld_wt0(Lin, e, !li_here);
-          xv[u] = ld_wt0(Lf, (long long)(k0 + q) * F.m + dro + r, h == 0 && sd < 0 && r < drl && q < kb);
-        }
-        const double yv = ld_wt0(ysol, F.c0 + k0 + tid, tid < kb);  // y_k rides with L_kk^-1 (the diagonal update)
-#pragma unroll
-        for (int u = 0; u < NB * NB / 256; ++u) {
-          const int e = tid + 256 * u, r = e & (NB - 1), q = e >> 5;
-          if (!li_here) S.Li[(e >> 5) * PS + (e & (NB - 1))] = lv[u];
-          S.Pb[(NB + r) * PS + q] = xv[u];
-        }
-        if (tid < NB) S.yk[tid] = yv;
-        li_tag = yk_tag = td[t].x * 65536 + k;
-        __syncthreads();
-      }
-      double* X = S.Lout[t];
-      dag_trsm16(S.Pa, X, S.Li, 16 * w, kb, lane);
-      __syncthreads();
-      double* Lw = lbuf + F.l_off;
-#pragma unroll
-      for (int u = 0; u < TT * NB / 256; ++u) {
-        const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-        if (r < rl && q < kb) st_wt(Lw + (size_t)(k0 + q) * F.m + ro + r, X[r * PS + q]);
-      }
-      pT[t] = k;
-      if (!defer) flush();
-      if (h == 0 && (w >> 1) == 1)  // the other half: -= L_Ik X1^T
-        dag_gemm_sub(acc[t], X, wr, sd >= 0 ? S.Lout[sd] : S.Pb, NB, lane);
-      __syncthreads();
-    }
-    // ---------------- UPDATE
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      if (td[t].x < 0) continue;
-      const DagFront F = frs[td[t].x];
-      const int I = td[t].y, J = td[t].z;
-      if (k >= F.np || J <= Jp) continue;
-      const int kb = min(NB, F.ns - k0);
-      const int roI = dag_off(F, I), rlI = dag_len(F, I), roJ = dag_off(F, J), rlJ = dag_len(F, J);
-      const int sI = dag_slot(td, td[t].x, I, Jp), sJ = I == J ? sI : dag_slot(td, td[t].x, J, Jp);
-      unsigned* pf = flags + F.flag_off + F.np;
-      const bool remote = sI < 0 || (sJ < 0 && I != J);
-      const bool yk_here = yk_tag == td[t].x * 65536 + k;
-      if (remote) {
-        flush();
-        dag_wait(sI < 0 ? pf + I * F.np + k : nullptr, sJ < 0 ? pf + J * F.np + k : nullptr, epoch, tmo, fail);
-      }
-      const double* Lf = lbuf + F.l_off;
-      double av[TT * NB / 256], bv[TT * NB / 256];
-#pragma unroll
-      for (int u = 0; u < TT * NB / 256; ++u) {
-        const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-        av[u] = ld_wt0(Lf, (long long)(k0 + q) * F.m + roI + r, sI < 0 && r < rlI && q < kb);
-        bv[u] = ld_wt0(Lf, (long long)(k0 + q) * F.m + roJ + r, sJ < 0 && I != J && r < rlJ && q < kb);
-      }
-      // y_k: from the TRSM / DIAG of this panel on this workgroup, else loaded (published before any flag this
-      // tile's operands depend on; a diagonal tile with local operands always has it here)
-      const bool yload = I == J && !yk_here;
-      const double ykv = ld_wt0(ysol, F.c0 + k0 + tid, yload && tid < kb);
-      if (remote) {
-#pragma unroll
-        for (int u = 0; u < TT * NB / 256; ++u) {
-          const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-          if (sI < 0) S.Pa[r * PS + q] = av[u];
-          if (sJ < 0 && I != J) S.Pb[r * PS + q] = bv[u];
-        }
-      }
-      if (yload) {
-        if (tid < NB) S.yk[tid] = ykv;
-        yk_tag = td[t].x * 65536 + k;
-      }
-      __syncthreads();
-      const double* A = sI >= 0 ? S.Lout[sI] : S.Pa;
-      const double* B = I == J ? A : (sJ >= 0 ? S.Lout[sJ] : S.Pb);
-      if (I == J && tid < TT) {
-        double s2 = 0.0;
-#pragma unroll
-        for (int q = 0; q < NB; ++q) s2 += A[tid * PS + q] * S.yk[q];
-        S.vacc[t][tid] -= s2;
-      }
-      dag_gemm_sub(acc[t], A, wr, B, wc, lane);
-      __syncthreads();
-    }
-    bool dcont = false;  // a diagonal tile factors its second panel next: keep that signal behind its factor
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) dcont |= pD[t] >= 0;
-    if (!dcont) flush();
-  }
-  flush();
-  // ---------------- contribution block and update vector (read by the parent's assembly in the next launch)
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    if (td[t].x < 0) continue;
-    const DagFront F = frs[td[t].x];
-    const int I = td[t].y, J = td[t].z;
-    if (J < F.nown) continue;
-    const int ro = dag_off(F, I), rl = dag_len(F, I), co = dag_off(F, J), cl = dag_len(F, J);
-    double* Fp = fronts + F.f_off;
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = wr + 16 * x + lk + 4 * i, c = wc + 16 * y + lr;
-          if (r < rl && c < cl && (I != J || r >= c)) Fp[(size_t)(co + c) * F.m + ro + r] = acc[t][x][y][i];
-        }
-    if (I == J && tid < rl) vecs[F.v_off + ro + tid] = S.vacc[t][tid];
-  }
-}
-
-// Backward solve of a k_dag front (no explicit X = L11^-1), right-looking: t (= y - L21^T x_rows from k_bwd_gemv) is
-// reduced in LDS; from the last block, x_b = L_bb^-T t_b, then t_c -= sum_r L(b0 + r, c) x_b[r] for every column c < b0
-// (row block b of L11, 4 threads per column). The sequential chain per block is one 32 x 32 product and one update
-// pass over registers; block b-1's rows of L and its L^-1 are loaded while block b is solved.
-constexpr int BSQ_C = 6;                 // column passes of 64: ns <= 64 * BSQ_C + 32
-constexpr int BSQ_N = 64 * BSQ_C + NB;   // largest ns
-__global__ void __launch_bounds__(256) k_bwd_seq(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                                 const double* __restrict__ lbuf, const double* __restrict__ linv,
-                                                 const double* __restrict__ tsol, double* __restrict__ xsol,
-                                                 const int* __restrict__ perm, double* __restrict__ xout) {
-  __shared__ double ts[BSQ_N];
-  __shared__ double Lis[2][NB * (NB + 1)];
-  __shared__ double xb[NB];
-  const Task t = tasks[blockIdx.x];
-  const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr, ns = me.ns;
-  const int tid = threadIdx.x, cq = tid >> 2, rq = tid & 3;
-  const double* L = lbuf + me.l_off;
-  const int np = (ns + NB - 1) / NB;
-  double cur[BSQ_C][8], nxt[BSQ_C][8], li[NB * NB / 256];
-  auto load_rows = [&](int b, double (&dst)[BSQ_C][8], double (&lv)[NB * NB / 256]) {
-    const int b0 = NB * b;
-#pragma unroll
-    for (int p = 0; p < BSQ_C; ++p)
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int c = 64 * p + cq, i = b0 + 8 * rq + r;
-        dst[p][r] = ld0(L, c * m + i, c < b0 && i < ns);
-      }
-    const double* Li = linv + (size_t)(me.c0 + b0) * (NB * NB);
-#pragma unroll
-    for (int u = 0; u < NB * NB / 256; ++u) lv[u] = Li[tid + 256 * u];
-  };
-  for (int i = tid; i < ns; i += 256) ts[i] = tsol[me.c0 + i];
-  load_rows(np - 1, cur, li);
-  int cb = 0;
-#pragma unroll
-  for (int u = 0; u < NB * NB / 256; ++u) {
-    const int e = tid + 256 * u;
-    Lis[0][(e >> 5) * (NB + 1) + (e & (NB - 1))] = li[u];
-  }
-  __syncthreads();
-  for (int b = np - 1; b >= 0; --b) {
-    const int b0 = NB * b, kb = min(NB, ns - b0);
-    if (b > 0) load_rows(b - 1, nxt, li);
-    if (tid < NB) {  // x_b = L_bb^-T t_b: x[j] = sum_i L^-1(i, j) t[i]
-      double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int i = 0; i < NB; ++i) a4[i & 3] += (i < kb ? Lis[cb][i * (NB + 1) + tid] * ts[b0 + min(i, kb - 1)] : 0.0);
-      const double x = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-      xb[tid] = tid < kb ? x : 0.0;
-      if (tid < kb) {
-        xsol[me.c0 + b0 + tid] = x;
-        xout[perm[me.c0 + b0 + tid]] = x;
-      }
-    }
-    __syncthreads();
-    if (b > 0) {
-#pragma unroll
-      for (int p = 0; p < BSQ_C; ++p) {
-        const int c = 64 * p + cq;
-        double part = 0.0;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) part += cur[p][r] * xb[8 * rq + r];
-        part += __shfl_xor(part, 1, 64);
-        part += __shfl_xor(part, 2, 64);
-        if (rq == 0 && c < b0) ts[c] -= part;
-      }
-      cb ^= 1;
-#pragma unroll
-      for (int u = 0; u < NB * NB / 256; ++u) {
-        const int e = tid + 256 * u;
-        Lis[cb][(e >> 5) * (NB + 1) + (e & (NB - 1))] = li[u];
-      }
-#pragma unroll
-      for (int p = 0; p < BSQ_C; ++p)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) cur[p][r] = nxt[p][r];
-    }
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------------------- distributed factorization glue
 // (landmark-sharded BA) contiguous copies between the front pool / front vectors and an exchange buffer:
 // ranges (src, dst, len) in doubles, one workgroup per range
@@ -2079,48 +974,6 @@ __global__ void __launch_bounds__(256) k_zero_idx(const int* __restrict__ idx, i
 }
 
 namespace launch {
-
-// one workgroup per CU (the validated form of the write-through hand-offs): dynamic LDS tops each instance up to more
-// than half of the CU's 160 KB
-template <int TPW>
-static int dag_reserve() {
-  static int r = -1;
-  if (r < 0) {
-    hipFuncAttributes a;
-    HIP_CHECK(hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&k_dag<TPW>)));
-    r = std::max(0, 82 * 1024 - (int)a.sharedSizeBytes);
-  }
-  return r;
-}
-void chol_dag(int nworkers, int tpw, const DagFront* fr, const int4* tiles, double* fronts, double* lbuf, double* vecs,
-              double* ysol, double* linv, unsigned* flags, unsigned epoch, int* fail, unsigned* tmo, hipStream_t s) {
-  if (nworkers <= 0) return;
-  if (tpw == 2)
-    hipLaunchKernelGGL(k_dag<2>, nworkers, 256, dag_reserve<2>(), s, fr, tiles, fronts, lbuf, vecs, ysol, linv, flags, epoch, fail, tmo);
-  else
-    hipLaunchKernelGGL(k_dag<4>, nworkers, 256, dag_reserve<4>(), s, fr, tiles, fronts, lbuf, vecs, ysol, linv, flags, epoch, fail, tmo);
-  KERNEL_CHECK();
-}
-int chol_dag_max_workers(int device) {
-  hipDeviceProp_t p;
-  HIP_CHECK(hipGetDeviceProperties(&p, device));
-  // every worker must be resident at once (they wait on each other): one 256-thread workgroup per CU fits when its
-  // LDS (static + the dynamic top-up) is within the CU's and its registers within a SIMD's budget for one wave each.
-  // (hipOccupancyMaxActiveBlocksPerMultiprocessor returned "unknown error" for these kernels on the MI355X boxes)
-  hipFuncAttributes a2, a4;
-  HIP_CHECK(hipFuncGetAttributes(&a2, reinterpret_cast<const void*>(&k_dag<2>)));
-  HIP_CHECK(hipFuncGetAttributes(&a4, reinterpret_cast<const void*>(&k_dag<4>)));
-  const bool fit = (int)a2.sharedSizeBytes + dag_reserve<2>() <= 160 * 1024 &&
-                   (int)a4.sharedSizeBytes + dag_reserve<4>() <= 160 * 1024 && a2.numRegs <= 512 && a4.numRegs <= 512 &&
-                   a2.maxThreadsPerBlock >= 256 && a4.maxThreadsPerBlock >= 256;
-  return fit ? p.multiProcessorCount : 0;
-}
-void chol_bwd_seq(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* linv,
-                  const double* tsol, double* xsol, const int* perm, double* xout, hipStream_t s) {
-  if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_bwd_seq, ntasks, 256, 0, s, tasks, fd, lbuf, linv, tsol, xsol, perm, xout);
-  KERNEL_CHECK();
-}
 
 void chol_copy_ranges(int n, const long long* rng, const double* src, double* dst, hipStream_t s) {
   if (n <= 0) return;
@@ -2183,16 +1036,16 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
-                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* linvn, double* xinv,
-                     int* fail, int assemble, bool w64, hipStream_t s) {
+                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv,
+                     int* fail, int assemble, hipStream_t s) {
   if (ntasks <= 0) return;
-#define G2OHIP_EA(A_, E_, W_)                                                                                        \
-  hipLaunchKernelGGL((k_extend_add<A_, E_, W_>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, \
-                     colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, linvn, xinv, fail)
+#define G2OHIP_EA(A_, E_)                                                                                        \
+  hipLaunchKernelGGL((k_extend_add<A_, E_>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, \
+                     colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, xinv, fail)
   // assemble 2: fronts up to 512 rows (a small column buffer keeps more workgroups per CU)
-  if (assemble == 2) { if (w64) G2OHIP_EA(true, 512, true); else G2OHIP_EA(true, 512, false); }
-  else if (assemble) { if (w64) G2OHIP_EA(true, 2048, true); else G2OHIP_EA(true, 2048, false); }
-  else { if (w64) G2OHIP_EA(false, 1, true); else G2OHIP_EA(false, 1, false); }
+  if (assemble == 2) G2OHIP_EA(true, 512);
+  else if (assemble) G2OHIP_EA(true, 2048);
+  else G2OHIP_EA(false, 1);
 #undef G2OHIP_EA
   KERNEL_CHECK();
 }
@@ -2203,12 +1056,6 @@ void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* 
     hipLaunchKernelGGL(k_step<true>, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   else
     hipLaunchKernelGGL(k_step<false>, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
-  KERNEL_CHECK();
-}
-void chol_step64(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs,
-                 double* ysol, double* linv, double* linvn, double* xinv, int* fail, hipStream_t s) {
-  if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_step64, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, linvn, xinv, fail);
   KERNEL_CHECK();
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <stdexcept>
@@ -74,5 +75,21 @@ class DevBuf {
 };
 
 inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+// t^3 rounded once, as the reference's std::pow(t, 3) (glibc's pow is correctly rounded): t^2 = p + e exactly (FMA),
+// t^3 = p t + e t with the product's rounding error carried, then one final rounding. The device's pow is not
+// guaranteed to round the same way; this is the same arithmetic on host and device.
+__host__ __device__ inline double cube_rn(double t) {
+  const double p = t * t, e = fma(t, t, -p);
+  const double h = p * t, l = fma(p, t, -h) + e * t;
+  return h + l;
+}
+// the accepted LM trial's lambda factor (optimization_algorithm_levenberg.cpp:127-136): alpha = 1 - (2 rho - 1)^3,
+// clipped to [goodStepLowerScale, goodStepUpperScale] = [1/3, 2/3]; host loop and device decision share it
+__host__ __device__ inline double lm_scale_factor(double rho) {
+  double alpha = 1. - cube_rn(2 * rho - 1);
+  alpha = alpha < 2. / 3. ? alpha : 2. / 3.;
+  return 1. / 3. > alpha ? 1. / 3. : alpha;
+}
 
 }  // namespace g2ohip

@@ -306,29 +306,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     for (int sn : sym.levels[l]) { lcols += sym.sn[sn].ns + sym.sn[sn].nr; sn_level[sn] = (int)l; }
     level_slab[l] = lcols >= 16LL * launch::CHOL_EA * 256 ? launch::CHOL_EA : 4;
   }
-  // 64-column panel steps (k_step64, G2OHIP_CHOL_W64=1) on every level none of whose fronts would be blocked (the wide /
-  // big-panel rules below)
-  sn_w64.assign(sym.sn.size(), 0);
-  n_w64_levels = 0;
-  {
-    const char* ew = getenv("G2OHIP_CHOL_W64");
-    // off by default: at C4 the 64-column steps measured break-even on the chain-bound levels (18.8 us per 64 columns
-    // against 2 x 9.2) and slower on the throughput-bound ones
-    const bool w64_on = ew && atoi(ew) != 0 && !(getenv("G2OHIP_CHOL_DAG") && atoi(getenv("G2OHIP_CHOL_DAG")) != 0);
-    const char* bm = getenv("G2OHIP_CHOL_BLOCK_MIN");
-    const int block_min = bm ? atoi(bm) : 512;
-    const char* wf = getenv("G2OHIP_CHOL_WIDE_FRONTS");
-    const int wide_fronts = wf ? atoi(wf) : 64;
-    const char* wp = getenv("G2OHIP_CHOL_WIDE_PB");
-    const int wide_pb = wp ? std::max(64, atoi(wp) / 64 * 64) : 128;
-    for (const auto& lv : sym.levels) {
-      int mx = 0;
-      for (int sn : lv) mx = std::max(mx, sym.sn[sn].ns);
-      const bool ok = w64_on && mx <= ((int)lv.size() >= wide_fronts ? wide_pb : block_min);
-      for (int sn : lv) sn_w64[sn] = ok;
-      n_w64_levels += ok;
-    }
-  }
   // ---- distribution over ranks (landmark-sharded BA): cut the elimination tree into a shared top and whole subtrees,
   // each subtree owned by one rank. Candidate cuts: starting from the tree's roots, the candidate subtree with the
   // largest serial work is split (its root joins the shared top), one cut per split, up to 4 candidates per rank; each
@@ -506,7 +483,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     if (q.parent >= 0) {
       const Supernode& pq = sym.sn[q.parent];
       const int mp = pq.ns + pq.nr, slab = level_slab[sn_level[q.parent]];
-      const int kb0 = std::min(sn_w64[q.parent] ? launch::CHOL_TT : launch::CHOL_NB, pq.ns);
+      const int kb0 = std::min(launch::CHOL_NB, pq.ns);
       const int* rel = sym.relmap.data() + q.rows_off;
       jt = (int)hjt.size();
       hjt.push_back((int)(std::lower_bound(rel, rel + q.nr, kb0) - rel));
@@ -593,29 +570,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const long long lag_fused_min = lag_mode >= 2 ? 0 : (lfm ? atoll(lfm) : 256);
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
     const long long pre_max = pm ? atoll(pm) : (256LL << 20);
-    // persistent tile DAG (k_dag): 0 (default) off, 1 latency-bound levels (those whose panel steps would fuse the
-    // contribution block), 2 every level whose tiles fit the resident workgroups. Off by default: at C4 its levels take
-    // 135-155 us against 121-161 us for the panel-step launches (the hand-off payload reads dominate)
-    const char* dm = getenv("G2OHIP_CHOL_DAG");
-    const int dag_mode = dm ? atoi(dm) : 0;
-    int dag_cap = 0;
-    if (dag_mode) {
-      int dev = 0;
-      HIP_CHECK(hipGetDevice(&dev));
-      dag_cap = launch::chol_dag_max_workers(dev);
-    }
-    std::vector<launch::DagFront> hdf;
-    std::vector<int4> hdt;
-    std::vector<char> level_dag(fplan.size(), 0);
-    int dag_flag_total = 0;
-    op_front_off.clear();
-    n_dag_levels = 0;
     std::vector<long long> zr, pdst;
     std::vector<int> psrc;
     for (size_t l = 0; l < fplan.size(); ++l) {
       if ((int)l == xch_at) {  // subtree roots -> every rank (before the first shared front is assembled)
         ops.push_back(Op{8, 0, 0});
-        op_front_off.push_back(0);
+       
       }
       const auto& lv = fplan[l];
       long long tiles0 = 0;  // fused tiles of the level's first step
@@ -626,22 +586,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         tiles0 += (long long)T * (T + 1) / 2;
       }
       const bool fused_contrib = tiles0 <= fused_max;
-      // the tile DAG: every 64 x 64 tile of the level's fronts (own and contribution parts tiled separately) owned by
-      // one resident workgroup, at most CHOL_DAG_TPW tiles each
-      long long dtiles = 0;
-      bool dag_fit = dag_mode != 0 && dag_cap > 0;
-      for (int sn : lv) {
-        const Supernode& q = sym.sn[sn];
-        const long long nt = (q.ns + TT - 1) / TT + (q.nr + TT - 1) / TT;
-        dtiles += nt * (nt + 1) / 2;
-        if (q.ns > 6 * 64 + NB) dag_fit = false;  // k_bwd_seq holds a block row of at most 6 x 64 columns
-      }
-      long long dpairs = 0;  // diagonal-pair workgroups (see the tile ownership below)
-      for (int sn : lv) dpairs += (sym.sn[sn].ns + TT - 1) / TT + (sym.sn[sn].nr + TT - 1) / TT;
-      const long long drest = dtiles - (2 * dpairs - (long long)lv.size());
-      const bool dag = dag_fit && (fused_contrib || dag_mode >= 2) && dpairs <= dag_cap &&
-                       dpairs + (std::max(0LL, drest - 2 * dpairs) + 3) / 4 <= dag_cap;
-      level_dag[l] = dag;
       // k_extend_add: every front's first-diagonal-block task first, then the slabs
       // small levels (all fronts <= pre_max bytes together) are zeroed + scattered before the first level
       // (two massively parallel passes off the critical chain); large ones are assembled in place
@@ -676,8 +620,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       int lmaxm = 0;
       for (int sn : lv) lmaxm = std::max(lmaxm, sym.sn[sn].ns + sym.sn[sn].nr);
       Op ea{pre ? 0 : (lmaxm <= 512 ? 5 : 4), (int)tk.size(), 0};
-      // first diagonal blocks: assembled and factored beside the slabs, or (DAG levels, a = -1) assembled into the front
-      for (int sn : lv) tk.push_back(Task{sn, dag ? -1 : 0, 0, 1});
+      // first diagonal blocks: assembled and factored beside the slabs
+      for (int sn : lv) tk.push_back(Task{sn, 0, 0, 1});
       // every front is assembled here (input entries, zeros, children); slabs of EA columns where the level
       // has enough of them to fill the chip several times over, else 4 (latency-bound upper levels)
       const int slab = level_slab[sn_level[lv[0]]];
@@ -688,114 +632,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         for (int a = 0; a < m; a += slab) tk.push_back(Task{sn, a, std::min(a + slab, m), 2 + a / slab});
       }
       ea.count = (int)tk.size() - ea.off;
-      ea.w64 = sn_w64[lv[0]];
       ops.push_back(ea);
-      op_front_off.push_back(0);
-      if (dag) {
-        const int f0 = (int)hdf.size();
-        std::vector<int> ntr_of;
-        for (int sn : lv) {
-          const Supernode& q = sym.sn[sn];
-          const int m = q.ns + q.nr, nown = (q.ns + TT - 1) / TT, ntr = nown + (q.nr + TT - 1) / TT;
-          const int np = (q.ns + NB - 1) / NB;
-          hdf.push_back(launch::DagFront{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, m, q.ns, q.c0, nown, ntr, np,
-                                         dag_flag_total, 0});
-          dag_flag_total += np + ntr * np;
-          ntr_of.push_back(ntr);
-        }
-        // ownership: the diagonal tile (J, J) and its left neighbour (J, J-1) share a workgroup, so the panel chain
-        // crosses workgroups once per 64 columns (the factor of panel 2j+1 -> the next diagonal's owner, which solves
-        // its own row's panel and updates its diagonal tile from LDS); the other tiles, column by column with the
-        // fronts interleaved, are dealt round-robin (a panel's TRSM / update tiles land on different workgroups)
-        std::vector<std::vector<int4>> bins;
-        std::vector<int4> rest;
-        int maxntr = 0;
-        for (int n : ntr_of) maxntr = std::max(maxntr, n);
-        for (size_t f = 0; f < ntr_of.size(); ++f)
-          for (int J = 0; J < ntr_of[f]; ++J) {
-            bins.push_back({int4{(int)f, J, J, 0}});
-            if (J > 0) bins.back().push_back(int4{(int)f, J, J - 1, 0});
-          }
-        for (int J = 0; J < maxntr; ++J)
-          for (size_t f = 0; f < ntr_of.size(); ++f)
-            for (int I = J + 2; I < ntr_of[f]; ++I) rest.push_back(int4{(int)f, I, J, 0});
-        const int npair = (int)bins.size(), nrest = (int)rest.size();
-        int tpw = 2;
-        if (npair + (nrest + 1) / 2 > dag_cap) tpw = 4;
-        const int extra = tpw == 4 ? std::max(0, nrest - 2 * npair) : nrest;  // tiles beyond the pair bins' spare slots
-        const int nnew = (extra + tpw - 1) / tpw;
-        if (npair + nnew > dag_cap) throw DeviceError("tile DAG: level does not fit the resident workgroups");
-        bins.resize(npair + nnew);
-        // spread: round-robin over the bins that still have room (pair bins first take up to tpw - 2 more)
-        size_t bi = tpw == 4 ? 0 : (size_t)npair;
-        for (const int4& tl : rest) {
-          for (size_t tries = 0; tries < bins.size(); ++tries) {
-            if ((int)bins[bi].size() < tpw) break;
-            bi = (bi + 1) % bins.size();
-          }
-          bins[bi].push_back(tl);
-          bi = (bi + 1) % bins.size();
-          if (tpw == 2 && bi < (size_t)npair) bi = npair;
-        }
-        const int nw = (int)bins.size();
-        Op dg{7, (int)hdt.size(), nw, tpw};
-        hdt.resize(hdt.size() + (size_t)nw * tpw, int4{-1, 0, 0, 0});
-        for (int b = 0; b < nw; ++b)
-          for (size_t q = 0; q < bins[b].size(); ++q) hdt[dg.off + (size_t)b * tpw + q] = bins[b][q];
-        ops.push_back(dg);
-        op_front_off.push_back(f0);
-        ++n_dag_levels;
-        continue;
-      }
-      if (sn_w64[lv[0]]) {
-        // 64-column panel steps (cholesky.hip k_step64): per launch the next 64 x 64 diagonal block, the rank-64 tiles
-        // of the current panel (into the contribution block when fused) and X = L11^-1 for the previous panel
-        int maxq = 0;
-        for (int sn : lv) maxq = std::max(maxq, (sym.sn[sn].ns + TT - 1) / TT);
-        for (int p = 0; p < maxq; ++p) {
-          Op st{9, (int)stk.size(), 0};
-          std::vector<launch::StepTask> diag_t, tile_t, inv_t;
-          for (int sn : lv) {
-            const Supernode& q = sym.sn[sn];
-            const int k0 = p * TT;
-            if (k0 >= q.ns) continue;
-            const int kb = std::min(TT, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
-            const int clim = fused_contrib ? m : q.ns;
-            const int T = (m - r0 + TT - 1) / TT, TJ = (clim - r0 + TT - 1) / TT;
-            auto mk = [&](int tile, int flags) {
-              return launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns, q.c0,
-                                      k0 | (kb << 16), tile, flags, clim};
-            };
-            if (r0 < q.ns) diag_t.push_back(mk(0, 4));
-            for (int tj = 0; tj < std::max(TJ, 1); ++tj)
-              for (int ti = tj; ti < T; ++ti) tile_t.push_back(mk(ti | (tj << 16), (tj < TJ ? 1 : 0) | (fused_contrib ? 8 : 0)));
-            // X = L11^-1: the previous panel's 32-blocks (2p - 2, 2p - 1) into every pending block row >= 2p + 2, and
-            // block rows 2p, 2p + 1 (this panel) final
-            const int nblk = (q.ns + NB - 1) / NB;
-            if (p >= 1 && !dev_noinv)
-              for (int bp = 2 * p; bp < nblk; ++bp) {
-                if (bp == 2 * p + 1) continue;  // finalised with row 2p
-                for (int j = 0; j < 2 * p; ++j) inv_t.push_back(mk(j | (bp << 16), 16));
-              }
-          }
-          stk.insert(stk.end(), diag_t.begin(), diag_t.end());
-          if (!dev_diagonly) stk.insert(stk.end(), tile_t.begin(), tile_t.end());
-          if (!dev_diagonly) stk.insert(stk.end(), inv_t.begin(), inv_t.end());
-          st.count = (int)stk.size() - st.off;
-          if (st.count) { ops.push_back(st); op_front_off.push_back(0); }
-        }
-        Op sy{3, (int)tk.size(), 0};
-        for (int sn : lv) {
-          if (fused_contrib) break;
-          const Supernode& q = sym.sn[sn];
-          const int T = (q.nr + TT - 1) / TT;
-          for (int tj = 0; tj < T; ++tj)
-            for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, 0, ti | (tj << 16), 0});
-        }
-        sy.count = (int)tk.size() - sy.off;
-        if (sy.count) { ops.push_back(sy); op_front_off.push_back(0); ++n_syrk_ops; }
-        continue;
-      }
+     
       int maxp = 0;
       for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
       // blocked fronts (wide supernodes on levels with a separate contribution pass): the rank-32 tile
@@ -856,7 +694,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         st.count = (int)stk.size() - st.off;
         for (int k = st.off; k < st.off + st.count; ++k)
           if (stk[k].flags & 64) st.kind = 6;
-        if (st.count) { ops.push_back(st); op_front_off.push_back(0); }
+        if (st.count) { ops.push_back(st); }
         if ((p + 1) * NB % lpb) continue;
         // end of a big panel: trailing update of the blocked fronts, then their next first blocks
         Op gm{3, (int)tk.size(), 0};
@@ -873,8 +711,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         }
         gm.count = (int)tk.size() - gm.off;
         d0.count = (int)stk.size() - d0.off;
-        if (gm.count) { ops.push_back(gm); op_front_off.push_back(0); ++n_syrk_ops; }
-        if (d0.count) { ops.push_back(d0); op_front_off.push_back(0); }
+        if (gm.count) { ops.push_back(gm); ++n_syrk_ops; }
+        if (d0.count) { ops.push_back(d0); }
       }
       Op sy{3, (int)tk.size(), 0};
       for (int sn : lv) {
@@ -885,7 +723,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, 0, ti | (tj << 16), 0});
       }
       sy.count = (int)tk.size() - sy.off;
-      if (sy.count) { ops.push_back(sy); op_front_off.push_back(0); ++n_syrk_ops; }
+      if (sy.count) { ops.push_back(sy); ++n_syrk_ops; }
       for (int sn : lv) n_blocked += blocked(sym.sn[sn]) ? 1 : 0;
     }
     // root exchange (distributed): per subtree root, the lower triangle of its contribution block column by column
@@ -928,13 +766,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       xzero_idx.upload(zx.empty() ? std::vector<int>{0} : zx, s);
       xred.resize((size_t)sym.n + 1);
     }
-    dag_fronts.upload(hdf.empty() ? std::vector<launch::DagFront>(1) : hdf, s);
-    dag_tiles.upload(hdt.empty() ? std::vector<int4>{int4{-1, 0, 0, 0}} : hdt, s);
-    dag_flags.resize(std::max(dag_flag_total, 1));
-    dag_flags.zero(s);
-    dag_tmo.resize(1);
-    dag_tmo.zero(s);
-    dag_epoch = 0;
     nzero = (int)(zr.size() / 2);
     npre = (long long)pdst.size();
     zero_rng.upload(zr.empty() ? std::vector<long long>{0, 0} : zr, s);
@@ -958,13 +789,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       bl.gemv.second = (int)tk.size() - bl.gemv.first;
       bl.xall = {(int)tk.size(), 0};
       int rounds = 0;
-      if (level_dag[l]) {  // no explicit X = L11^-1: one sequential block solve per front
-        bl.seq = {(int)tk.size(), (int)lv.size()};
-        for (int sn : lv) tk.push_back(Task{sn, 0, 0, 0});
-        bwd_ops.push_back(bl);
-        bwd_off.push_back((int)tk.size());
-        continue;
-      }
       for (int sn : lv) {
         const int ns = sym.sn[sn].ns;
         if (sn_pb[sn]) { rounds = std::max(rounds, (ns + sn_pb[sn] - 1) / sn_pb[sn]); continue; }
@@ -1002,7 +826,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
     heads.assign(ops.size(), launch::StepHead{});
     for (size_t k = 0; k < ops.size(); ++k) {
-      if (ops[k].kind != 2 && ops[k].kind != 6 && ops[k].kind != 9) continue;
+      if (ops[k].kind != 2 && ops[k].kind != 6) continue;
       launch::StepHead& h = heads[k];
       h.n = 0;
       while (h.n < launch::CHOL_HEAD && h.n < ops[k].count) {  // the first workgroups (diagonal tasks among them)
@@ -1021,7 +845,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   y_p.resize(std::max(sym.n, 1));
   lbuf.resize(std::max<long long>(lpool, 1));
   linv.resize((size_t)(sym.n + launch::CHOL_NB) * launch::CHOL_NB * launch::CHOL_NB);  // one 32x32 L_kk^-1 per panel start
-  linvn.resize(n_w64_levels ? (size_t)(sym.n + launch::CHOL_NB) * launch::CHOL_NB * launch::CHOL_NB : 1);
   xinv.resize(std::max<long long>(xoff, 1));
   t_p.resize(std::max(sym.n, 1));
   x_p.resize(std::max(sym.n, 1));
@@ -1029,7 +852,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
 
 void DeviceCholesky::factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s,
                             bool prezeroed) {
-  if (n_dag_levels) ++dag_epoch;  // flag value of this call (flags only ever equal the epoch of the call that set them)
   last_fail = fail;
   launch::chol_prescatter(prezeroed ? 0 : nzero, zero_rng.get(), npre, vals, pre_dst.get(), pre_src.get(), lam,
                           fronts.get(), (int)sym.sn.size(), fd.get(), perm.get(), rhs, vecs.get(), s);
@@ -1042,11 +864,8 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
                                       cment.get(), colptr.get(),
                                       ent_row.get(),
                                       ent_src.get(), vals, lam, fronts.get(), vecs.get(),
-                                      lbuf.get(), y_p.get(), linv.get(), linvn.get(), xinv.get(), fail,
-                                      op.kind == 0 ? 0 : (op.kind == 5 ? 2 : 1), op.w64 != 0, s); break;
-      case 9: launch::chol_step64(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
-                                  vecs.get(), y_p.get(), linv.get(), linvn.get(), xinv.get(), fail, s);
-        break;
+                                      lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail,
+                                      op.kind == 0 ? 0 : (op.kind == 5 ? 2 : 1), s); break;
       case 2:
       case 6: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
                                 vecs.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 6, s);
@@ -1062,10 +881,6 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
                                  vecs.get(), s);
         break;
       }
-      case 7: launch::chol_dag(op.count, op.tpw, dag_fronts.get() + op_front_off[&op - ops.data()], dag_tiles.get() + op.off,
-                               fronts.get(), lbuf.get(), vecs.get(), y_p.get(), linv.get(), dag_flags.get(), dag_epoch,
-                               fail, dag_tmo.get(), s);
-        break;
       default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;
     }
   }
@@ -1076,16 +891,6 @@ void DeviceCholesky::reduce_input(const double* vals, hipStream_t s) {
   launch::chol_copy_ranges(1, rs_rhs_rng.get(), vals, rs_buf.get(), s);
   reduce_scatter(rs_buf.get(), (size_t)rs_seg);
   allreduce(rs_buf.get() + (size_t)dist_nranks * rs_seg, (size_t)rs_tail_len);
-}
-
-void DeviceCholesky::check_dag(hipStream_t s) {
-  if (!n_dag_levels) return;
-  unsigned t = 0;
-  HIP_CHECK(hipMemcpyAsync(&t, dag_tmo.get(), sizeof t, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  if (t == dag_epoch && t != 0)
-    throw DeviceError("supernodal factorization: the tile DAG of a level stopped waiting for a flag (epoch " +
-                      std::to_string(t) + ")");
 }
 
 void DeviceCholesky::solve(double* x, hipStream_t s) {
@@ -1102,8 +907,6 @@ void DeviceCholesky::solve(double* x, hipStream_t s) {
                           x_p.get(), t_p.get(), s);
     launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
                        perm.get(), xo, s);
-    launch::chol_bwd_seq(bl.seq.second, tasks.get() + bl.seq.first, fd.get(), lbuf.get(), linv.get(), t_p.get(), x_p.get(),
-                         perm.get(), xo, s);
     for (const auto& rd : bl.rounds) {
       launch::chol_bwd_inner(rd.first.second, tasks.get() + rd.first.first, fd.get(), lbuf.get(), x_p.get(), t_p.get(), s);
       launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
@@ -2427,6 +2230,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
   } else if (use_pcg()) {
     pcg.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
   } else {
+    chol.set_replicated();
     chol.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
   }
   HIP_CHECK(hipStreamSynchronize(stream));
@@ -2672,7 +2476,6 @@ int Engine::solve_sync() {
   HIP_CHECK(hipMemcpyAsync(f, failp(), sizeof f, hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
   timer.collect();
-  if (f[0] && !use_pcg() && !use_cgls()) chol.check_dag(stream);
   if (f[0] && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
   return f[0] ? 0 : 1;
 }
@@ -2888,7 +2691,6 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
     int f[2];
     std::memcpy(f, hs + 8, sizeof f);
     const bool ok2 = f[0] == 0;
-    if (!ok2 && !use_pcg() && !use_cgls()) chol.check_dag(stream);
     if (!ok2 && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
     if (ev2 && first_trial) {
       float mq = 0;
@@ -2925,10 +2727,7 @@ int Engine::lm_solve(int iteration, const g2ohip_config& cfg, g2ohip_batch_stats
       rho /= scale;
       accept = rho > 0 && std::isfinite(tempChi);
       if (accept) {
-        double alpha = 1. - std::pow((2 * rho - 1), 3);
-        alpha = std::min(alpha, 2. / 3.);
-        const double scaleFactor = std::max(1. / 3., alpha);
-        current_lambda *= scaleFactor;
+        current_lambda *= lm_scale_factor(rho);  // optimization_algorithm_levenberg.cpp:127-136
       } else {
         current_lambda *= ni;
       }
@@ -3001,7 +2800,6 @@ int Engine::gn_solve(int iteration, g2ohip_batch_stats* st) {
     st->timeUpdate = b * 1e-3;
   }
   levenberg_iterations = 0;
-  if (f[0] != 0 && !use_pcg() && !use_cgls()) chol.check_dag(stream);
   if (f[0] != 0 && write_debug && rank == 0 && !use_pcg() && !use_cgls()) write_debug_dump();
   return f[0] == 0 ? 0 : 2;
 }
@@ -3196,6 +2994,16 @@ int Engine::linear_residual(double* out) {
   const double* vals = do_schur ? dS.get() : dH.get();
   const double* lam = do_schur ? nullptr : dscal.get();
   const double* rhs = do_schur ? dS.get() + (size_t)nS * pd * pd : db.get();
+  if (do_schur && chol.rs_on) {
+    // the distributed factorization reduce-scattered S: dS holds this rank's partial sums only, so the residual is
+    // taken against an all-reduced copy (a collective: every rank calls linear_residual, as it calls solve)
+    const size_t len = (size_t)nS * pd * pd + size_poses;
+    dsfull.resize(len);
+    HIP_CHECK(hipMemcpyAsync(dsfull.get(), dS.get(), len * sizeof(double), hipMemcpyDeviceToDevice, stream));
+    allreduce_sum(dsfull.get(), len);
+    vals = dsfull.get();
+    rhs = vals + (size_t)nS * pd * pd;
+  }
   dtmp.resize(2 * (size_t)std::max(n, 1) + 2);
   launch::block_symv(pd, n, M.rptr.get(), M.ent.get(), M.diag.get(), vals, lam, dx.get(), nullptr, rhs, dtmp.get(),
                      dtmp.get() + n, stream);
@@ -3221,6 +3029,7 @@ int Engine::compute_marginals(int nblocks, const int* brow, const int* bcol, dou
   const bool own = !do_schur && !use_pcg() && !use_cgls();
   DeviceCholesky& C = own ? chol : marg_chol;
   if (!own && marg_ver != structure_ver) {
+    marg_chol.set_replicated();
     marg_chol.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
     marg_ver = structure_ver;
   }
@@ -3238,7 +3047,6 @@ int Engine::compute_marginals(int nblocks, const int* brow, const int* bcol, dou
   int fail = 0;
   HIP_CHECK(hipMemcpyAsync(&fail, dmarg_fail.get(), sizeof fail, hipMemcpyDeviceToHost, stream));
   HIP_CHECK(hipStreamSynchronize(stream));
-  if (fail) C.check_dag(stream);
   if (fail) return 0;
   // distinct block columns, batched K / pd per multi-right-hand-side solve
   std::vector<int> ucol(bcol, bcol + nblocks);
@@ -3289,11 +3097,11 @@ int Engine::factor_info(double* out, int n) {
   const double v[] = {(double)S.n, (double)S.nnzL, S.flops, (double)S.sn.size(), (double)S.num_levels,
                       (double)S.max_front, (double)chol.n_blocked, (double)chol.n_inplace_levels,
                       (double)chol.n_pre_levels, (double)chol.n_syrk_ops, (double)chol.n_bwd_rounds,
-                      (double)chol.n_dag_levels, (double)chol.n_owned_fronts, (double)chol.n_shared_fronts,
+                      0.0 /* retired: tile-DAG levels */, (double)chol.n_owned_fronts, (double)chol.n_shared_fronts,
                       (double)chol.n_roots, (double)chol.xch_len, chol.dist_model[0], chol.dist_model[1],
                       chol.dist_model[2], chol.dist_model[3], chol.dist_model[4], chol.rs_on ? 1.0 : 0.0,
                       (double)chol.rs_seg, (double)chol.rs_tail_len, chol.rs_model[0], chol.rs_model[1],
-                      (double)chol.n_w64_levels};
+                      0.0 /* retired: 64-column-step levels */};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;

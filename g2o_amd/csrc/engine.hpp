@@ -109,27 +109,15 @@ struct DeviceCholesky {
   std::vector<int> bwd_off;    // per level: offset of its backward-gemv tasks in `tasks` (+1 end)
   struct BwdLevel {            // backward solve of one level: (offset, count) task ranges in `tasks`
     std::pair<int, int> gemv, xall;
-    std::pair<int, int> seq{0, 0};  // fronts factored by k_dag: k_bwd_seq (one task per front)
     std::vector<std::pair<std::pair<int, int>, std::pair<int, int>>> rounds;  // blocked fronts: (inner, x)
   };
   std::vector<BwdLevel> bwd_ops;
   int max_ns = 0;
   // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
   // trailing-update (k_syrk) launches, big-panel backward rounds
-  int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0, n_dag_levels = 0;
-  struct Op { int kind, off, count, tpw = 1, w64 = 0; };  // kind 0 extend-add (pre-scattered level), 4 assembly + extend-add,
-                                                 // 2 panel step (6: with lagged-pair tasks), 3 syrk, 7 tile DAG,
-                                                 // 9 64-column panel step; w64: extend-add of a 64-column level
-                                                 // (off: first worker's tile slots, off2 fronts), tpw tiles per worker
-  std::vector<int> op_front_off;  // per op: first DagFront of a kind-7 op
-  // persistent tile DAG of latency-bound levels (cholesky.hip k_dag)
-  DevBuf<launch::DagFront> dag_fronts;
-  DevBuf<int4> dag_tiles;
-  DevBuf<unsigned> dag_flags, dag_tmo;
-  unsigned dag_epoch = 0;
-  // throws when the last factorization's tile DAG gave up waiting (a bug, never expected): called where a failed
-  // factorization is observed (the DAG also raises the not-PD flag then)
-  void check_dag(hipStream_t s);
+  int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
+  struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 / 5 assembly + extend-add,
+                                        // 2 panel step (6: with lagged-pair tasks), 3 syrk, 8 root exchange
   // ---- distributed factorization (landmark-sharded BA). Set dist_rank / dist_nranks / allreduce before
   // setup. The elimination tree is cut: every front below the cut belongs to one rank (whole subtrees, balanced by
   // modelled time), the fronts above it are factored by every rank. A rank factors its subtrees, the subtree roots'
@@ -156,6 +144,9 @@ struct DeviceCholesky {
   // rs_seg doubles) | shared blocks + rhs] — one reduce-scatter sums each rank's own segment, one all-reduce the tail;
   // the factor reads its entries from rs_buf (ent_src remapped), never another rank's segment
   bool rs_enable = false, rs_on = false;
+  // a factorization of the whole system on this rank alone (pose graphs, computeMarginals' Hpp factor): clears any
+  // distribution state an earlier sharded setup of the same object left behind
+  void set_replicated() { dist_rank = 0; dist_nranks = 1; dist_force = false; rs_enable = false; }
   std::function<void(double*, size_t)> reduce_scatter;  // in place, `count` doubles per rank
   long long rs_seg = 0, rs_tail_len = 0, rs_rhs_off = 0, rs_nblk = 0;
   double rs_model[2] = {0, 0};                // modelled seconds: reduce-scatter + tail all-reduce, full all-reduce
@@ -169,9 +160,6 @@ struct DeviceCholesky {
   DevBuf<launch::Task> tasks;
   DevBuf<launch::StepTask> step_tasks;
   DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, t_p, lbuf, linv, xinv;
-  DevBuf<double> linvn;              // 64-column levels: N = -L_b^-1 L_ba L_a^-1 per 64-panel start (32 x 32, row-major)
-  std::vector<char> sn_w64;          // per supernode: its level runs 64-column panel steps (k_step64)
-  int n_w64_levels = 0;
   long long lpool = 0;
   void setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj, hipStream_t s);
   // numeric LL^T fused with the forward solve of rhs (y = L^-1 P rhs)
@@ -384,6 +372,7 @@ class Engine {
   DevBuf<long long> dmarg_idx;
   BlockSymv symv_hpp, symv_s;
   DevBuf<double> dtmp;
+  DevBuf<double> dsfull;  // linear_residual under a reduce-scattered S: the all-reduced copy of [S blocks | bschur]
   DevicePCG pcg;  // {lm,gn}_pcg* algorithms (linear_solver_pcg.hpp)
   bool use_cgls() const { return algorithm.size() > 12 && algorithm.compare(algorithm.size() - 12, 12, "pcg6_3_eigen") == 0; }
   bool use_pcg() const { return algorithm.find("_pcg") != std::string::npos && !use_cgls(); }

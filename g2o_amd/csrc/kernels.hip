@@ -1080,9 +1080,7 @@ __device__ __forceinline__ void lm_decide_body(double* __restrict__ p, double cu
   const double lam = p[0];
   double nl, acc;
   if (rho > 0 && isfinite(temp)) {
-    double alpha = 1. - pow(2 * rho - 1, 3);
-    alpha = alpha < 2. / 3. ? alpha : 2. / 3.;
-    nl = lam * (1. / 3. > alpha ? 1. / 3. : alpha);
+    nl = lam * lm_scale_factor(rho);
     acc = 1.0;
   } else {
     nl = lam * ni;

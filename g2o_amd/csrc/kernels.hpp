@@ -190,12 +190,9 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
 // column c (permuted): ent_row/ent_src[colptr[c] .. colptr[c+1]) = row in the front | diag << 30, index in vals
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
-                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* linvn, double* xinv,
-                     int* fail, int assemble, bool w64, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place,
-                                                                         // 2 in place (m <= 512); w64: 64-column level
-// 64-column panel steps (cholesky.hip k_step64): linvn holds N = -L_b^-1 L_ba L_a^-1 per 64-panel start
-void chol_step64(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs,
-                 double* ysol, double* linv, double* linvn, double* xinv, int* fail, hipStream_t s);
+                     double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv,
+                     int* fail, int assemble, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place,
+                                                               // 2 in place (m <= 512)
 void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs, double* ysol,
                double* linv, double* xinv, int* fail, bool pairs, hipStream_t s);  // pairs: lagged-pair tasks present
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
@@ -212,24 +209,6 @@ void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double
                 const int* perm, double* xout, hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only
 constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 16, CHOL_BW = 4;
-// ---- persistent tile DAG of a latency-bound level (cholesky.hip k_dag) ----
-// A front is cut into 64 x 64 tiles: own rows/columns [0, ns) from 0, contribution rows/columns [ns, m) from ns, so no
-// tile mixes the two. Tile (I, J), I >= J, is owned by one resident workgroup for the whole factorization of the level
-// (its values stay in registers); panels of 32 columns advance by flags instead of kernel boundaries.
-struct DagFront {
-  long long f_off, l_off, v_off;
-  int m, ns, c0;
-  int nown;      // own tile rows / columns (ceil(ns / 64))
-  int ntr;       // tile rows (own + contribution)
-  int np;        // 32-column panels (ceil(ns / 32))
-  int flag_off;  // flags: [np diagonal flags | ntr * np panel flags (row-major by tile row)]
-  int pad;
-};
-constexpr int CHOL_DAG_TPW = 4;  // tiles per workgroup at most
-// nworkers workgroups, tpw tile slots each (int4 {front, I, J, 0}, front < 0: empty); epoch: this call's flag value
-void chol_dag(int nworkers, int tpw, const DagFront* fr, const int4* tiles, double* fronts, double* lbuf, double* vecs,
-              double* ysol, double* linv, unsigned* flags, unsigned epoch, int* fail, unsigned* tmo, hipStream_t s);
-int chol_dag_max_workers(int device);  // resident one per CU
 // distributed factorization glue: contiguous range copies (src, dst, len) in doubles; the distributed
 // solve's not-PD flag into / x and flag out of its all-reduce buffer; x[idx[k]] = 0
 void chol_copy_ranges(int n, const long long* rng, const double* src, double* dst, hipStream_t s);
@@ -238,10 +217,8 @@ void chol_pack_blocks(long long nblk, int bb, const long long* boff, const doubl
 void chol_dist_fail_in(const int* fail, double* xr, int n, hipStream_t s);
 void chol_dist_x_out(const double* xr, int n, double* x, int* fail, hipStream_t s);
 void chol_zero_idx(const int* idx, int n, double* x, hipStream_t s);
-// backward solve x = L11^-T t of fronts factored by k_dag (no explicit L11^-1): one workgroup per front, blocks of 32
-// columns from the last, L's columns of the next block prefetched while the current one is solved
-void chol_bwd_seq(int ntasks, const Task* tasks, const FrontDesc* fd, const double* lbuf, const double* linv,
-                  const double* tsol, double* xsol, const int* perm, double* xout, hipStream_t s);
+// measured roofline peaks (peaks.hip): out[0] HBM copy GB/s, out[1] FP64 MFMA TFLOP/s, out[2] FP64 VALU TFLOP/s, out[3] CUs
+void measure_peaks(int device, double* out);
 // computeMarginals multi-right-hand-side solves (marginals.hip): one launch per tree level, one workgroup per front
 void marg_forward(int nf, const int* lfronts, const FrontDesc* fd, const int* children, const int* relmap,
                   const double* lbuf, const double* linv, const long long* woff, double* W, double* Y, double* T, int n,

@@ -174,18 +174,20 @@ int g2ohip_solver_set_eta(g2ohip_graph* g, double eta);
 /* G2OBatchStatistics::iterationsLinearSolver of the last lm_pcg6_3_eigen solve */
 int g2ohip_solver_linear_iterations(g2ohip_graph* g);
 /* ||(A + lambda I) x - b|| / ||b|| of the last Solver::solve, evaluated on the device (A = the Schur complement
- * with Schur, else Hpp): a size-independent check of the factorization at any problem size. */
+ * with Schur, else Hpp): a size-independent check of the factorization at any problem size. With landmark shards
+ * (g2ohip_set_comm) it is a collective: every rank calls it (the reduced system is summed over ranks first when the
+ * distributed factorization reduce-scattered it). */
 int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel);
 /* Symbolic / schedule summary of the device factorization: out[0..20] = n, nnz(L), flops (this ordering),
  * supernodes, tree levels, largest front, blocked fronts, levels assembled in place, pre-scattered levels,
- * trailing-update launches, big-panel backward rounds, levels factored by the persistent tile DAG, and for landmark
+ * trailing-update launches, big-panel backward rounds, out[11] = 0 (retired slot), and for landmark
  * shards (nranks > 1) this rank's fronts, the shared fronts, the subtree roots, the doubles of the root exchange, the
  * cost model of the best cut of the elimination tree (modelled seconds of this rank's subtrees, of the shared top, of
  * the replicated factorization, of the cut's two all-reduces) and whether the factorization is distributed (1) or
  * replicated (0: the model preferred replication, or G2OHIP_DIST_FACTOR=0); then out[21..25] = whether the reduced
  * system is reduce-scattered by subtree ownership (1) instead of all-reduced, its per-rank segment and all-reduced tail
- * (doubles), and the modelled seconds of that input exchange and of the plain all-reduce; out[26] = tree levels factored
- * with 64-column panel steps (G2OHIP_CHOL_W64=1). Returns the number of entries available. */
+ * (doubles), and the modelled seconds of that input exchange and of the plain all-reduce; out[26] = 0 (retired slot).
+ * Returns the number of entries available. */
 int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n);
 /* Solver::computeMarginals (core/solver.h:108; BlockSolver::computeMarginals block_solver.hpp:451-460 ->
  * LinearSolverCSparse::solvePattern linear_solver_csparse.h:190-225, MarginalCovarianceCholesky): the pose-block
@@ -232,10 +234,13 @@ int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int
  * call sequence as g2ohip_set_comm; used to test the sharded path on a single-GPU box. */
 int g2ohip_set_comm_local(g2ohip_graph* g, const char* group_key, int rank, int nranks);
 /* RCCL transport self-test on one device (a one-rank communicator from `uid`): the product's allreduce sum and max
- * and its in-place reduce-scatter sum (the calls g2ohip_set_comm's ranks make) over n doubles of `in` on a stream of
- * `device`; out (3n doubles) = [sum | max | reduce-scatter segment].
- * A one-GPU box cannot host two ranks of one RCCL communicator, so this is the binding's smoke test there. */
+ * (the calls g2ohip_set_comm's ranks make) over n doubles of `in` on a stream of `device`; out (2n doubles) =
+ * [sum | max]. A one-GPU box cannot host two ranks of one RCCL communicator, so this is the binding's smoke test there. */
 int g2ohip_comm_selftest(int device, const unsigned char uid[128], int n, const double* in, double* out);
+/* As g2ohip_comm_selftest, plus the in-place reduce-scatter sum the distributed factorization uses: rs_out (n doubles)
+ * = this rank's segment. (0.1.x wrote the segment as a third block of `out`; 0.2 restored the 2n contract above.) */
+int g2ohip_comm_selftest_rs(int device, const unsigned char uid[128], int n, const double* in, double* out,
+                            double* rs_out);
 /* The test transport's rank-ordered host reduction alone (no GPU): `nranks` host threads that share `group_key` each
  * call this with their buffer; every call is checked to be the same collective on every rank (call number, length,
  * operation) and a mismatch returns G2OHIP_ERR_DEVICE on every rank (g2ohip_last_error says which) instead of reading
@@ -272,6 +277,13 @@ double g2ohip_kernel_flops(g2ohip_graph* g, const char* name);
  * 8 x u64 per record {kernel id, t0, t1..t6}; returns the record count (0 in product builds) */
 int g2ohip_debug_phases(unsigned long long* out, int max_records);
 const char* g2ohip_last_error(void);
+/* Measured roofline peaks of `device` (peaks.hip, ~1 s): out[0] HBM streaming-copy GB/s (read + written bytes of a
+ * 2 GiB double4 copy), out[1] FP64 MFMA TFLOP/s (v_mfma_f64_16x16x4f64 issue loop), out[2] FP64 VALU TFLOP/s (v_fma_f64
+ * issue loop), out[3] compute units; n >= 4. Returns 4 or a negative error. */
+int g2ohip_measure_peaks(int device, double* out, int n);
+/* The accepted LM trial's lambda factor max(1/3, min(2/3, 1 - (2 rho - 1)^3)) exactly as the device decision and the
+ * host loop compute it (optimization_algorithm_levenberg.cpp:127-136; the cube rounded once, like glibc's pow). */
+double g2ohip_lm_scale_factor(double rho);
 const char* g2ohip_version(void);
 
 #ifdef __cplusplus

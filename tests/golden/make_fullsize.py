@@ -1,8 +1,10 @@
 """Full-size BASELINE fixtures (C2, C3, C4, C5, and C4R: C4 with random covisibility, a dense reduced camera system)
 for the -m gpu parity tests.
 
-C4 covers the exact sequence bench.py times (iteration 0 with the structure, then 29 more: the driver runs
---warmup 5 --steps 20, the default is 5 + 30 minus the untimed stage iterations), C2 / C3 / C5 at least 5 iterations.
+Every fixture of a config bench.py times covers exactly the iterations it runs: C4 30 (iteration 0 with the
+structure, then 29 more: the driver runs --warmup 5 --steps 20, the default is 5 + 30 minus the untimed stage
+iterations), C3 8 (posegraph_leg: 1 warmup + 5 timed + 2 factor-timer iterations), C5 14 (c5_leg: 2 warmup + 10
+timed + 2 stage-timer iterations); C2 6, C4R 3.
 
 Run in the development container, where oracle/_ref (the reference's vendored CSparse compiled
 from /root/reference) is available.  Each fixture is data only: the synth recipe, the oracle's LM
@@ -27,7 +29,7 @@ import oracle_py  # noqa: E402
 from g2o_amd import synth  # noqa: E402
 
 # name -> LM iterations recorded
-ITERS = {"C2": 6, "C3": 5, "C4": 30, "C5": 5, "C4R": 3}
+ITERS = {"C2": 6, "C3": 8, "C4": 30, "C5": 14, "C4R": 3}
 C5_POINT_STRIDE = 97      # every 97th point's coordinates stored exactly
 C5_CHUNK = 4096           # per-chunk sums of the point block of the minimal state
 

@@ -131,6 +131,53 @@ def test_c4_bench_sequence(g2o_amd_mod):
     assert np.linalg.norm(x - xr) <= RTOL * np.linalg.norm(xr)
 
 
+def _bench_sequence(g2o_amd_mod, name, warmup, timed, first_timer, stage_timer=None):
+    """optimize_step from iteration 0 through exactly the iterations a bench.py leg runs: `warmup` at the default
+    statistics, `timed` at stats level 1 (with `first_timer` kernel timing, as the leg's timed region), then the leg's
+    two stage iterations with every kernel timer on at stats level 2 — each switch where the leg makes it, since the
+    kernel timers change what the LM loop enqueues (the speculative next assembly is off while assembly kernels are
+    timed). Every iteration's chi2, lambda and trial count against the fixture, then the final state."""
+    fx = _fixture(name)
+    prob = synth.by_name(name)
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_algorithm(ALG[name])
+    chi0 = opt.chi2()
+    assert abs(chi0 - float(fx["chi2_0"])) <= 1e-9 * float(fx["chi2_0"])
+    n = int(fx["iterations"])
+    assert n == warmup + timed + 2, (name, n)
+    st = []
+    for it in range(n):
+        if it == warmup:
+            if first_timer:
+                opt.enable_kernel_timing(True, only=first_timer)
+            opt.set_stats_level(1)
+        if it == warmup + timed:
+            if stage_timer:
+                opt.enable_kernel_timing(True, only=stage_timer)
+            else:
+                opt.enable_kernel_timing(True)
+            opt.set_stats_level(2)
+        r, s = opt.optimize_step(it)
+        st.append(s)
+        assert r == 0, (it, r)
+    _check_trajectory(fx, st, n, chi0)
+    return prob, opt
+
+
+def test_c5_bench_sequence(g2o_amd_mod):
+    """C5 over exactly bench.py's c5_leg: 2 warmup + 10 timed + 2 stage-timer iterations (14, the fixture's length)."""
+    prob, opt = _bench_sequence(g2o_amd_mod, "C5", 2, 10, None)
+    _check_c5_state(prob, opt.minimal_state(), _fixture("C5"))
+
+
+def test_c3_bench_sequence(g2o_amd_mod):
+    """C3 over exactly bench.py's posegraph_leg: 1 warmup + 5 timed + 2 factor-timer iterations (8, the fixture's
+    length; the leg times chol_factor alone in its last two iterations)."""
+    prob, opt = _bench_sequence(g2o_amd_mod, "C3", 1, 5, None, "chol_factor")
+    x, xr = opt.minimal_state(), _fixture("C3")["state"]
+    assert np.linalg.norm(x - xr) <= RTOL * np.linalg.norm(xr)
+
+
 def test_c4r_full_random_covisibility(g2o_amd_mod):
     """SURVEY.md §8d's C4 variant covis=random at full size (1k cameras x 100k points x 1M observations, every point
     seen by 10 of ALL 1000 cameras): the reduced camera system is dense (6000 x 6000, 72 GFLOP per factorization), one

@@ -95,8 +95,7 @@ def test_marginals_many_batches(g2o_amd_mod, oracle):
     {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
     {"G2OHIP_CHOL_LAG": "2"},
     {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_LAG": "1"},
-    {"G2OHIP_CHOL_W64": "1"},
-], ids=["blocked_fronts", "lagged_all_levels", "lagged_separate_contrib", "w64_steps"])
+], ids=["blocked_fronts", "lagged_all_levels", "lagged_separate_contrib"])
 @pytest.mark.parametrize("name", ["C1", "C3"])
 def test_marginals_blocked_and_lagged_schedules(g2o_amd_mod, oracle, monkeypatch, knobs, name):
     """The marginal solves read the factor's layout (L21 per front, L_kk^-1 per panel, no stored diagonal blocks).
@@ -113,8 +112,6 @@ def test_marginals_blocked_and_lagged_schedules(g2o_amd_mod, oracle, monkeypatch
     info = opt.factor_info()
     if "G2OHIP_CHOL_BLOCK_MIN" in knobs:
         assert info["blocked_fronts"] > 0 and info["bwd_rounds"] > 0, info
-    if "G2OHIP_CHOL_W64" in knobs:
-        assert info["w64_levels"] > 0, info
     pd, _, npose, _ = opt.block_dims()
     pat = _pattern(npose)
     blocks = opt.compute_marginals(pat)

@@ -338,15 +338,23 @@ def test_ba_assembly_paths(g2o_amd_mod, oracle, monkeypatch, fused):
         _check(*_run_both(g2o_amd_mod, oracle, prob, 4))
 
 
-@pytest.mark.parametrize("mode", ["0", "2", "w64"], ids=["panel_steps_only", "tile_dag_every_fitting_level", "w64_steps"])
+SCHEDULES = {
+    "default": {},
+    "lagged_all_levels": {"G2OHIP_CHOL_LAG": "2"},
+    "blocked_separate_contrib": {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64",
+                                 "G2OHIP_CHOL_WIDE_PB": "64"},
+}
+
+
+@pytest.mark.parametrize("mode", list(SCHEDULES))
 @pytest.mark.parametrize("name", ["C1", "C2", "C3", "C4", "C5"])
 def test_factor_schedules(g2o_amd_mod, oracle, monkeypatch, name, mode):
-    """The factorization schedules of a tree level against the oracle: the launch-per-panel 32-column steps
-    (G2OHIP_CHOL_DAG=0), the persistent tile DAG (k_dag) on every level whose tiles fit the resident workgroups (=2) and
-    the 64-column panel steps (k_step64, G2OHIP_CHOL_W64=1, every unblocked level). Reduced system, solution and an LM
-    trajectory."""
-    monkeypatch.setenv("G2OHIP_CHOL_DAG", "0" if mode == "w64" else mode)
-    monkeypatch.setenv("G2OHIP_CHOL_W64", "1" if mode == "w64" else "0")
+    """The factorization schedules of a tree level against the oracle: the default launch-per-panel 32-column steps,
+    lagged rank-64 pair steps forced on every level, and blocked fronts (big-panel trailing updates, separate
+    contribution passes, backward rounds) forced on the small configs. Reduced system, solution, an LM trajectory and
+    marginals from the same factor layout."""
+    for k, v in SCHEDULES[mode].items():
+        monkeypatch.setenv(k, v)
     prob = synth.by_name(name, "small")
     opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
     ref = oracle.OracleGraph(prob)
@@ -356,8 +364,8 @@ def test_factor_schedules(g2o_amd_mod, oracle, monkeypatch, name, mode):
     for k in ("bschur", "x"):
         assert np.linalg.norm(g[k] - r[k]) <= 1e-9 * np.linalg.norm(r[k]), k
     info = opt.factor_info()
-    assert (info["dag_levels"] > 0) == (mode == "2"), info
-    assert (info["w64_levels"] > 0) == (mode == "w64"), info
+    if mode == "blocked_separate_contrib" and name in ("C1", "C3"):
+        assert info["blocked_fronts"] > 0, info
     opt.build_system()
     opt.set_lambda(1e-3)
     assert opt.solve()

@@ -194,3 +194,49 @@ def test_distributed_reduce_scatter_equals_allreduce(g2o_amd_mod, monkeypatch):
     assert np.array_equal(x, xa)
     for r in range(3):
         assert [s.chi2 for s in res[r][1]] == [s.chi2 for s in ares[r][1]]
+
+
+def test_distributed_linear_residual(g2o_amd_mod, monkeypatch):
+    """linear_residual under the distributed factorization with the reduce-scattered S (each rank's dS holds only its
+    partial sums): the residual is taken against the all-reduced system, so every rank reports the same small value,
+    and it agrees with the single-GPU residual of the same staged solve."""
+    prob = synth.by_name("C5", "small")
+    monkeypatch.setenv("G2OHIP_DIST_FACTOR", "1")
+    nranks, lam = 3, 1e-3
+    key = uuid.uuid4().hex
+    opts = [g2o_amd_mod.SparseOptimizer(0).add_problem(prob) for _ in range(nranks)]
+    for r, o in enumerate(opts):
+        o.set_comm_local(key, r, nranks)
+    out, errs = [None] * nranks, []
+
+    def body(r):
+        try:
+            o = opts[r]
+            o.initialize_optimization()
+            o.build_structure()
+            o.build_system()
+            o.set_lambda(lam, True)
+            assert o.solve()
+            out[r] = o.linear_residual()
+            o.restore_diagonal()
+        except Exception as ex:  # surfaced below
+            errs.append(ex)
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    assert all(o.factor_info()["reduce_scatter"] == 1 for o in opts)
+    assert all(v == out[0] for v in out), out
+    assert out[0] <= 1e-10, out
+    monkeypatch.delenv("G2OHIP_DIST_FACTOR")
+    single = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    single.initialize_optimization()
+    single.build_structure()
+    single.build_system()
+    single.set_lambda(lam, True)
+    assert single.solve()
+    r1 = single.linear_residual()
+    assert r1 <= 1e-10 and abs(out[0] - r1) <= 1e-10, (out[0], r1)

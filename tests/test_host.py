@@ -32,6 +32,26 @@ def test_version(g2o_amd_mod):
     assert b"gfx950" in g2o_amd_mod.lib().g2ohip_version()
 
 
+def test_lm_scale_factor_matches_pow(g2o_amd_mod):
+    """The LM trial's lambda factor max(1/3, min(2/3, 1 - (2 rho - 1)^3)) (optimization_algorithm_levenberg.cpp:127-136)
+    as the library computes it on host and device (one shared __host__ __device__ function): bitwise the formula with
+    the cube rounded once (exact rational arithmetic), and within one ulp of the C library's pow (glibc's pow is
+    accurate to 0.52 ulp, not correctly rounded), over a sweep of gain ratios."""
+    import math
+    from fractions import Fraction
+    f = g2o_amd_mod.lib().g2ohip_lm_scale_factor
+    rng = np.random.default_rng(11)
+    rhos = np.concatenate([rng.uniform(0.0, 1.2, 6000), 10.0 ** rng.uniform(-12, 2, 6000),
+                           0.5 + rng.uniform(-1e-3, 1e-3, 6000), [1e-300, 0.5, 1.0, 1.5]])
+    for rho in rhos.tolist():
+        t = 2 * rho - 1
+        exact = max(1.0 / 3.0, min(1.0 - float(Fraction(t) ** 3), 2.0 / 3.0))
+        libm = max(1.0 / 3.0, min(1.0 - math.pow(t, 3), 2.0 / 3.0))
+        got = f(rho)
+        assert got == exact, (rho, got, exact)
+        assert abs(got - libm) <= np.spacing(libm), (rho, got, libm)
+
+
 def _pose_pattern(prob):
     e = prob.edges[0]
     fixed = set(prob.vertices[0].ids[prob.vertices[0].fixed.astype(bool)].tolist())

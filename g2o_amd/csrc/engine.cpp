@@ -537,6 +537,17 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   {
     using launch::Task;
     const int NB = launch::CHOL_NB, TT = launch::CHOL_TT, EA = launch::CHOL_EA;
+    // envelope of a band supernode (Supernode::env_off): the first own column with a structural nonzero among the
+    // front rows [r, r + 64); dense supernodes: 0
+    auto tile_fnz = [&](int sn, int r) {
+      const Supernode& q = sym.sn[sn];
+      if (q.env_off < 0) return 0;
+      const int m = q.ns + q.nr;
+      int f = 1 << 30;
+      for (int i = r; i < std::min(r + TT, m); ++i) f = std::min(f, sym.fnz[q.env_off + i]);
+      return f;
+    };
+    auto tile_nz = [&](int sn, int r, int kend) { return tile_fnz(sn, r) < kend; };
     std::vector<Task> tk;
     std::vector<launch::StepTask> stk;
     std::vector<int> sn_pb(sym.sn.size(), 0);  // big-panel width of blocked fronts (0: unblocked)
@@ -675,8 +686,16 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
                                     k0 | (kb << 16), tile, flags, clim};
           };
           if (r0 < q.ns && !bnd) diag_t.push_back(mk(0, 4 | (pair ? 64 : 0)));
-          for (int tj = 0; tj < std::max(TJ, 1); ++tj)
-            for (int ti = tj; ti < T; ++ti) tile_t.push_back(mk(ti | (tj << 16), (tj < TJ ? 1 : 0) | fl));
+          // band supernodes: a tile whose rows carry no structural nonzero in the panel (or, for the update, whose
+          // column rows carry none) would only move exact zeros: no task (its L rows stay zero in the pre-zeroed lbuf)
+          for (int tj = 0; tj < std::max(TJ, 1); ++tj) {
+            const bool nzj = tile_nz(sn, r0 + TT * tj, k0 + kb);
+            if (tj > 0 && !nzj) continue;
+            for (int ti = tj; ti < T; ++ti) {
+              if (!tile_nz(sn, r0 + TT * ti, k0 + kb)) continue;
+              tile_t.push_back(mk(ti | (tj << 16), (tj < TJ && nzj ? 1 : 0) | fl));
+            }
+          }
           // inverse tasks: block row p-1's term into every pending block (bp, j), bp >= p, j < p;
           // block row p is final after this step. Blocked fronts build only the diagonal big-panel
           // blocks of X (their backward solve substitutes big panel by big panel)
@@ -704,8 +723,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           const int kb = (p + 1) * NB, ka = kb - lpb, m = q.ns + q.nr;
           if (!blocked(q) || kb >= q.ns) continue;
           const int T = (m - kb + TT - 1) / TT, TJ = (q.ns - kb + TT - 1) / TT;
-          for (int tj = 0; tj < TJ; ++tj)
-            for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, ka, ti | (tj << 16), kb});
+          for (int tj = 0; tj < TJ; ++tj) {
+            if (!tile_nz(sn, kb + TT * tj, kb)) continue;
+            for (int ti = tj; ti < T; ++ti)
+              if (tile_nz(sn, kb + TT * ti, kb)) tk.push_back(Task{sn, ka, ti | (tj << 16), kb});
+          }
           stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns,
                                          q.c0, kb, 0, 4, q.ns});
         }
@@ -719,8 +741,15 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         if (fused_contrib) break;
         const Supernode& q = sym.sn[sn];
         const int T = (q.nr + TT - 1) / TT;
+        const bool childless = sym.children_ptr[sn + 1] == sym.children_ptr[sn];
         for (int tj = 0; tj < T; ++tj)
-          for (int ti = tj; ti < T; ++ti) tk.push_back(Task{sn, 0, ti | (tj << 16), 0});
+          for (int ti = tj; ti < T; ++ti) {
+            // band supernodes: K starts where both tile row sets have structural nonzeros; a tile with none only keeps
+            // its entries (childless fronts' contribution blocks are written, not read: an empty K writes the zeros)
+            const int ka = std::max(tile_fnz(sn, q.ns + TT * ti), tile_fnz(sn, q.ns + TT * tj));
+            if (ka >= q.ns && !childless) continue;
+            tk.push_back(Task{sn, std::min(ka, q.ns), ti | (tj << 16), 0});
+          }
       }
       sy.count = (int)tk.size() - sy.off;
       if (sy.count) { ops.push_back(sy); ++n_syrk_ops; }
@@ -843,7 +872,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   vecs.resize(std::max<int64_t>(sym.vec_pool, 1));
   rhs_p.resize(std::max(sym.n, 1));
   y_p.resize(std::max(sym.n, 1));
-  lbuf.resize(std::max<long long>(lpool, 1));
+  lbuf.resize(std::max<long long>(lpool, 1) + 2);  // + one 16-byte piece of slack after the last front (GemmNTd)
+  if (!sym.fnz.empty()) lbuf.zero(s);  // band supernodes: the L rows of skipped tiles are read as zeros
   linv.resize((size_t)(sym.n + launch::CHOL_NB) * launch::CHOL_NB * launch::CHOL_NB);  // one 32x32 L_kk^-1 per panel start
   xinv.resize(std::max<long long>(xoff, 1));
   t_p.resize(std::max(sym.n, 1));

@@ -153,5 +153,156 @@ struct GemmNT {
   }
 };
 
+// The same tile update with the operands staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging)
+// in an NS-stage ring: chunk c + NS - 1 is issued while chunk c is multiplied, so NS - 1 chunks (KC columns each) are
+// in flight across every barrier (counted s_waitcnt vmcnt, raw s_barrier: __syncthreads would drain the DMA).
+// The DMA writes lane-linear 1 KiB per wave instruction, so the LDS image of a chunk is CPI = 128 / BM columns per
+// instruction (a column = BM contiguous rows of the column-major operand), column groups padded by PAD doubles.
+// Out-of-range sources are clamped (rows >= mrows only feed outputs that are never stored; columns >= kb are zeroed at
+// the fragment read of the last chunk). A piece is two consecutive rows: the one starting at row mrows - 1 also reads
+// the element after the column's last row (the next column's first, or past the operand's end: callers leave one
+// 16-byte piece of slack after A).
+template <int BM, int BN, int WM = 2, int WN = 2, int KC_ = 16, int NS = 3>
+struct GemmNTd {
+  static constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  static constexpr int KC = KC_;
+  static_assert(BM == 64 || BM == 128, "BM: one or two columns per DMA instruction");
+  static_assert(BN == 64 || BN == 128, "BN: one or two columns per DMA instruction");
+  static constexpr int CPA = 128 / BM, CPB = 128 / BN;      // columns per instruction
+  static constexpr int PAD = 16;
+  static constexpr int GA = CPA * BM + PAD, GB = CPB * BN + PAD;  // column-group strides (doubles)
+  static constexpr int IA = KC / CPA, IB = KC / CPB;           // instructions per chunk and operand
+  static_assert(IA % NW == 0 && IB % NW == 0, "every wave issues the same number of DMA instructions");
+  static constexpr int JA = IA / NW, JB = IB / NW;             // per wave (= per thread)
+  static constexpr int STAGE = IA * GA + IB * GB;              // doubles per stage
+  static constexpr int LDS_DOUBLES = NS * STAGE > BM * (BN + 1) ? NS * STAGE : BM * (BN + 1);
+  static constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;
+  static constexpr int G = JA + JB;                            // DMA instructions per thread per chunk
+
+  __device__ static double* aptr(double* st, int k, int r) { return st + (k / CPA) * GA + (k % CPA) * BM + r; }
+  __device__ static double* bptr(double* st, int k, int r) { return st + IA * GA + (k / CPB) * GB + (k % CPB) * BN + r; }
+
+  __device__ __forceinline__ static void run(const double* __restrict__ A, int lda, double* __restrict__ C, int ldc, int mrows,
+                             int climit, int I0, int J0, int ka, int kb, double* lds, bool overwrite = false) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w % WM, wc = w / WM;
+    const int lr = lane & 15, lk = lane >> 4;
+    // chunk kc -> stage st: instruction j of wave w covers column group g = j NW + w, lane l the 16-B piece l of it
+    auto issue = [&](int kc, double* st) {
+#pragma unroll
+      for (int j = 0; j < JA; ++j) {
+        const int g = j * NW + w, col = g * CPA + lane / (BM / 2), row = 2 * (lane % (BM / 2));
+        const int k = min(kc + col, kb - 1), r = min(I0 + row, mrows - 1);  // (row mrows - 1, mrows): see below
+        __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)k * lda + r),
+                                         (__attribute__((address_space(3))) void*)(st + g * GA), 16, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < JB; ++j) {
+        const int g = j * NW + w, col = g * CPB + lane / (BN / 2), row = 2 * (lane % (BN / 2));
+        const int k = min(kc + col, kb - 1), r = min(J0 + row, mrows - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)k * lda + r),
+                                         (__attribute__((address_space(3))) void*)(st + IA * GA + g * GB), 16, 0, 0);
+      }
+    };
+    gdx4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = gdx4{0.0, 0.0, 0.0, 0.0};
+    const int nch = (kb - ka + KC - 1) / KC;
+#pragma unroll
+    for (int c = 0; c < NS - 1; ++c)
+      if (c < nch) issue(ka + c * KC, lds + c * STAGE);
+    for (int c = 0; c < nch; ++c) {
+      // chunk c landed (the younger chunks issued after it may stay in flight), then every wave's pieces of it are
+      // visible and every wave is done with the stage chunk c + NS - 1 overwrites
+      const int ahead = min(nch - 1 - c, NS - 2);  // chunks issued after c
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + NS - 1 < nch) issue(ka + (c + NS - 1) * KC, lds + ((c + NS - 1) % NS) * STAGE);
+      double* st = lds + (c % NS) * STAGE;
+      const int kv = min(KC, kb - ka - c * KC);  // valid columns of this chunk
+      if (kv == KC) {
+#pragma unroll
+        for (int kk = 0; kk < KC / 4; ++kk) {
+          const int k = kk * 4 + lk;
+          double fa[MI], fb[NJ];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) fa[i] = *aptr(st, k, wr * (BM / WM) + 16 * i + lr);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) fb[j] = *bptr(st, k, wc * (BN / WN) + 16 * j + lr);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+      } else {
+        for (int kk = 0; kk < (kv + 3) / 4; ++kk) {
+          const int k = kk * 4 + lk;
+          double fa[MI], fb[NJ];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) fa[i] = k < kv ? *aptr(st, k, wr * (BM / WM) + 16 * i + lr) : 0.0;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) fb[j] = k < kv ? *bptr(st, k, wc * (BN / WN) + 16 * j + lr) : 0.0;
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    // every DMA retired (the last chunk waited vmcnt(0)); the LDS epilogue reuses the ring after a barrier
+    if ((overwrite || kb - ka <= 2 * KC) && NT % BM == 0) {
+      __syncthreads();
+      constexpr int CS = BN + 1, CPI = NT / BM;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            lds[(wr * (BM / WM) + 16 * i + lk + 4 * q) * CS + wc * (BN / WN) + 16 * j + lr] = acc[i][j][q];
+      __syncthreads();
+      const int r = tid % BM, gi = I0 + r;
+      constexpr int NP = BN / CPI;
+      double cv[NP];
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const int c = tid / BM + CPI * u, gj = J0 + c;
+        cv[u] = overwrite ? 0.0 : ld0(C, gj * ldc + gi, gi < mrows && gj < climit && gi >= gj);
+      }
+#pragma unroll
+      for (int u = 0; u < NP; ++u) {
+        const int c = tid / BM + CPI * u, gj = J0 + c;
+        if (gi < mrows && gj < climit && gi >= gj) C[(size_t)gj * ldc + gi] = cv[u] - lds[r * CS + c];
+      }
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int gj = J0 + wc * (BN / WN) + 16 * j + lr;
+      double cv[MI][4];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gi = I0 + wr * (BM / WM) + 16 * i + lk + 4 * q;
+          cv[i][q] = overwrite ? 0.0 : ld0(C, gj * ldc + gi, gi < mrows && gj < climit && gi >= gj);
+        }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gi = I0 + wr * (BM / WM) + 16 * i + lk + 4 * q;
+          if (gi < mrows && gj < climit && gi >= gj) C[(size_t)gj * ldc + gi] = cv[i][q] - acc[i][j][q];
+        }
+    }
+  }
+};
+
 }  // namespace g2ohip
 

@@ -21,9 +21,36 @@ struct NDState {
   bool do_refine, do_windows, part_degree;
   std::vector<int> rank;  // scratch: position of a vertex in its part's BFS visitation order
   const bool no_small_windows = getenv("G2OHIP_ND_NO_SMALLWIN") != nullptr;  // dev A/B
+  int band_leaf = 0;                  // parts of at most this many blocks become band leaves (0: off)
+  std::vector<int>* groups = nullptr;  // band-leaf group per block
+  int next_group = 0;
   explicit NDState(const BlockPattern& p, int leaf_, bool refine_, bool windows_, bool part_degree_)
       : P(p), part(p.nb, 0), dist(p.nb, -1), mark(p.nb, 0), leaf(leaf_), do_refine(refine_), do_windows(windows_),
         part_degree(part_degree_), rank(p.nb, -1) {}
+
+  // BFS visitation order of a part's level structure, each level's vertices with fewer neighbours in the next level
+  // first (ties: discovery order): on a band the prefix of this order grows one position at a time
+  std::vector<int> level_order(const std::vector<std::vector<int>>& lv, int id) {
+    const int h = (int)lv.size();
+    std::vector<int> ord;
+    for (int k = 0; k < h; ++k) {
+      for (int v : lv[k]) rank[v] = k;  // level index, temporarily
+      ord.insert(ord.end(), lv[k].begin(), lv[k].end());
+    }
+    for (int k = 0, base = 0; k < h; base += (int)lv[k].size(), ++k) {
+      std::vector<std::pair<int, int>> key(lv[k].size());
+      for (size_t q = 0; q < lv[k].size(); ++q) {
+        const int v = lv[k][q];
+        int nn = 0;
+        for (int p = P.adjp[v]; p < P.adjp[v + 1]; ++p) nn += part[P.adji[p]] == id && rank[P.adji[p]] == k + 1;
+        key[q] = {nn, (int)q};
+      }
+      std::sort(key.begin(), key.end());
+      for (size_t q = 0; q < key.size(); ++q) ord[base + q] = lv[k][key[q].second];
+    }
+    for (int v : ord) rank[v] = -1;
+    return ord;
+  }
 
   // Exact minimum-degree elimination on a small vertex set.
   void min_degree(const std::vector<int>& vs) {
@@ -177,6 +204,15 @@ struct NDState {
       return;
     }
     const int N = (int)vs.size();
+    if (band_leaf > 0 && N <= band_leaf && groups) {
+      // band leaf: the sequential (band) order from one end; the analysis makes it one band supernode
+      const int gid = next_group++;
+      for (int v : level_order(lv, id)) {
+        order.push_back(v);
+        (*groups)[v] = gid;
+      }
+      return;
+    }
     std::vector<int> before(h + 1, 0);
     for (int k = 0; k < h; ++k) before[k + 1] = before[k] + (int)lv[k].size();
     int kbest = -1;
@@ -202,26 +238,7 @@ struct NDState {
     if (do_windows) {
       // within a level, vertices with fewer neighbours in the next level first (ties: discovery order), so the
       // reach of a prefix grows gradually instead of jumping to the end of the next level
-      std::vector<int> ord;
-      ord.reserve(N);
-      for (int k = 0; k < h; ++k) {
-        for (int v : lv[k]) rank[v] = k;  // level index, temporarily
-        std::vector<std::pair<int, int>> key;
-        key.reserve(lv[k].size());
-        for (size_t q = 0; q < lv[k].size(); ++q) key.push_back({0, (int)q});
-        ord.insert(ord.end(), lv[k].begin(), lv[k].end());
-      }
-      for (int k = 0, base = 0; k < h; base += (int)lv[k].size(), ++k) {
-        std::vector<std::pair<int, int>> key(lv[k].size());
-        for (size_t q = 0; q < lv[k].size(); ++q) {
-          const int v = lv[k][q];
-          int nn = 0;
-          for (int p = P.adjp[v]; p < P.adjp[v + 1]; ++p) nn += part[P.adji[p]] == id && rank[P.adji[p]] == k + 1;
-          key[q] = {nn, (int)q};
-        }
-        std::sort(key.begin(), key.end());
-        for (size_t q = 0; q < key.size(); ++q) ord[base + q] = lv[k][key[q].second];
-      }
+      const std::vector<int> ord = level_order(lv, id);
       for (int k = 0; k < N; ++k) rank[ord[k]] = k;
       // balanced windows as the level candidates (both sides >= 20 %); failing that, on a part too small to
       // split in balance (a leaf-sized band segment a bit wider than the bandwidth), the window that shortens
@@ -290,8 +307,12 @@ struct NDState {
 
 }  // namespace
 
-std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size, bool refine, bool windows, bool part_degree) {
+std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size, bool refine, bool windows, bool part_degree,
+                                   int band_leaf, std::vector<int>* groups) {
   NDState st(P, std::max(leaf_size, 1), refine, windows, part_degree || windows);
+  if (groups) groups->assign(P.nb, -1);
+  st.band_leaf = band_leaf;
+  st.groups = groups;
   std::vector<int> all(P.nb);
   std::iota(all.begin(), all.end(), 0);
   st.run(all, 0);
@@ -309,7 +330,8 @@ double gpu_cost(const Symbolic& S) {
   return S.flops / 30e12 + lsteps * 12e-6;
 }
 
-Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, int relax_max_blocks) {
+Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, int relax_max_blocks,
+                 const std::vector<int>* groups) {
   const int nb = P.nb;
   if (bperm.empty() && nb > 0) {
     if (const char* rm = getenv("G2OHIP_ND_RMAX")) relax_max_blocks = atoi(rm);  // dev A/B
@@ -322,10 +344,31 @@ Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, in
     const double base = gpu_cost(best);
     double bc = base;
     const bool var[4][3] = {{true, false, false}, {false, false, true}, {true, false, true}, {false, true, true}};
-    for (const auto& v : var) {
+    int bv = -1;  // the variant kept (-1: plain)
+    for (int k = 0; k < 4; ++k) {
+      const auto& v = var[k];
       Symbolic c = analyze(P, nested_dissection(P, 48, v[0], v[1], v[2]), relax, relax_max_blocks);
       const double cc = gpu_cost(c);
-      if (cc < 0.95 * base && cc < bc) { bc = cc; best = std::move(c); }
+      if (cc < 0.95 * base && cc < bc) { bc = cc; best = std::move(c); bv = k; }
+    }
+    // band leaves (hybrid ordering): the kept variant's dissection down to parts of at most `bl` blocks, each such
+    // part that is a long band ordered sequentially and factored as one band supernode — the reference's own
+    // sequential order inside the leaves (fewer flops) for a chain no longer than the dissection levels it replaces
+    const char* eb = getenv("G2OHIP_BAND_LEAF");  // dev A/B: 0 off, N force leaves of N blocks
+    const int force_bl = eb ? atoi(eb) : -1;
+    if (force_bl != 0) {
+      const bool* v = bv >= 0 ? var[bv] : nullptr;
+      for (int bl : {96, 128, 192, 256, 384}) {
+        if (force_bl > 0 && bl != 96) break;
+        const int leafb = force_bl > 0 ? force_bl : bl;
+        if (leafb >= nb) break;
+        std::vector<int> grp;
+        std::vector<int> ord = nested_dissection(P, 48, v ? v[0] : false, v ? v[1] : false, v ? v[2] : false, leafb, &grp);
+        Symbolic c = analyze(P, ord, relax, relax_max_blocks, &grp);
+        c.band_leaf = leafb;
+        const double cc = gpu_cost(c);
+        if (force_bl > 0 || cc < 0.95 * bc) { bc = cc; best = std::move(c); }
+      }
     }
     return best;
   }
@@ -430,7 +473,8 @@ Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, in
     sns.push_back(std::move(t));
   }
   // relaxed amalgamation: merge a supernode into the next one when it is that one's
-  // (postorder-last) child and the added explicit zeros stay small
+  // (postorder-last) child and the added explicit zeros stay small; blocks of one band-leaf group are merged whole
+  auto grp_of = [&](int newb) { return groups ? (*groups)[bperm[newb]] : -1; };
   {
     std::vector<Tmp> out;
     for (auto& t : sns) {
@@ -442,7 +486,8 @@ Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, in
           const double rp = (double)t.rows.size(), rc = (double)c.rows.size();
           const double zeros = wc * (wp + rp - rc);
           const double total = w * (w + 1) / 2 + w * rp;
-          if (w <= relax_max_blocks && zeros <= relax * total) {
+          const bool band = grp_of(c.b0) >= 0 && grp_of(c.b0) == grp_of(t.b0);
+          if (band || (w <= relax_max_blocks && zeros <= relax * total)) {
             c.b1 = t.b1;
             c.rows = t.rows;
             continue;
@@ -453,8 +498,31 @@ Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, in
     }
     sns.swap(out);
   }
-  std::vector<std::vector<int>>().swap(st);
   const int ns_count = (int)sns.size();
+  // envelopes of the band supernodes (a group merged into a supernode of more than one block): per front row the first
+  // own column with a structural nonzero (see Supernode::env_off)
+  std::vector<std::vector<int>> env(ns_count);
+  for (int s = 0; s < ns_count; ++s) {
+    const Tmp& t = sns[s];
+    if (t.b1 - t.b0 < 2 || grp_of(t.b0) < 0 || grp_of(t.b0) != grp_of(t.b1 - 1)) continue;
+    const int c0 = S.boffset_new[t.b0], ns = S.boffset_new[t.b1] - c0;
+    std::vector<int> roff(t.rows.size() + 1, 0);
+    for (size_t q = 0; q < t.rows.size(); ++q) roff[q + 1] = roff[q] + S.bdim_new[t.rows[q]];
+    std::vector<int>& f = env[s];
+    f.assign(ns + roff.back(), 1 << 30);
+    auto setb = [&](int bi, int cb) {  // block row bi of the front gets column cb
+      int r0, d = S.bdim_new[bi];
+      if (bi < t.b1) r0 = S.boffset_new[bi] - c0;
+      else r0 = ns + roff[std::lower_bound(t.rows.begin(), t.rows.end(), bi) - t.rows.begin()];
+      for (int r = r0; r < r0 + d; ++r) f[r] = std::min(f[r], cb);
+    };
+    for (int b = t.b0; b < t.b1; ++b) {
+      const int cb = S.boffset_new[b] - c0;
+      setb(b, cb);
+      for (int i : st[b]) setb(i, cb);
+    }
+  }
+  std::vector<std::vector<int>>().swap(st);
   S.block_sn.assign(nb, -1);
   for (int s = 0; s < ns_count; ++s)
     for (int j = sns[s].b0; j < sns[s].b1; ++j) S.block_sn[j] = s;
@@ -480,11 +548,26 @@ Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, in
     q.vec_off = voff;
     voff += m;
     S.max_front = std::max<int>(S.max_front, (int)m);
-    for (int k = 0; k < q.ns; ++k) {
-      const double r = (double)(m - k - 1);
-      S.flops += 1 + r + r * (r + 1);  // sqrt, column scale, rank-1 update of the lower trailing part
+    if (!env[s].empty()) {
+      // band supernode: column k's entries below the diagonal are the rows whose envelope starts at or before k
+      q.env_off = (int64_t)S.fnz.size();
+      S.fnz.insert(S.fnz.end(), env[s].begin(), env[s].end());
+      std::vector<int> hist(q.ns + 1, 0);
+      for (int f : env[s]) hist[std::min(f, q.ns)]++;
+      int le = 0;
+      for (int k = 0; k < q.ns; ++k) {
+        le += hist[k];
+        const double r = (double)(le - (k + 1));
+        S.flops += 1 + r + r * (r + 1);
+        S.nnzL += 1 + r;
+      }
+    } else {
+      for (int k = 0; k < q.ns; ++k) {
+        const double r = (double)(m - k - 1);
+        S.flops += 1 + r + r * (r + 1);  // sqrt, column scale, rank-1 update of the lower trailing part
+      }
+      S.nnzL += (double)q.ns * (q.ns + 1) / 2 + (double)q.ns * q.nr;
     }
-    S.nnzL += (double)q.ns * (q.ns + 1) / 2 + (double)q.ns * q.nr;
   }
   S.front_pool = foff;
   S.vec_pool = voff;

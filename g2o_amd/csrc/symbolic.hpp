@@ -29,6 +29,10 @@ struct Supernode {
   int64_t rows_off;  // offset into row index list (length nr): scalar rows (permuted numbering)
   int64_t rel_off;   // offset into relmap (length nr): position of each row in the parent front
   int64_t vec_off;   // offset into the front-vector pool (length m)
+  // band supernode (a band leaf of the ordering, amalgamated whole): env_off >= 0 indexes Symbolic::fnz, the first own
+  // column (front-relative) of each of the m front rows with a structural nonzero in L — the row's envelope. Entries of
+  // L outside every row's envelope are zero, so the factor skips the tiles that lie entirely outside it.
+  int64_t env_off = -1;
 };
 
 struct Symbolic {
@@ -52,12 +56,18 @@ struct Symbolic {
   double nnzL = 0;                 // scalar nnz of L including the dense supernode fill
   int max_front = 0;
   int num_levels = 0;
+  std::vector<int> fnz;            // envelopes of the band supernodes (see Supernode::env_off)
+  int band_leaf = 0;               // ordering parameter that produced this analysis (0: plain nested dissection)
 };
 
 // Nested-dissection ordering of the block graph. leaf_size: subgraphs at most this
 // large are ordered by minimum degree; refine: greedy separator refinement after each bisection.
+// band_leaf > 0: parts of at most band_leaf blocks whose BFS level structure is a long band (at least 3 levels deep)
+// become band leaves — ordered by BFS level from a pseudo-peripheral end (the reference's cs_amd order on a band is
+// this sequential order too), their group ids (per block, -1 elsewhere) written to *groups; the analysis amalgamates
+// each group into one band supernode whose structural zeros the factor skips.
 std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size = 48, bool refine = false, bool windows = false,
-                                   bool part_degree = false);
+                                   bool part_degree = false, int band_leaf = 0, std::vector<int>* groups = nullptr);
 
 // Modelled GPU factor time of a symbolic analysis (seconds): flops at the MFMA rate plus the
 // level-synchronous panel-step chain.
@@ -65,6 +75,9 @@ double gpu_cost(const Symbolic& S);
 
 // Full symbolic analysis with a given block ordering (bperm: new->old). If bperm is
 // empty, nested dissection is used (with or without separator refinement, whichever models faster).
-Symbolic analyze(const BlockPattern& P, std::vector<int> bperm = {}, double relax = 0.25, int relax_max_blocks = 64);
+// groups (per original block, optional): blocks of one group >= 0 that are consecutive in the order and chained in the
+// elimination tree are amalgamated into one band supernode regardless of the relaxation limits.
+Symbolic analyze(const BlockPattern& P, std::vector<int> bperm = {}, double relax = 0.25, int relax_max_blocks = 64,
+                 const std::vector<int>* groups = nullptr);
 
 }  // namespace g2ohip

@@ -17,7 +17,7 @@ case $STAGE in
 test)
   timeout -k 10 300 python -u tools/parity_probe.py > $O/${TAG}_probe.log 2>&1 || { echo PROBE_FAIL; tail -20 $O/${TAG}_probe.log; exit 1; }
   echo PROBE_OK
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread > $O/${TAG}_pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 $O/${TAG}_pytest_gpu.log; exit 1; }
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/${TAG}_pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 $O/${TAG}_pytest_gpu.log; exit 1; }
   echo PYTEST_OK
   tail -3 $O/${TAG}_pytest_gpu.log
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $O/${TAG}_smoke.log; exit 1; }

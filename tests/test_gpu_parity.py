@@ -343,6 +343,11 @@ SCHEDULES = {
     "lagged_all_levels": {"G2OHIP_CHOL_LAG": "2"},
     "blocked_separate_contrib": {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64",
                                  "G2OHIP_CHOL_WIDE_PB": "64"},
+    # band leaves forced small: sequentially ordered leaf parts amalgamated into band supernodes whose structural-zero
+    # tiles the steps, the trailing updates and the contribution passes skip
+    "band_leaves": {"G2OHIP_BAND_LEAF": "24"},
+    "band_leaves_blocked": {"G2OHIP_BAND_LEAF": "24", "G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64",
+                            "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
 }
 
 

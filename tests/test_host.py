@@ -112,6 +112,36 @@ def test_symbolic_covers_factor_pattern(g2o_amd_mod, name):
     assert st["flops"] > 0 and st["supernodes"] >= 1 and st["levels"] >= 1
 
 
+@pytest.mark.parametrize("leaf", [8, 16, 32])
+def test_symbolic_band_leaves(g2o_amd_mod, monkeypatch, leaf):
+    """Band leaves (G2OHIP_BAND_LEAF forces the hybrid ordering: dissection down to parts of `leaf` blocks, each ordered
+    sequentially and amalgamated into one band supernode): a valid block permutation, and the envelope counts the
+    factor relies on (its structural-zero tiles are skipped) bound the true nonzeros of L. Fewer flops than the
+    dense fronts of the same tree would do."""
+    prob = synth.ba(num_cameras=160, num_points=6000, obs_per_point=6, window=12)
+    bd = prob.pose_dim
+    nb, bi, bj = _schur_pattern(prob)
+    monkeypatch.setenv("G2OHIP_BAND_LEAF", str(leaf))
+    perm, st = g2o_amd_mod.symbolic_analyze(nb, bd, bi, bj)
+    n = nb * bd
+    assert sorted(perm.tolist()) == list(range(n))
+    blocks = perm.reshape(nb, bd)
+    assert np.all(blocks % bd == np.arange(bd)) and np.all(blocks // bd == (blocks[:, :1] // bd))
+    rng = np.random.default_rng(2)
+    A = np.zeros((n, n))
+    for a, b in zip(bi, bj):
+        B = rng.standard_normal((bd, bd)) * 0.1
+        A[a * bd:(a + 1) * bd, b * bd:(b + 1) * bd] += B
+        if a != b:
+            A[b * bd:(b + 1) * bd, a * bd:(a + 1) * bd] += B.T
+    A = A + A.T + n * np.eye(n)
+    L = np.linalg.cholesky(A[np.ix_(perm, perm)])
+    assert np.count_nonzero(np.abs(L) > 1e-300) <= st["nnzL"]
+    monkeypatch.setenv("G2OHIP_BAND_LEAF", "0")
+    _, st0 = g2o_amd_mod.symbolic_analyze(nb, bd, bi, bj)
+    assert st["supernodes"] < st0["supernodes"] or st["flops"] <= st0["flops"], (st, st0)
+
+
 def test_symbolic_disconnected_and_trivial(g2o_amd_mod):
     # three disconnected cliques + isolated blocks
     bi, bj = [], []
@@ -129,7 +159,7 @@ def test_symbolic_disconnected_and_trivial(g2o_amd_mod):
     assert perm1.tolist() == list(range(6)) and st1["supernodes"] == 1
 
 
-def test_symbolic_band_windows(g2o_amd_mod):
+def test_symbolic_band_windows(g2o_amd_mod, monkeypatch):
     """C4's reduced camera system is a band (cameras within a 64-camera window share points): 998 camera blocks
     of dimension 6, half-bandwidth 63 blocks — a path of 15.8 bandwidths. Level separators from a path's end cut
     only at multiples of the bandwidth (5 levels of 12 panel steps); the window separators at the exact middles
@@ -138,6 +168,7 @@ def test_symbolic_band_windows(g2o_amd_mod):
     nb, w = 998, 63
     bi = [i for i in range(nb) for j in range(i, min(nb, i + w + 1))]
     bj = [j for i in range(nb) for j in range(i, min(nb, i + w + 1))]
+    monkeypatch.setenv("G2OHIP_BAND_LEAF", "0")  # the dissection itself (band leaves are a separate candidate)
     perm, st = g2o_amd_mod.symbolic_analyze(nb, 6, bi, bj)
     assert sorted(perm.tolist()) == list(range(nb * 6))
     assert st["panel_steps"] <= 50, st

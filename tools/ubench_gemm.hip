@@ -105,6 +105,34 @@ __global__ void __launch_bounds__(64 * WM * WN, OCC) k_tri(const int* tiles, con
   GemmNT<BM, BN, WM, WN, KC>::run(A, lda, C, m, m, m, ti * BM, tj * BN, 0, K, lds);
 }
 
+template <int BM, int BN, int WM, int WN, int OCC, int KC, int NS>
+__global__ void __launch_bounds__(64 * WM * WN, OCC) k_tri_d(const int* tiles, const double* A, int lda, double* C, int m, int K) {
+  extern __shared__ double lds[];
+  const int t = tiles[blockIdx.x];
+  const int ti = t & 0xffff, tj = t >> 16;
+  GemmNTd<BM, BN, WM, WN, KC, NS>::run(A, lda, C, m, m, m, ti * BM, tj * BN, 0, K, lds);
+}
+template <int BM, int BN, int WM = 2, int WN = 2, int OCC = 2, int KC = 16, int NS = 3>
+double run_d(const double* dA, double* dC, int m, int K, int reps, double* flops_out) {
+  std::vector<int> tl;
+  for (int tj = 0; tj * BN < m; ++tj)
+    for (int ti = 0; ti * BM < m; ++ti)
+      if (ti * BM + BM > tj * BN) tl.push_back(ti | (tj << 16));
+  int* dt; CK(hipMalloc(&dt, tl.size() * 4)); CK(hipMemcpy(dt, tl.data(), tl.size() * 4, hipMemcpyHostToDevice));
+  const size_t lds = GemmNTd<BM, BN, WM, WN, KC, NS>::LDS_DOUBLES * 8;
+  const int nt = 64 * WM * WN;
+  CK(hipFuncSetAttribute((const void*)k_tri_d<BM, BN, WM, WN, OCC, KC, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  k_tri_d<BM, BN, WM, WN, OCC, KC, NS><<<(unsigned)tl.size(), nt, lds, 0>>>(dt, dA, m, dC, m, K);
+  CK(hipEventRecord(a));
+  for (int r = 0; r < reps; ++r) k_tri_d<BM, BN, WM, WN, OCC, KC, NS><<<(unsigned)tl.size(), nt, lds, 0>>>(dt, dA, m, dC, m, K);
+  CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+  float ms; CK(hipEventElapsedTime(&ms, a, b));
+  *flops_out = (double)m * (m + 1) * K;
+  CK(hipFree(dt));
+  return ms / reps;
+}
+
 template <int BM, int BN, int WM = 2, int WN = 2, int OCC = 1, int KC = 16, int XCD = 0>
 double run(const double* dA, double* dC, int m, int K, int reps, double* flops_out) {
   std::vector<int> tl;
@@ -223,7 +251,7 @@ int main(int argc, char** argv) {
   srand(1);
   for (auto& x : hA) x = rand() / (double)RAND_MAX - 0.5;
   double *dA, *dC, *dC2;
-  CK(hipMalloc(&dA, hA.size() * 8)); CK(hipMalloc(&dC, (size_t)m * m * 8)); CK(hipMalloc(&dC2, (size_t)m * m * 8));
+  CK(hipMalloc(&dA, hA.size() * 8 + 64)); CK(hipMalloc(&dC, (size_t)m * m * 8)); CK(hipMalloc(&dC2, (size_t)m * m * 8));
   CK(hipMemcpy(dA, hA.data(), hA.size() * 8, hipMemcpyHostToDevice));
   double fl;
   auto report = [&](const char* name, double ms) { printf("m %d K %d %-12s %8.3f ms  %6.2f TF/s\n", m, K, name, ms, fl / ms * 1e-9); };
@@ -266,6 +294,35 @@ int main(int argc, char** argv) {
     }
     printf("check v: max rel err %.3e, upper entries touched %d\n", maxerr, bad_upper);
   }
+  auto check = [&](const char* name, auto runner) {  // C = 0 - A A^T after one launch, sampled against the host
+    CK(hipMemset(dC, 0, (size_t)m * m * 8));
+    double f0; runner(0, &f0);
+    CK(hipDeviceSynchronize());
+    std::vector<double> hC((size_t)m * m);
+    CK(hipMemcpy(hC.data(), dC, hC.size() * 8, hipMemcpyDeviceToHost));
+    double maxerr = 0; int bad_upper = 0;
+    for (int s2 = 0; s2 < 3000; ++s2) {
+      int i = rand() % m, j = rand() % m;
+      if (s2 < 64) { i = m - 1 - (s2 & 7); j = m - 1 - (s2 >> 3); }  // the ragged corner
+      double ref = 0; for (int k = 0; k < K; ++k) ref -= hA[(size_t)k * m + i] * hA[(size_t)k * m + j];
+      double g = hC[(size_t)j * m + i];
+      if (i >= j) maxerr = std::max(maxerr, std::fabs(g - ref) / (1 + std::fabs(ref)));
+      else if (g != 0.0) bad_upper++;
+    }
+    printf("check %s: max rel err %.3e, upper entries touched %d\n", name, maxerr, bad_upper);
+  };
+  check("d64", [&](int r, double* f) { return run_d<64, 64>(dA, dC, m, K, r, f); });
+  check("d128x64", [&](int r, double* f) { return run_d<128, 64, 4, 2, 1>(dA, dC, m, K, r, f); });
+  check("d128", [&](int r, double* f) { return run_d<128, 128, 4, 2, 1>(dA, dC, m, K, r, f); });
+  report("d64x64o2", run_d<64, 64, 2, 2, 2>(dA, dC, m, K, reps, &fl));
+  report("d64x64o3", run_d<64, 64, 2, 2, 3>(dA, dC, m, K, reps, &fl));
+  report("d64x64s4", run_d<64, 64, 2, 2, 2, 16, 4>(dA, dC, m, K, reps, &fl));
+  report("d64x64k32s2", run_d<64, 64, 2, 2, 2, 32, 2>(dA, dC, m, K, reps, &fl));
+  report("d64x64k32s3", run_d<64, 64, 2, 2, 1, 32, 3>(dA, dC, m, K, reps, &fl));
+  report("d128x64w8", run_d<128, 64, 4, 2, 1>(dA, dC, m, K, reps, &fl));
+  report("d128x64w4", run_d<128, 64, 2, 2, 1>(dA, dC, m, K, reps, &fl));
+  report("d128x128w8", run_d<128, 128, 4, 2, 1>(dA, dC, m, K, reps, &fl));
+  report("d128x128w4", run_d<128, 128, 2, 2, 1>(dA, dC, m, K, reps, &fl));
   report("valu128", run_v(dA, dC, m, K, reps, &fl));
   report("128x128w4o2", run<128, 128, 2, 2, 2>(dA, dC, m, K, reps, &fl));
   report("128x128w8", run<128, 128, 4, 2, 1>(dA, dC, m, K, reps, &fl));

@@ -447,7 +447,8 @@ class SparseOptimizer:
                         "owned_fronts", "shared_fronts", "subtree_roots", "root_exchange_doubles",
                         "model_rank_subtrees_s", "model_shared_s", "model_single_gpu_s", "model_exchange_s",
                         "distributed", "reduce_scatter", "rs_segment_doubles", "rs_tail_doubles", "model_input_s",
-                        "model_input_allreduce_s", None)  # None: retired slots (always 0), kept for the ABI layout
+                        "model_input_allreduce_s", None,  # None: retired slots (always 0), kept for the ABI layout
+                        "band_leaf")
 
     def factor_info(self) -> dict:
         out = np.zeros(len(self.FACTOR_INFO_KEYS))

@@ -3131,7 +3131,7 @@ int Engine::factor_info(double* out, int n) {
                       (double)chol.n_roots, (double)chol.xch_len, chol.dist_model[0], chol.dist_model[1],
                       chol.dist_model[2], chol.dist_model[3], chol.dist_model[4], chol.rs_on ? 1.0 : 0.0,
                       (double)chol.rs_seg, (double)chol.rs_tail_len, chol.rs_model[0], chol.rs_model[1],
-                      0.0 /* retired: 64-column-step levels */};
+                      0.0 /* retired: 64-column-step levels */, (double)S.band_leaf};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;

@@ -354,8 +354,12 @@ Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, in
     // band leaves (hybrid ordering): the kept variant's dissection down to parts of at most `bl` blocks, each such
     // part that is a long band ordered sequentially and factored as one band supernode — the reference's own
     // sequential order inside the leaves (fewer flops) for a chain no longer than the dissection levels it replaces
-    const char* eb = getenv("G2OHIP_BAND_LEAF");  // dev A/B: 0 off, N force leaves of N blocks
-    const int force_bl = eb ? atoi(eb) : -1;
+    // Off unless G2OHIP_BAND_LEAF is set (N: force leaves of N blocks, -1: let the cost model choose): measured at C5
+    // (r04b, profiles/r04b_c5_bandleaf_factor_levels.txt) the 256-block band leaves cut the flops 18.9 -> 14.2 GFLOP
+    // but their level took 1.21 ms against ~0.7 for the three dissection levels they replace (every panel of a band
+    // leaf updates its whole border rows, 41 rank-32 passes instead of 12): factor 1.84 -> 1.93 ms
+    const char* eb = getenv("G2OHIP_BAND_LEAF");
+    const int force_bl = eb ? atoi(eb) : 0;
     if (force_bl != 0) {
       const bool* v = bv >= 0 ? var[bv] : nullptr;
       for (int bl : {96, 128, 192, 256, 384}) {

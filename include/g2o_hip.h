@@ -186,8 +186,9 @@ int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel);
  * the replicated factorization, of the cut's two all-reduces) and whether the factorization is distributed (1) or
  * replicated (0: the model preferred replication, or G2OHIP_DIST_FACTOR=0); then out[21..25] = whether the reduced
  * system is reduce-scattered by subtree ownership (1) instead of all-reduced, its per-rank segment and all-reduced tail
- * (doubles), and the modelled seconds of that input exchange and of the plain all-reduce; out[26] = 0 (retired slot).
- * Returns the number of entries available. */
+ * (doubles), and the modelled seconds of that input exchange and of the plain all-reduce; out[26] = 0 (retired slot);
+ * out[27] = the band-leaf size of the ordering (blocks; 0: plain nested dissection). Returns the number of entries
+ * available. */
 int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n);
 /* Solver::computeMarginals (core/solver.h:108; BlockSolver::computeMarginals block_solver.hpp:451-460 ->
  * LinearSolverCSparse::solvePattern linear_solver_csparse.h:190-225, MarginalCovarianceCholesky): the pose-block

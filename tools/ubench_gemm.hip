@@ -317,6 +317,8 @@ int main(int argc, char** argv) {
   report("d64x64o2", run_d<64, 64, 2, 2, 2>(dA, dC, m, K, reps, &fl));
   report("d64x64o3", run_d<64, 64, 2, 2, 3>(dA, dC, m, K, reps, &fl));
   report("d64x64s4", run_d<64, 64, 2, 2, 2, 16, 4>(dA, dC, m, K, reps, &fl));
+  report("d64x64k8s3o4", run_d<64, 64, 2, 2, 4, 8, 3>(dA, dC, m, K, reps, &fl));
+  report("d64x64k8s4o3", run_d<64, 64, 2, 2, 3, 8, 4>(dA, dC, m, K, reps, &fl));
   report("d64x64k32s2", run_d<64, 64, 2, 2, 2, 32, 2>(dA, dC, m, K, reps, &fl));
   report("d64x64k32s3", run_d<64, 64, 2, 2, 1, 32, 3>(dA, dC, m, K, reps, &fl));
   report("d128x64w8", run_d<128, 64, 4, 2, 1>(dA, dC, m, K, reps, &fl));

@@ -844,10 +844,11 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
 // double-buffered 16-column LDS chunks). Task: s, b = ti | tj << 16, K = [a, c) (c = 0: [0, ns)).
 // The same kernel is the trailing update of a blocked front after each big panel: rows >= kb, columns
 // [kb, ns), K = the big panel's columns [ka, kb) of the finished factor.
-using SyrkTile = GemmNT<TT, TT>;
+// Tile: GemmNT (register-staged double buffer) or GemmNTd (LDS-DMA ring, G2OHIP_SYRK_DMA)
+template <class SyrkTile>
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                               double* __restrict__ fronts, const double* __restrict__ lbuf) {
-  __shared__ double sh[SyrkTile::LDS_DOUBLES];
+  __shared__ __attribute__((aligned(16))) double sh[SyrkTile::LDS_DOUBLES];
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, ns = me.ns;
@@ -1060,7 +1061,17 @@ void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* 
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_syrk, ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
+  // the LDS-DMA tile with two 32-column stages: 47.9 against 41.2 TF/s (register-staged GemmNT) on a 4096^2 SYRK at
+  // K = 2048, 19.7 against 13.7 at 1152^2, K = 384 (tools/ubench_gemm.hip, profiles/r04_ubench_gemm.log);
+  // G2OHIP_SYRK_DMA=0 keeps the register-staged tile (A/B)
+  static const int dma = [] {
+    const char* e = getenv("G2OHIP_SYRK_DMA");
+    return e ? atoi(e) : 1;
+  }();
+  if (dma)
+    hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 32, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
+  else
+    hipLaunchKernelGGL((k_syrk<GemmNT<TT, TT>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
   KERNEL_CHECK();
 }
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s) {

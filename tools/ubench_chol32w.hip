@@ -1,0 +1,188 @@
+// Dev micro-benchmark: the 32x32 diagonal factor split over the four waves of a workgroup (wave w owns columns
+// 8w .. 8w+7 of every row, lanes 32..63 the identity rows whose elimination leaves L^-1), against the one-wave chol32
+// of cholesky.hip (restated here). s_memtime cycles from the first load to the last wave's finish; L^-1 checked
+// against a host factorization. Not product code.
+//   hipcc -O3 --offload-arch=gfx950 tools/ubench_chol32w.hip -o tools/ubench_chol32w
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+constexpr int NB = 32, DS = NB + 1;
+
+__device__ __forceinline__ double rlane(double v, int l) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double rsq_nr(double d) {
+  const double r0 = __builtin_amdgcn_rsq(d);
+  const double t1 = 0.5 * d * r0;
+  return r0 * __builtin_fma(-r0, t1, 1.5);
+}
+
+// ---- one wave, right-looking, no look-ahead (reference shape: row per lane)
+__device__ bool chol32_1w(double (&row)[NB], int lane, double* col) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const double d = rlane(row[j], j);
+    ok &= d > 0.0;
+    const double r = rsq_nr(d);
+    row[j] *= r;
+    col[j * 64 + lane] = row[j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int c = j + 1; c < NB; ++c) row[c] -= row[j] * col[j * 64 + c];
+  }
+  return ok;
+}
+
+// ---- four waves: wave w owns columns 8w .. 8w+7. ready: number of finished columns (LDS), col: 32 x 64 column buffer
+template <int W>
+__device__ __forceinline__ bool chol32_w4_wave(double (&row)[8], int lane, double* col, volatile int* ready) {
+  bool ok = true;
+  // updates from the columns of the earlier waves, as they are published
+  for (int j = 0; j < 8 * W; ++j) {
+    if (j % 8 == 0 || true) {
+      while (ready[0] <= j) __builtin_amdgcn_s_sleep(0);
+    }
+    const double lij = col[j * 64 + lane];
+    double lc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) lc[k] = col[j * 64 + 8 * W + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row[k] -= lij * lc[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int j = 8 * W + k;
+    const double d = rlane(row[k], j);
+    ok &= d > 0.0;
+    const double r = rsq_nr(d);
+    row[k] *= r;
+    col[j * 64 + lane] = row[k];
+    if (k + 1 < 8) row[k + 1] -= row[k] * rlane(row[k], j + 1);  // the next pivot's column first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) ready[0] = j + 1;
+#pragma unroll
+    for (int kk = k + 2; kk < 8; ++kk) row[kk] -= row[k] * col[j * 64 + 8 * W + kk];
+  }
+  return ok;
+}
+
+__global__ void __launch_bounds__(256) k_w4(const double* A, double* out, unsigned long long* cyc, int reps) {
+  __shared__ double D[NB * DS];
+  __shared__ __attribute__((aligned(16))) double col[NB * 64];
+  __shared__ int ready;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  unsigned long long t0 = 0, t1 = 0;
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int e = tid; e < NB * NB; e += 256) D[(e >> 5) * DS + (e & 31)] = A[e];
+    if (tid == 0) ready = 0;
+    __syncthreads();
+    if (rep == reps - 1) t0 = __builtin_amdgcn_s_memtime();
+    double row[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = 8 * w + k;
+      row[k] = lane < NB ? (c <= lane ? D[lane * DS + c] : 0.0) : (lane - NB == c ? 1.0 : 0.0);
+    }
+    bool ok;
+    switch (__builtin_amdgcn_readfirstlane(w)) {
+      case 0: ok = chol32_w4_wave<0>(row, lane, col, &ready); break;
+      case 1: ok = chol32_w4_wave<1>(row, lane, col, &ready); break;
+      case 2: ok = chol32_w4_wave<2>(row, lane, col, &ready); break;
+      default: ok = chol32_w4_wave<3>(row, lane, col, &ready); break;
+    }
+    // L^-1 transposed into D as factor_block leaves it: D[c * DS + i] = L^-1(i, c)
+    if (lane >= NB)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) D[(lane - NB) * DS + 8 * w + k] = row[k];
+    (void)ok;
+    __syncthreads();
+    if (rep == reps - 1) t1 = __builtin_amdgcn_s_memtime();
+  }
+  for (int e = tid; e < NB * NB; e += 256) out[e] = D[(e & 31) * DS + (e >> 5)];  // out[i * 32 + c] = L^-1(i, c)
+  if (tid == 0) cyc[0] = t1 - t0;
+}
+
+__global__ void __launch_bounds__(256) k_1w(const double* A, double* out, unsigned long long* cyc, int reps) {
+  __shared__ double D[NB * DS];
+  __shared__ __attribute__((aligned(16))) double col[NB * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  unsigned long long t0 = 0, t1 = 0;
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int e = tid; e < NB * NB; e += 256) D[(e >> 5) * DS + (e & 31)] = A[e];
+    __syncthreads();
+    if (rep == reps - 1) t0 = __builtin_amdgcn_s_memtime();
+    if (tid < 64) {
+      double row[NB];
+#pragma unroll
+      for (int c = 0; c < NB; ++c) row[c] = lane < NB ? (c <= lane ? D[lane * DS + c] : 0.0) : (lane - NB == c ? 1.0 : 0.0);
+      chol32_1w(row, lane, col);
+      if (lane >= NB)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) D[(lane - NB) * DS + i] = row[i];
+    }
+    __syncthreads();
+    if (rep == reps - 1) t1 = __builtin_amdgcn_s_memtime();
+  }
+  for (int e = tid; e < NB * NB; e += 256) out[e] = D[(e & 31) * DS + (e >> 5)];
+  if (tid == 0) cyc[0] = t1 - t0;
+}
+
+int main() {
+  // SPD test block
+  std::vector<double> A(NB * NB), L(NB * NB, 0.0), Li(NB * NB, 0.0);
+  srand(3);
+  std::vector<double> B(NB * NB);
+  for (auto& x : B) x = rand() / (double)RAND_MAX - 0.5;
+  for (int i = 0; i < NB; ++i)
+    for (int j = 0; j < NB; ++j) {
+      double s = i == j ? NB : 0.0;
+      for (int k = 0; k < NB; ++k) s += B[i * NB + k] * B[j * NB + k];
+      A[i * NB + j] = s;
+    }
+  for (int j = 0; j < NB; ++j) {  // host Cholesky and inverse
+    double s = A[j * NB + j];
+    for (int k = 0; k < j; ++k) s -= L[j * NB + k] * L[j * NB + k];
+    L[j * NB + j] = std::sqrt(s);
+    for (int i = j + 1; i < NB; ++i) {
+      double t = A[i * NB + j];
+      for (int k = 0; k < j; ++k) t -= L[i * NB + k] * L[j * NB + k];
+      L[i * NB + j] = t / L[j * NB + j];
+    }
+  }
+  for (int c = 0; c < NB; ++c)
+    for (int i = 0; i < NB; ++i) {
+      double t = i == c ? 1.0 : 0.0;
+      for (int k = 0; k < i; ++k) t -= L[i * NB + k] * Li[k * NB + c];
+      Li[i * NB + c] = t / L[i * NB + i];
+    }
+  double *dA, *dO;
+  unsigned long long* dc;
+  CK(hipMalloc(&dA, NB * NB * 8)); CK(hipMalloc(&dO, NB * NB * 8)); CK(hipMalloc(&dc, 8));
+  CK(hipMemcpy(dA, A.data(), NB * NB * 8, hipMemcpyHostToDevice));
+  auto run = [&](const char* name, auto kern) -> int {
+    unsigned long long best = ~0ull;
+    for (int t = 0; t < 20; ++t) {
+      hipLaunchKernelGGL(kern, 1, 256, 0, 0, dA, dO, dc, 3);
+      CK(hipDeviceSynchronize());
+      unsigned long long c;
+      CK(hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost));
+      best = std::min(best, c);
+    }
+    std::vector<double> o(NB * NB);
+    CK(hipMemcpy(o.data(), dO, NB * NB * 8, hipMemcpyDeviceToHost));
+    double md = 0;
+    for (int i = 0; i < NB; ++i)
+      for (int c = 0; c <= i; ++c) md = std::max(md, std::fabs(o[i * NB + c] - Li[i * NB + c]) / (1e-12 + std::fabs(Li[i * NB + c]) + 1.0));
+    printf("%-24s %7llu cycles (memtime units)  max rel diff of L^-1 vs host %.2e\n", name, best, md);
+    return 0;
+  };
+  run("one wave, right-looking", k_1w);
+  run("four waves, 8 columns each", k_w4);
+  return 0;
+}

@@ -39,6 +39,150 @@ __device__ bool chol32_1w(double (&row)[NB], int lane, double* col) {
   return ok;
 }
 
+// ---- the product's one-wave chol32 (cholesky.hip), restated verbatim for the comparison
+#define CHOL_SB() __builtin_amdgcn_sched_barrier(0)
+constexpr int C32_NCH = 3;  // chunks of the deferred update per column
+struct C32State {
+  double dn, a1, b1, c2, lp;  // next pivot; A(j+1,j+1), A(j+1,j), A(j+2,j); column j-1's own entry
+  double2 cc[NB / 2];         // column j-1 (entries >= j+2) from LDS
+  bool ok;
+};
+template <int J, int K>
+__device__ __forceinline__ void c32_fill(double (&row)[NB], const C32State& st) {
+  constexpr int c0 = (J + 2) & ~1;
+  constexpr int nf = J >= 1 ? (NB - c0) / 2 : 0;
+  constexpr int qa = nf * K / C32_NCH, qb = nf * (K + 1) / C32_NCH;
+#pragma unroll
+  for (int q = qa; q < qb; ++q) {
+    const int c = c0 + 2 * q;
+    if (c > J + 1) row[c] -= st.lp * st.cc[c >> 1].x;
+    row[c + 1] -= st.lp * st.cc[c >> 1].y;
+  }
+}
+template <int J>
+__device__ __forceinline__ void c32_step(double (&row)[NB], int lane, double* col, C32State& st) {
+  if constexpr (J < NB) {
+    const double d = st.dn;
+    st.ok &= d > 0.0;
+    const double r0 = __builtin_amdgcn_rsq(d);  // ~5e-8 relative; one Newton step -> ~4e-15
+    const double hd = 0.5 * d;
+    CHOL_SB();
+    c32_fill<J, 0>(row, st);
+    CHOL_SB();
+    const double t1 = hd * r0;
+    CHOL_SB();
+    c32_fill<J, 1>(row, st);
+    CHOL_SB();
+    const double t2 = __builtin_fma(-r0, t1, 1.5);
+    CHOL_SB();
+    c32_fill<J, 2>(row, st);
+    CHOL_SB();
+    const double r = r0 * t2;
+    const double l1 = st.b1 * r, l2 = st.c2 * r;  // l_{j+1,j}, l_{j+2,j}
+    if constexpr (J + 1 < NB) st.dn = __builtin_fma(-l1, l1, st.a1);
+    CHOL_SB();
+    // column j of L (or of L^-1 e_c in lanes >= 32); lane j's own row[j] is the pivot d
+    const double lj = row[J] * r;
+    row[J] = lj;
+    if constexpr (J + 1 < NB) {
+      row[J + 1] -= lj * l1;
+      col[(J & 1) * 2 * NB + lane] = lj;  // every lane writes (lanes >= 32 into the unused half)
+    }
+    if constexpr (J + 2 < NB) row[J + 2] -= lj * l2;
+    CHOL_SB();
+    if constexpr (J + 1 < NB) {  // column j for the next column's deferred update (entries >= j+3)
+      constexpr int n0 = (J + 3) & ~1;
+      const double* cb = col + (J & 1) * 2 * NB;
+#pragma unroll
+      for (int c = n0; c < NB; c += 2) st.cc[c >> 1] = *reinterpret_cast<const double2*>(cb + c);
+      st.lp = lj;
+    }
+    // pivot inputs of column j+2's step (rows j+1, j+2 hold every update of columns <= j now)
+    if constexpr (J + 2 < NB) { st.a1 = rlane(row[J + 2], J + 2); st.b1 = rlane(row[J + 1], J + 2); }
+    if constexpr (J + 3 < NB) st.c2 = rlane(row[J + 1], J + 3);
+    CHOL_SB();
+    c32_step<J + 1>(row, lane, col, st);
+  }
+}
+__device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col) {
+  C32State st;
+  st.ok = true;
+  st.lp = 0.0;
+  st.dn = rlane(row[0], 0);
+  st.a1 = rlane(row[1], 1);
+  st.b1 = rlane(row[0], 1);
+  st.c2 = rlane(row[0], 2);
+  c32_step<0>(row, lane, col, st);
+  return st.ok;
+}
+
+
+// ---- four waves with the product's scheduling idea inside each wave: column k's chain (rsq, Newton) with the deferred
+// update of column k-1 (columns >= k+1 of this wave, broadcast values read from LDS one column early) cut into chunks
+// between its dependent steps; the next column's own entry updated right after the scaling (critical)
+template <int W, int K>
+__device__ __forceinline__ void w4_defer(double (&row)[8], double lp, const double (&lc)[8], int q, int nq) {
+  // deferred update of column 8W + K - 1 applied to this wave's columns K + 1 .. 7, chunk q of nq
+  constexpr int c0 = K + 1;
+  constexpr int n = 8 - c0 > 0 ? 8 - c0 : 0;
+#pragma unroll
+  for (int t = 0; t < n; ++t)
+    if (t * nq / (n > 0 ? n : 1) == q || (n < nq && t == q)) row[c0 + t] -= lp * lc[c0 + t];
+}
+template <int W>
+__device__ __forceinline__ bool chol32_w4b_wave(double (&row)[8], int lane, double* col, volatile int* ready) {
+  bool ok = true;
+  for (int j = 0; j < 8 * W; ++j) {
+    while (ready[0] <= j) __builtin_amdgcn_s_sleep(1);
+    const double lij = col[j * 64 + lane];
+    double lc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) lc[k] = col[j * 64 + 8 * W + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row[k] -= lij * lc[k];
+  }
+  double lp = 0.0, lc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) lc[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int j = 8 * W + k;
+    const double d = rlane(row[k], j);
+    ok &= d > 0.0;
+    const double r0 = __builtin_amdgcn_rsq(d);
+    const double hd = 0.5 * d;
+    CHOL_SB();
+    if (k >= 1) {  // deferred: column j-1 into columns k+1.. (row[k] got it at step k-1)
+#pragma unroll
+      for (int c = k + 1; c < 8; c += 2) row[c] -= lp * lc[c];
+    }
+    CHOL_SB();
+    const double t1 = hd * r0;
+    CHOL_SB();
+    if (k >= 1) {
+#pragma unroll
+      for (int c = k + 2; c < 8; c += 2) row[c] -= lp * lc[c];
+    }
+    CHOL_SB();
+    const double t2 = __builtin_fma(-r0, t1, 1.5);
+    const double r = r0 * t2;
+    row[k] *= r;
+    col[j * 64 + lane] = row[k];
+    if (k + 1 < 8) row[k + 1] -= row[k] * rlane(row[k], j + 1);  // the next pivot's column first
+    CHOL_SB();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) ready[0] = j + 1;
+    lp = row[k];
+#pragma unroll
+    for (int c = k + 2; c < 8; ++c) lc[c] = col[j * 64 + 8 * W + c];  // lands while the next chain runs
+  }
+  return ok;
+}
+template <int W>
+__device__ __forceinline__ bool w4b_dispatch(double (&row)[8], int lane, double* col, volatile int* ready) {
+  return chol32_w4b_wave<W>(row, lane, col, ready);
+}
+
 // ---- four waves: wave w owns columns 8w .. 8w+7. ready: number of finished columns (LDS), col: 32 x 64 column buffer
 template <int W>
 __device__ __forceinline__ bool chol32_w4_wave(double (&row)[8], int lane, double* col, volatile int* ready) {
@@ -133,6 +277,63 @@ __global__ void __launch_bounds__(256) k_1w(const double* A, double* out, unsign
   if (tid == 0) cyc[0] = t1 - t0;
 }
 
+__global__ void __launch_bounds__(256) k_prod(const double* A, double* out, unsigned long long* cyc, int reps) {
+  __shared__ double D[NB * DS];
+  __shared__ __attribute__((aligned(16))) double col[4 * NB];
+  const int tid = threadIdx.x, lane = tid & 63;
+  unsigned long long t0 = 0, t1 = 0;
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int e = tid; e < NB * NB; e += 256) D[(e >> 5) * DS + (e & 31)] = A[e];
+    __syncthreads();
+    if (rep == reps - 1) t0 = __builtin_amdgcn_s_memtime();
+    if (tid < 64) {
+      double row[NB];
+#pragma unroll
+      for (int c = 0; c < NB; ++c) row[c] = lane < NB ? (c <= lane ? D[lane * DS + c] : 0.0) : (lane - NB == c ? 1.0 : 0.0);
+      chol32(row, lane, col);
+      if (lane >= NB)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) D[(lane - NB) * DS + i] = row[i];
+    }
+    __syncthreads();
+    if (rep == reps - 1) t1 = __builtin_amdgcn_s_memtime();
+  }
+  for (int e = tid; e < NB * NB; e += 256) out[e] = D[(e & 31) * DS + (e >> 5)];
+  if (tid == 0) cyc[0] = t1 - t0;
+}
+__global__ void __launch_bounds__(256) k_w4b(const double* A, double* out, unsigned long long* cyc, int reps) {
+  __shared__ double D[NB * DS];
+  __shared__ __attribute__((aligned(16))) double col[NB * 64];
+  __shared__ int ready;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  unsigned long long t0 = 0, t1 = 0;
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int e = tid; e < NB * NB; e += 256) D[(e >> 5) * DS + (e & 31)] = A[e];
+    if (tid == 0) ready = 0;
+    __syncthreads();
+    if (rep == reps - 1) t0 = __builtin_amdgcn_s_memtime();
+    double row[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = 8 * w + k;
+      row[k] = lane < NB ? (c <= lane ? D[lane * DS + c] : 0.0) : (lane - NB == c ? 1.0 : 0.0);
+    }
+    switch (__builtin_amdgcn_readfirstlane(w)) {
+      case 0: w4b_dispatch<0>(row, lane, col, &ready); break;
+      case 1: w4b_dispatch<1>(row, lane, col, &ready); break;
+      case 2: w4b_dispatch<2>(row, lane, col, &ready); break;
+      default: w4b_dispatch<3>(row, lane, col, &ready); break;
+    }
+    if (lane >= NB)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) D[(lane - NB) * DS + 8 * w + k] = row[k];
+    __syncthreads();
+    if (rep == reps - 1) t1 = __builtin_amdgcn_s_memtime();
+  }
+  for (int e = tid; e < NB * NB; e += 256) out[e] = D[(e & 31) * DS + (e >> 5)];
+  if (tid == 0) cyc[0] = t1 - t0;
+}
+
 int main() {
   // SPD test block
   std::vector<double> A(NB * NB), L(NB * NB, 0.0), Li(NB * NB, 0.0);
@@ -184,5 +385,7 @@ int main() {
   };
   run("one wave, right-looking", k_1w);
   run("four waves, 8 columns each", k_w4);
+  run("product chol32 (one wave)", k_prod);
+  run("four waves, deferred chunks", k_w4b);
   return 0;
 }

@@ -1061,17 +1061,24 @@ void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* 
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
   if (ntasks <= 0) return;
-  // the LDS-DMA tile with two 32-column stages: 47.9 against 41.2 TF/s (register-staged GemmNT) on a 4096^2 SYRK at
-  // K = 2048, 19.7 against 13.7 at 1152^2, K = 384 (tools/ubench_gemm.hip, profiles/r04_ubench_gemm.log);
-  // G2OHIP_SYRK_DMA=0 keeps the register-staged tile (A/B)
+  // G2OHIP_SYRK_DMA=k (dev A/B): the LDS-DMA tile GemmNTd with (K chunk, stages) = (32, 2), (16, 3), (8, 4), (16, 2)
+  // for k = 1..4. Alone on one 4096^2 SYRK at K = 2048 the (32, 2) ring reaches 47.9 against 41.2 TF/s for the
+  // register-staged GemmNT (profiles/r04_ubench_gemm.log), but inside the C3 factorization (contribution passes and
+  // big-panel trailing updates of many sizes, next to other launches) it measured slower: factor 29.84 vs 29.18 ms
+  // (profiles/r04_ab_c3_syrk.log; 74 KB of LDS leave 2 workgroups per CU against 3). The (16, 2) ring (37 KB, four
+  // workgroups per CU) is the one that wins there: C3 factor 29.07 -> 28.54 ms (profiles/r04_ab_c3_knobs.log), the
+  // default; G2OHIP_SYRK_DMA=0 is the register-staged GemmNT.
   static const int dma = [] {
     const char* e = getenv("G2OHIP_SYRK_DMA");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 4;
   }();
-  if (dma)
-    hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 32, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
-  else
-    hipLaunchKernelGGL((k_syrk<GemmNT<TT, TT>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
+  switch (dma) {
+    case 1: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 32, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
+    case 2: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 16, 3>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
+    case 3: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 8, 4>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
+    case 4: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 16, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
+    default: hipLaunchKernelGGL((k_syrk<GemmNT<TT, TT>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
+  }
   KERNEL_CHECK();
 }
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s) {

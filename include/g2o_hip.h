@@ -279,7 +279,7 @@ double g2ohip_kernel_flops(g2ohip_graph* g, const char* name);
 int g2ohip_debug_phases(unsigned long long* out, int max_records);
 const char* g2ohip_last_error(void);
 /* Measured roofline peaks of `device` (peaks.hip, ~1 s): out[0] HBM streaming-copy GB/s (read + written bytes of a
- * 2 GiB double4 copy), out[1] FP64 MFMA TFLOP/s (v_mfma_f64_16x16x4f64 issue loop), out[2] FP64 VALU TFLOP/s (v_fma_f64
+ * 2 GiB 16-byte-per-lane copy), out[1] FP64 MFMA TFLOP/s (v_mfma_f64_16x16x4f64 issue loop), out[2] FP64 VALU TFLOP/s (v_fma_f64
  * issue loop), out[3] compute units; n >= 4. Returns 4 or a negative error. */
 int g2ohip_measure_peaks(int device, double* out, int n);
 /* The accepted LM trial's lambda factor max(1/3, min(2/3, 1 - (2 rho - 1)^3)) exactly as the device decision and the

@@ -334,6 +334,112 @@ __global__ void __launch_bounds__(256) k_w4b(const double* A, double* out, unsig
   if (tid == 0) cyc[0] = t1 - t0;
 }
 
+
+// ---- lag-2 deferral: column j's rank-1 update reaches columns j+1..j+3 at once (three chain values l1..l3) and the
+// rest two steps later, so the LDS reads of the broadcast column have a whole step to land before their first use
+struct C32L {
+  double dn, a1, b1, c2, c3;
+  double lp[2];
+  double2 cc0[NB / 2], cc1[NB / 2];
+  bool ok;
+};
+template <int J, int K>
+__device__ __forceinline__ void l2_fill(double (&row)[NB], C32L& st) {
+  constexpr int c0 = (J + 2) & ~1;
+  constexpr int nf = J >= 2 ? (NB - c0) / 2 : 0;
+  constexpr int qa = nf * K / C32_NCH, qb = nf * (K + 1) / C32_NCH;
+  const double lp = st.lp[J & 1];
+#pragma unroll
+  for (int q = qa; q < qb; ++q) {
+    const int c = c0 + 2 * q;
+    const double2 v = (J & 1) ? st.cc1[c >> 1] : st.cc0[c >> 1];
+    if (c > J + 1) row[c] -= lp * v.x;
+    row[c + 1] -= lp * v.y;
+  }
+}
+template <int J>
+__device__ __forceinline__ void l2_step(double (&row)[NB], int lane, double* col, C32L& st) {
+  if constexpr (J < NB) {
+    const double d = st.dn;
+    st.ok &= d > 0.0;
+    const double r0 = __builtin_amdgcn_rsq(d);
+    const double hd = 0.5 * d;
+    CHOL_SB();
+    l2_fill<J, 0>(row, st);
+    CHOL_SB();
+    const double t1 = hd * r0;
+    CHOL_SB();
+    l2_fill<J, 1>(row, st);
+    CHOL_SB();
+    const double t2 = __builtin_fma(-r0, t1, 1.5);
+    CHOL_SB();
+    l2_fill<J, 2>(row, st);
+    CHOL_SB();
+    const double r = r0 * t2;
+    const double l1 = st.b1 * r, l2 = st.c2 * r, l3 = st.c3 * r;
+    if constexpr (J + 1 < NB) st.dn = __builtin_fma(-l1, l1, st.a1);
+    CHOL_SB();
+    const double lj = row[J] * r;
+    row[J] = lj;
+    if constexpr (J + 1 < NB) row[J + 1] -= lj * l1;
+    if constexpr (J + 2 < NB) row[J + 2] -= lj * l2;
+    if constexpr (J + 3 < NB) row[J + 3] -= lj * l3;
+    constexpr int n0 = (J + 4) & ~1;
+    if constexpr (n0 < NB) {
+      double* cb = col + (J & 1) * 2 * NB;
+      cb[lane] = lj;
+      CHOL_SB();
+#pragma unroll
+      for (int c = n0; c < NB; c += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(cb + c);
+        if (J & 1) st.cc1[c >> 1] = v; else st.cc0[c >> 1] = v;
+      }
+      st.lp[J & 1] = lj;
+    }
+    if constexpr (J + 2 < NB) { st.a1 = rlane(row[J + 2], J + 2); st.b1 = rlane(row[J + 1], J + 2); }
+    if constexpr (J + 3 < NB) st.c2 = rlane(row[J + 1], J + 3);
+    if constexpr (J + 4 < NB) st.c3 = rlane(row[J + 1], J + 4);
+    CHOL_SB();
+    l2_step<J + 1>(row, lane, col, st);
+  }
+}
+__device__ __forceinline__ bool chol32_lag2(double (&row)[NB], int lane, double* col) {
+  C32L st;
+  st.ok = true;
+  st.lp[0] = st.lp[1] = 0.0;
+  st.dn = rlane(row[0], 0);
+  st.a1 = rlane(row[1], 1);
+  st.b1 = rlane(row[0], 1);
+  st.c2 = rlane(row[0], 2);
+  st.c3 = rlane(row[0], 3);
+  l2_step<0>(row, lane, col, st);
+  return st.ok;
+}
+__global__ void __launch_bounds__(256) k_lag2(const double* A, double* out, unsigned long long* cyc, int reps) {
+  __shared__ double D[NB * DS];
+  __shared__ __attribute__((aligned(16))) double col[4 * NB];
+  const int tid = threadIdx.x, lane = tid & 63;
+  unsigned long long t0 = 0, t1 = 0;
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int e = tid; e < NB * NB; e += 256) D[(e >> 5) * DS + (e & 31)] = A[e];
+    __syncthreads();
+    if (rep == reps - 1) t0 = __builtin_amdgcn_s_memtime();
+    if (tid < 64) {
+      double row[NB];
+#pragma unroll
+      for (int c = 0; c < NB; ++c) row[c] = lane < NB ? (c <= lane ? D[lane * DS + c] : 0.0) : (lane - NB == c ? 1.0 : 0.0);
+      chol32_lag2(row, lane, col);
+      if (lane >= NB)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) D[(lane - NB) * DS + i] = row[i];
+    }
+    __syncthreads();
+    if (rep == reps - 1) t1 = __builtin_amdgcn_s_memtime();
+  }
+  for (int e = tid; e < NB * NB; e += 256) out[e] = D[(e & 31) * DS + (e >> 5)];
+  if (tid == 0) cyc[0] = t1 - t0;
+}
+
 int main() {
   // SPD test block
   std::vector<double> A(NB * NB), L(NB * NB, 0.0), Li(NB * NB, 0.0);
@@ -387,5 +493,6 @@ int main() {
   run("four waves, 8 columns each", k_w4);
   run("product chol32 (one wave)", k_prod);
   run("four waves, deferred chunks", k_w4b);
+  run("lag-2 chol32 (one wave)", k_lag2);
   return 0;
 }

@@ -605,7 +605,10 @@ constexpr int SCH_PPB = SCH_SL + 1;       // slot-CSR entries per batch
 constexpr int SCH_NI = (SCH_SB + 255) / 256;
 }  // namespace
 
-template <int PD, int LD>
+// P3 (default): three index buffers, so a batch's indices are loaded one whole iteration before they are stored to LDS,
+// and one raw barrier per batch that waits only for the batch's G blocks (counted vmcnt: the younger index loads stay
+// in flight); !P3: two index buffers, the index loads drained by each batch's __syncthreads (G2OHIP_SCHUR_PIPE=0, A/B)
+template <int PD, int LD, bool P3>
 __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
                  const int* __restrict__ st_obs, const int* __restrict__ pairs, const int* __restrict__ pp,
@@ -618,9 +621,10 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
   constexpr int CW = (PD + 1) / 2;                   // output columns (and rows) per half
   static_assert(SCH_SB * NPC % 64 == 0, "a wave's LDS-DMA pieces must tile the batch image");
   __shared__ __attribute__((aligned(16))) double Gs[2][SCH_SB * GB];
-  __shared__ int so[2][SCH_SB];  // staged observation per block
-  __shared__ int sp[2][SCH_SB];  // pair lists (posA | posB << 16), slot-sorted
-  __shared__ int spp[2][SCH_PPB];
+  constexpr int NIB = P3 ? 3 : 2;  // index buffers
+  __shared__ int so[NIB][SCH_SB];  // staged observation per block
+  __shared__ int sp[NIB][SCH_SB];  // pair lists (posA | posB << 16), slot-sorted
+  __shared__ int spp[NIB][SCH_PPB];
   if ((int)blockIdx.x >= ntasks) {  // side job: zero one range of the factorization's front pool
     const long long off = zr[2 * (blockIdx.x - ntasks)], len = zr[2 * (blockIdx.x - ntasks) + 1];
     for (long long i = threadIdx.x; i < len; i += 256) fronts[off + i] = 0.0;
@@ -653,7 +657,7 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     }
     if (tid < SCH_PPB) spp[buf][tid] = ppv;
   };
-  auto stage = [&](const launch::SchurBatch B, int buf) {  // so[buf] holds B's observations
+  auto stage = [&](const launch::SchurBatch B, int buf, int ib) {  // so[ib] holds B's observations
     const int np = B.nst * NPC;
 #pragma unroll
     for (int u = 0; u < NC; ++u) {
@@ -661,12 +665,89 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
       if (i < np) {
         const int item = i / NPC, ch = i - item * NPC;
         __builtin_amdgcn_global_load_lds(
-            (const void*)(G + (size_t)so[buf][item] * GB + 2 * ch),
+            (const void*)(G + (size_t)so[ib][item] * GB + 2 * ch),
             (__attribute__((address_space(3))) void*)(&Gs[buf][(256 * u + 64 * w) * 2]), 16, 0, 0);
       }
     }
   };
-  auto compute = [&](int buf) { schur_pairs<PD, LD>(Gs[buf], sp[buf], spp[buf], t.noff, ls, q, acc); };
+  auto compute = [&](int buf, int ib) { schur_pairs<PD, LD>(Gs[buf], sp[ib], spp[ib], t.noff, ls, q, acc); };
+
+  if constexpr (P3) {
+    // Invariant at the top of iteration k: Gs[k&1] holds batch k (landed), index buffers k%3 and (k+1)%3 hold batches
+    // k and k+1 (visible), ov / pv / ppv hold batch k+2's indices (loads issued during iteration k-1, the youngest
+    // vector-memory operations then), B1 / B3 the records k+1 / k+3.
+    // The index loads are raw (clamped addresses, no select on the loaded value: a select right behind the load would
+    // wait for it); entries past the batch's counts are never read, and the slot CSR is rebased at the store.
+    constexpr int NIDX = 2 * SCH_NI + 1;  // vector loads of one idx_load3 (always issued)
+    int rpr0 = 0;
+    auto idx_load3 = [&](const launch::SchurBatch B, int k) {
+#pragma unroll
+      for (int u = 0; u < SCH_NI; ++u) {
+        const int i = tid + 256 * u;
+        ov[u] = st_obs[i < B.nst ? B.st0 + i : 0];
+        pv[u] = pairs[i < B.npr ? B.pr0 + i : 0];
+      }
+      ppv = pp[tid < SCH_PPB ? (t.b0 + k) * SCH_PPB + tid : 0];
+      rpr0 = B.pr0;
+    };
+    auto idx_store3 = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < SCH_NI; ++u) {
+        const int i = tid + 256 * u;
+        if (i < SCH_SB) { so[buf][i] = ov[u]; sp[buf][i] = pv[u]; }
+      }
+      if (tid < SCH_PPB) spp[buf][tid] = ppv - rpr0;
+    };
+    launch::SchurBatch B1 = rec(1), B2 = rec(2), B3 = rec(3);
+    if (nb > 0) {
+      idx_load3(rec(0), 0);
+      idx_store3(0);
+      if (nb > 1) {
+        idx_load3(B1, 1);
+        idx_store3(1);
+      }
+      __syncthreads();  // so[0], so[1] visible
+      if (!(mode & 2)) stage(rec(0), 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (nb > 2) {
+        idx_load3(B2, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIDX) : "memory");  // batch 0 landed, batch 2's indices in flight
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int k = 0; k < nb; ++k) {
+      const int cur = k & 1, i0 = k % 3, i1 = (k + 1) % 3, i2 = (k + 2) % 3;
+      // buffer i2 last held batch k-1 (its reads ended before the last barrier); stale values past the task's last
+      // batch are never read. The wait (vmcnt(0): the previous iteration's index loads, the only vector-memory
+      // operations in flight here) is explicit and compiler-visible so that no wave's path keeps those loads
+      // outstanding into the next index loads (which would make the compiler drain the G staging before them).
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      idx_store3(i2);
+      if (k + 1 < nb && !(mode & 2)) stage(B1, cur ^ 1, i1);
+      __builtin_amdgcn_sched_barrier(0);
+      const bool more = k + 3 < nb;
+      if (more) idx_load3(B3, k + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      const launch::SchurBatch B4 = rec(k + 4);
+      if (!(mode & 1)) compute(cur, i0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NIDX) : "memory");  // batch k+1's G blocks landed
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // batch k+2's indices visible, Gs[cur] / buffer i0 free
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      B1 = B2;
+      B2 = B3;
+      B3 = B4;
+    }
+    schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S);
+    return;
+  }
 
   // Invariant at the top of iteration k: Gs[k&1] holds batch k (landed), so/sp/spp[k&1] its indices
   // and pair list, so/sp/spp[(k+1)&1] those of batch k+1; B1, B2 = records k+1, k+2 (already landed:
@@ -677,16 +758,16 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     idx_store(0);
     if (nb > 1) idx_load(B1, 1);
     __syncthreads();  // so[0] visible
-    if (!(mode & 2)) stage(rec(0), 0);
+    if (!(mode & 2)) stage(rec(0), 0, 0);
     if (nb > 1) idx_store(1);
     __syncthreads();  // batch 0 landed (the barrier drains the DMA), so[1] visible
   }
   for (int k = 0; k < nb; ++k) {
     const int cur = k & 1;
-    if (k + 1 < nb && !(mode & 2)) stage(B1, cur ^ 1);
+    if (k + 1 < nb && !(mode & 2)) stage(B1, cur ^ 1, cur ^ 1);
     if (k + 2 < nb) idx_load(B2, k + 2);
     const launch::SchurBatch B3 = rec(k + 3);
-    if (!(mode & 1)) compute(cur);
+    if (!(mode & 1)) compute(cur, cur);
     __syncthreads();  // batch k+1 landed; Gs, so, sp, spp [cur] free
     if (k + 2 < nb) {
       idx_store(cur);
@@ -1332,10 +1413,15 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
                 int nzero, const long long* zr, double* fronts, hipStream_t s) {
   if (ntasks <= 0 && nzero <= 0) return;
   static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;  // dev A/B only
+  static const bool p3 = !(getenv("G2OHIP_SCHUR_PIPE") && atoi(getenv("G2OHIP_SCHUR_PIPE")) == 0);
   const int nz = nzero > 0 ? nzero : 0;
   pl_dispatch(pd, ld, [&](auto P, auto L) {
-    hipLaunchKernelGGL((k_schur_rows<decltype(P)::value, decltype(L)::value>), ntasks + nz, 256, 0, s, tasks, batches,
-                       st_obs, pairs, pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
+    if (p3)
+      hipLaunchKernelGGL((k_schur_rows<decltype(P)::value, decltype(L)::value, true>), ntasks + nz, 256, 0, s, tasks,
+                         batches, st_obs, pairs, pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
+    else
+      hipLaunchKernelGGL((k_schur_rows<decltype(P)::value, decltype(L)::value, false>), ntasks + nz, 256, 0, s, tasks,
+                         batches, st_obs, pairs, pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
   });
   KERNEL_CHECK();
 }

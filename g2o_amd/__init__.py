@@ -62,7 +62,7 @@ EXPORTS = [
     "g2ohip_solver_get_x", "g2ohip_solver_get_b", "g2ohip_solver_multiply_hessian",
     "g2ohip_solver_linear_residual", "g2ohip_solver_factor_info", "g2ohip_solver_compute_marginals", "g2ohip_update", "g2ohip_push", "g2ohip_pop",
     "g2ohip_discard_top", "g2ohip_stage", "g2ohip_linear_solve_ccs", "g2ohip_comm_unique_id",
-    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_comm_selftest", "g2ohip_comm_selftest_rs", "g2ohip_symbolic_analyze", "g2ohip_enable_kernel_timing",
+    "g2ohip_set_comm", "g2ohip_set_comm_local", "g2ohip_comm_selftest", "g2ohip_comm_selftest_rs", "g2ohip_symbolic_analyze", "g2ohip_dist_plan", "g2ohip_local_landmarks", "g2ohip_enable_kernel_timing",
     "g2ohip_kernel_timing_only", "g2ohip_set_stats_level", "g2ohip_kernel_ms",
     "g2ohip_kernel_count", "g2ohip_kernel_bytes", "g2ohip_kernel_flops", "g2ohip_last_error",
     "g2ohip_version", "g2ohip_host_payload_len", "g2ohip_solver_save_hessian", "g2ohip_solver_set_write_debug",
@@ -136,6 +136,8 @@ def lib() -> C.CDLL:
         "g2ohip_comm_selftest_rs": ([I, P, I, P, P, P], I),
         "g2ohip_debug_phases": ([P, I], I),
         "g2ohip_symbolic_analyze": ([I, I, I, P, P, P, P], I),
+        "g2ohip_dist_plan": ([I, I, I, P, P, I, I, I, P, P, P, I], I),
+        "g2ohip_local_landmarks": ([P, P, I], I),
         "g2ohip_enable_kernel_timing": ([P, I], None),
         "g2ohip_kernel_timing_only": ([P, C.c_char_p], None),
         "g2ohip_set_stats_level": ([P, I], None),
@@ -216,6 +218,30 @@ def symbolic_analyze(nblocks: int, bdim: int, bi, bj):
     n = lib().g2ohip_symbolic_analyze(nblocks, bdim, len(bi), _p(bi), _p(bj), _p(perm), _p(st))
     _check(n, "symbolic_analyze")
     return perm, dict(nnzL=st[0], flops=st[1], supernodes=int(st[2]), levels=int(st[3]), panel_steps=int(st[4]))
+
+
+DIST_PLAN_KEYS = ("distributed", "rank_subtrees_s", "shared_s", "replicated_s", "exchange_s", "input_s",
+                  "input_replicated_s", "max_rank_subtrees_s", "root_allgather_doubles", "rs_segment_doubles",
+                  "rs_tail_doubles", "supernodes", "shard_s", "shard_replicated_s")
+
+
+def dist_plan(nblocks: int, bdim: int, bi, bj, nranks: int, rank: int = 0, reduce_scatter: bool = True,
+              aligned: bool = True, pose_work=None):
+    """Host-only: the distributed factorization's cut for `nranks` landmark shards (the model the solver's setup
+    runs; aligned: shards follow the cut, the default); returns (model dict, per-supernode owner
+    array: rank, -1 shared)."""
+    bi = np.ascontiguousarray(bi, np.int32)
+    bj = np.ascontiguousarray(bj, np.int32)
+    out = np.zeros(len(DIST_PLAN_KEYS))
+    cap = 4 * nblocks + 16
+    owner = np.full(cap, -1, np.int32)
+    pw = None if pose_work is None else np.ascontiguousarray(pose_work, np.float64)
+    n = lib().g2ohip_dist_plan(nblocks, bdim, len(bi), _p(bi), _p(bj), nranks, rank,
+                               int(reduce_scatter) | (2 if aligned else 0), None if pw is None else _p(pw), _p(out),
+                               _p(owner), cap)
+    _check(n, "dist_plan")
+    d = dict(zip(DIST_PLAN_KEYS, out.tolist()))
+    return d, owner[:n]
 
 
 def linear_solve_ccs(n, Ap, Ai, Ax, b, block_dim=1, device=0):
@@ -448,12 +474,20 @@ class SparseOptimizer:
                         "model_rank_subtrees_s", "model_shared_s", "model_single_gpu_s", "model_exchange_s",
                         "distributed", "reduce_scatter", "rs_segment_doubles", "rs_tail_doubles", "model_input_s",
                         "model_input_allreduce_s", None,  # None: retired slots (always 0), kept for the ABI layout
-                        "band_leaf")
+                        "band_leaf", "aligned_shards", "local_block_doubles", "exchange_bytes_per_rank",
+                        "local_landmarks", "model_shard_s")
 
     def factor_info(self) -> dict:
         out = np.zeros(len(self.FACTOR_INFO_KEYS))
         _check(lib().g2ohip_solver_factor_info(self.h, _p(out), len(out)), "factor_info")
         return {k: v for k, v in zip(self.FACTOR_INFO_KEYS, out.tolist()) if k is not None}
+
+    def local_landmark_ids(self) -> np.ndarray:
+        """Ids of the free landmarks this rank's shard holds (landmark sharding; all of them on one rank)."""
+        n = _check(lib().g2ohip_local_landmarks(self.h, None, 0), "local_landmarks")
+        ids = np.zeros(max(n, 1), np.int32)
+        lib().g2ohip_local_landmarks(self.h, _p(ids), n)
+        return ids[:n]
 
     def stage(self, lam: float):
         dims = np.zeros(3, np.int64)

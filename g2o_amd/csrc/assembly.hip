@@ -436,7 +436,9 @@ __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* 
     while (tid >= base + c + 1) base += ++c;
     const int r = tid - base;
     if constexpr (FG) {  // S(i,i) = lambda I + sum B^T (Omega - M) B
-      const double o = r == c ? t + (sp.lamp ? sp.lamp[1] : sp.lam_rank) : t;
+      const double lr = sp.lam_own ? (sp.lam_own[i] ? (sp.lamp ? sp.lamp[0] : sp.lam) : 0.0)
+                                   : (sp.lamp ? sp.lamp[1] : sp.lam_rank);
+      const double o = r == c ? t + lr : t;
       double* So = sp.S + (size_t)sp.sdiag[i] * DB * DB;
       So[c * DB + r] = o;
       So[r * DB + c] = o;

@@ -212,6 +212,10 @@ int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel) {
   if (!g || !rel) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->linear_residual(rel); });
 }
+int g2ohip_local_landmarks(g2ohip_graph* g, int* ids, int cap) {
+  if (!g || cap < 0) return G2OHIP_ERR_ARG;
+  return guarded([&] { return g->e->local_landmarks(ids, cap); });
+}
 int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n) {
   if (!g || !out || n < 0) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->factor_info(out, n); });
@@ -405,29 +409,41 @@ int g2ohip_debug_phases(unsigned long long* out, int max_records) {
   }
 }
 
+int g2ohip_dist_plan(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int nranks, int rank,
+                     int flags, const double* pose_work, double* out, int* sn_owner, int cap) {
+  if (nblocks <= 0 || bdim <= 0 || nblk < 0 || (nblk > 0 && (!bi || !bj)) || nranks < 1 || rank < 0 ||
+      rank >= nranks || !out)
+    return G2OHIP_ERR_ARG;
+  try {
+    for (int k = 0; k < nblk; ++k)
+      if (bi[k] < 0 || bj[k] < 0 || bi[k] >= nblocks || bj[k] >= nblocks) return G2OHIP_ERR_ARG;
+    const std::vector<int> vbi(bi, bi + nblk), vbj(bj, bj + nblk);
+    const g2ohip::Symbolic S = g2ohip::analyze(g2ohip::block_pattern(nblocks, bdim, vbi, vbj));
+    std::vector<double> pw;
+    if (pose_work) pw.assign(pose_work, pose_work + nblocks);
+    const g2ohip::DistPlan D = g2ohip::plan_distribution(S, vbi, vbj, bdim, nblocks, nranks, rank, flags & 1, false,
+                                                         (flags & 2) != 0, pose_work ? &pw : nullptr);
+    const double v[14] = {D.on ? 1.0 : 0.0, D.rank_s, D.shared_s, D.repl_s, D.xch_s, D.input_s, D.input_repl_s,
+                          D.max_rank_s, (double)D.xch_seg, (double)D.rs_seg, (double)D.tail, (double)S.sn.size(),
+                          D.shard_s, D.shard_repl_s};
+    std::memcpy(out, v, sizeof v);
+    if (sn_owner)
+      for (int k = 0; k < (int)S.sn.size() && k < cap; ++k) sn_owner[k] = D.owner.empty() ? -1 : D.owner[k];
+    return (int)S.sn.size();
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return G2OHIP_ERR_STATE;
+  }
+}
+
 int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int* perm, double* stats) {
   if (nblocks <= 0 || bdim <= 0 || nblk < 0 || (nblk > 0 && (!bi || !bj))) return G2OHIP_ERR_ARG;
   try {
-    g2ohip::BlockPattern P;
-    P.nb = nblocks;
-    P.dim.assign(nblocks, bdim);
-    P.offset.resize(nblocks + 1);
-    for (int k = 0; k <= nblocks; ++k) P.offset[k] = k * bdim;
-    std::vector<std::vector<int>> adj(nblocks);
-    for (int k = 0; k < nblk; ++k) {
+    for (int k = 0; k < nblk; ++k)
       if (bi[k] < 0 || bj[k] < 0 || bi[k] >= nblocks || bj[k] >= nblocks) return G2OHIP_ERR_ARG;
-      if (bi[k] == bj[k]) continue;
-      adj[bi[k]].push_back(bj[k]);
-      adj[bj[k]].push_back(bi[k]);
-    }
-    P.adjp.assign(nblocks + 1, 0);
-    for (int k = 0; k < nblocks; ++k) {
-      std::sort(adj[k].begin(), adj[k].end());
-      adj[k].erase(std::unique(adj[k].begin(), adj[k].end()), adj[k].end());
-      P.adjp[k + 1] = P.adjp[k] + (int)adj[k].size();
-      P.adji.insert(P.adji.end(), adj[k].begin(), adj[k].end());
-    }
-    g2ohip::Symbolic S = g2ohip::analyze(P);
+    // the pattern exactly as the solver's setup builds it (adjacency in block order): the same analysis
+    g2ohip::Symbolic S = g2ohip::analyze(g2ohip::block_pattern(nblocks, bdim, std::vector<int>(bi, bi + nblk),
+                                                               std::vector<int>(bj, bj + nblk)));
     if (perm) std::memcpy(perm, S.perm.data(), sizeof(int) * S.n);
     if (stats) {
       stats[0] = S.nnzL;

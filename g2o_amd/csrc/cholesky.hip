@@ -956,7 +956,7 @@ __global__ void __launch_bounds__(256) k_pack_blocks(long long n, int bb, const 
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const long long t = i / bb;
-  dst[boff[t] + (i - t * bb)] = src[i];
+  if (boff[t] >= 0) dst[boff[t] + (i - t * bb)] = src[i];  // -1: a block this rank never reads
 }
 // x of the distributed solve: every rank holds its own columns (and rank 0 the shared ones) in xr[0 .. n), zeros
 // elsewhere, the not-PD flag of its fronts in xr[n]; after the all-reduce: x = xr, fail |= xr[n] > 0

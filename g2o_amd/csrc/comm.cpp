@@ -18,10 +18,11 @@ namespace g2ohip {
 
 namespace {
 
-enum : int { OP_SUM = 1, OP_MAX = 2, OP_RS = 3 };
+enum : int { OP_SUM = 1, OP_MAX = 2, OP_RS = 3, OP_AG = 4 };
 
 std::string call_desc(long long seq, size_t n, int op) {
-  return "call #" + std::to_string(seq) + " (" + (op == OP_MAX ? "max" : op == OP_RS ? "reduce-scatter" : "sum") +
+  return "call #" + std::to_string(seq) + " (" +
+         (op == OP_MAX ? "max" : op == OP_RS ? "reduce-scatter" : op == OP_AG ? "all-gather" : "sum") +
          ", n=" + std::to_string(n) + ")";
 }
 
@@ -70,6 +71,13 @@ struct RcclComm : Comm {
     const ncclResult_t r = ncclReduceScatter(p, p + (size_t)rank * count, count, ncclDouble, ncclSum, c, s);
     if (r != ncclSuccess) throw DeviceError(std::string("ncclReduceScatter(sum): ") + ncclGetErrorString(r));
   }
+  void allgather(double* p, size_t count, hipStream_t s) override {
+    verify(count, OP_AG, s);
+    ++seq;
+    // in place (sendbuff = recvbuff + rank * sendcount)
+    const ncclResult_t r = ncclAllGather(p + (size_t)rank * count, p, count, ncclDouble, c, s);
+    if (r != ncclSuccess) throw DeviceError(std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  }
 };
 
 // ---- in-process group for LocalComm ----
@@ -106,6 +114,15 @@ struct Group {
         throw DeviceError("collective mismatch across ranks: rank 0 entered " +
                           call_desc(meta[0].seq, meta[0].n, meta[0].op) + ", rank " + std::to_string(r) + " " +
                           call_desc(meta[r].seq, meta[r].n, meta[r].op) + " (seen by rank " + std::to_string(rank) + ")");
+    if (op == OP_AG) {  // n = nranks segments: segment r from rank r
+      const size_t cnt = n / nranks;
+      std::vector<double> all(n);
+      for (int r = 0; r < nranks; ++r)
+        std::copy(bufs[r].begin() + (size_t)r * cnt, bufs[r].begin() + (size_t)(r + 1) * cnt, all.begin() + (size_t)r * cnt);
+      barrier();  // everyone has read every buffer
+      std::copy(all.begin(), all.end(), out);
+      return;
+    }
     std::vector<double> acc(bufs[0]);
     for (int r = 1; r < nranks; ++r)
       for (size_t k = 0; k < n; ++k) acc[k] = op == OP_MAX ? std::max(acc[k], bufs[r][k]) : acc[k] + bufs[r][k];
@@ -144,6 +161,7 @@ struct LocalComm : Comm {
   void allreduce_sum(double* p, size_t n, hipStream_t s) override { reduce(p, n, s, OP_SUM); }
   void allreduce_max(double* p, size_t n, hipStream_t s) override { reduce(p, n, s, OP_MAX); }
   void reduce_scatter_sum(double* p, size_t count, hipStream_t s) override { reduce(p, count * g->nranks, s, OP_RS); }
+  void allgather(double* p, size_t count, hipStream_t s) override { reduce(p, count * g->nranks, s, OP_AG); }
 };
 
 }  // namespace

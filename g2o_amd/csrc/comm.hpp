@@ -2,7 +2,8 @@
 // per LM trial (one sum all-reduce, or with the distributed factorization a reduce-scatter of the blocks each rank's
 // subtrees read plus an all-reduce of the shared ones) plus scalar reductions.
 //
-//   RcclComm   production transport: ncclAllReduce / ncclReduceScatter on the solver's stream (RCCL over xGMI).
+//   RcclComm   production transport: ncclAllReduce / ncclReduceScatter / ncclAllGather on the solver's stream (RCCL
+//              over xGMI).
 //   LocalComm  test transport: N engines driven by N host threads of ONE process on one GPU;
 //              host-staged, summed in rank order. Lets the sharding logic run under pytest on
 //              a single-GPU box; never selected by the product path.
@@ -26,6 +27,8 @@ struct Comm {
   // in place: dptr holds nranks segments of `count` doubles; afterwards segment `rank` holds the sum over ranks of that
   // segment (the other segments are left as they were: this rank's own partial values)
   virtual void reduce_scatter_sum(double* dptr, size_t count, hipStream_t s) = 0;
+  // in place: dptr holds nranks segments of `count` doubles; afterwards every segment r holds rank r's segment r
+  virtual void allgather(double* dptr, size_t count, hipStream_t s) = 0;
   long long seq = 0;  // collectives issued so far on this communicator
 };
 

@@ -227,21 +227,7 @@ KernelTimer::~KernelTimer() {
 void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj,
                            hipStream_t s) {
   pd = bdim;
-  BlockPattern P;
-  P.nb = nblocks;
-  P.dim.assign(nblocks, bdim);
-  P.offset.resize(nblocks + 1);
-  for (int k = 0; k <= nblocks; ++k) P.offset[k] = k * bdim;
-  std::vector<int> deg(nblocks, 0);
-  for (size_t t = 0; t < bi.size(); ++t)
-    if (bi[t] != bj[t]) { deg[bi[t]]++; deg[bj[t]]++; }
-  P.adjp.assign(nblocks + 1, 0);
-  for (int k = 0; k < nblocks; ++k) P.adjp[k + 1] = P.adjp[k] + deg[k];
-  P.adji.assign(P.adjp[nblocks], 0);
-  std::vector<int> fill(P.adjp.begin(), P.adjp.end() - 1);
-  for (size_t t = 0; t < bi.size(); ++t)
-    if (bi[t] != bj[t]) { P.adji[fill[bi[t]]++] = bj[t]; P.adji[fill[bj[t]]++] = bi[t]; }
-  sym = analyze(P);
+  sym = analyze(block_pattern(nblocks, bdim, bi, bj));
   if ((long long)sym.max_front * sym.max_front >= (1LL << 31))
     throw DeviceError("front too large for 32-bit in-front indexing");
   // input entries per (permuted) scalar column: input block t (bi, bj) col-major bdim x bdim, value index
@@ -310,8 +296,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   // each subtree owned by one rank. Candidate cuts: starting from the tree's roots, the candidate subtree with the
   // largest serial work is split (its root joins the shared top), one cut per split, up to 4 candidates per rank; each
   // cut's subtrees go to ranks largest first (longest-processing-time rule). Every cut is priced with the level-
-  // synchronous model below (a rank's fronts of one tree level run in the same launches, as do the shared ones) plus
-  // the two all-reduces it adds (root exchange, x), and kept only if it beats the replicated factorization's model:
+  // synchronous model (plan_distribution, symbolic.cpp: a rank's fronts of one tree level run in the same launches, as
+  // do the shared ones) plus the exchanges it adds (root all-gather, x all-reduce) and its input (reduce-scatter +
+  // tail all-reduce), and kept only if it beats the replicated factorization's model:
   // a tree whose top is all chain (C4 at 8 ranks: one-bandwidth separators) gains less from distribution than its
   // exchange costs. dist_force (G2OHIP_DIST_FACTOR=1, the simulation mode) takes the best cut regardless.
   sn_owner.assign(sym.sn.size(), -1);
@@ -319,104 +306,21 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   dist_on = false;
   std::fill(dist_model, dist_model + 5, 0.0);
   if (dist_nranks > 1) {
-    const int nsn = (int)sym.sn.size(), N = dist_nranks;
-    std::vector<double> fl(nsn), chain(nsn), st(nsn);
-    for (int k = 0; k < nsn; ++k) {
-      const double m = sym.sn[k].ns + sym.sn[k].nr;
-      double f = 0;
-      for (int c = 0; c < sym.sn[k].ns; ++c) f += (m - c) * (m - c);
-      fl[k] = f;
-      chain[k] = ((sym.sn[k].ns + 31) / 32) * dist_cost::STEP_S;
-      st[k] = std::max(chain[k], f / dist_cost::TILE_FLOPS);
-    }
-    for (int k = 0; k < nsn; ++k)  // children precede parents (postorder): subtree serial work
-      if (sym.sn[k].parent >= 0) st[sym.sn[k].parent] += st[k];
-    // a set of fronts run level by level: per level the longer of its longest panel chain and its flops at the tile rate
-    auto levels_time = [&](const std::vector<int>& owner, int who) {
-      double t = 0;
-      for (const auto& lv : sym.levels) {
-        double ch = 0, f = 0;
-        bool any = false;
-        for (int sn : lv)
-          if (owner[sn] == who) { any = true; ch = std::max(ch, chain[sn]); f += fl[sn]; }
-        if (any) t += std::max(ch, f / dist_cost::TILE_FLOPS) + dist_cost::LEVEL_S;
-      }
-      return t;
-    };
-    auto allreduce_time = [&](double doubles) {
-      return dist_cost::ALLREDUCE_LAT_S + 2.0 * (N - 1) / N * 8.0 * doubles / dist_cost::ALLREDUCE_BW;
-    };
-    // the reduced system's own communication: one all-reduce of every block + rhs when replicated; with rs_enable a
-    // reduce-scatter of the blocks each rank's subtrees read (segments padded to the largest) + an all-reduce of the
-    // shared blocks and the rhs. Blocks per supernode: a block lands in the front of its smaller permuted column.
-    const double bb = (double)bdim * bdim;
-    std::vector<double> sn_blocks(nsn, 0.0);
-    for (size_t t = 0; t < bi.size(); ++t)
-      sn_blocks[sym.block_sn[std::min(sym.bpinv[bi[t]], sym.bpinv[bj[t]])]] += 1.0;
-    const double ar_full = allreduce_time(bi.size() * bb + (double)nblocks * bdim);
-    auto input_time = [&](const std::vector<int>& owner) {
-      if (!rs_enable) return ar_full;
-      std::vector<double> ob(N + 1, 0.0);
-      for (int k = 0; k < nsn; ++k) ob[owner[k] >= 0 ? owner[k] : N] += sn_blocks[k];
-      const double seg = *std::max_element(ob.begin(), ob.begin() + N) * bb;
-      return dist_cost::ALLREDUCE_LAT_S + (N - 1) * 8.0 * seg / dist_cost::ALLREDUCE_BW +
-             allreduce_time(ob[N] * bb + (double)nblocks * bdim);
-    };
-    std::vector<int> none(nsn, -2);  // the replicated model: every front in one set
-    const double t_repl = levels_time(none, -2) + ar_full;
-    std::vector<int> cand;
-    for (int k = 0; k < nsn; ++k)
-      if (sym.sn[k].parent < 0) cand.push_back(k);
-    std::vector<char> shared(nsn, 0);
-    std::vector<int> best_owner, owner(nsn);
-    double best = 1e30, best_rank = 0, best_shared = 0, best_xch = 0;
-    for (;;) {
-      int arg = -1;
-      for (size_t i = 0; i < cand.size(); ++i)
-        if (sym.children_ptr[cand[i] + 1] > sym.children_ptr[cand[i]] && (arg < 0 || st[cand[i]] > st[cand[arg]])) arg = (int)i;
-      if (arg < 0 || (int)cand.size() >= 4 * N) break;
-      const int c = cand[arg];
-      shared[c] = 1;
-      cand.erase(cand.begin() + arg);
-      for (int ci = sym.children_ptr[c]; ci < sym.children_ptr[c + 1]; ++ci) cand.push_back(sym.children[ci]);
-      if (cand.size() < 2) continue;
-      std::vector<int> srt(cand);
-      std::sort(srt.begin(), srt.end(), [&](int a, int b) { return st[a] > st[b] || (st[a] == st[b] && a < b); });
-      std::vector<double> load(N, 0.0);
-      std::vector<int> sub_owner(nsn, -1);
-      double xd = 0;
-      for (int s : srt) {
-        const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-        load[r] += st[s];
-        sub_owner[s] = r;
-        const double nr = sym.sn[s].nr;
-        xd += nr * (nr + 1) / 2 + nr;
-      }
-      for (int k = nsn - 1; k >= 0; --k)  // parents after children: walk down from the subtree roots
-        owner[k] = shared[k] ? -1 : sub_owner[k] >= 0 ? sub_owner[k] : owner[sym.sn[k].parent];
-      double tr = 0;
-      for (int r = 0; r < N; ++r) tr = std::max(tr, levels_time(owner, r));
-      const double ts = levels_time(owner, -1), tx = allreduce_time(xd) + allreduce_time(sym.n + 1.0);
-      const double ti = input_time(owner);
-      if (tr + ts + tx + ti < best) {
-        best = tr + ts + tx + ti;
-        rs_model[0] = ti;
-        best_owner = owner;
-        best_rank = levels_time(owner, dist_rank);
-        best_shared = ts;
-        best_xch = tx;
-      }
-    }
-    rs_model[1] = ar_full;
-    dist_on = !best_owner.empty() && (dist_force || best < t_repl);
-    dist_model[0] = best_rank;
-    dist_model[1] = best_shared;
-    dist_model[2] = t_repl;
-    dist_model[3] = best_xch;
+    const DistPlan P = plan_distribution(sym, bi, bj, bdim, nblocks, dist_nranks, dist_rank,
+                                         rs_enable && (bool)reduce_scatter, dist_force, aligned,
+                                         pose_work.empty() ? nullptr : &pose_work);
+    rs_model[0] = P.input_s;
+    rs_model[1] = P.input_repl_s;
+    dist_on = P.on;
+    dist_model[0] = P.rank_s;
+    dist_model[1] = P.shared_s;
+    dist_model[2] = P.repl_s;
+    dist_model[3] = P.xch_s;
     dist_model[4] = dist_on ? 1.0 : 0.0;
+    shard_model = dist_on ? P.shard_s : P.shard_repl_s;
     if (dist_on) {
-      sn_owner = best_owner;
-      for (int k = 0; k < nsn; ++k) {
+      sn_owner = P.owner;
+      for (int k = 0; k < (int)sym.sn.size(); ++k) {
         if (sn_owner[k] < 0) ++n_shared_fronts;
         else if (sn_owner[k] == dist_rank) ++n_owned_fronts;
       }
@@ -424,32 +328,38 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   }
   // reduce-scatter layout of the input (see engine.hpp): block t -> rs_buf offset; the entry sources remapped into it
   rs_on = dist_on && rs_enable && reduce_scatter;
-  rs_seg = rs_tail_len = rs_rhs_off = 0;
+  rs_seg = rs_tail_len = rs_rhs_off = rs_local = 0;
   rs_nblk = (long long)bi.size();
   if (rs_on) {
+    // block classes: 0..N-1 reduce-scattered to that rank, N shared (tail all-reduce), N+1 complete on this rank
+    // (aligned shards: read from its own partial S), N+2 another rank's complete block (never read here)
     const int N = dist_nranks, B = bdim * bdim;
-    std::vector<long long> cnt(N + 1, 0), boff(bi.size());
+    const bool al = aligned && blk_local.size() == bi.size();
+    std::vector<long long> cnt(N + 3, 0), boff(bi.size());
     std::vector<int> own(bi.size());
     for (size_t t = 0; t < bi.size(); ++t) {
       const int o = sn_owner[sym.block_sn[std::min(sym.bpinv[bi[t]], sym.bpinv[bj[t]])]];
-      own[t] = o >= 0 ? o : N;
+      own[t] = o < 0 ? N : (al && blk_local[t]) ? (o == dist_rank ? N + 1 : N + 2) : o;
       cnt[own[t]]++;
     }
     rs_seg = *std::max_element(cnt.begin(), cnt.begin() + N) * B;
-    std::vector<long long> fillc(N + 1, 0);
-    for (size_t t = 0; t < bi.size(); ++t) {
-      const int o = own[t];
-      boff[t] = (o < N ? (long long)o * rs_seg : (long long)N * rs_seg) + fillc[o]++ * B;
-    }
     rs_rhs_off = (long long)N * rs_seg + cnt[N] * B;
     rs_tail_len = cnt[N] * B + (long long)nblocks * bdim;
-    if (rs_rhs_off + (long long)nblocks * bdim >= (1LL << 31))
-      throw DeviceError("reduce-scatter layout too large for 32-bit entry indexing");
-    for (int& k : ent_srcv) k = (int)(boff[k / B] + k % B);
+    rs_local = cnt[N + 1] * B;
+    const long long loc0 = rs_rhs_off + (long long)nblocks * bdim;
+    std::vector<long long> fillc(N + 3, 0);
+    for (size_t t = 0; t < bi.size(); ++t) {
+      const int o = own[t];
+      const long long k = fillc[o]++ * B;
+      boff[t] = o < N ? (long long)o * rs_seg + k : o == N ? (long long)N * rs_seg + k : o == N + 1 ? loc0 + k : -1;
+    }
+    if (loc0 + rs_local >= (1LL << 31)) throw DeviceError("reduce-scatter layout too large for 32-bit entry indexing");
+    // another rank's complete blocks feed only that rank's fronts: their entries are never assembled here
+    for (int& k : ent_srcv) k = boff[k / B] < 0 ? 0 : (int)(boff[k / B] + k % B);
     ent_src.upload(ent_srcv.empty() ? std::vector<int>{0} : ent_srcv, s);
     rs_bmap.upload(boff.empty() ? std::vector<long long>{0} : boff, s);
     rs_rhs_rng.upload(std::vector<long long>{(long long)bi.size() * B, rs_rhs_off, (long long)nblocks * bdim}, s);
-    rs_buf.resize(std::max<long long>(rs_rhs_off + (long long)nblocks * bdim, 1));
+    rs_buf.resize(std::max<long long>(loc0 + rs_local, 1));
     rs_buf.zero(s);  // segment padding is never written: zeros go into the reduce-scatter
   }
   // forward plan: the level front lists in execution order (distributed: this rank's fronts level by level, the root
@@ -756,20 +666,30 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       for (int sn : lv) n_blocked += blocked(sym.sn[sn]) ? 1 : 0;
     }
     // root exchange (distributed): per subtree root, the lower triangle of its contribution block column by column
-    // and its update vector, at fixed offsets of one buffer; a rank packs its own roots, the all-reduce sums zeros
-    // elsewhere, every rank unpacks the others' into its front pool / front vectors
+    // and its update vector, packed into the owning rank's segment of one buffer (segments of xch_seg doubles, the
+    // largest rank's roots); one all-gather hands every segment to every rank, which unpacks the others' roots into its
+    // front pool / front vectors
     if (distributed()) {
-      std::vector<long long> pf, pv, uf, uv, zi;
-      long long off = 0;
+      std::vector<long long> pf, pv, uf, uv, zi, roff(dist_nranks, 0);
       n_roots = 0;
       auto add = [](std::vector<long long>& v, long long a, long long b, long long n) { v.push_back(a); v.push_back(b); v.push_back(n); };
+      for (size_t k = 0; k < sym.sn.size(); ++k) {  // segment sizes first
+        const int par = sym.sn[k].parent;
+        if (sn_owner[k] < 0 || par < 0 || sn_owner[par] >= 0) continue;
+        const long long nr = sym.sn[k].nr;
+        roff[sn_owner[k]] += nr * (nr + 1) / 2 + nr;
+      }
+      xch_seg = std::max<long long>(*std::max_element(roff.begin(), roff.end()), 1);
+      std::fill(roff.begin(), roff.end(), 0);
       for (size_t k = 0; k < sym.sn.size(); ++k) {
         const int par = sym.sn[k].parent;
         if (sn_owner[k] < 0 || par < 0 || sn_owner[par] >= 0) continue;
         ++n_roots;
         const Supernode& q = sym.sn[k];
         const long long m = q.ns + q.nr;
-        const bool mine = sn_owner[k] == dist_rank;
+        const int o = sn_owner[k];
+        const bool mine = o == dist_rank;
+        long long off = (long long)o * xch_seg + roff[o];
         for (int j = 0; j < q.nr; ++j) {
           const long long fo = q.front_off + (long long)(q.ns + j) * m + q.ns + j, len = q.nr - j;
           if (mine) add(pf, fo, off, len); else add(uf, off, fo, len);
@@ -779,8 +699,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           if (mine) add(pv, q.vec_off + q.ns, off, q.nr); else add(uv, off, q.vec_off + q.ns, q.nr);
           off += q.nr;
         }
+        roff[o] = off - (long long)o * xch_seg;
       }
-      xch_len = off;
+      xch_len = (long long)dist_nranks * xch_seg;
       xch_pack_f = (int)pf.size() / 3; xch_pack_v = (int)pv.size() / 3;
       xch_unpack_f = (int)uf.size() / 3; xch_unpack_v = (int)uv.size() / 3;
       std::vector<long long> all;
@@ -902,10 +823,9 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
         break;
       case 8: {  // subtree roots -> every rank
         const long long* R = xch_ranges.get();
-        xch_buf.zero(s);
         launch::chol_copy_ranges(xch_pack_f, R, fronts.get(), xch_buf.get(), s);
         launch::chol_copy_ranges(xch_pack_v, R + 3LL * xch_pack_f, vecs.get(), xch_buf.get(), s);
-        allreduce(xch_buf.get(), (size_t)xch_len);
+        allgather(xch_buf.get(), (size_t)xch_seg);
         launch::chol_copy_ranges(xch_unpack_f, R + 3LL * (xch_pack_f + xch_pack_v), xch_buf.get(), fronts.get(), s);
         launch::chol_copy_ranges(xch_unpack_v, R + 3LL * (xch_pack_f + xch_pack_v + xch_unpack_f), xch_buf.get(),
                                  vecs.get(), s);
@@ -919,7 +839,7 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
 void DeviceCholesky::reduce_input(const double* vals, hipStream_t s) {
   launch::chol_pack_blocks(rs_nblk, pd * pd, rs_bmap.get(), vals, rs_buf.get(), s);
   launch::chol_copy_ranges(1, rs_rhs_rng.get(), vals, rs_buf.get(), s);
-  reduce_scatter(rs_buf.get(), (size_t)rs_seg);
+  if (rs_seg > 0) reduce_scatter(rs_buf.get(), (size_t)rs_seg);  // rs_seg is the same on every rank
   allreduce(rs_buf.get() + (size_t)dist_nranks * rs_seg, (size_t)rs_tail_len);
 }
 
@@ -1635,17 +1555,19 @@ void Engine::refresh_host_payload(bool jacobians) {
 }
 
 void Engine::setup_edges_device() {
+  // landmark shards: contiguous ranges of the hessian order, aligned with the factorization's cut (align_shards) or
+  // the uniform split
+  std::vector<int> bnd(nranks + 1);
+  for (int r = 0; r <= nranks; ++r) bnd[r] = lm_bnd.empty() ? (int)((long long)num_landmarks * r / nranks) : lm_bnd[r];
   int lm_begin = 0, lm_end = num_landmarks;
   if (do_schur && nranks > 1) {
-    lm_begin = (int)((long long)num_landmarks * rank / nranks);
-    lm_end = (int)((long long)num_landmarks * (rank + 1) / nranks);
+    lm_begin = bnd[rank];
+    lm_end = bnd[rank + 1];
   }
   local_lm.clear();
   for (int l = lm_begin; l < lm_end; ++l) local_lm.push_back(l);
-  // landmark shards: an edge belongs to the rank owning its landmark endpoint; edges without a (free) landmark
-  // are assembled by rank 0 once. Pose graphs run replicas: every rank assembles every edge.
-  std::vector<int> bnd(nranks + 1);
-  for (int r = 0; r <= nranks; ++r) bnd[r] = (int)((long long)num_landmarks * r / nranks);
+  // an edge belongs to the rank owning its landmark endpoint; edges without a (free) landmark are assembled by rank 0
+  // once. Pose graphs run replicas: every rank assembles every edge.
   auto owner_of = [&](int va, int vb) {
     if (!(do_schur && nranks > 1)) return rank;
     const int h = hidx[va] >= num_poses ? hidx[va] : (hidx[vb] >= num_poses ? hidx[vb] : -1);
@@ -1846,12 +1768,128 @@ void Engine::setup_edges_device() {
   ++state_ver;  // the edge set (and so chi2) changed
 }
 
+// Upper block pattern (i <= j, row-major, sorted) of the reduced camera system from ALL edges (identical on every
+// rank whatever its shard): the diagonal, pose-pose edges and the pose clique of every free landmark
+// (block_solver.hpp:216-251).
+void Engine::schur_pattern(std::vector<int>& sbi, std::vector<int>& sbj, std::vector<int>& srow_ptr) const {
+  std::vector<std::vector<int>> lmposes(num_landmarks);
+  std::vector<std::vector<int>> rowcols(num_poses);
+  for (int i = 0; i < num_poses; ++i) rowcols[i].push_back(i);
+  for (const HEdgeSet& es : hg.esets)
+    for (size_t e = 0; e < es.ev0.size(); ++e) {
+      const int i1 = hidx[es.ev0[e]], i2 = hidx[es.ev1[e]];
+      if (i1 < 0 || i2 < 0) continue;
+      if (i1 >= num_poses && i2 < num_poses) lmposes[i1 - num_poses].push_back(i2);
+      else if (i2 >= num_poses && i1 < num_poses) lmposes[i2 - num_poses].push_back(i1);
+      else if (i1 < num_poses && i2 < num_poses) rowcols[std::min(i1, i2)].push_back(std::max(i1, i2));
+    }
+  for (auto& ps : lmposes) {
+    std::sort(ps.begin(), ps.end());
+    ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
+    for (size_t u = 0; u < ps.size(); ++u)
+      for (size_t v = u; v < ps.size(); ++v) rowcols[ps[u]].push_back(ps[v]);
+  }
+  srow_ptr.assign(num_poses + 1, 0);
+  sbi.clear();
+  sbj.clear();
+  for (int i = 0; i < num_poses; ++i) {
+    auto& rc = rowcols[i];
+    std::sort(rc.begin(), rc.end());
+    rc.erase(std::unique(rc.begin(), rc.end()), rc.end());
+    for (int j : rc) { sbi.push_back(i); sbj.push_back(j); }
+    srow_ptr[i + 1] = (int)sbi.size();
+  }
+}
+
+// Per pose: the landmark-sharded work that follows it in the cut's model (its observations of free landmarks).
+std::vector<double> Engine::pose_work() const {
+  std::vector<double> w(num_poses, 0.0);
+  for (const HEdgeSet& es : hg.esets)
+    for (size_t e = 0; e < es.ev0.size(); ++e) {
+      const int i1 = hidx[es.ev0[e]], i2 = hidx[es.ev1[e]];
+      if (i1 >= num_poses && i2 >= 0 && i2 < num_poses) w[i2] += dist_cost::OBS_S;
+      else if (i2 >= num_poses && i1 >= 0 && i1 < num_poses) w[i1] += dist_cost::OBS_S;
+    }
+  return w;
+}
+
+// Landmark shards aligned with the distributed factorization's cut. With landmark sharding and a cut
+// the model takes (plan_distribution with aligned input: the same plan DeviceCholesky::setup will make), every
+// landmark goes to the rank whose subtrees its Schur blocks land in (align_landmarks), and the landmarks' hessian order
+// is regrouped by rank (stable within a rank), so every shard is one contiguous range [lm_bnd[r], lm_bnd[r+1]). A
+// rank's subtree blocks of S are then complete on that rank (lambda on their diagonal included: lam_own); only the
+// shared blocks and the rhs are exchanged. G2OHIP_DIST_ALIGN=0 keeps the uniform split of the landmark order.
+void Engine::align_shards() {
+  lm_bnd.clear();
+  dist_aligned = false;
+  al_bpinv.clear();
+  al_bowner.clear();
+  // the hessian order buildIndexMapping gives (initialize): poses, then the free landmarks in id order
+  ivmap.resize(num_poses);
+  for (int vi : active) {
+    const HVertex& v = hg.verts[vi];
+    if (!v.fixed && v.marg) {
+      hidx[vi] = (int)ivmap.size();
+      ivmap.push_back(vi);
+    }
+  }
+  if (!(do_schur && nranks > 1 && comm) || use_pcg() || use_cgls() || write_debug) return;
+  auto env0 = [](const char* n) { const char* e = getenv(n); return e && atoi(e) == 0; };
+  if (env0("G2OHIP_DIST_FACTOR") || env0("G2OHIP_DIST_ALIGN")) return;
+  std::vector<int> sbi, sbj, srp;
+  schur_pattern(sbi, sbj, srp);
+  const Symbolic sym = analyze(block_pattern(num_poses, pd, sbi, sbj));
+  const char* df = getenv("G2OHIP_DIST_FACTOR");
+  // the flags and weights build_structure gives DeviceCholesky::setup, so that both make the same plan
+  const bool rs = !env0("G2OHIP_DIST_RS");
+  const std::vector<double> pw = pose_work();
+  const DistPlan D = plan_distribution(sym, sbi, sbj, pd, num_poses, nranks, rank, rs, df && atoi(df) == 1, true, &pw);
+  if (!D.on) return;
+  // per landmark its free poses (all edges)
+  std::vector<std::vector<int>> lp(num_landmarks);
+  for (const HEdgeSet& es : hg.esets)
+    for (size_t e = 0; e < es.ev0.size(); ++e) {
+      const int i1 = hidx[es.ev0[e]], i2 = hidx[es.ev1[e]];
+      if (i1 >= num_poses && i2 >= 0 && i2 < num_poses) lp[i1 - num_poses].push_back(i2);
+      else if (i2 >= num_poses && i1 >= 0 && i1 < num_poses) lp[i2 - num_poses].push_back(i1);
+    }
+  std::vector<int> lm_ptr(num_landmarks + 1, 0), lm_cams;
+  for (int l = 0; l < num_landmarks; ++l) {
+    lm_cams.insert(lm_cams.end(), lp[l].begin(), lp[l].end());
+    lm_ptr[l + 1] = (int)lm_cams.size();
+  }
+  const std::vector<int> own = align_landmarks(sym, D.owner, nranks, lm_ptr, lm_cams);
+  std::vector<int> order(num_landmarks);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return own[a] < own[b]; });
+  const std::vector<int> lmv(ivmap.begin() + num_poses, ivmap.end());
+  ivmap.resize(num_poses);
+  lm_bnd.assign(nranks + 1, 0);
+  for (int l : order) {
+    hidx[lmv[l]] = (int)ivmap.size();
+    ivmap.push_back(lmv[l]);
+    lm_bnd[own[l] + 1]++;
+  }
+  for (int r = 0; r < nranks; ++r) lm_bnd[r + 1] += lm_bnd[r];
+  al_bpinv = sym.bpinv;
+  al_bowner.resize(sym.nb);
+  for (int k = 0; k < sym.nb; ++k) al_bowner[k] = D.owner[sym.block_sn[k]];
+  lam_own_h.assign(num_poses, 0);
+  for (int i = 0; i < num_poses; ++i) {
+    const int o = al_bowner[al_bpinv[i]];
+    lam_own_h[i] = (o == rank || (o < 0 && rank == 0)) ? 1 : 0;
+  }
+  d_lam_own.upload(lam_own_h, stream);
+  dist_aligned = true;
+}
+
 int Engine::build_structure() {  // block_solver.hpp:102-256
   if (!initialized) {
     int r = initialize();
     if (r) return r;
   }
   ensure_device_state();
+  align_shards();
   setup_edges_device();
   ++structure_ver;  // every cache keyed on the block pattern (marginals factor, BlockSymv) is stale from here
   // per-type hessian index and x offsets
@@ -2063,35 +2101,8 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     d_blk_pose.upload(blk_pose, stream);
     d_blk_lm.upload(blk_lm, stream);
     // global Schur pattern from ALL edges (identical on every rank)
-    std::vector<std::vector<int>> lmposes(num_landmarks);
-    std::vector<std::vector<int>> rowcols(num_poses);
-    for (int i = 0; i < num_poses; ++i) rowcols[i].push_back(i);
-    for (int b = num_poses; b < nHpp; ++b) rowcols[hpp_bi[b]].push_back(hpp_bj[b]);
-    for (const HEdgeSet& es : hg.esets)
-      for (size_t e = 0; e < es.ev0.size(); ++e) {
-        const int i1 = hidx[es.ev0[e]], i2 = hidx[es.ev1[e]];
-        if (i1 < 0 || i2 < 0) continue;
-        if (i1 >= num_poses && i2 < num_poses) lmposes[i1 - num_poses].push_back(i2);
-        else if (i2 >= num_poses && i1 < num_poses) lmposes[i2 - num_poses].push_back(i1);
-        // pose-pose edges owned by other ranks must also be in the global pattern
-        else if (i1 < num_poses && i2 < num_poses) rowcols[std::min(i1, i2)].push_back(std::max(i1, i2));
-      }
-    for (auto& ps : lmposes) {
-      std::sort(ps.begin(), ps.end());
-      ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
-      for (size_t u = 0; u < ps.size(); ++u)
-        for (size_t v = u; v < ps.size(); ++v) rowcols[ps[u]].push_back(ps[v]);
-    }
-    std::vector<int> srow_ptr(num_poses + 1, 0);
-    s_bi.clear();
-    s_bj.clear();
-    for (int i = 0; i < num_poses; ++i) {
-      auto& rc = rowcols[i];
-      std::sort(rc.begin(), rc.end());
-      rc.erase(std::unique(rc.begin(), rc.end()), rc.end());
-      for (int j : rc) { s_bi.push_back(i); s_bj.push_back(j); }
-      srow_ptr[i + 1] = (int)s_bi.size();
-    }
+    std::vector<int> srow_ptr;
+    schur_pattern(s_bi, s_bj, srow_ptr);
     nS = (int)s_bi.size();
     // Schur tasks. Diagonal blocks (k_schur_diag): per camera row its observations in landmark order.
     // Off-diagonal blocks (k_schur_rows): per camera row, chunks of <= SCHUR_SL off-diagonal slots;
@@ -2238,6 +2249,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       chol.dist_nranks = dist ? nranks : 1;
       chol.dist_force = df && atoi(df) == 1;
       chol.allreduce = [this](double* p, size_t n) { allreduce_sum(p, n); };
+      chol.allgather = [this](double* p, size_t n) { comm->allgather(p, n, stream); };
       // the reduced system itself reduce-scattered by subtree ownership (G2OHIP_DIST_RS=0: all-reduced whole, A/B);
       // not with the not-PD dump, which writes the whole S from rank 0
       const char* drs = getenv("G2OHIP_DIST_RS");
@@ -2252,10 +2264,42 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         chol.dist_nranks = sn;
         chol.dist_force = true;
         chol.allreduce = [](double*, size_t) {};
+        chol.allgather = [](double*, size_t) {};
         chol.reduce_scatter = [](double*, size_t) {};
         chol.rs_enable = !(drs && atoi(drs) == 0);
       }
+      chol.aligned = dist_aligned && dist;
+      chol.blk_local.clear();
+      if (chol.aligned) {
+        // blocks written by a rank other than the one whose subtrees read them: those of edges without a free
+        // landmark (assembled by rank 0: pose-pose edges, edges to fixed landmarks) — both endpoints' diagonal blocks
+        // and their off-diagonal block — where the reading rank is not rank 0. Landmark blocks and lambda (lam_own)
+        // are written by the reading rank itself.
+        std::vector<unsigned char> by0(nS, 0);
+        auto blk = [&](int i, int j) {
+          const int* b = s_bj.data() + srow_ptr[i];
+          const int* e = s_bj.data() + srow_ptr[i + 1];
+          const int* it = std::lower_bound(b, e, j);
+          return it != e && *it == j ? (int)(it - s_bj.data()) : -1;
+        };
+        for (const HEdgeSet& es : hg.esets)
+          for (size_t e = 0; e < es.ev0.size(); ++e) {
+            const int i1 = hidx[es.ev0[e]], i2 = hidx[es.ev1[e]];
+            if (i1 >= num_poses || i2 >= num_poses) continue;  // a free landmark endpoint: its owner's
+            for (int h : {i1, i2})
+              if (h >= 0) { const int t = blk(h, h); if (t >= 0) by0[t] = 1; }
+            if (i1 >= 0 && i2 >= 0 && i1 != i2) { const int t = blk(std::min(i1, i2), std::max(i1, i2)); if (t >= 0) by0[t] = 1; }
+          }
+        chol.blk_local.assign(nS, 1);
+        for (int t = 0; t < nS; ++t) {
+          const int o = al_bowner[std::min(al_bpinv[s_bi[t]], al_bpinv[s_bj[t]])];
+          if (by0[t] && o != 0) chol.blk_local[t] = 0;
+        }
+      }
+      chol.pose_work = pose_work();
       chol.setup(num_poses, pd, s_bi, s_bj, stream);
+      if (chol.aligned && !chol.distributed())
+        throw DeviceError("aligned landmark shards without the distributed factorization they were cut for");
     }
   } else if (use_pcg()) {
     pcg.setup(num_poses, pd, hpp_bi, hpp_bj, stream);
@@ -2330,6 +2374,7 @@ int Engine::build_system_split(double lambda, const double* lamp) {  // block_so
       sp.lam = lambda;
       sp.lam_rank = rank == 0 ? lambda : 0.0;
       sp.lamp = lamp;
+      sp.lam_own = dist_aligned ? d_lam_own.get() : nullptr;
       sp.Ufac = dUfac.get();
       sp.cl = dCl.get();
       sp.G = dG.get();
@@ -2456,8 +2501,8 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
     timer.end(stream);
     timer.begin("schur_diag", stream);
     launch::schur_diag(pd, ld, num_poses, sch_rptr.get(), sch_robs.get(), sch_obs_lm.get(), lm_begin, Hpl, dUfac.get(),
-                       dCl.get(), sch_sdiag.get(), ds_hpp.get(), dH.get(), db.get(), dscal.get() + 4, S, bschur, dG.get(),
-                       stream);
+                       dCl.get(), sch_sdiag.get(), ds_hpp.get(), dH.get(), db.get(), dscal.get() + 4,
+                       dist_aligned ? d_lam_own.get() : nullptr, dscal.get(), S, bschur, dG.get(), stream);
     timer.end(stream);
   }
   // the Cholesky's pre-scattered fronts are cleared by extra workgroups of the Schur pass (they are dead since the
@@ -3131,10 +3176,31 @@ int Engine::factor_info(double* out, int n) {
                       (double)chol.n_roots, (double)chol.xch_len, chol.dist_model[0], chol.dist_model[1],
                       chol.dist_model[2], chol.dist_model[3], chol.dist_model[4], chol.rs_on ? 1.0 : 0.0,
                       (double)chol.rs_seg, (double)chol.rs_tail_len, chol.rs_model[0], chol.rs_model[1],
-                      0.0 /* retired: 64-column-step levels */, (double)S.band_leaf};
+                      0.0 /* retired: 64-column-step levels */, (double)S.band_leaf, dist_aligned ? 1.0 : 0.0,
+                      (double)chol.rs_local, exchange_bytes(), (double)local_lm.size(), chol.shard_model};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;
+}
+
+// Bytes this rank sends per LM trial through the collectives of the reduced system and its factorization (ring
+// algorithms: a reduce-scatter or all-gather of N segments sends N-1 of them, an all-reduce 2 (N-1)/N of the buffer),
+// the scalar reductions aside
+double Engine::exchange_bytes() const {
+  if (nranks <= 1 || !do_schur || !comm) return 0.0;
+  const double N = nranks, ar = 2.0 * (N - 1) / N;
+  if (!chol.distributed()) return 8.0 * ar * ((double)nS * pd * pd + size_poses);
+  double b = 8.0 * (N - 1) * (double)chol.xch_seg + 8.0 * ar * (chol.sym.n + 1.0);  // root all-gather, x
+  if (chol.rs_on) b += 8.0 * (N - 1) * (double)chol.rs_seg + 8.0 * ar * (double)chol.rs_tail_len;
+  else b += 8.0 * ar * ((double)nS * pd * pd + size_poses);
+  return b;
+}
+
+int Engine::local_landmarks(int* ids, int cap) const {
+  const int n = (int)local_lm.size();
+  if (ids)
+    for (int k = 0; k < n && k < cap; ++k) ids[k] = hg.verts[ivmap[num_poses + local_lm[k]]].id;
+  return n;
 }
 
 double Engine::kernel_bytes(const std::string& name) const {

@@ -83,13 +83,6 @@ void set_state_from_est(int vtype, const double* est, double* st);
 void est_from_state(int vtype, const double* st, double* est);
 void minimal_from_state(int vtype, const double* st, double* out);
 
-// Cost model of the distributed factorization's cut, calibrated on C4 / C5 (rank schedules timed alone
-// on one GPU, tools/dist_factor_time.py): a 32-column panel step on the chain, the panel steps' tile rate, a level's
-// fixed launches, and an all-reduce over xGMI (latency + bus bandwidth, ring traffic 2 (N-1)/N).
-namespace dist_cost {
-constexpr double STEP_S = 10e-6, TILE_FLOPS = 12e12, LEVEL_S = 20e-6, ALLREDUCE_LAT_S = 30e-6, ALLREDUCE_BW = 120e9;
-}
-
 // Device-resident multifrontal factor of one block-sparse SPD matrix.
 struct DeviceCholesky {
   Symbolic sym;
@@ -121,17 +114,19 @@ struct DeviceCholesky {
   // ---- distributed factorization (landmark-sharded BA). Set dist_rank / dist_nranks / allreduce before
   // setup. The elimination tree is cut: every front below the cut belongs to one rank (whole subtrees, balanced by
   // modelled time), the fronts above it are factored by every rank. A rank factors its subtrees, the subtree roots'
-  // contribution blocks and update vectors meet in one all-reduce (zeros elsewhere), every rank factors the top;
-  // the backward solve runs top-down the same way and x meets in one all-reduce (with the not-PD flag).
+  // contribution blocks and update vectors meet in one all-gather (each rank's roots in its own segment), every rank
+  // factors the top; the backward solve runs top-down the same way and x meets in one all-reduce (with the not-PD
+  // flag).
   int dist_rank = 0, dist_nranks = 1;
   std::function<void(double*, size_t)> allreduce;
+  std::function<void(double*, size_t)> allgather;  // in place: nranks segments of `count` doubles
   std::vector<int> sn_owner;                 // per supernode: owning rank, -1 shared (every rank)
   int n_owned_fronts = 0, n_shared_fronts = 0, n_roots = 0;
   bool dist_on = false;                      // setup chose a cut (the model beat the replicated factorization, or forced)
   bool dist_force = false;                   // take the best cut even when the model prefers replication
   double dist_model[5] = {0, 0, 0, 0, 0};    // modelled seconds: this rank's subtrees, the shared top, replicated
                                              // factorization, the two all-reduces of the cut; 1 if distributed
-  long long xch_len = 0;                      // doubles of the root exchange
+  long long xch_len = 0, xch_seg = 0;         // doubles of the root exchange (nranks segments of xch_seg)
   int xch_pack_f = 0, xch_pack_v = 0, xch_unpack_f = 0, xch_unpack_v = 0;
   DevBuf<long long> xch_ranges;               // (src, dst, len): pack fronts | pack vecs | unpack fronts | unpack vecs
   DevBuf<double> xch_buf, xred;
@@ -144,9 +139,25 @@ struct DeviceCholesky {
   // rs_seg doubles) | shared blocks + rhs] — one reduce-scatter sums each rank's own segment, one all-reduce the tail;
   // the factor reads its entries from rs_buf (ent_src remapped), never another rank's segment
   bool rs_enable = false, rs_on = false;
+  // landmark shards aligned with the cut (Engine::align_shards, set before setup): the plan's input model counts only
+  // the shared tail, and blk_local (per input block) marks the blocks whose only writer is the rank that reads them —
+  // read from the rank's own partial S, never exchanged
+  bool aligned = false;
+  std::vector<unsigned char> blk_local;
+  std::vector<double> pose_work;              // per pose block: the sharded work the cut's model weighs (optional)
+  double shard_model = 0;                     // modelled busiest rank's sharded work (s) of the chosen layout
+  long long rs_local = 0;                     // doubles of this rank's own complete blocks (rs_buf's last region)
   // a factorization of the whole system on this rank alone (pose graphs, computeMarginals' Hpp factor): clears any
   // distribution state an earlier sharded setup of the same object left behind
-  void set_replicated() { dist_rank = 0; dist_nranks = 1; dist_force = false; rs_enable = false; }
+  void set_replicated() {
+    dist_rank = 0;
+    dist_nranks = 1;
+    dist_force = false;
+    rs_enable = false;
+    aligned = false;
+    blk_local.clear();
+    pose_work.clear();
+  }
   std::function<void(double*, size_t)> reduce_scatter;  // in place, `count` doubles per rank
   long long rs_seg = 0, rs_tail_len = 0, rs_rhs_off = 0, rs_nblk = 0;
   double rs_model[2] = {0, 0};                // modelled seconds: reduce-scatter + tail all-reduce, full all-reduce
@@ -288,6 +299,9 @@ class Engine {
   int set_comm_local(const std::string& key, int rank, int nranks);
   KernelTimer timer;
   double kernel_bytes(const std::string& name) const;
+  double exchange_bytes() const;
+  // ids of the free landmarks this rank's shard holds (landmark-sharded BA); returns the count
+  int local_landmarks(int* ids, int cap) const;
   double kernel_flops(const std::string& name) const;
 
  private:
@@ -309,6 +323,16 @@ class Engine {
   int rank = 0, nranks = 1;
   std::unique_ptr<Comm> comm;
   std::vector<int> local_lm;     // landmark (hessian - num_poses) this rank owns
+  // aligned landmark shards (align_shards): per rank its landmark range of the hessian order [lm_bnd[r], lm_bnd[r+1]),
+  // empty: the uniform split. The landmarks' hessian order is then grouped by rank (ivmap / hidx renumbered).
+  std::vector<int> lm_bnd;
+  bool dist_aligned = false;
+  std::vector<int> al_bpinv, al_bowner;  // the cut's pattern: pose block -> permuted block, permuted block -> owner
+  std::vector<unsigned char> lam_own_h;  // per pose: this rank adds lambda to its diagonal block of S
+  DevBuf<unsigned char> d_lam_own;
+  void align_shards();
+  void schur_pattern(std::vector<int>& sbi, std::vector<int>& sbj, std::vector<int>& srow_ptr) const;
+  std::vector<double> pose_work() const;
 
   // device state
   DevBuf<double> dstate[NVT];

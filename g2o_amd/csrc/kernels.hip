@@ -436,7 +436,8 @@ __global__ void __launch_bounds__(256)
                  const int* __restrict__ obs_lm, int lm0, const double* __restrict__ Hpl,
                  const double* __restrict__ Ufac, const double* __restrict__ cl_all, const int* __restrict__ sdiag,
                  const int* __restrict__ s_hpp, const double* __restrict__ Hpp, const double* __restrict__ b,
-                 const double* __restrict__ lam, double* __restrict__ S, double* __restrict__ bschur,
+                 const double* __restrict__ lam, const unsigned char* __restrict__ lam_own,
+                 const double* __restrict__ lam_full, double* __restrict__ S, double* __restrict__ bschur,
                  double* __restrict__ G) {
   constexpr int GB = PD * LD, UF = LmTraits<LD>::UF, NPK = PD * (PD + 1) / 2, NA = NPK + PD;
   static_assert(GB % 2 == 0 && UF % 2 == 0, "16-byte block loads");
@@ -514,7 +515,9 @@ __global__ void __launch_bounds__(256)
   int cc = 0, r = tid;  // packed upper index tid -> (r, cc), r <= cc
   while (r > cc) { r -= cc + 1; ++cc; }
   const double h0 = hp >= 0 ? Hh[cc * PD + r] : 0.0;
-  const double o = (r == cc ? h0 + *lam : h0) - v;
+  // lambda on the diagonal: by the rank lam_own names for this row (aligned shards), else lam (rank 0's lambda)
+  const double lv = lam_own ? (lam_own[row] ? *lam_full : 0.0) : *lam;
+  const double o = (r == cc ? h0 + lv : h0) - v;
   So[cc * PD + r] = o;
   So[r * PD + cc] = o;
 }
@@ -605,13 +608,16 @@ constexpr int SCH_PPB = SCH_SL + 1;       // slot-CSR entries per batch
 constexpr int SCH_NI = (SCH_SB + 255) / 256;
 }  // namespace
 
-// P3 (default): three index buffers, so a batch's indices are loaded one whole iteration before they are stored to LDS,
-// and one raw barrier per batch that waits only for the batch's G blocks (counted vmcnt: the younger index loads stay
-// in flight); !P3: two index buffers, the index loads drained by each batch's __syncthreads (G2OHIP_SCHUR_PIPE=0, A/B)
-template <int PD, int LD, bool P3>
+// PIPE 1 (default): three index buffers, so a batch's indices are loaded one whole iteration before they are stored to
+// LDS, and one raw barrier per batch that waits only for the batch's G blocks (counted vmcnt: the younger index loads
+// stay in flight); PIPE 0: two index buffers, the index loads drained by each batch's __syncthreads
+// (G2OHIP_SCHUR_PIPE=0, A/B). A variant issuing the next batch's staging right after the barrier and storing the
+// indices behind the products (two register sets, the staging as inline assembly) measured the same (C4 142 vs 139 us,
+// profiles/r04_ab_schur_pipe2.log) and was dropped.
+template <int PD, int LD, int PIPE>
 __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
-                 const int* __restrict__ st_obs, const int* __restrict__ pairs, const int* __restrict__ pp,
+                 const int* st_obs, const int* pairs, const int* pp,
                  const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,
                  double* __restrict__ S, int mode, int ntasks, const long long* __restrict__ zr,
                  double* __restrict__ fronts) {
@@ -621,7 +627,7 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
   constexpr int CW = (PD + 1) / 2;                   // output columns (and rows) per half
   static_assert(SCH_SB * NPC % 64 == 0, "a wave's LDS-DMA pieces must tile the batch image");
   __shared__ __attribute__((aligned(16))) double Gs[2][SCH_SB * GB];
-  constexpr int NIB = P3 ? 3 : 2;  // index buffers
+  constexpr int NIB = PIPE ? 3 : 2;  // index buffers
   __shared__ int so[NIB][SCH_SB];  // staged observation per block
   __shared__ int sp[NIB][SCH_SB];  // pair lists (posA | posB << 16), slot-sorted
   __shared__ int spp[NIB][SCH_PPB];
@@ -671,8 +677,12 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     }
   };
   auto compute = [&](int buf, int ib) { schur_pairs<PD, LD>(Gs[buf], sp[ib], spp[ib], t.noff, ls, q, acc); };
+  // index loads the pipelined passes count with vmcnt. Their pointers are not __restrict__ and every counted wait is
+  // an inline-assembly memory clobber, so the compiler can neither sink them below the wait nor hoist them above the
+  // staging (read-only restrict loads may move across assembly and barriers).
+  auto vld = [](const int* p) { return *p; };
 
-  if constexpr (P3) {
+  if constexpr (PIPE == 1) {
     // Invariant at the top of iteration k: Gs[k&1] holds batch k (landed), index buffers k%3 and (k+1)%3 hold batches
     // k and k+1 (visible), ov / pv / ppv hold batch k+2's indices (loads issued during iteration k-1, the youngest
     // vector-memory operations then), B1 / B3 the records k+1 / k+3.
@@ -684,10 +694,10 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
 #pragma unroll
       for (int u = 0; u < SCH_NI; ++u) {
         const int i = tid + 256 * u;
-        ov[u] = st_obs[i < B.nst ? B.st0 + i : 0];
-        pv[u] = pairs[i < B.npr ? B.pr0 + i : 0];
+        ov[u] = vld(st_obs + (i < B.nst ? B.st0 + i : 0));
+        pv[u] = vld(pairs + (i < B.npr ? B.pr0 + i : 0));
       }
-      ppv = pp[tid < SCH_PPB ? (t.b0 + k) * SCH_PPB + tid : 0];
+      ppv = vld(pp + (tid < SCH_PPB ? (t.b0 + k) * SCH_PPB + tid : 0));
       rpr0 = B.pr0;
     };
     auto idx_store3 = [&](int buf) {
@@ -1399,12 +1409,12 @@ void schur_prep(int ld, int nl, int lm0, const double* Hll, const double* bl_all
 int schur_ufac_stride(int ld) { return ld == 3 ? LmTraits<3>::UF : LmTraits<2>::UF; }
 void schur_diag(int pd, int ld, int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0,
                 const double* Hpl, const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp,
-                const double* Hpp, const double* b, const double* lam, double* S, double* bschur, double* G,
-                hipStream_t s) {
+                const double* Hpp, const double* b, const double* lam, const unsigned char* lam_own,
+                const double* lam_full, double* S, double* bschur, double* G, hipStream_t s) {
   if (nrows <= 0) return;
   pl_dispatch(pd, ld, [&](auto P, auto L) {
     hipLaunchKernelGGL((k_schur_diag<decltype(P)::value, decltype(L)::value>), nrows, 256, 0, s, nrows, rptr, robs,
-                       obs_lm, lm0, Hpl, Ufac, cl_all, sdiag, s_hpp, Hpp, b, lam, S, bschur, G);
+                       obs_lm, lm0, Hpl, Ufac, cl_all, sdiag, s_hpp, Hpp, b, lam, lam_own, lam_full, S, bschur, G);
   });
   KERNEL_CHECK();
 }
@@ -1413,15 +1423,16 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
                 int nzero, const long long* zr, double* fronts, hipStream_t s) {
   if (ntasks <= 0 && nzero <= 0) return;
   static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;  // dev A/B only
-  static const bool p3 = !(getenv("G2OHIP_SCHUR_PIPE") && atoi(getenv("G2OHIP_SCHUR_PIPE")) == 0);
+  static const int pipe = getenv("G2OHIP_SCHUR_PIPE") ? atoi(getenv("G2OHIP_SCHUR_PIPE")) : 1;
   const int nz = nzero > 0 ? nzero : 0;
   pl_dispatch(pd, ld, [&](auto P, auto L) {
-    if (p3)
-      hipLaunchKernelGGL((k_schur_rows<decltype(P)::value, decltype(L)::value, true>), ntasks + nz, 256, 0, s, tasks,
-                         batches, st_obs, pairs, pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
+    constexpr int pv = decltype(P)::value, lv = decltype(L)::value;
+    if (pipe == 0)
+      hipLaunchKernelGGL((k_schur_rows<pv, lv, 0>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs, pp, G, s_hpp,
+                         Hpp, S, mode, ntasks, zr, fronts);
     else
-      hipLaunchKernelGGL((k_schur_rows<decltype(P)::value, decltype(L)::value, false>), ntasks + nz, 256, 0, s, tasks,
-                         batches, st_obs, pairs, pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
+      hipLaunchKernelGGL((k_schur_rows<pv, lv, 1>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs, pp, G, s_hpp,
+                         Hpp, S, mode, ntasks, zr, fronts);
   });
   KERNEL_CHECK();
 }

@@ -44,6 +44,8 @@ struct SchurSplit {
   double lam_rank;       // lambda on S's diagonal (rank 0 only when sharded)
   const double* lamp;    // non-null: lam, lam_rank read from the device ([0], [1]) — the next iteration's assembly
                          // enqueued before the host knows the LM decision (lm_decide writes them)
+  const unsigned char* lam_own;  // non-null (aligned shards): per camera, this rank adds lambda (lam) to S(i,i)
+                                 // instead of lam_rank
   double* Ufac;          // per local landmark U record (6 doubles)
   double* cl;            // c = U^-1 b_l, global landmark index
   double* G;             // Hpl's block order
@@ -70,8 +72,8 @@ int schur_ufac_stride(int ld);  // doubles of the per-landmark U factor record
 // diagonal blocks + bschur (and G per observation): one workgroup per camera row over its observations (CSR rptr/robs)
 void schur_diag(int pd, int ld, int nrows, const int* rptr, const int* robs, const int* obs_lm, int lm0,
                 const double* Hpl, const double* Ufac, const double* cl_all, const int* sdiag, const int* s_hpp,
-                const double* Hpp, const double* b, const double* lam, double* S, double* bschur, double* G,
-                hipStream_t s);
+                const double* Hpp, const double* b, const double* lam, const unsigned char* lam_own,
+                const double* lam_full, double* S, double* bschur, double* G, hipStream_t s);
 // row-stationary off-diagonal Schur pass (k_schur_rows): task = (camera row, <= SCHUR_SL off-diagonal
 // slots), batch = <= SCHUR_SB staged observation blocks of the row's landmarks
 constexpr int SCHUR_SB = 128, SCHUR_SL = 64;  // 128: 4 workgroups per CU (LDS), 150 vs 172 us at C4

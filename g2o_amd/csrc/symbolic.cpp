@@ -307,6 +307,24 @@ struct NDState {
 
 }  // namespace
 
+BlockPattern block_pattern(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj) {
+  BlockPattern P;
+  P.nb = nblocks;
+  P.dim.assign(nblocks, bdim);
+  P.offset.resize(nblocks + 1);
+  for (int k = 0; k <= nblocks; ++k) P.offset[k] = k * bdim;
+  std::vector<int> deg(nblocks, 0);
+  for (size_t t = 0; t < bi.size(); ++t)
+    if (bi[t] != bj[t]) { deg[bi[t]]++; deg[bj[t]]++; }
+  P.adjp.assign(nblocks + 1, 0);
+  for (int k = 0; k < nblocks; ++k) P.adjp[k + 1] = P.adjp[k] + deg[k];
+  P.adji.assign(P.adjp[nblocks], 0);
+  std::vector<int> fill(P.adjp.begin(), P.adjp.end() - 1);
+  for (size_t t = 0; t < bi.size(); ++t)
+    if (bi[t] != bj[t]) { P.adji[fill[bi[t]]++] = bj[t]; P.adji[fill[bj[t]]++] = bi[t]; }
+  return P;
+}
+
 std::vector<int> nested_dissection(const BlockPattern& P, int leaf_size, bool refine, bool windows, bool part_degree,
                                    int band_leaf, std::vector<int>* groups) {
   NDState st(P, std::max(leaf_size, 1), refine, windows, part_degree || windows);
@@ -617,6 +635,160 @@ Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, in
   S.levels.assign(S.num_levels, {});
   for (int s = 0; s < ns_count; ++s) S.levels[S.sn[s].level].push_back(s);
   return S;
+}
+
+DistPlan plan_distribution(const Symbolic& sym, const std::vector<int>& bi, const std::vector<int>& bj, int bdim,
+                           int nblocks, int nranks, int rank, bool reduce_scatter, bool force, bool aligned,
+                           const std::vector<double>* pose_work) {
+  DistPlan P;
+  if (nranks <= 1) return P;
+  const int nsn = (int)sym.sn.size(), N = nranks;
+  std::vector<double> fl(nsn), chain(nsn), st(nsn);
+  for (int k = 0; k < nsn; ++k) {
+    const double m = sym.sn[k].ns + sym.sn[k].nr;
+    double f = 0;
+    for (int c = 0; c < sym.sn[k].ns; ++c) f += (m - c) * (m - c);
+    fl[k] = f;
+    chain[k] = ((sym.sn[k].ns + 31) / 32) * dist_cost::STEP_S;
+    st[k] = std::max(chain[k], f / dist_cost::TILE_FLOPS);
+  }
+  for (int k = 0; k < nsn; ++k)  // children precede parents (postorder): subtree serial work
+    if (sym.sn[k].parent >= 0) st[sym.sn[k].parent] += st[k];
+  // a set of fronts run level by level: per level the longer of its longest panel chain and its flops at the tile rate
+  auto levels_time = [&](const std::vector<int>& owner, int who) {
+    double t = 0;
+    for (const auto& lv : sym.levels) {
+      double ch = 0, f = 0;
+      bool any = false;
+      for (int sn : lv)
+        if (owner[sn] == who) { any = true; ch = std::max(ch, chain[sn]); f += fl[sn]; }
+      if (any) t += std::max(ch, f / dist_cost::TILE_FLOPS) + dist_cost::LEVEL_S;
+    }
+    return t;
+  };
+  auto allreduce_time = [&](double doubles) {
+    return dist_cost::ALLREDUCE_LAT_S + 2.0 * (N - 1) / N * 8.0 * doubles / dist_cost::ALLREDUCE_BW;
+  };
+  auto segments_time = [&](double seg) {  // all-gather / reduce-scatter of N segments of `seg` doubles
+    return dist_cost::ALLREDUCE_LAT_S + (N - 1) * 8.0 * seg / dist_cost::ALLREDUCE_BW;
+  };
+  // the reduced system's own communication: one all-reduce of every block + rhs when replicated; with reduce_scatter a
+  // reduce-scatter of the blocks each rank's subtrees read (segments padded to the largest) + an all-reduce of the
+  // shared blocks and the rhs. Blocks per supernode: a block lands in the front of its smaller permuted column.
+  const double bb = (double)bdim * bdim;
+  std::vector<double> sn_blocks(nsn, 0.0);
+  for (size_t t = 0; t < bi.size(); ++t) sn_blocks[sym.block_sn[std::min(sym.bpinv[bi[t]], sym.bpinv[bj[t]])]] += 1.0;
+  const double ar_full = allreduce_time(bi.size() * bb + (double)nblocks * bdim);
+  auto input_cost = [&](const std::vector<int>& owner, long long& seg, long long& tail) {
+    if (!reduce_scatter) { seg = 0; tail = (long long)(bi.size() * bb) + (long long)nblocks * bdim; return ar_full; }
+    std::vector<double> ob(N + 1, 0.0);
+    for (int k = 0; k < nsn; ++k) ob[owner[k] >= 0 ? owner[k] : N] += sn_blocks[k];
+    tail = (long long)(ob[N] * bb) + (long long)nblocks * bdim;
+    if (aligned) {  // subtree blocks complete where they are read (blocks written by pose-pose edges aside)
+      seg = 0;
+      return allreduce_time((double)tail);
+    }
+    seg = (long long)(*std::max_element(ob.begin(), ob.begin() + N) * bb);
+    return segments_time((double)seg) + allreduce_time((double)tail);
+  };
+  // sharded work per supernode (its pose blocks' observations) and in total
+  std::vector<double> sn_work(nsn, 0.0);
+  double work_all = 0;
+  if (pose_work)
+    for (int b = 0; b < nblocks && b < (int)pose_work->size(); ++b) {
+      sn_work[sym.block_sn[sym.bpinv[b]]] += (*pose_work)[b];
+      work_all += (*pose_work)[b];
+    }
+  auto shard_cost = [&](const std::vector<int>& owner) {
+    if (!aligned) return work_all / N;  // uniform split of the landmark order
+    std::vector<double> w(N, 0.0);
+    double sh = 0;
+    for (int k = 0; k < nsn; ++k) (owner[k] >= 0 ? w[owner[k]] : sh) += sn_work[k];
+    return *std::max_element(w.begin(), w.end()) + sh / N;
+  };
+  std::vector<int> none(nsn, -2);  // the replicated model: every front in one set
+  P.shard_repl_s = work_all / N;
+  P.repl_s = levels_time(none, -2) + ar_full + P.shard_repl_s;
+  P.input_repl_s = ar_full;
+  std::vector<int> cand;
+  for (int k = 0; k < nsn; ++k)
+    if (sym.sn[k].parent < 0) cand.push_back(k);
+  std::vector<char> shared(nsn, 0);
+  std::vector<int> owner(nsn);
+  double best = 1e30;
+  for (;;) {
+    int arg = -1;
+    for (size_t i = 0; i < cand.size(); ++i)
+      if (sym.children_ptr[cand[i] + 1] > sym.children_ptr[cand[i]] && (arg < 0 || st[cand[i]] > st[cand[arg]])) arg = (int)i;
+    if (arg < 0 || (int)cand.size() >= 4 * N) break;
+    const int c = cand[arg];
+    shared[c] = 1;
+    cand.erase(cand.begin() + arg);
+    for (int ci = sym.children_ptr[c]; ci < sym.children_ptr[c + 1]; ++ci) cand.push_back(sym.children[ci]);
+    if (cand.size() < 2) continue;
+    std::vector<int> srt(cand);
+    std::sort(srt.begin(), srt.end(), [&](int a, int b) { return st[a] > st[b] || (st[a] == st[b] && a < b); });
+    std::vector<double> load(N, 0.0), xr(N, 0.0);
+    std::vector<int> sub_owner(nsn, -1);
+    for (int s : srt) {
+      const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      load[r] += st[s];
+      sub_owner[s] = r;
+      const double nr = sym.sn[s].nr;
+      xr[r] += nr * (nr + 1) / 2 + nr;  // the root's contribution block (lower triangle) and update vector
+    }
+    for (int k = nsn - 1; k >= 0; --k)  // parents after children: walk down from the subtree roots
+      owner[k] = shared[k] ? -1 : sub_owner[k] >= 0 ? sub_owner[k] : owner[sym.sn[k].parent];
+    double tr = 0;
+    for (int r = 0; r < N; ++r) tr = std::max(tr, levels_time(owner, r));
+    const long long xseg = (long long)*std::max_element(xr.begin(), xr.end());
+    const double ts = levels_time(owner, -1), tx = segments_time((double)xseg) + allreduce_time(sym.n + 1.0);
+    long long seg = 0, tail = 0;
+    const double ti = input_cost(owner, seg, tail), tw = shard_cost(owner);
+    if (tr + ts + tx + ti + tw < best) {
+      best = tr + ts + tx + ti + tw;
+      P.shard_s = tw;
+      P.owner = owner;
+      P.rank_s = levels_time(owner, rank);
+      P.max_rank_s = tr;
+      P.shared_s = ts;
+      P.xch_s = tx;
+      P.input_s = ti;
+      P.xch_seg = xseg;
+      P.rs_seg = seg;
+      P.tail = tail;
+    }
+  }
+  P.on = !P.owner.empty() && (force || best < P.repl_s);
+  return P;
+}
+
+std::vector<int> align_landmarks(const Symbolic& sym, const std::vector<int>& sn_owner, int nranks,
+                                 const std::vector<int>& lm_ptr, const std::vector<int>& lm_cams) {
+  const int nl = (int)lm_ptr.size() - 1;
+  std::vector<int> own(std::max(nl, 0), -1);
+  std::vector<long long> load(nranks, 0);
+  std::vector<int> later;
+  for (int l = 0; l < nl; ++l) {
+    int first = -1;
+    for (int a = lm_ptr[l]; a < lm_ptr[l + 1]; ++a) {
+      const int p = sym.bpinv[lm_cams[a]];
+      if (first < 0 || p < first) first = p;
+    }
+    const int o = first >= 0 ? sn_owner[sym.block_sn[first]] : -1;
+    if (o >= 0) {
+      own[l] = o;
+      load[o] += lm_ptr[l + 1] - lm_ptr[l];
+    } else {
+      later.push_back(l);
+    }
+  }
+  for (int l : later) {
+    const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    own[l] = r;
+    load[r] += std::max(lm_ptr[l + 1] - lm_ptr[l], 1);
+  }
+  return own;
 }
 
 }  // namespace g2ohip

@@ -60,6 +60,10 @@ struct Symbolic {
   int band_leaf = 0;               // ordering parameter that produced this analysis (0: plain nested dissection)
 };
 
+// Block pattern of a symmetric matrix given by its upper blocks (bi <= bj) of a uniform block size, adjacency in the
+// order the blocks are listed (the order DeviceCholesky::setup analyses).
+BlockPattern block_pattern(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj);
+
 // Nested-dissection ordering of the block graph. leaf_size: subgraphs at most this
 // large are ordered by minimum degree; refine: greedy separator refinement after each bisection.
 // band_leaf > 0: parts of at most band_leaf blocks whose BFS level structure is a long band (at least 3 levels deep)
@@ -79,5 +83,53 @@ double gpu_cost(const Symbolic& S);
 // elimination tree are amalgamated into one band supernode regardless of the relaxation limits.
 Symbolic analyze(const BlockPattern& P, std::vector<int> bperm = {}, double relax = 0.25, int relax_max_blocks = 64,
                  const std::vector<int>* groups = nullptr);
+
+// ---- distribution of the factorization over ranks (landmark-sharded BA)
+// Cost model of the cut, calibrated on C4 / C5 (rank schedules timed alone on one GPU, tools/dist_factor_time.py): a
+// 32-column panel step on the chain, the panel steps' tile rate, a level's fixed launches, and collectives over xGMI
+// (latency + bus bandwidth; ring traffic 2 (N-1)/N of the buffer for an all-reduce, (N-1) segments for an all-gather
+// or reduce-scatter).
+namespace dist_cost {
+constexpr double STEP_S = 10e-6, TILE_FLOPS = 12e12, LEVEL_S = 20e-6, ALLREDUCE_LAT_S = 30e-6, ALLREDUCE_BW = 120e9;
+// landmark-sharded work per observation (BA: linearize, camera pass, Schur rows, back-substitution, chi2): C4 0.35 ms
+// for 1 M observations, C5 2.7 ms for 10 M (r04 stage times)
+constexpr double OBS_S = 0.3e-9;
+}
+
+struct DistPlan {
+  std::vector<int> owner;  // per supernode: owning rank, -1 shared (every rank); empty: no candidate cut
+  bool on = false;         // the best cut beats the replicated factorization's model (or force)
+  // modelled seconds: the given rank's subtrees, the shared top, the replicated factorization, the cut's exchanges
+  // (root all-gather + x all-reduce), the input (reduce-scatter + tail all-reduce, or the whole all-reduce), the
+  // replicated input (whole all-reduce), the slowest rank's subtrees
+  double rank_s = 0, shared_s = 0, repl_s = 0, xch_s = 0, input_s = 0, input_repl_s = 0, max_rank_s = 0;
+  // modelled seconds of the landmark-sharded assembly / Schur / back-substitution on the busiest rank: with aligned
+  // shards each rank's share follows its subtrees (the shared poses' spread evenly), replicated the uniform split
+  double shard_s = 0, shard_repl_s = 0;
+  long long xch_seg = 0;   // doubles per rank of the root all-gather (the largest rank's roots)
+  long long rs_seg = 0;    // doubles per rank of the input reduce-scatter (the largest rank's blocks), 0 without
+  long long tail = 0;      // doubles of the input's tail all-reduce (shared blocks + rhs)
+};
+
+// Chooses the cut of the elimination tree of the block pattern (bi, bj: upper blocks of `nblocks` blocks of size bdim,
+// analysed into sym) for `nranks` ranks: candidate cuts split the candidate subtree with the largest serial work (its
+// root joins the shared top), up to 4 candidates per rank, subtrees to ranks largest first; the cheapest cut by the
+// model above is kept. reduce_scatter: the input is reduce-scattered by subtree ownership (else one all-reduce);
+// aligned: the landmark shards follow the cut (align_landmarks), so a rank's subtree blocks are complete on that rank
+// and only the shared blocks and the rhs are reduced (one all-reduce).
+// pose_work (optional, per pose block of the pattern, seconds): the landmark-sharded work that follows the pose (its
+// observations), added to every candidate as the busiest rank's share.
+DistPlan plan_distribution(const Symbolic& sym, const std::vector<int>& bi, const std::vector<int>& bj, int bdim,
+                           int nblocks, int nranks, int rank, bool reduce_scatter, bool force, bool aligned = false,
+                           const std::vector<double>* pose_work = nullptr);
+
+// Landmark shards aligned with a cut: landmark l, observing the pose blocks lm_cams[lm_ptr[l] ..
+// lm_ptr[l+1]) of the pattern, goes to the rank owning the supernode of its first-eliminated pose. Its poses form a
+// clique of the pattern, so every other one is eliminated in an ancestor of that supernode: all of l's Schur blocks
+// land in that rank's subtrees or in the shared top, and no other rank writes a block of that rank's subtrees. A
+// landmark whose poses are all shared goes to the rank with the fewest observations so far (landmark order).
+// Landmarks without free poses go to the least-loaded rank as well. Returns the rank per landmark.
+std::vector<int> align_landmarks(const Symbolic& sym, const std::vector<int>& sn_owner, int nranks,
+                                 const std::vector<int>& lm_ptr, const std::vector<int>& lm_cams);
 
 }  // namespace g2ohip

@@ -181,15 +181,24 @@ int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel);
 /* Symbolic / schedule summary of the device factorization: out[0..20] = n, nnz(L), flops (this ordering),
  * supernodes, tree levels, largest front, blocked fronts, levels assembled in place, pre-scattered levels,
  * trailing-update launches, big-panel backward rounds, out[11] = 0 (retired slot), and for landmark
- * shards (nranks > 1) this rank's fronts, the shared fronts, the subtree roots, the doubles of the root exchange, the
- * cost model of the best cut of the elimination tree (modelled seconds of this rank's subtrees, of the shared top, of
- * the replicated factorization, of the cut's two all-reduces) and whether the factorization is distributed (1) or
+ * shards (nranks > 1) this rank's fronts, the shared fronts, the subtree roots, the doubles of the root exchange
+ * buffer (nranks all-gathered segments), the cost model of the best cut of the elimination tree (modelled seconds of
+ * this rank's subtrees, of the shared top, of the replicated factorization, of the cut's exchanges: root all-gather and
+ * x all-reduce) and whether the factorization is distributed (1) or
  * replicated (0: the model preferred replication, or G2OHIP_DIST_FACTOR=0); then out[21..25] = whether the reduced
  * system is reduce-scattered by subtree ownership (1) instead of all-reduced, its per-rank segment and all-reduced tail
  * (doubles), and the modelled seconds of that input exchange and of the plain all-reduce; out[26] = 0 (retired slot);
- * out[27] = the band-leaf size of the ordering (blocks; 0: plain nested dissection). Returns the number of entries
- * available. */
+ * out[27] = the band-leaf size of the ordering (blocks; 0: plain nested dissection); out[28] = 1 when the landmark
+ * shards are aligned with the cut (each landmark on the rank whose subtrees its Schur blocks land in, G2OHIP_DIST_ALIGN),
+ * out[29] = doubles of this rank's subtree blocks read from its own partial reduced system (never exchanged), out[30] =
+ * bytes this rank sends per LM trial through the reduced system's and the factorization's collectives (ring
+ * algorithms), out[31] = free landmarks in this rank's shard, out[32] = the modelled sharded work (s) of the busiest
+ * rank under this layout. Returns the number of entries available. */
 int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n);
+/* Landmark shards (g2ohip_set_comm / _set_comm_local): the ids of the free landmarks this rank holds (their estimates
+ * are current on this rank only); ids may be NULL. Returns the count. With the distributed factorization the shards
+ * follow its cut (not id ranges); otherwise they are contiguous ranges of the landmark order. */
+int g2ohip_local_landmarks(g2ohip_graph* g, int* ids, int cap);
 /* Solver::computeMarginals (core/solver.h:108; BlockSolver::computeMarginals block_solver.hpp:451-460 ->
  * LinearSolverCSparse::solvePattern linear_solver_csparse.h:190-225, MarginalCovarianceCholesky): the pose-block
  * entries (block_rows[k], block_cols[k]) (Hessian indices) of Hpp^-1, Hpp as the last build_system left it (no
@@ -228,7 +237,7 @@ int g2ohip_linear_solve_ccs(int device, int n, const int* Ap, const int* Ai, con
 
 /* ---- multi-GPU (landmark sharding + RCCL all-reduce of the reduced camera system) ---- */
 int g2ohip_comm_unique_id(unsigned char out[128]);
-/* this rank keeps landmark shard `rank` of `nranks` (contiguous ranges of the point order) */
+/* this rank keeps landmark shard `rank` of `nranks` (g2ohip_local_landmarks lists it) */
 int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int nranks);
 /* Test transport: `nranks` graphs in ONE process (one host thread each, same GPU) that share
  * `group_key` reduce through host memory in rank order instead of RCCL. Same sharding, same
@@ -258,6 +267,16 @@ int g2ohip_device_synchronize(int device);
  * size bdim: returns n = nblocks*bdim, fills perm[n] (new -> old scalar) and
  * stats[5] = {nnz(L), factor flops, #supernodes, #levels, level-synchronous 32-column panel steps}. */
 int g2ohip_symbolic_analyze(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int* perm, double* stats);
+/* Host-only: the distributed factorization's cut for `nranks` landmark shards of the same block pattern (DESIGN.md §6,
+ * the model the solver's setup runs; flags: 1 the input is reduce-scattered by subtree ownership, 2 the landmark shards
+ * are aligned with the cut; pose_work, optional: per pose block the seconds of landmark-sharded work that follow it).
+ * out[14] = {distributed (the cut beats the replicated model), this rank's subtrees s, shared top s, replicated
+ * iteration s (factorization + whole-S all-reduce + uniform sharded work), exchanges s (root all-gather + x
+ * all-reduce), input s, replicated input s, slowest rank's subtrees s, root all-gather doubles per rank, input
+ * reduce-scatter doubles per rank, input tail all-reduce doubles, supernodes, busiest rank's sharded work s, uniform
+ * sharded work s}; sn_owner (cap entries, optional): per supernode its rank, -1 shared. Returns the supernodes. */
+int g2ohip_dist_plan(int nblocks, int bdim, int nblk, const int* bi, const int* bj, int nranks, int rank,
+                     int flags, const double* pose_work, double* out, int* sn_owner, int cap);
 
 /* ---- measurement hooks ---- */
 void g2ohip_enable_kernel_timing(g2ohip_graph* g, int on);

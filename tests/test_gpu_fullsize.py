@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 
 from g2o_amd import synth
+from shard_util import gather_sharded_state
 
 pytestmark = pytest.mark.gpu
 
@@ -258,12 +259,17 @@ def test_c5_full_sharded_8_ranks(g2o_amd_mod):
     for r in range(nranks):
         n, st = res[r]
         _check_trajectory(fx, st, n)
-    C, P = prob.vertices[0].ids.size, prob.vertices[1].ids.size
-    states = [o.minimal_state() for o in opts]
-    x = states[0].copy()
-    for r in range(nranks):
-        a, b = P * r // nranks, P * (r + 1) // nranks
-        x[6 * C + 3 * a: 6 * C + 3 * b] = states[r][6 * C + 3 * a: 6 * C + 3 * b]
+    info = [o.factor_info() for o in opts]
+    for r, i in enumerate(info):  # the layout the cost model chose, per rank
+        print(f"rank {r}: distributed {int(i['distributed'])} aligned {int(i['aligned_shards'])} owned fronts "
+              f"{int(i['owned_fronts'])} landmarks {int(i['local_landmarks'])} exchange {i['exchange_bytes_per_rank'] / 1e6:.2f} MB"
+              f" (rs segment {int(i['rs_segment_doubles'])}, tail {int(i['rs_tail_doubles'])}, local "
+              f"{int(i['local_block_doubles'])} doubles), model: subtrees {i['model_rank_subtrees_s'] * 1e3:.3f} ms, "
+              f"shared {i['model_shared_s'] * 1e3:.3f} ms, exchanges {i['model_exchange_s'] * 1e3:.3f} ms, input "
+              f"{i['model_input_s'] * 1e3:.3f} ms, sharded work {i['model_shard_s'] * 1e3:.3f} ms")
+    assert sum(i["local_landmarks"] for i in info) == prob.vertices[1].ids.size
+    C = prob.vertices[0].ids.size
+    x, states = gather_sharded_state(prob, opts)
     for s in states[1:]:
         assert np.array_equal(s[:6 * C], states[0][:6 * C])  # every rank factors the same reduced system
     _check_c5_state(prob, x, fx)

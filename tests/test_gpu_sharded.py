@@ -3,6 +3,7 @@ through the in-process test transport (g2ohip_set_comm_local) exactly where the 
 calls RCCL (reduced camera system + bschur, chi2, scale, lambda-init max).  Every rank runs the
 same LM decisions; its own landmark shard and the (replicated) cameras must match the
 single-GPU run and the oracle within the north_star tolerance."""
+import os
 import threading
 import uuid
 
@@ -10,8 +11,10 @@ import numpy as np
 import pytest
 
 from g2o_amd import synth
+from shard_util import gather_sharded_state
 
 pytestmark = pytest.mark.gpu
+os.environ.setdefault("G2OHIP_COMM_CHECK", "1")  # RcclComm verifies every collective's (call, length, op) across ranks
 
 RTOL = 1e-6
 
@@ -41,17 +44,7 @@ def _run_sharded(g2o_amd_mod, prob, nranks, iters, algo=None):
 
 
 def _gather_state(prob, opts):
-    """cameras from rank 0 (identical on all ranks), landmarks from their owning shard
-    (contiguous ranges of the landmark order, engine.cpp setup_edges_device)."""
-    C = prob.vertices[0].ids.size
-    P = prob.vertices[1].ids.size
-    n = len(opts)
-    states = [o.minimal_state() for o in opts]
-    out = states[0].copy()
-    for r in range(n):
-        a, b = P * r // n, P * (r + 1) // n
-        out[6 * C + 3 * a: 6 * C + 3 * b] = states[r][6 * C + 3 * a: 6 * C + 3 * b]
-    return out, states
+    return gather_sharded_state(prob, opts)
 
 
 @pytest.mark.parametrize("nranks", [2, 3])
@@ -136,22 +129,35 @@ def test_rccl_binding_single_rank(g2o_amd_mod):
     assert np.array_equal(s, v) and np.array_equal(m, v) and np.array_equal(r, v)
 
 
-@pytest.mark.parametrize("name,nranks", [("C5", 2), ("C5", 3), ("mid", 4), ("mid", 7)])
-def test_distributed_factorization(g2o_amd_mod, oracle, monkeypatch, name, nranks):
+@pytest.mark.parametrize("name,nranks,aligned", [("C5", 2, True), ("C5", 3, True), ("mid", 4, True), ("mid", 7, True),
+                                                 ("C5", 3, False), ("mid", 4, False)])
+def test_distributed_factorization(g2o_amd_mod, oracle, monkeypatch, name, nranks, aligned):
     """The distributed factorization: the elimination tree cut into per-rank subtrees and a shared top,
-    the subtree roots' contribution blocks exchanged in one all-reduce, x in another. Against the replicated
-    factorization (G2OHIP_DIST_FACTOR=0: every rank factors all of S), the single-GPU run and the oracle.
-    G2OHIP_DIST_FACTOR=1 forces the cut at these sizes (unset, the cost model decides per tree)."""
+    the subtree roots' contribution blocks exchanged in one all-gather, x in one all-reduce. Against the replicated
+    factorization (G2OHIP_DIST_FACTOR=0: every rank factors all of S, landmarks split uniformly), the single-GPU run
+    and the oracle. G2OHIP_DIST_FACTOR=1 forces the cut at these sizes (unset, the cost model decides per tree).
+    aligned (the default): the landmark shards follow the cut, so a rank's subtree blocks are complete on that rank
+    and only the shared tail is reduced; G2OHIP_DIST_ALIGN=0: uniform shards, the subtree blocks reduce-scattered."""
     prob = synth.by_name(name, "small") if name != "mid" else synth.ba(400, 20000)
     iters = 4
     monkeypatch.setenv("G2OHIP_DIST_FACTOR", "1")  # the best cut even where the cost model would replicate
+    monkeypatch.setenv("G2OHIP_DIST_ALIGN", "1" if aligned else "0")
     opts, res = _run_sharded(g2o_amd_mod, prob, nranks, iters)
     info = [o.factor_info() for o in opts]
     assert all(i["distributed"] == 1 for i in info), info
     assert sum(i["owned_fronts"] for i in info) + info[0]["shared_fronts"] == info[0]["supernodes"], info
     assert info[0]["subtree_roots"] > 0 and info[0]["root_exchange_doubles"] > 0, info[0]
-    # the reduced system reaches each rank as a reduce-scatter of the blocks its subtrees read + the shared tail
-    assert all(i["reduce_scatter"] == 1 and i["rs_segment_doubles"] > 0 and i["rs_tail_doubles"] > 0 for i in info), info
+    assert all(i["aligned_shards"] == (1 if aligned else 0) for i in info), info
+    assert sum(i["local_landmarks"] for i in info) == prob.vertices[1].ids.size, info
+    assert all(i["exchange_bytes_per_rank"] > 0 for i in info), info
+    if aligned:
+        # every block of a rank's subtrees is complete on that rank (BA: no pose-pose edges): only the shared tail and
+        # the rhs are reduced
+        assert all(i["reduce_scatter"] == 1 and i["rs_segment_doubles"] == 0 and i["rs_tail_doubles"] > 0 for i in info)
+        assert all(i["local_block_doubles"] > 0 for i in info if i["owned_fronts"] > 0), info
+    else:
+        # the reduced system reaches each rank as a reduce-scatter of the blocks its subtrees read + the shared tail
+        assert all(i["reduce_scatter"] == 1 and i["rs_segment_doubles"] > 0 and i["rs_tail_doubles"] > 0 for i in info)
     x, states = _gather_state(prob, opts)
     C = prob.vertices[0].ids.size
     for s in states[1:]:
@@ -184,6 +190,7 @@ def test_distributed_reduce_scatter_equals_allreduce(g2o_amd_mod, monkeypatch):
     LocalComm sums are rank-ordered in both, so the trajectories agree bitwise."""
     prob = synth.by_name("C5", "small")
     monkeypatch.setenv("G2OHIP_DIST_FACTOR", "1")
+    monkeypatch.setenv("G2OHIP_DIST_ALIGN", "0")  # the same (uniform) shards in both runs
     opts, res = _run_sharded(g2o_amd_mod, prob, 3, 3)
     assert all(o.factor_info()["reduce_scatter"] == 1 for o in opts)
     monkeypatch.setenv("G2OHIP_DIST_RS", "0")

@@ -142,6 +142,31 @@ def test_symbolic_band_leaves(g2o_amd_mod, monkeypatch, leaf):
     assert st["supernodes"] < st0["supernodes"] or st["flops"] <= st0["flops"], (st, st0)
 
 
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_dist_plan_model(g2o_amd_mod, nranks):
+    """The distributed factorization's cut (plan_distribution, the model DeviceCholesky::setup and the landmark
+    alignment run) on a 400-camera BA pattern: every supernode owned by a rank or shared; aligned shards
+    reduce only the shared tail (no reduce-scattered segment) and never cost more input than uniform shards; the
+    replicated alternative is priced with the same sharded work."""
+    prob = synth.ba(num_cameras=400, num_points=20000, obs_per_point=8, window=40)
+    nb, bi, bj = _schur_pattern(prob)
+    pw = np.full(nb, 20000 * 8 / nb * 0.3e-9)
+    a, own_a = g2o_amd_mod.dist_plan(nb, prob.pose_dim, bi, bj, nranks, pose_work=pw)
+    u, own_u = g2o_amd_mod.dist_plan(nb, prob.pose_dim, bi, bj, nranks, aligned=False, pose_work=pw)
+    _, st = g2o_amd_mod.symbolic_analyze(nb, prob.pose_dim, bi, bj)
+    assert a["supernodes"] == u["supernodes"] == st["supernodes"] == own_a.size
+    for d, own in ((a, own_a), (u, own_u)):
+        assert np.all((own >= -1) & (own < nranks))
+        if (own >= 0).any():
+            assert (own < 0).any(), "a cut keeps at least the root shared"
+        assert d["shard_replicated_s"] == pytest.approx(pw.sum() / nranks)
+    assert a["rs_segment_doubles"] == 0 and a["rs_tail_doubles"] > 0
+    assert a["input_s"] <= u["input_s"] + 1e-12
+    # the aligned layout's chosen total is no worse than the uniform one's
+    tot = lambda d: d["max_rank_subtrees_s"] + d["shared_s"] + d["exchange_s"] + d["input_s"] + d["shard_s"]
+    assert tot(a) <= tot(u) + 1e-12 or not u["distributed"]
+
+
 def test_symbolic_disconnected_and_trivial(g2o_amd_mod):
     # three disconnected cliques + isolated blocks
     bi, bj = [], []

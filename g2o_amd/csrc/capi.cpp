@@ -329,14 +329,19 @@ int g2ohip_comm_selftest_rs(int device, const unsigned char uid[128], int n, con
     hipStream_t s = nullptr;
     HIP_CHECK(hipStreamCreate(&s));
     double* d = nullptr;
-    HIP_CHECK(hipMalloc(&d, sizeof(double) * 3 * (size_t)n));
-    for (int k = 0; k < 3; ++k) HIP_CHECK(hipMemcpyAsync(d + (size_t)k * n, in, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMalloc(&d, sizeof(double) * 4 * (size_t)n));
+    for (int k = 0; k < 4; ++k) HIP_CHECK(hipMemcpyAsync(d + (size_t)k * n, in, sizeof(double) * n, hipMemcpyHostToDevice, s));
     c->allreduce_sum(d, (size_t)n, s);
     c->allreduce_max(d + n, (size_t)n, s);
     c->reduce_scatter_sum(d + 2 * (size_t)n, (size_t)n, s);  // in place: rank r's segment is [r n, (r + 1) n)
+    c->allgather(d + 3 * (size_t)n, (size_t)n, s);           // in place: the distributed factorization's root exchange
     HIP_CHECK(hipMemcpyAsync(out, d, sizeof(double) * 2 * (size_t)n, hipMemcpyDeviceToHost, s));
     if (rs_out) HIP_CHECK(hipMemcpyAsync(rs_out, d + 2 * (size_t)n, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    std::vector<double> ag((size_t)n);
+    HIP_CHECK(hipMemcpyAsync(ag.data(), d + 3 * (size_t)n, sizeof(double) * n, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    if (std::memcmp(ag.data(), in, sizeof(double) * n) != 0)
+      throw g2ohip::DeviceError("ncclAllGather (in place, one rank) changed its segment");
     HIP_CHECK(hipFree(d));
     HIP_CHECK(hipStreamDestroy(s));
     c.reset();  // ncclCommDestroy

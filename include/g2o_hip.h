@@ -248,7 +248,8 @@ int g2ohip_set_comm_local(g2ohip_graph* g, const char* group_key, int rank, int 
  * [sum | max]. A one-GPU box cannot host two ranks of one RCCL communicator, so this is the binding's smoke test there. */
 int g2ohip_comm_selftest(int device, const unsigned char uid[128], int n, const double* in, double* out);
 /* As g2ohip_comm_selftest, plus the in-place reduce-scatter sum the distributed factorization uses: rs_out (n doubles)
- * = this rank's segment. (0.1.x wrote the segment as a third block of `out`; 0.2 restored the 2n contract above.) */
+ * = this rank's segment, and the in-place all-gather of its root exchange (checked internally: an error if the
+ * rank's own segment changes). (0.1.x wrote the segment as a third block of `out`; 0.2 restored the 2n contract.) */
 int g2ohip_comm_selftest_rs(int device, const unsigned char uid[128], int n, const double* in, double* out,
                             double* rs_out);
 /* The test transport's rank-ordered host reduction alone (no GPU): `nranks` host threads that share `group_key` each

@@ -121,8 +121,9 @@ def test_sharded_pcg_matches_single(g2o_amd_mod):
 
 
 def test_rccl_binding_single_rank(g2o_amd_mod):
-    """The RCCL transport itself (RcclComm: ncclGetUniqueId, ncclCommInitRank, ncclAllReduce sum / max and the in-place
-    ncclReduceScatter on a HIP stream, ncclCommDestroy) on a one-rank communicator: a one-GPU box cannot host two ranks of one RCCL
+    """The RCCL transport itself (RcclComm: ncclGetUniqueId, ncclCommInitRank, ncclAllReduce sum / max, the in-place
+    ncclReduceScatter and ncclAllGather on a HIP stream, with the G2OHIP_COMM_CHECK consistency all-reduce before each,
+    ncclCommDestroy) on a one-rank communicator: a one-GPU box cannot host two ranks of one RCCL
     communicator (RCCL refuses duplicate GPUs), so the multi-rank path is covered by the LocalComm tests above."""
     v = np.linspace(-3.0, 5.0, 1000)
     s, m, r = g2o_amd_mod.SparseOptimizer.comm_selftest(v)

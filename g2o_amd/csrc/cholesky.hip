@@ -312,7 +312,7 @@ template <bool ASM, int EAC>
 __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
                                                     const int* __restrict__ children, const int* __restrict__ relmap,
                                                     const int* __restrict__ jtab, const int* __restrict__ cmptr,
-                                                    const int2* __restrict__ cment, const int* __restrict__ colptr, const int* __restrict__ ent_row,
+                                                    const longlong2* __restrict__ cment, const int* __restrict__ colptr, const int* __restrict__ ent_row,
                                                     const int* __restrict__ ent_src, const double* __restrict__ vals,
                                                     const double* __restrict__ lam, double* __restrict__ fronts,
                                                     double* __restrict__ vecs, double* __restrict__ lbuf,
@@ -408,27 +408,45 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     // entries, then every (child, child column) pair mapping to it in child order) and writes each entry
     // of the front once; rows in chunks of EAC. The children's update vectors follow below.
     __shared__ double cbuf[4][EAC];
+    // per column its pair range (cmptr), input-entry range (colptr) and first pair record, loaded one column ahead
+    // (cment ends with a sentinel record, so cment[q0] is valid for an empty range)
+    struct ColMeta { int q0, q1, e0, e1; longlong2 f; };
+    auto meta = [&](int jj) {
+      ColMeta c;
+      c.q0 = cmptr[me.cm_off + jj];
+      c.q1 = cmptr[me.cm_off + jj + 1];
+      const bool inp = jj < me.ns;
+      c.e0 = inp ? colptr[me.c0 + jj] : 0;
+      c.e1 = inp ? colptr[me.c0 + jj + 1] : 0;
+      c.f = cment[c.q0];
+      return c;
+    };
+    ColMeta cur = a + w < b ? meta(a + w) : ColMeta{0, 0, 0, 0, longlong2{0, 0}};
     for (int j = a + w; j < b; j += 4) {
+      const ColMeta nxt = j + 4 < b ? meta(j + 4) : cur;
       const int rlo = j < kb0 ? kb0 : j;  // rows of the first diagonal block: block-0 task
       double* Fj = F + (size_t)j * m;
-      const int q0 = cmptr[me.cm_off + j], q1 = cmptr[me.cm_off + j + 1];
+      const int q0 = cur.q0, q1 = cur.q1;
       for (int rc = rlo; rc < m; rc += EAC) {
         const int rce = min(m, rc + EAC);
         double* cb = cbuf[w] - rc;
         for (int i = rc + lane; i < rce; i += 64) cb[i] = 0.0;
-        if (j < me.ns)
-          for (int e = colptr[me.c0 + j] + lane; e < colptr[me.c0 + j + 1]; e += 64) {
-            int r;
-            const double x = input_entry(vals, ent_src, ent_row, e, lam, r);
-            if (r >= rc && r < rce) cb[r] = x;
-          }
+        for (int e = cur.e0 + lane; e < cur.e1; e += 64) {
+          int r;
+          const double x = input_entry(vals, ent_src, ent_row, e, lam, r);
+          if (r >= rc && r < rce) cb[r] = x;
+        }
+        // one 16-byte record per pair (no dependent descriptor read), the next pair's record in flight while this
+        // pair's rows are added; a child's rows map to increasing parent rows, so a batch that starts past the chunk
+        // ends the pair
+        longlong2 nx = cur.f;
         for (int q = q0; q < q1; ++q) {
-          const int2 ce = cment[q];
-          const FrontDesc cd = fd[ce.x];
-          const int mc = cd.ns + cd.nr, nrc = cd.nr;
-          const double* Uj = fronts + cd.front_off + (size_t)(cd.ns + ce.y) * mc + cd.ns;
-          const int* rel = relmap + cd.rows_off;
-          for (int i0 = ce.y + lane; i0 < nrc; i0 += 256) {
+          const longlong2 ce = nx;
+          if (q + 1 < q1) nx = cment[q + 1];
+          const double* Uj = fronts + ce.x;
+          const int* rel = relmap + (int)(ce.y & 0x7fffffff);
+          const int y = (int)((ce.y >> 32) & 0xffff), nrc = (int)(ce.y >> 48);
+          for (int i0 = y + lane; i0 < nrc; i0 += 256) {
             double val[4];
             int ri[4];
 #pragma unroll
@@ -441,10 +459,12 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
 #pragma unroll
             for (int u = 0; u < 4; ++u)
               if (ri[u] >= rc && ri[u] < rce) cb[ri[u]] += val[u];
+            if (__builtin_amdgcn_readfirstlane(ri[0]) >= rce) break;  // lane 0 holds the batch's first (smallest) row
           }
         }
         for (int i = rc + lane; i < rce; i += 64) Fj[i] = cb[i];
       }
+      cur = nxt;
     }
     for (int k = me.child_begin; k < me.child_end; ++k) {  // update vectors, children in fixed order
       const FrontDesc cd = fd[children[k]];
@@ -1036,7 +1056,7 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
   }
 }
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
-                     const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
+                     const int* jtab, const int* cmptr, const longlong2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv,
                      int* fail, int assemble, hipStream_t s) {
   if (ntasks <= 0) return;
@@ -1045,6 +1065,7 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
                      colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, xinv, fail)
   // assemble 2: fronts up to 512 rows (a small column buffer keeps more workgroups per CU)
   if (assemble == 2) G2OHIP_EA(true, 512);
+  else if (assemble == 3) G2OHIP_EA(true, 1024);
   else if (assemble) G2OHIP_EA(true, 2048);
   else G2OHIP_EA(false, 1);
 #undef G2OHIP_EA

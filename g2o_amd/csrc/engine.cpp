@@ -384,7 +384,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   // per child: [#rows mapping into the parent's first diagonal block | first child row of every parent
   // slab] (rel is increasing), so the extend-add tasks need no search on the chain
   std::vector<int> hjt, hcmp;
-  std::vector<int2> hcme;
+  std::vector<longlong2> hcme;
   std::vector<launch::FrontDesc> hfd(sym.sn.size());
   long long loff = 0, xoff = 0;
   for (size_t k = 0; k < sym.sn.size(); ++k) {
@@ -414,7 +414,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       for (int ci = sym.children_ptr[k]; ci < sym.children_ptr[k + 1]; ++ci) {
         const int c = sym.children[ci];
         const Supernode& cq = sym.sn[c];
-        for (int jc = 0; jc < cq.nr; ++jc) hcme[base + fillc[sym.relmap[cq.rows_off + jc]]++] = int2{c, jc};
+        // per pair: its update-matrix column (child rows jc .. nr-1 at U + i), the child's relmap, jc and nr
+        const long long mc = cq.ns + cq.nr, u0 = cq.front_off + (cq.ns + 0) * mc + cq.ns;
+        if (cq.rows_off >= (1LL << 31) || cq.nr >= (1 << 16)) throw DeviceError("extend-add record overflow");
+        for (int jc = 0; jc < cq.nr; ++jc)
+          hcme[base + fillc[sym.relmap[cq.rows_off + jc]]++] =
+              longlong2{u0 + (long long)jc * mc, cq.rows_off | ((long long)jc << 32) | ((long long)cq.nr << 48)};
       }
       for (int j = 0; j <= m; ++j) hcmp.push_back(base + cnt[j]);
     }
@@ -427,7 +432,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   fd.upload(hfd, s);
   jtab.upload(hjt.empty() ? std::vector<int>{0} : hjt, s);
   cmptr.upload(hcmp.empty() ? std::vector<int>{0} : hcmp, s);
-  cment.upload(hcme.empty() ? std::vector<int2>{int2{0, 0}} : hcme, s);
+  hcme.push_back(longlong2{0, 0});  // sentinel: k_extend_add reads a column's first record even for an empty range
+  cment.upload(hcme, s);
   std::vector<int> ll;
   level_off.assign(1, 0);
   for (auto& lv : sym.levels) {
@@ -489,6 +495,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     // level, 183 -> 161 us; the 1- and 2-front levels are bound by the diagonal chain and lose ~6 us each)
     const char* lfm = getenv("G2OHIP_CHOL_LAG_FUSED_MIN");
     const long long lag_fused_min = lag_mode >= 2 ? 0 : (lfm ? atoll(lfm) : 256);
+    const char* eb = getenv("G2OHIP_EA_BIG");
+    const int ea_big = eb ? atoi(eb) : 1024;  // C3 factor 28.29 (2048) -> 27.71 ms (1024), 28.31 (512)
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
     const long long pre_max = pm ? atoll(pm) : (256LL << 20);
     std::vector<long long> zr, pdst;
@@ -540,7 +548,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         }
       int lmaxm = 0;
       for (int sn : lv) lmaxm = std::max(lmaxm, sym.sn[sn].ns + sym.sn[sn].nr);
-      Op ea{pre ? 0 : (lmaxm <= 512 ? 5 : 4), (int)tk.size(), 0};
+      // column buffer of the in-place assembly: 512 rows (five workgroups per CU) up to m = 512, else ea_big rows
+      // (G2OHIP_EA_BIG, dev A/B: 512 / 1024 / 2048; profiles/r04_ab_c3_ea.log)
+      Op ea{pre ? 0 : (lmaxm <= 512 || ea_big == 512 ? 5 : ea_big == 1024 ? 9 : 4), (int)tk.size(), 0};
       // first diagonal blocks: assembled and factored beside the slabs
       for (int sn : lv) tk.push_back(Task{sn, 0, 0, 1});
       // every front is assembled here (input entries, zeros, children); slabs of EA columns where the level
@@ -811,12 +821,13 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
     switch (op.kind) {
       case 0:
       case 4:
-      case 5: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), cmptr.get(),
+      case 5:
+      case 9: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), cmptr.get(),
                                       cment.get(), colptr.get(),
                                       ent_row.get(),
                                       ent_src.get(), vals, lam, fronts.get(), vecs.get(),
                                       lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail,
-                                      op.kind == 0 ? 0 : (op.kind == 5 ? 2 : 1), s); break;
+                                      op.kind == 0 ? 0 : op.kind == 5 ? 2 : op.kind == 9 ? 3 : 1, s); break;
       case 2:
       case 6: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
                                 vecs.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 6, s);

@@ -91,7 +91,7 @@ struct DeviceCholesky {
   DevBuf<int> colptr, ent_row, ent_src;  // input entries per permuted scalar column (k_extend_add)
   DevBuf<int> jtab;                       // per child: row ranges per parent slab (FrontDesc::jt_off)
   DevBuf<int> cmptr;                      // per front column: range of (child, child column) pairs
-  DevBuf<int2> cment;
+  DevBuf<longlong2> cment;  // per (front column, child column): U column, child relmap | jc << 32 | nr << 48
   long long npre = 0;                     // entries of pre-scattered (small-level) fronts
   DevBuf<long long> pre_dst, zero_rng;
   DevBuf<int> pre_src;

@@ -191,7 +191,7 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
 // diagonal block assembled, factored and forward-solved beside it (t.c == 1). Input entries of scalar
 // column c (permuted): ent_row/ent_src[colptr[c] .. colptr[c+1]) = row in the front | diag << 30, index in vals
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
-                     const int* jtab, const int* cmptr, const int2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
+                     const int* jtab, const int* cmptr, const longlong2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv,
                      int* fail, int assemble, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place,
                                                                // 2 in place (m <= 512)

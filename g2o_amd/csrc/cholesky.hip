@@ -152,7 +152,7 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 // the scaled column l_j = row[j] r_j, its two-column look-ahead (l_{j+1,j}, l_{j+2,j} are chain
 // values, no broadcast), the rest of column j-1's rank-1 update (through LDS, one column late,
 // columns >= j+2), cut into chunks that sched_barriers pin between the chain's dependent steps.
-// The block's forward solve is not in this loop (publish_inverse multiplies by L^-1). Entries
+// The block's forward solve is not in this loop (factor_block multiplies by L^-1 afterwards). Entries
 // above a lane's diagonal may collect garbage; they are never read. One template instance per
 // column keeps every register index a compile-time constant.
 #define CHOL_SB() __builtin_amdgcn_sched_barrier(0)
@@ -234,11 +234,14 @@ __device__ __forceinline__ bool chol32(double (&row)[NB], int lane, double* col)
 // Wave 0: factor the kb x kb block staged in D (LDS, row stride DS, lower triangle valid).
 // Lanes 32..63 run the same instruction stream on the identity: lane 32 + c ends holding column c
 // of L^-1 (right-looking substitution on the broadcast columns of L), left transposed in D
-// (D[c * DS + i] = L^-1(i, c)) for publish_inverse, which the whole workgroup runs after a barrier.
-// The diagonal block of L itself is not stored: every consumer of the factor (tile TRSM, next-diagonal
-// update, inverse tasks, backward and multi-right-hand-side solves) uses L^-1 for diagonal blocks.
+// (D[c * DS + i] = L^-1(i, c)) for the block's forward solve below, and (linv_out) stored row-major straight from the
+// registers: row i of the 32 x 32 block is one coalesced 256-byte store of lanes 32..63, so the caller publishes it
+// without a barrier or an LDS pass (r04; X's diagonal blocks, the same values column-major, are copied by k_xdiag
+// after the factorization). The diagonal block of L itself is not stored: every consumer of the factor (tile TRSM,
+// next-diagonal update, inverse tasks, backward and multi-right-hand-side solves) uses L^-1 for diagonal blocks.
 __device__ __forceinline__ void factor_block(double* D, int kb, const double* vy, double* col, int lane, int* fail,
-                                             double* ysol, unsigned long long* ph = nullptr, double* ylds = nullptr) {
+                                             double* ysol, unsigned long long* ph = nullptr, double* ylds = nullptr,
+                                             double* linv_out = nullptr) {
   double row[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
@@ -250,6 +253,10 @@ __device__ __forceinline__ void factor_block(double* D, int kb, const double* vy
   if (ph) { asm volatile("" : "+v"(row[NB - 1])); ph[6] = __builtin_amdgcn_s_memtime(); }
   if (lane == 0 && !ok) *fail = 1;
   if (lane >= NB) {  // every read of D (the row loads above) is done: this wave's LDS traffic is in order
+    if (linv_out) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) linv_out[i * NB + (lane - NB)] = row[i];  // L^-1(i, lane - NB), identity-padded
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) D[(lane - NB) * DS + i] = row[i];
   }
@@ -271,21 +278,6 @@ __device__ __forceinline__ void factor_block(double* D, int kb, const double* vy
     if (ylds) ylds[lane] = lane < kb ? yv : 0.0;  // (same wave: in-order LDS traffic for its later readers)
   }
 }
-// After factor_block and a workgroup barrier: L_kk^-1 row-major to linv and the diagonal block of
-// X = L11^-1 (column-major, leading dimension ldx), both coalesced over the 256 threads.
-__device__ __forceinline__ void publish_inverse(const double* D, int kb, int tid, double* linv, double* X, int ldx) {
-#pragma unroll
-  for (int u = 0; u < NB * NB / 256; ++u) {
-    const int e = tid + 256 * u, i = e >> 5, c = e & (NB - 1);
-    linv[e] = D[c * DS + i];  // row i, column c of L^-1 (identity-padded past kb)
-  }
-#pragma unroll
-  for (int u = 0; u < NB * NB / 256; ++u) {
-    const int e = tid + 256 * u, c = e >> 5, i = e & (NB - 1);
-    if (c < kb && i < kb) X[(size_t)c * ldx + i] = D[c * DS + i];
-  }
-}
-
 // ---------------------------------------------------------------------------- assembly + extend-add
 // One launch per level assembles every front of the level from scratch (no front-pool memset, no
 // separate scatter pass), with two kinds of workgroup:
@@ -394,9 +386,8 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
       }
     }
     PH(2)
-    if (tid < 64) factor_block(D, kb0, vy, col, tid, fail, ysol + me.c0, PH_REC);
-    __syncthreads();
-    publish_inverse(D, kb0, tid, linv + (size_t)me.c0 * (NB * NB), xinv + me.x_off, me.ns);
+    // L_00^-1 straight from wave 0's registers to linv (X's diagonal blocks: k_xdiag after the factorization)
+    if (tid < 64) factor_block(D, kb0, vy, col, tid, fail, ysol + me.c0, PH_REC, nullptr, linv + (size_t)me.c0 * (NB * NB));
     PH(3)
     PH(4)
     return;
@@ -667,9 +658,9 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
     }
     __syncthreads();
     PH(2)
-    if (tid < 64) factor_block(Dn, kbn, vn, col, tid, fail, ysol + t.c0 + r0, PH_REC);
-    __syncthreads();
-    publish_inverse(Dn, kbn, tid, linv + (size_t)(t.c0 + r0) * (NB * NB), xinv + t.x_off + (size_t)r0 * ns + r0, ns);
+    // L^-1 leaves from wave 0's registers; the block of X = L11^-1 it also is reaches xinv by k_xdiag after the
+    // factorization (the inverse tasks read it from linv meanwhile): no barrier and no LDS pass on the chain
+    if (tid < 64) factor_block(Dn, kbn, vn, col, tid, fail, ysol + t.c0 + r0, PH_REC, nullptr, linv + (size_t)(t.c0 + r0) * (NB * NB));
     PH(3)
     PH(4)
     return;
@@ -691,7 +682,8 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
       const int e = tid + 256 * u, r = e & (NB - 1), c = e >> 5;
       wv[u] = ld0(Xf, (NB * j + c) * ns + NB * pp + r, kq > j && r < kbp);  // W_pj so far
       lq[u] = ld0(L, (NB * kq + c) * m + NB * pp + r, r < kbp);              // L_{p,kq}(r, c)
-      xq[u] = Xf[(NB * j + c) * ns + NB * kq + r];                           // X_{kq,j}(r, c)
+      // X_{kq,j}(r, c); the diagonal block X_{kq,kq} = L_{kq}^-1 from linv (k_xdiag copies it to X after the factor)
+      xq[u] = kq == j ? linv[(size_t)(t.c0 + NB * kq) * (NB * NB) + r * NB + c] : Xf[(NB * j + c) * ns + NB * kq + r];
       li[u] = ld0(Lin, e, fin);                                              // L_ss^-1, row-major
     }
     double* Ts = Dn;  // 32 x DS
@@ -909,8 +901,19 @@ __global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks
   if (j >= ns) return;
   const double* col = lbuf + me.l_off + (size_t)j * m + ns;
   const int* rw = rows + me.rows_off;
-  double acc = 0.0;
-  for (int i = lane; i < me.nr; i += 64) acc += col[i] * xsol[rw[i]];
+  // four rows per lane in flight (the column and row-index loads of a batch, then their x gathers), four partial sums
+  double a4[4] = {0.0, 0.0, 0.0, 0.0};
+  int i = lane;
+  for (; i + 192 < me.nr; i += 256) {
+    double c[4];
+    int r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { c[u] = col[i + 64 * u]; r[u] = rw[i + 64 * u]; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a4[u] += c[u] * xsol[r[u]];
+  }
+  for (; i < me.nr; i += 64) a4[0] += col[i] * xsol[rw[i]];
+  double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if (lane == 0) tsol[me.c0 + j] = ysol[me.c0 + j] - acc;
@@ -956,11 +959,33 @@ __global__ void __launch_bounds__(256) k_bwd_inner(const Task* __restrict__ task
   if (j >= t.b) return;
   const double* col = lbuf + me.l_off + (size_t)j * m;
   const double* xx = xsol + me.c0;
-  double acc = 0.0;
-  for (int i = t.b + lane; i < ns; i += 64) acc += col[i] * xx[i];
+  double a4[4] = {0.0, 0.0, 0.0, 0.0};
+  int i = t.b + lane;
+  for (; i + 192 < ns; i += 256) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a4[u] += col[i + 64 * u] * xx[i + 64 * u];
+  }
+  for (; i < ns; i += 64) a4[0] += col[i] * xx[i];
+  double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if (lane == 0) tsol[me.c0 + j] -= acc;
+}
+
+// Diagonal 32 x 32 blocks of X = L11^-1 from linv (the panel steps publish L^-1 only there): task (front s, panel
+// start a); X column-major with leading dimension ns, rows/columns [a, a + kb)
+__global__ void __launch_bounds__(256) k_xdiag(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                               const double* __restrict__ linv, double* __restrict__ xinv) {
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int a = t.a, kb = min(NB, me.ns - a);
+  const double* L = linv + (size_t)(me.c0 + a) * (NB * NB);
+  double* X = xinv + me.x_off + (size_t)a * me.ns + a;
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u, c = e >> 5, i = e & (NB - 1);  // X(i, c): consecutive threads down a column
+    if (c < kb && i < kb) X[(size_t)c * me.ns + i] = L[i * NB + c];
+  }
 }
 
 // ---------------------------------------------------------------------------- distributed factorization glue
@@ -1122,6 +1147,11 @@ void chol_bwd_inner(int ntasks, const Task* tasks, const FrontDesc* fd, const do
                     hipStream_t s) {
   if (ntasks <= 0) return;
   hipLaunchKernelGGL(k_bwd_inner, ntasks, 256, 0, s, tasks, fd, lbuf, xsol, tsol);
+  KERNEL_CHECK();
+}
+void chol_xdiag(int ntasks, const Task* tasks, const FrontDesc* fd, const double* linv, double* xinv, hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_xdiag, ntasks, 256, 0, s, tasks, fd, linv, xinv);
   KERNEL_CHECK();
 }
 void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,

@@ -782,6 +782,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       bwd_ops.push_back(bl);
       bwd_off.push_back((int)tk.size());
     }
+    // diagonal blocks of X = L11^-1 (the factorization publishes every L_kk^-1 to linv only): one k_xdiag task per
+    // block, after the factorization's last launch
+    xdiag_off = (int)tk.size();
+    for (const auto& lv : fplan)
+      for (int sn : lv)
+        for (int a = 0; a < sym.sn[sn].ns; a += NB) tk.push_back(Task{sn, a, 0, 0});
+    n_xdiag = (int)tk.size() - xdiag_off;
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
     heads.assign(ops.size(), launch::StepHead{});
@@ -845,6 +852,7 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;
     }
   }
+  launch::chol_xdiag(n_xdiag, tasks.get() + xdiag_off, fd.get(), linv.get(), xinv.get(), s);
 }
 
 void DeviceCholesky::reduce_input(const double* vals, hipStream_t s) {

@@ -167,6 +167,7 @@ struct DeviceCholesky {
   // pack this rank's partial [blocks | rhs] (the caller's layout) and reduce; factor(rs_buf, ..., rs_buf + rs_rhs_off)
   void reduce_input(const double* vals, hipStream_t s);
   std::vector<Op> ops;
+  int xdiag_off = 0, n_xdiag = 0;  // k_xdiag tasks (in `tasks`): X's diagonal blocks from linv after the factor
   std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
   DevBuf<launch::Task> tasks;
   DevBuf<launch::StepTask> step_tasks;

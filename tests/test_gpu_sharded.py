@@ -185,6 +185,30 @@ def test_distributed_factorization(g2o_amd_mod, oracle, monkeypatch, name, nrank
     assert np.linalg.norm(x - xo) <= RTOL * np.linalg.norm(xo)
 
 
+def test_aligned_shards_many_ranks_small_problem(g2o_amd_mod, monkeypatch):
+    """Aligned shards on more ranks than the cut has subtrees (a 400-camera BA, 6 ranks, forced cut: two subtrees):
+    four ranks hold no subtree and only the landmarks seen by shared cameras alone, possibly none; the run must still
+    follow the single-GPU trajectory, every landmark held once."""
+    prob = synth.ba(400, 20000)
+    iters = 4
+    monkeypatch.setenv("G2OHIP_DIST_FACTOR", "1")
+    opts, res = _run_sharded(g2o_amd_mod, prob, 6, iters)
+    info = [o.factor_info() for o in opts]
+    assert all(i["aligned_shards"] == 1 for i in info), info
+    assert sum(i["local_landmarks"] for i in info) == prob.vertices[1].ids.size
+    single = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    n1, st1 = single.optimize(iters)
+    for r in range(6):
+        n, st = res[r]
+        assert n == n1
+        for a, b in zip(st, st1):
+            assert a.levenbergIterations == b.levenbergIterations
+            assert abs(a.chi2 - b.chi2) <= RTOL * b.chi2
+    x, _ = _gather_state(prob, opts)
+    xs = single.minimal_state()
+    assert np.linalg.norm(x - xs) <= 1e-9 * np.linalg.norm(xs)
+
+
 def test_distributed_reduce_scatter_equals_allreduce(g2o_amd_mod, monkeypatch):
     """The reduce-scatter of S by subtree ownership (each rank receives only the blocks its fronts read, plus the shared
     tail) against the same distributed factorization fed by the plain all-reduce of the whole S (G2OHIP_DIST_RS=0): the

@@ -19,6 +19,7 @@ namespace g2ohip {
 namespace {
 
 enum : int { OP_SUM = 1, OP_MAX = 2, OP_RS = 3, OP_AG = 4 };
+constexpr long long kCheckFirst = 8;  // RcclComm: collectives verified after each structure build by default
 
 std::string call_desc(long long seq, size_t n, int op) {
   return "call #" + std::to_string(seq) + " (" +
@@ -29,16 +30,21 @@ std::string call_desc(long long seq, size_t n, int op) {
 struct RcclComm : Comm {
   ncclComm_t c = nullptr;
   int rank = 0;
-  bool check = false;
+  long long check_all = 0;   // G2OHIP_COMM_CHECK: 1 every call, 0 none, unset: the first kCheckFirst calls per structure
+  long long check_left = 0;  // calls still to verify (-1: all)
   double* dchk = nullptr;  // 6 doubles: [seq, n, op, -seq, -n, -op] max-reduced
   ~RcclComm() override {
     if (dchk) (void)hipFree(dchk);
     if (c) ncclCommDestroy(c);
   }
-  // G2OHIP_COMM_CHECK=1: every rank must enter the same (call number, length, operation). max over ranks of
-  // (v, -v) gives (max, -min); any difference between them is a rank-dependent collective sequence.
+  // every rank must enter the same (call number, length, operation). max over ranks of (v, -v) gives (max, -min); any
+  // difference between them is a rank-dependent collective sequence. The check synchronises the stream, so by default
+  // it covers only the first kCheckFirst calls after each structure build (the structure decides the sequence);
+  // G2OHIP_COMM_CHECK=1 checks every call, =0 none.
+  void rearm() override { check_left = check_all; }
   void verify(size_t n, int op, hipStream_t s) {
-    if (!check) return;
+    if (check_left == 0) return;
+    if (check_left > 0) --check_left;
     if (!dchk) HIP_CHECK(hipMalloc(&dchk, 6 * sizeof(double)));
     const double v[6] = {(double)seq, (double)n, (double)op, -(double)seq, -(double)n, -(double)op};
     double r[6];
@@ -180,7 +186,8 @@ Comm* make_rccl_comm(const unsigned char* uid128, int rank, int nranks, std::str
   }
   c->rank = rank;
   const char* chk = std::getenv("G2OHIP_COMM_CHECK");
-  c->check = chk && *chk && std::strcmp(chk, "0") != 0;
+  c->check_all = !(chk && *chk) ? kCheckFirst : (std::strcmp(chk, "0") != 0 ? -1 : 0);
+  c->check_left = c->check_all;
   return c;
 }
 

@@ -11,7 +11,8 @@
 // Every collective carries a per-communicator call number. LocalComm always checks that all ranks
 // entered the same call (number, length, operation) and throws DeviceError on every rank otherwise (a
 // rank-dependent call sequence was a heap over-read here and a silent hang under RCCL); RcclComm runs
-// the same check as one extra 6-double max all-reduce per call when G2OHIP_COMM_CHECK=1.
+// the same check as one extra 6-double max all-reduce (and a stream synchronisation) per call: for the first 8 calls
+// after each structure build by default (rearm), for every call with G2OHIP_COMM_CHECK=1, never with =0.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -29,6 +30,8 @@ struct Comm {
   virtual void reduce_scatter_sum(double* dptr, size_t count, hipStream_t s) = 0;
   // in place: dptr holds nranks segments of `count` doubles; afterwards every segment r holds rank r's segment r
   virtual void allgather(double* dptr, size_t count, hipStream_t s) = 0;
+  // a new structure (a new collective sequence) starts: RcclComm re-arms its call-sequence check
+  virtual void rearm() {}
   long long seq = 0;  // collectives issued so far on this communicator
 };
 

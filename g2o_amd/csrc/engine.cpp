@@ -1908,6 +1908,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     if (r) return r;
   }
   ensure_device_state();
+  if (comm) comm->rearm();  // a new collective sequence: RCCL's call-sequence check covers its first calls again
   align_shards();
   setup_edges_device();
   ++structure_ver;  // every cache keyed on the block pattern (marginals factor, BlockSymv) is stale from here

@@ -309,7 +309,17 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
                                                     const double* __restrict__ lam, double* __restrict__ fronts,
                                                     double* __restrict__ vecs, double* __restrict__ lbuf,
                                                     double* __restrict__ ysol, double* __restrict__ linv,
-                                                    double* __restrict__ xinv, int* __restrict__ fail) {
+                                                    double* __restrict__ xinv, int* __restrict__ fail,
+                                                    const launch::ScatterJob sj) {
+  if ((int)blockIdx.x >= sj.ntask) {  // deferred input scatter of a later level (the launch's chip is mostly idle)
+    const long long k = sj.sc0 + (long long)((int)blockIdx.x - sj.ntask) * 256 + threadIdx.x;
+    if (k < sj.sc1) {
+      const int sr = sj.src[k];
+      const double v = vals[sr & 0x7fffffff];
+      fronts[sj.dst[k]] = sr < 0 ? v + *lam : v;
+    }
+    return;
+  }
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, kb0 = min(NB, me.ns);
@@ -571,6 +581,15 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   __shared__ double Dn[NB * DS];      // next diagonal block
   __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
   __shared__ double vn[NB];
+  if ((int)blockIdx.x >= head.ntask) {  // deferred input scatter of a later level (off this step's chain)
+    const long long k = head.sc0 + (long long)((int)blockIdx.x - head.ntask) * 256 + threadIdx.x;
+    if (k < head.sc1) {
+      const int sr = head.sc_src[k];
+      const double v = head.sc_vals[sr & 0x7fffffff];
+      fronts[head.sc_dst[k]] = sr < 0 ? v + *head.sc_lam : v;
+    }
+    return;
+  }
   PH_BEGIN(2)
   PH1_BEGIN(3)
   const StepTask t = (int)blockIdx.x < head.n ? head.t[blockIdx.x] : tasks[blockIdx.x];
@@ -1083,11 +1102,14 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const longlong2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv,
-                     int* fail, int assemble, hipStream_t s) {
+                     int* fail, int assemble, hipStream_t s, const ScatterJob* sj) {
   if (ntasks <= 0) return;
+  ScatterJob job{ntasks, 0, 0, nullptr, nullptr};
+  if (sj && sj->sc1 > sj->sc0) job = ScatterJob{ntasks, sj->sc0, sj->sc1, sj->dst, sj->src};
+  const int grid = ntasks + (int)((job.sc1 - job.sc0 + 255) / 256);
 #define G2OHIP_EA(A_, E_)                                                                                        \
-  hipLaunchKernelGGL((k_extend_add<A_, E_>), ntasks, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, \
-                     colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, xinv, fail)
+  hipLaunchKernelGGL((k_extend_add<A_, E_>), grid, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, \
+                     colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, xinv, fail, job)
   // assemble 2: fronts up to 512 rows (a small column buffer keeps more workgroups per CU)
   if (assemble == 2) G2OHIP_EA(true, 512);
   else if (assemble == 3) G2OHIP_EA(true, 1024);
@@ -1099,10 +1121,12 @@ void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const i
 void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs,
                double* ysol, double* linv, double* xinv, int* fail, bool pairs, hipStream_t s) {
   if (ntasks <= 0) return;
+  if (head.ntask != ntasks) throw DeviceError("chol_step: head.ntask does not match the task count");
+  const int grid = ntasks + (head.sc1 > head.sc0 ? (int)((head.sc1 - head.sc0 + 255) / 256) : 0);
   if (pairs)
-    hipLaunchKernelGGL(k_step<true>, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
+    hipLaunchKernelGGL(k_step<true>, grid, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   else
-    hipLaunchKernelGGL(k_step<false>, ntasks, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
+    hipLaunchKernelGGL(k_step<false>, grid, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {

@@ -501,7 +501,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const long long pre_max = pm ? atoll(pm) : (256LL << 20);
     std::vector<long long> zr, pdst;
     std::vector<int> psrc;
+    std::vector<long long> pre_lev_off;  // per level: its first entry in pdst / psrc (level-major)
     for (size_t l = 0; l < fplan.size(); ++l) {
+      pre_lev_off.push_back((long long)pdst.size());
       if ((int)l == xch_at) {  // subtree roots -> every rank (before the first shared front is assembled)
         ops.push_back(Op{8, 0, 0});
        
@@ -728,6 +730,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     }
     nzero = (int)(zr.size() / 2);
     npre = (long long)pdst.size();
+    pre_lev_off.push_back(npre);
     zero_rng.upload(zr.empty() ? std::vector<long long>{0, 0} : zr, s);
     pre_dst.upload(pdst.empty() ? std::vector<long long>{0} : pdst, s);
     pre_src.upload(psrc.empty() ? std::vector<int>{0} : psrc, s);
@@ -796,9 +799,55 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       if (ops[k].kind != 2 && ops[k].kind != 6) continue;
       launch::StepHead& h = heads[k];
       h.n = 0;
+      h.ntask = ops[k].count;
       while (h.n < launch::CHOL_HEAD && h.n < ops[k].count) {  // the first workgroups (diagonal tasks among them)
         h.t[h.n] = stk[ops[k].off + h.n];
         ++h.n;
+      }
+    }
+    // Deferred input scatter: a pre-scattered level's entries are needed only from its own extend-add on, so they ride
+    // as extra workgroups in the previous level's first panel-step launch (chain-bound: the chip is mostly idle beside
+    // its diagonal task) instead of all in one scatter launch before the first level. Its fronts were zeroed before the
+    // factorization and no earlier level touches them. Levels up to the last one without a preceding step launch keep
+    // the up-front scatter. Single-process factorizations only (G2OHIP_SCATTER_DEFER=0: all up front, A/B).
+    {
+      const char* dv = getenv("G2OHIP_SCATTER_DEFER");
+      const bool defer = !distributed() && !(dv && atoi(dv) == 0);
+      const int nlev = (int)fplan.size();
+      std::vector<int> first_step(nlev, -1), ea_op(nlev, -1);
+      int lev = -1;
+      for (size_t k = 0; k < ops.size(); ++k) {
+        const int kd = ops[k].kind;
+        if (kd == 0 || kd == 4 || kd == 5 || kd == 9) {  // every level opens with its extend-add op
+          if (++lev < nlev) ea_op[lev] = (int)k;
+        } else if ((kd == 2 || kd == 6) && lev >= 0 && lev < nlev && first_step[lev] < 0) {
+          first_step[lev] = (int)k;
+        }
+      }
+      auto ents = [&](int l) { return pre_lev_off[l + 1] - pre_lev_off[l]; };
+      // host launch of level l's entries: the previous level's extend-add when it is a few workgroups (latency-bound,
+      // the chip idle beside it), else that level's first panel step
+      auto host = [&](int l) {
+        const int e = ea_op[l - 1];
+        if (e >= 0 && ops[e].count > 0 && ops[e].count <= 256) return e;
+        return first_step[l - 1];
+      };
+      int P = 0;  // levels 0 .. P scattered up front
+      for (int l = 1; l < nlev; ++l)
+        if (ents(l) > 0 && (!defer || lev != nlev - 1 || host(l) < 0)) P = l;
+      npre_first = npre > 0 ? pre_lev_off[P + 1] : 0;
+      n_deferred_levels = 0;
+      for (int l = P + 1; l < nlev; ++l) {
+        if (ents(l) == 0) continue;
+        const int k = host(l);
+        if (ops[k].kind == 2 || ops[k].kind == 6) {
+          heads[k].sc0 = pre_lev_off[l];
+          heads[k].sc1 = pre_lev_off[l + 1];
+        } else {
+          ops[k].sc0 = pre_lev_off[l];
+          ops[k].sc1 = pre_lev_off[l + 1];
+        }
+        ++n_deferred_levels;
       }
     }
   }
@@ -821,7 +870,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
 void DeviceCholesky::factor(const double* vals, const double* lam, const double* rhs, int* fail, hipStream_t s,
                             bool prezeroed) {
   last_fail = fail;
-  launch::chol_prescatter(prezeroed ? 0 : nzero, zero_rng.get(), npre, vals, pre_dst.get(), pre_src.get(), lam,
+  launch::chol_prescatter(prezeroed ? 0 : nzero, zero_rng.get(), npre_first, vals, pre_dst.get(), pre_src.get(), lam,
                           fronts.get(), (int)sym.sn.size(), fd.get(), perm.get(), rhs, vecs.get(), s);
   for (const Op& op : ops) {
     const launch::Task* t = tasks.get() + op.off;
@@ -829,16 +878,27 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       case 0:
       case 4:
       case 5:
-      case 9: launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), cmptr.get(),
-                                      cment.get(), colptr.get(),
-                                      ent_row.get(),
-                                      ent_src.get(), vals, lam, fronts.get(), vecs.get(),
-                                      lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail,
-                                      op.kind == 0 ? 0 : op.kind == 5 ? 2 : op.kind == 9 ? 3 : 1, s); break;
-      case 2:
-      case 6: launch::chol_step(op.count, step_tasks.get() + op.off, heads[&op - ops.data()], fronts.get(), lbuf.get(),
-                                vecs.get(), y_p.get(), linv.get(), xinv.get(), fail, op.kind == 6, s);
+      case 9: {
+        const launch::ScatterJob sj{op.count, op.sc0, op.sc1, pre_dst.get(), pre_src.get()};
+        launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), cmptr.get(),
+                                cment.get(), colptr.get(), ent_row.get(), ent_src.get(), vals, lam, fronts.get(),
+                                vecs.get(), lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail,
+                                op.kind == 0 ? 0 : op.kind == 5 ? 2 : op.kind == 9 ? 3 : 1, s, &sj);
         break;
+      }
+      case 2:
+      case 6: {
+        launch::StepHead h = heads[&op - ops.data()];
+        if (h.sc1 > h.sc0) {  // this launch also scatters a later level's input entries (setup: deferred scatter)
+          h.sc_vals = vals;
+          h.sc_dst = pre_dst.get();
+          h.sc_src = pre_src.get();
+          h.sc_lam = lam;
+        }
+        launch::chol_step(op.count, step_tasks.get() + op.off, h, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),
+                          linv.get(), xinv.get(), fail, op.kind == 6, s);
+        break;
+      }
       case 8: {  // subtree roots -> every rank
         const long long* R = xch_ranges.get();
         launch::chol_copy_ranges(xch_pack_f, R, fronts.get(), xch_buf.get(), s);

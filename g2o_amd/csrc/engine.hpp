@@ -93,6 +93,8 @@ struct DeviceCholesky {
   DevBuf<int> cmptr;                      // per front column: range of (child, child column) pairs
   DevBuf<longlong2> cment;  // per (front column, child column): U column, child relmap | jc << 32 | nr << 48
   long long npre = 0;                     // entries of pre-scattered (small-level) fronts
+  long long npre_first = 0;               // of them scattered before the first level (the rest: deferred, see factor)
+  int n_deferred_levels = 0;              // levels whose entries ride in the previous level's first step launch
   DevBuf<long long> pre_dst, zero_rng;
   DevBuf<int> pre_src;
   int nzero = 0;
@@ -109,7 +111,7 @@ struct DeviceCholesky {
   // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
   // trailing-update (k_syrk) launches, big-panel backward rounds
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
-  struct Op { int kind, off, count; };  // kind 0 extend-add (pre-scattered level), 4 / 5 assembly + extend-add,
+  struct Op { int kind, off, count; long long sc0 = 0, sc1 = 0; };  // sc: deferred scatter range (extend-add ops)  // kind 0 extend-add (pre-scattered level), 4 / 5 assembly + extend-add,
                                         // 2 panel step (6: with lagged-pair tasks), 3 syrk, 8 root exchange
   // ---- distributed factorization (landmark-sharded BA). Set dist_rank / dist_nranks / allreduce before
   // setup. The elimination tree is cut: every front below the cut belongs to one rank (whole subtrees, balanced by

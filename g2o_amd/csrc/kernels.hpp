@@ -180,6 +180,23 @@ constexpr int CHOL_HEAD = 8;
 struct StepHead {
   StepTask t[CHOL_HEAD];
   int n;
+  // deferred input scatter (DeviceCholesky::factor): workgroups past the launch's ntask tasks scatter the input entries
+  // [sc0, sc1) of a later level's pre-scattered fronts (as k_chol_scatter: fronts[dst[k]] = vals[src[k] & 0x7fffffff],
+  // + lambda when src[k] < 0), 256 entries each
+  int ntask;
+  long long sc0, sc1;
+  const double* sc_vals;
+  const long long* sc_dst;
+  const int* sc_src;
+  const double* sc_lam;
+};
+// deferred input scatter riding in an extend-add launch (DeviceCholesky::factor): workgroups past its ntask tasks
+// scatter entries [sc0, sc1) as k_chol_scatter does, 256 each
+struct ScatterJob {
+  int ntask;
+  long long sc0, sc1;
+  const long long* dst;
+  const int* src;
 };
 // zero ranges (offset, length pairs) of the front pool, then scatter input entries: fronts[dst[k]] =
 // vals[src[k] & 0x7fffffff] (+ lambda when src[k] < 0), and the front vectors v_s = [rhs(perm[c0 ..]) (own
@@ -193,10 +210,11 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
 void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const longlong2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv,
-                     int* fail, int assemble, hipStream_t s);  // assemble: 0 pre-scattered level, 1 in place,
-                                                               // 2 in place (m <= 512)
+                     int* fail, int assemble, hipStream_t s,  // assemble: 0 pre-scattered level, 1 in place,
+                     const ScatterJob* sj = nullptr);          // 2 in place (m <= 512); sj: + scatter workgroups
 void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* fronts, double* lbuf, double* vecs, double* ysol,
-               double* linv, double* xinv, int* fail, bool pairs, hipStream_t s);  // pairs: lagged-pair tasks present
+               double* linv, double* xinv, int* fail, bool pairs, hipStream_t s);  // pairs: lagged-pair tasks present;
+                                                                                    // + head's scatter workgroups
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
 // the contribution block, K = [0, ns)); columns stop at ns unless kb = ns (then m)
 void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s);

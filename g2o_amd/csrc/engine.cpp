@@ -538,10 +538,14 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           // only the lower triangle is ever read (tiles, contribution passes and extend-add touch rows >= columns):
           // zero column j's rows [j, m), whole small fronts in one range
           const long long m = q.ns + q.nr, len = m * m;
+          // a childless front whose contribution block comes from a separate k_syrk pass gets it written, not added
+          // (k_syrk's overwrite): its columns >= ns need no zeros
+          const bool cb_written = !fused_contrib && sym.children_ptr[sn + 1] == sym.children_ptr[sn];
+          const long long zcols = cb_written ? q.ns : m;
           if (m <= 64)
             for (long long o = 0; o < len; o += 65536) { zr.push_back(q.front_off + o); zr.push_back(std::min(65536LL, len - o)); }
           else
-            for (long long j = 0; j < m; ++j) { zr.push_back(q.front_off + j * m + j); zr.push_back(m - j); }
+            for (long long j = 0; j < zcols; ++j) { zr.push_back(q.front_off + j * m + j); zr.push_back(m - j); }
           for (int c = q.c0; c < q.c0 + q.ns; ++c)
             for (int e = cpv[c]; e < cpv[c + 1]; ++e) {
               pdst.push_back(edsts[e]);

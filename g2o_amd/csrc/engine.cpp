@@ -829,12 +829,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         }
       }
       auto ents = [&](int l) { return pre_lev_off[l + 1] - pre_lev_off[l]; };
-      // host launch of level l's entries: the previous level's extend-add when it is a few workgroups (latency-bound,
-      // the chip idle beside it), else that level's first panel step
+      // host launch of level l's entries: the previous level's extend-add, else its first panel step, whichever has
+      // at most 256 workgroups of its own (latency-bound: the chip idle beside it); none: the entries stay up front
       auto host = [&](int l) {
-        const int e = ea_op[l - 1];
+        const int e = ea_op[l - 1], f = first_step[l - 1];
         if (e >= 0 && ops[e].count > 0 && ops[e].count <= 256) return e;
-        return first_step[l - 1];
+        if (f >= 0 && ops[f].count <= 256) return f;
+        return -1;
       };
       int P = 0;  // levels 0 .. P scattered up front
       for (int l = 1; l < nlev; ++l)

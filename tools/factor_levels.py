@@ -6,7 +6,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-sc = [i for i, r in enumerate(rows) if 'k_chol_scatter' in r['Kernel_Name']]
+sc = [i for i, r in enumerate(rows) if 'k_chol_scatter' in r['Kernel_Name'] or 'k_vec_init' in r['Kernel_Name']]
 a = sc[-2]
 b = next(i for i in range(a, len(rows)) if 'k_bwd_gemv' in rows[i]['Kernel_Name'])
 seg = rows[a + 1:b]

@@ -786,6 +786,13 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         bl.rounds.push_back({g, x});
         if (g.second) ++n_bwd_rounds;
       }
+      // a level of roots only (no rows below: t = y - 0) skips its gemv launch; k_bwd_x reads y itself
+      bool roots = bl.rounds.empty();
+      for (int sn : lv) roots = roots && sym.sn[sn].nr == 0;
+      if (roots) {
+        bl.t_is_y = true;
+        bl.gemv.second = 0;
+      }
       bwd_ops.push_back(bl);
       bwd_off.push_back((int)tk.size());
     }
@@ -939,8 +946,8 @@ void DeviceCholesky::solve(double* x, hipStream_t s) {
     const BwdLevel& bl = bwd_ops[l];
     launch::chol_bwd_gemv(bl.gemv.second, tasks.get() + bl.gemv.first, fd.get(), rows.get(), lbuf.get(), y_p.get(),
                           x_p.get(), t_p.get(), s);
-    launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
-                       perm.get(), xo, s);
+    launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), bl.t_is_y ? y_p.get() : t_p.get(),
+                       x_p.get(), perm.get(), xo, s);
     for (const auto& rd : bl.rounds) {
       launch::chol_bwd_inner(rd.first.second, tasks.get() + rd.first.first, fd.get(), lbuf.get(), x_p.get(), t_p.get(), s);
       launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),

@@ -105,6 +105,7 @@ struct DeviceCholesky {
   struct BwdLevel {            // backward solve of one level: (offset, count) task ranges in `tasks`
     std::pair<int, int> gemv, xall;
     std::vector<std::pair<std::pair<int, int>, std::pair<int, int>>> rounds;  // blocked fronts: (inner, x)
+    bool t_is_y = false;  // every front of the level is a root (no rows below its columns): t = y, no gemv launch
   };
   std::vector<BwdLevel> bwd_ops;
   int max_ns = 0;

@@ -504,10 +504,8 @@ Symbolic analyze(const BlockPattern& P, std::vector<int> bperm, double relax, in
   // columns. C4: 31 -> 15 supernodes, 5 -> 4 levels, factor 0.752 -> 0.733 ms; C5: 7 -> 6 levels, 84 -> 73 panel
   // steps, factor 1.84 -> 1.71 ms; C2 / C3 unchanged (profiles/r04_ab_absorb.log). G2OHIP_ND_ABSORB=k sets the ratio,
   // 0 turns it off (dev A/B).
-  static const int absorb = [] {
-    const char* e = getenv("G2OHIP_ND_ABSORB");
-    return e ? atoi(e) : 8;
-  }();
+  const char* absorb_env = getenv("G2OHIP_ND_ABSORB");
+  const int absorb = absorb_env ? atoi(absorb_env) : 8;
   auto childless = [&](const Tmp& c) {
     for (int b = c.b0; b < c.b1; ++b)
       for (int k : kids[b])

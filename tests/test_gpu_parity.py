@@ -348,6 +348,10 @@ SCHEDULES = {
     "band_leaves": {"G2OHIP_BAND_LEAF": "24"},
     "band_leaves_blocked": {"G2OHIP_BAND_LEAF": "24", "G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64",
                             "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
+    # every input entry scattered before the first level (default: later levels' entries ride in earlier launches)
+    "scatter_up_front": {"G2OHIP_SCATTER_DEFER": "0"},
+    # no small leaf absorption in the symbolic analysis (the r03 tree shapes)
+    "no_leaf_absorption": {"G2OHIP_ND_ABSORB": "0"},
 }
 
 

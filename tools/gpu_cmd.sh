@@ -1,5 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out; mkdir -p $O
-T=r04ai
-bash tools/gpu_ab.sh ${T} "C4 - G2OHIP_ZERO_PER_WG=4 G2OHIP_ZERO_PER_WG=16 - G2OHIP_ZERO_PER_WG=4 G2OHIP_ZERO_PER_WG=16" "C5 - G2OHIP_ZERO_PER_WG=4 G2OHIP_ZERO_PER_WG=16 - --steps 6"
+T=r04aj
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/${T}_tests.log 2>&1 || { echo TEST_FAIL; tail -40 $O/${T}_tests.log; exit 1; }
+tail -2 $O/${T}_tests.log

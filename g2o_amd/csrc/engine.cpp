@@ -1836,11 +1836,18 @@ void Engine::setup_edges_device() {
     {  // per local landmark its edge range in the (landmark-major) group order
       const int lm_b = local_lm.empty() ? 0 : local_lm.front();
       lm_eptr_h.assign(local_lm.size() + 1, 0);
+      std::vector<int2> erng(std::max<size_t>(local_lm.size(), 1), int2{0, 0});
+      std::vector<char> seen(local_lm.size(), 0);
       for (int k = 0; k < g.ne; ++k) {
         const int h = hidx[es.ev0[g.edges[k]]];
-        if (h >= num_poses) lm_eptr_h[h - num_poses - lm_b + 1]++;
+        if (h < num_poses) continue;
+        const int l = h - num_poses - lm_b;
+        lm_eptr_h[l + 1]++;
+        if (!seen[l]) { seen[l] = 1; erng[l].x = k; }
+        erng[l].y = k + 1;  // contiguous: the group is sorted landmark-major
       }
       for (size_t l = 0; l < local_lm.size(); ++l) lm_eptr_h[l + 1] += lm_eptr_h[l];
+      d_bs_erng.upload(erng, stream);
     }
     cm_ptr.upload(ptr, stream);
     cm_v0.upload(nz_i(cv0), stream);
@@ -2627,7 +2634,15 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   }
   if (sev) HIP_CHECK(hipEventRecord(ev_[3], stream));
   timer.begin("backsub", stream);
-  if (split)
+  // the split's back-substitution recomputes each observation's Jacobians instead of reading its 144-byte G block
+  // (k_backsub_j: C5 4.58 -> 4.48 ms per iteration, profiles/r04_ab_backsub_recompute.log); G2OHIP_BACKSUB_RECOMPUTE=0
+  // reads G (k_backsub_g, dev A/B)
+  const char* bsr = getenv("G2OHIP_BACKSUB_RECOMPUTE");
+  const bool bs_recompute = !(bsr && atoi(bsr) == 0);
+  if (split && bs_recompute && ld == 3 && pd == 6)
+    launch::backsub_j(group_args(groups[0]), nLloc, d_bs_erng.get(), d_hidx[groups[0].vtB].get(), dUfac.get(),
+                      dCl.get(), size_poses, lm_begin, dx.get(), stream);
+  else if (split)
     launch::backsub_g(pd, ld, nLloc, d_lm_ptr.get(), d_blk_pose.get(), dG.get(), dUfac.get(), dCl.get(), size_poses,
                       lm_begin, dx.get(), stream);
   else

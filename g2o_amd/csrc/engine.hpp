@@ -379,6 +379,7 @@ class Engine {
   VRed vr_pose, vr_lm;
   // schur
   DevBuf<int> d_lm_ptr, d_blk_pose, d_blk_lm;
+  DevBuf<int2> d_bs_erng;  // fused BA: per local landmark its edge range (k_backsub_j)
   DevBuf<double> dDinv, dUfac, dS, dCl, dG;
   int nS = 0, nHppUsed = 0;
   long long npairs = 0, nstaged = 0;  // off-diagonal pair products, staged blocks per Schur pass

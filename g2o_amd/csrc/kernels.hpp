@@ -65,6 +65,10 @@ void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, doubl
               int lm_begin, const SchurSplit* sp, hipStream_t s);
 void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, int num_poses, int lm_begin,
                   const SchurSplit* sp, hipStream_t s);
+// back-substitution of the Schur split recomputing each observation's Jacobians (no G blocks read): per local landmark
+// its edge range erng (landmark-major group order), hcam = camera vertex -> hessian index (-1 fixed)
+void backsub_j(const EdgeArgs& a, int nl, const int2* erng, const int* hcam, const double* Ufac, const double* cl_all,
+               int size_poses, int lm0, double* x, hipStream_t s);
 // Schur kernels for (pd, ld) = (6, 3) (BlockSolver_6_3) and (3, 2) (BlockSolver_3_2)
 void schur_prep(int ld, int nl, int lm0, const double* Hll, const double* bl_all, const double* lam, double* Dinv,
                 double* Ufac, double* cl_all, int* fail, hipStream_t s);

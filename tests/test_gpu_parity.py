@@ -352,6 +352,8 @@ SCHEDULES = {
     "scatter_up_front": {"G2OHIP_SCATTER_DEFER": "0"},
     # no small leaf absorption in the symbolic analysis (the r03 tree shapes)
     "no_leaf_absorption": {"G2OHIP_ND_ABSORB": "0"},
+    # the Schur split's back-substitution from the stored G blocks (default: Jacobians recomputed per observation)
+    "backsub_from_g": {"G2OHIP_BACKSUB_RECOMPUTE": "0"},
 }
 
 

@@ -548,8 +548,21 @@ void backsub_j(const EdgeArgs& a, int nl, const int2* erng, const int* hcam, con
                int size_poses, int lm0, double* x, hipStream_t s) {
   if (nl <= 0) return;
   const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
-  hipLaunchKernelGGL((k_backsub_j<FamilyBA, 8>), grid_for((size_t)nl * 8, 256), 256, 0, s, d, nl, erng, hcam, Ufac,
-                     cl_all, size_poses, lm0, x);
+  // lanes per landmark (dev A/B G2OHIP_BACKSUB_J_LANES; profiles/r04_ab_backsub_lanes.log): 4 against 8 / 16, C5
+  // 224.7-225.3 -> 227.5-227.6 / 222.6 LM it/s; 2 against 4, C5 225.0-225.1 -> 226.0-226.3, C4 907.5 -> 912.4
+  static const int lanes = getenv("G2OHIP_BACKSUB_J_LANES") ? atoi(getenv("G2OHIP_BACKSUB_J_LANES")) : 2;
+  if (lanes == 2)
+    hipLaunchKernelGGL((k_backsub_j<FamilyBA, 2>), grid_for((size_t)nl * 2, 256), 256, 0, s, d, nl, erng, hcam, Ufac,
+                       cl_all, size_poses, lm0, x);
+  else if (lanes == 4)
+    hipLaunchKernelGGL((k_backsub_j<FamilyBA, 4>), grid_for((size_t)nl * 4, 256), 256, 0, s, d, nl, erng, hcam, Ufac,
+                       cl_all, size_poses, lm0, x);
+  else if (lanes == 16)
+    hipLaunchKernelGGL((k_backsub_j<FamilyBA, 16>), grid_for((size_t)nl * 16, 256), 256, 0, s, d, nl, erng, hcam, Ufac,
+                       cl_all, size_poses, lm0, x);
+  else
+    hipLaunchKernelGGL((k_backsub_j<FamilyBA, 8>), grid_for((size_t)nl * 8, 256), 256, 0, s, d, nl, erng, hcam, Ufac,
+                       cl_all, size_poses, lm0, x);
   KERNEL_CHECK();
 }
 

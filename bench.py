@@ -28,7 +28,11 @@ PEAK_FP64_TFLOPS = 78.6    # MI355X FP64 vector == FP64 matrix (spec)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); N > 1 without a launcher spawns N ranks itself (default: "
+                         "WORLD_SIZE under torch.distributed.run, else 1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="control plane only (rank spawn, gloo barrier, max over ranks, JSON shape): no GPU call")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C4", help="C4 (default, BASELINE metric) or C5/C3/C2/C1; C4R (random covisibility), S2 (BlockSolver_3_2)")
@@ -46,13 +50,51 @@ def make_problem(cfg):
     return synth.by_name(cfg)
 
 
-def dist_setup(n):
+def spawn_ranks(n):
+    """`--gpus N` (N > 1) without a launcher: start N child ranks of this same command line, one process per GPU, with
+    the torch.distributed.run environment (RANK / LOCAL_RANK / WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free port), and
+    return the worst exit code. Runs before this process makes any HIP call (nothing here loads libg2o_hip.so). Rank
+    0's stdout is this process's (it prints the one JSON line); the other ranks print nothing on stdout. If a rank
+    fails, the others are terminated (by their own PIDs) so no rank is left waiting in a collective."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    pending = set(range(n))
+    while pending:
+        for r in sorted(pending):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            pending.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in pending:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dist_setup(n=None):
     """torch.distributed (gloo, CPU only) is the multi-process control plane: uid broadcast, barriers, max over
     ranks. libg2o_hip.so is loaded BEFORE torch so its HIP runtime and RCCL are /opt/rocm's (ROCm 7.2, the ones it
-    was built against) and not the copies torch bundles; torch never touches the GPU here."""
+    was built against) and not the copies torch bundles; torch never touches the GPU here. `n` (the --gpus request)
+    must equal the launcher's WORLD_SIZE: the line can never report fewer GPUs than asked for."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if n is not None and n != world:
+        raise SystemExit(f"bench.py: --gpus {n} but WORLD_SIZE={world}")
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -74,6 +116,16 @@ def allmax(v, world):
     t = torch.tensor([v], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def allgather_obj(obj, world):
+    """Per-rank records, in rank order (gloo)."""
+    if world <= 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def bcast_bytes(b, world):
@@ -222,20 +274,52 @@ def posegraph_leg(local, steps=5, warmup=1):
     }
 
 
-def c5_leg(local, steps=10, warmup=2):
-    """BASELINE config C5 (4k cameras x 1M points x 10M observations, the multi-GPU target) on this GPU, measured like
-    the headline: LM it/s, ms/linear-solve, the factorization's time and its stage split."""
+RANK_KEYS = ("distributed", "aligned_shards", "exchange_bytes_per_rank", "local_landmarks", "owned_fronts",
+             "shared_fronts", "local_block_doubles", "rs_segment_doubles", "rs_tail_doubles", "root_exchange_doubles",
+             "reduce_scatter")
+
+
+def rank_record(opt, rank, local, stages=None):
+    """What one rank saw: its device, the RCCL its communicator was built on, its landmark shard and its share of the
+    distributed factorization (factor_info), and optionally its own stage times."""
+    fi = opt.factor_info()
+    rt = {}
+    try:
+        import g2o_amd
+        rt = g2o_amd.runtime_info()
+    except Exception as ex:  # reported, not fatal
+        rt = {"error": repr(ex)}
+    rec = {"rank": rank, "device": local, "rccl_version": rt.get("rccl_version"), "librccl": rt.get("librccl")}
+    rec.update({k: fi.get(k) for k in RANK_KEYS})
+    if stages is not None:
+        rec["stages_ms_avg"] = stages
+    return rec
+
+
+def c5_leg(local, steps=10, warmup=2, rank=0, world=1):
+    """BASELINE config C5 (4k cameras x 1M points x 10M observations), measured like the headline: LM it/s,
+    ms/linear-solve, the factorization's time and its stage split. With N > 1 ranks this is the configuration BASELINE
+    defines as "landmarks sharded over 8xMI355X": every rank holds all cameras and its landmark shard (aligned with the
+    cut of the elimination tree), the reduced camera system meets in RCCL collectives over xGMI
+    (block_solver.hpp:340-393 is the loop each shard runs), and the timed region is bracketed by a barrier + device sync
+    on every rank, max over ranks."""
     import g2o_amd
     t0 = time.time()
     prob = make_problem("C5")
     gen = time.time() - t0
     opt = g2o_amd.SparseOptimizer(local).add_problem(prob)
     opt.set_algorithm("lm_hip_fix6_3")
+    if world > 1:
+        uid = g2o_amd.SparseOptimizer.comm_unique_id() if rank == 0 else None
+        opt.set_comm(bcast_bytes(uid, world), rank, world)
+    t0 = time.time()
     it = 0
     for _ in range(max(warmup, 1)):
         opt.optimize_step(it)
         it += 1
+    warm_s = time.time() - t0
     opt.set_stats_level(1)
+    barrier(world)
     g2o_amd.device_synchronize(local)
     t0 = time.perf_counter()
     timed = []
@@ -243,7 +327,8 @@ def c5_leg(local, steps=10, warmup=2):
         timed.append(opt.optimize_step(it)[1])
         it += 1
     g2o_amd.device_synchronize(local)
-    dt = time.perf_counter() - t0
+    barrier(world)
+    dt = allmax(time.perf_counter() - t0, world)
     names = ["linearize", "vreduce", "schur_rows", "chol_factor", "chol_solve", "backsub", "error", "oplus"]
     opt.enable_kernel_timing(True)
     opt.set_stats_level(2)
@@ -251,16 +336,18 @@ def c5_leg(local, steps=10, warmup=2):
         opt.optimize_step(it)
         it += 1
     kt = {k: opt.kernel_ms(k) for k in names}
+    ranks = allgather_obj(rank_record(opt, rank, local, kt), world)
     rows_bytes = opt.kernel_bytes("schur_rows")
-    tr = traffic_lookup("C5")
+    tr = traffic_lookup("C5") if world == 1 else (lambda *a: None)  # the PMC files are one-GPU measurements
     cf = load_json("chol_flops.json").get("C5", {}).get("ref_cs_amd", {}).get("flops")
     own = opt.kernel_flops("chol_factor")
     fms = kt["chol_factor"]
     lin = [1e3 * s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
     out = {
         "workload": f"C5: {prob.name} ({prob.num_vertices} vertices, {prob.num_edges} edges), {solver_name(prob)}, "
-                    f"{int(prob.vertices[0].fixed.sum())} fixed cameras, 1 GPU",
-        "value": steps / dt, "unit": "LM it/s", "steps": steps, "warmup": warmup,
+                    f"{int(prob.vertices[0].fixed.sum())} fixed cameras, "
+                    + ("1 GPU" if world == 1 else f"landmarks sharded over {world} GPUs (RCCL)"),
+        "value": steps / dt, "unit": "LM it/s", "n_gpus": world, "scaling": "strong", "steps": steps, "warmup": warmup,
         "ms_per_step": 1e3 * dt / steps, "ms_per_linear_solve": float(np.median(lin)),
         "levenberg_trials": sum(s.levenbergIterations for s in timed), "final_chi2": timed[-1].chi2,
         "stages_ms_avg": kt,
@@ -270,8 +357,11 @@ def c5_leg(local, steps=10, warmup=2):
                               "frac": (cf or own) / (fms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if fms > 0 else 0.0,
                               "backend_ordering_achieved": own / (fms * 1e-3) / 1e12 if fms > 0 else 0.0,
                               "traffic": tr("chol_factor"), "traffic_fetch_doubled": tr("chol_factor", "bytes_fetch_doubled")}),
-        "generate_s": gen,
+        "generate_s": gen, "warmup_incl_structure_s": warm_s,
     }
+    if world > 1:
+        out["ranks"] = ranks
+        out["comm"] = comm_record(ranks, world)
     if kt["schur_rows"] > 0:
         a = rows_bytes / (kt["schur_rows"] * 1e-3) / 1e9
         out["schur_rows"] = with_peaks({"bound": "hbm", "achieved": a, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -280,6 +370,13 @@ def c5_leg(local, steps=10, warmup=2):
                                         "traffic_fetch_doubled": tr("schur_rows", "bytes_fetch_doubled")})
     opt.close()
     return out
+
+
+def comm_record(ranks, world):
+    """The transport the ranks actually used: RCCL communicator size and the RCCL build each rank bound to."""
+    vers = sorted({r.get("rccl_version") for r in ranks if r.get("rccl_version") is not None})
+    return {"transport": "RCCL (ncclCommInitRank, one process per GPU)", "nranks": world, "ranks_reporting": len(ranks),
+            "rccl_versions": vers, "librccl": sorted({r.get("librccl") for r in ranks if r.get("librccl")})}
 
 
 def load_json(name):
@@ -359,8 +456,39 @@ def stage_bytes(prob):
             "shared_records": {"information": shared_info, "intrinsics": shared_par}}
 
 
+METRIC = "LM iterations/sec + ms/linear-solve, synthetic BA 1k×100k at 1/2/4/8 GPUs"
+
+
+def dry_run(args):
+    """The multi-rank control plane without a GPU (tests/test_dist_cpu.py): ranks, barrier-bracketed max-over-ranks
+    timing, per-rank records, and the JSON line's shape with value = null."""
+    rank, world, local = dist_setup(args.gpus)
+    barrier(world)
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    barrier(world)
+    dt = allmax(time.perf_counter() - t0, world)
+    ranks = allgather_obj({"rank": rank, "device": local, "pid": os.getpid(),
+                           "world_size_env": int(os.environ.get("WORLD_SIZE", "1"))}, world)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "LM it/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": 1e3 * dt, "higher_is_better": True,
+                          "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "none (dry run)",
+                          "config": {"workload": f"{args.config} (dry run: no GPU call)",
+                                     "parallelism": f"landmark-shard{world}" if world > 1 else "single"},
+                          "dry_run": True, "ranks": ranks,
+                          "comm": {"transport": "gloo control plane only", "nranks": world}}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))  # before any HIP call: the children are the ranks
+    if args.dry_run:
+        return dry_run(args)
     import g2o_amd
     g2o_amd.lib()  # bind the ROCm 7.2 HIP runtime + RCCL first (dist_setup imports torch)
     rank, world, local = dist_setup(args.gpus)
@@ -422,6 +550,7 @@ def main():
         it += 1
     kt = {k: {"avg_ms": opt.kernel_ms(k), "count": opt.kernel_count(k)} for k in names}
     finfo = opt.factor_info()
+    ranks = allgather_obj(rank_record(opt, rank, local, {k: v["avg_ms"] for k, v in kt.items()}), world)
     try:  # after the timed region: ~1 s of streaming copy and MFMA / VALU issue loops
         PEAKS_MEASURED.update(g2o_amd.measure_peaks(local))
     except Exception as ex:  # reported, not fatal
@@ -508,7 +637,7 @@ def main():
     if prob.landmark_dim:
         fixed = f", {int(prob.vertices[0].fixed.sum())} fixed cameras (gauge + monocular scale; ba_demo.cpp fixes 1)"
     out = {
-        "metric": "LM iterations/sec + ms/linear-solve, synthetic BA 1k×100k at 1/2/4/8 GPUs",
+        "metric": METRIC,
         "value": value,
         "unit": "LM it/s",
         "n_gpus": world,
@@ -543,12 +672,19 @@ def main():
             out["pose_graph"] = posegraph_leg(local)
         except Exception as ex:  # reported, not fatal
             out["pose_graph"] = {"error": repr(ex)}
-    if rank == 0 and world == 1 and not args.no_c5 and args.config == "C4":
-        try:
-            opt.close()
-            out["c5"] = c5_leg(local)
-        except Exception as ex:  # reported, not fatal
-            out["c5"] = {"error": repr(ex)}
+    if world > 1:
+        out["ranks"] = ranks
+        out["comm"] = comm_record(ranks, world)
+    if not args.no_c5 and args.config == "C4":
+        # every rank: at N > 1 the C5 leg is the landmark-sharded multi-GPU configuration (its collectives need all)
+        opt.close()
+        if world == 1:
+            try:
+                out["c5"] = c5_leg(local)
+            except Exception as ex:  # reported, not fatal
+                out["c5"] = {"error": repr(ex)}
+        else:  # a rank failing inside collectives cannot be reported around: let the launcher see it
+            out["c5"] = c5_leg(local, rank=rank, world=world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(prob, args.cpu_iters, args.cpu_threads)

@@ -550,7 +550,8 @@ void backsub_j(const EdgeArgs& a, int nl, const int2* erng, const int* hcam, con
   const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
   // lanes per landmark (dev A/B G2OHIP_BACKSUB_J_LANES; profiles/r04_ab_backsub_lanes.log): 4 against 8 / 16, C5
   // 224.7-225.3 -> 227.5-227.6 / 222.6 LM it/s; 2 against 4, C5 225.0-225.1 -> 226.0-226.3, C4 907.5 -> 912.4
-  static const int lanes = getenv("G2OHIP_BACKSUB_J_LANES") ? atoi(getenv("G2OHIP_BACKSUB_J_LANES")) : 2;
+  static EnvKnob lanes_k{"G2OHIP_BACKSUB_J_LANES", 2};
+  const int lanes = lanes_k.get();
   if (lanes == 2)
     hipLaunchKernelGGL((k_backsub_j<FamilyBA, 2>), grid_for((size_t)nl * 2, 256), 256, 0, s, d, nl, erng, hcam, Ufac,
                        cl_all, size_poses, lm0, x);

@@ -1138,10 +1138,8 @@ void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* front
   // (profiles/r04_ab_c3_syrk.log; 74 KB of LDS leave 2 workgroups per CU against 3). The (16, 2) ring (37 KB, four
   // workgroups per CU) is the one that wins there: C3 factor 29.07 -> 28.54 ms (profiles/r04_ab_c3_knobs.log), the
   // default; G2OHIP_SYRK_DMA=0 is the register-staged GemmNT.
-  static const int dma = [] {
-    const char* e = getenv("G2OHIP_SYRK_DMA");
-    return e ? atoi(e) : 4;
-  }();
+  static EnvKnob dma_k{"G2OHIP_SYRK_DMA", 4};
+  const int dma = dma_k.get();
   switch (dma) {
     case 1: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 32, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
     case 2: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 16, 3>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;

@@ -2,8 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <stdexcept>
 #include <string>
@@ -74,11 +76,37 @@ class DevBuf {
   size_t n_ = 0;
 };
 
+// A launch-time A/B knob read from the environment: cached per call site, re-read after every structure build
+// (Engine::build_structure bumps the epoch), so a process can switch schedules between optimizers (the parity tests
+// do) without a getenv per launch.
+inline std::atomic<int>& knob_epoch() {
+  static std::atomic<int> e{0};
+  return e;
+}
+struct EnvKnob {
+  const char* name;
+  int dflt;
+  std::atomic<int> epoch{-1}, val{0};
+  EnvKnob(const char* n, int d) : name(n), dflt(d) {}
+  int get() {
+    const int e = knob_epoch().load(std::memory_order_relaxed);
+    if (epoch.load(std::memory_order_relaxed) != e) {
+      const char* v = std::getenv(name);
+      val.store(v && *v ? std::atoi(v) : dflt, std::memory_order_relaxed);
+      epoch.store(e, std::memory_order_relaxed);
+    }
+    return val.load(std::memory_order_relaxed);
+  }
+};
+
 inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
-// t^3 rounded once, as the reference's std::pow(t, 3) (glibc's pow is correctly rounded): t^2 = p + e exactly (FMA),
-// t^3 = p t + e t with the product's rounding error carried, then one final rounding. The device's pow is not
-// guaranteed to round the same way; this is the same arithmetic on host and device.
+// t^3 with the products' rounding errors carried (t^2 = p + e exactly by FMA, t^3 = p t + (fma error + e t)) and one
+// final rounding: within ~0.5 ulp of the exact cube. The reference computes std::pow(t, 3) with glibc, which is accurate
+// to < 1 ulp but NOT guaranteed correctly rounded, and the device has no glibc pow. So lambda parity with the reference
+// is within 1 ulp of the factor per accepted trial, not bitwise (tests/test_host.py::test_lm_scale_factor_matches_pow
+// checks the 1-ulp bound; the lambda traces of the full-size tests allow it). What this buys is that the host loop and
+// the device decision (k_sum_final2_decide) run the same arithmetic and so take bitwise identical lambda paths.
 __host__ __device__ inline double cube_rn(double t) {
   const double p = t * t, e = fma(t, t, -p);
   const double h = p * t, l = fma(p, t, -h) + e * t;

@@ -227,7 +227,11 @@ KernelTimer::~KernelTimer() {
 void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, const std::vector<int>& bj,
                            hipStream_t s) {
   pd = bdim;
-  sym = analyze(block_pattern(nblocks, bdim, bi, bj));
+  if (pre_sym) sym = *pre_sym;
+  else sym = analyze(block_pattern(nblocks, bdim, bi, bj));
+  pre_sym.reset();
+  const std::shared_ptr<const DistPlan> plan_given = std::move(pre_plan);
+  pre_plan.reset();
   if ((long long)sym.max_front * sym.max_front >= (1LL << 31))
     throw DeviceError("front too large for 32-bit in-front indexing");
   // input entries per (permuted) scalar column: input block t (bi, bj) col-major bdim x bdim, value index
@@ -306,9 +310,10 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   dist_on = false;
   std::fill(dist_model, dist_model + 5, 0.0);
   if (dist_nranks > 1) {
-    const DistPlan P = plan_distribution(sym, bi, bj, bdim, nblocks, dist_nranks, dist_rank,
-                                         rs_enable && (bool)reduce_scatter, dist_force, aligned,
-                                         pose_work.empty() ? nullptr : &pose_work);
+    const DistPlan P = plan_given ? *plan_given
+                                  : plan_distribution(sym, bi, bj, bdim, nblocks, dist_nranks, dist_rank,
+                                                      rs_enable && (bool)reduce_scatter, dist_force, aligned,
+                                                      pose_work.empty() ? nullptr : &pose_work);
     rs_model[0] = P.input_s;
     rs_model[1] = P.input_repl_s;
     dist_on = P.on;
@@ -482,8 +487,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const int wide_fronts = wf ? atoi(wf) : 64;
     const char* wp = getenv("G2OHIP_CHOL_WIDE_PB");
     const int wide_pb = wp ? std::max(64, atoi(wp) / 64 * 64) : 128;
-    const bool dev_noinv = getenv("G2OHIP_DEV_NOINV") != nullptr;  // timing experiments only (wrong solve)
-    const bool dev_diagonly = getenv("G2OHIP_DEV_DIAGONLY") != nullptr;  // timing experiments only (wrong factor)
+#ifdef G2OHIP_DEV  // development build only (make dev): timing experiments that give a wrong result on purpose
+    const bool dev_noinv = getenv("G2OHIP_DEV_NOINV") != nullptr;  // no inverse tasks (wrong solve)
+    const bool dev_diagonly = getenv("G2OHIP_DEV_DIAGONLY") != nullptr;  // diagonal tasks only (wrong factor)
+#else
+    constexpr bool dev_noinv = false, dev_diagonly = false;
+#endif
     // lagged trailing updates on levels with a separate contribution pass (their steps are bound by the rank-32
     // tile traffic, not the diagonal chain): even steps update only the next panel's column strip, odd steps
     // apply two panels at once (rank 64) to the rest of the supernode's columns (G2OHIP_CHOL_LAG=0: every step
@@ -1922,6 +1931,10 @@ void Engine::align_shards() {
   dist_aligned = false;
   al_bpinv.clear();
   al_bowner.clear();
+  al_sym.reset();
+  al_plan.reset();
+  al_sbi.clear();
+  al_sbj.clear();
   // the hessian order buildIndexMapping gives (initialize): poses, then the free landmarks in id order
   ivmap.resize(num_poses);
   for (int vi : active) {
@@ -1936,13 +1949,21 @@ void Engine::align_shards() {
   if (env0("G2OHIP_DIST_FACTOR") || env0("G2OHIP_DIST_ALIGN")) return;
   std::vector<int> sbi, sbj, srp;
   schur_pattern(sbi, sbj, srp);
-  const Symbolic sym = analyze(block_pattern(num_poses, pd, sbi, sbj));
+  auto symp = std::make_shared<const Symbolic>(analyze(block_pattern(num_poses, pd, sbi, sbj)));
+  const Symbolic& sym = *symp;
   const char* df = getenv("G2OHIP_DIST_FACTOR");
-  // the flags and weights build_structure gives DeviceCholesky::setup, so that both make the same plan
+  // the flags and weights build_structure gives DeviceCholesky::setup (which takes this analysis and plan instead of
+  // making them again: al_sym / al_plan)
   const bool rs = !env0("G2OHIP_DIST_RS");
   const std::vector<double> pw = pose_work();
-  const DistPlan D = plan_distribution(sym, sbi, sbj, pd, num_poses, nranks, rank, rs, df && atoi(df) == 1, true, &pw);
+  auto planp = std::make_shared<const DistPlan>(
+      plan_distribution(sym, sbi, sbj, pd, num_poses, nranks, rank, rs, df && atoi(df) == 1, true, &pw));
+  const DistPlan& D = *planp;
+  al_sym = symp;
+  al_sbi = sbi;
+  al_sbj = sbj;
   if (!D.on) return;
+  al_plan = planp;
   // per landmark its free poses (all edges)
   std::vector<std::vector<int>> lp(num_landmarks);
   for (const HEdgeSet& es : hg.esets)
@@ -1982,6 +2003,7 @@ void Engine::align_shards() {
 }
 
 int Engine::build_structure() {  // block_solver.hpp:102-256
+  knob_epoch().fetch_add(1, std::memory_order_relaxed);  // launch-time knobs re-read from here on
   if (!initialized) {
     int r = initialize();
     if (r) return r;
@@ -2396,6 +2418,12 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         }
       }
       chol.pose_work = pose_work();
+      if (al_sym && s_bi == al_sbi && s_bj == al_sbj) {  // the pattern align_shards analysed: reuse its work
+        chol.pre_sym = al_sym;
+        if (chol.aligned && al_plan) chol.pre_plan = al_plan;
+      }
+      al_sym.reset();
+      al_plan.reset();
       chol.setup(num_poses, pd, s_bi, s_bj, stream);
       if (chol.aligned && !chol.distributed())
         throw DeviceError("aligned landmark shards without the distributed factorization they were cut for");

@@ -148,6 +148,10 @@ struct DeviceCholesky {
   bool aligned = false;
   std::vector<unsigned char> blk_local;
   std::vector<double> pose_work;              // per pose block: the sharded work the cut's model weighs (optional)
+  // analysis already made for this pattern (Engine::align_shards plans the cut before the landmarks are placed): setup
+  // takes them instead of analysing again; both are consumed (reset) by the next setup
+  std::shared_ptr<const Symbolic> pre_sym;
+  std::shared_ptr<const DistPlan> pre_plan;
   double shard_model = 0;                     // modelled busiest rank's sharded work (s) of the chosen layout
   long long rs_local = 0;                     // doubles of this rank's own complete blocks (rs_buf's last region)
   // a factorization of the whole system on this rank alone (pose graphs, computeMarginals' Hpp factor): clears any
@@ -332,6 +336,10 @@ class Engine {
   std::vector<int> lm_bnd;
   bool dist_aligned = false;
   std::vector<int> al_bpinv, al_bowner;  // the cut's pattern: pose block -> permuted block, permuted block -> owner
+  // align_shards' analysis of the Schur pattern (al_sbi, al_sbj) and its aligned plan, handed to DeviceCholesky::setup
+  std::shared_ptr<const Symbolic> al_sym;
+  std::shared_ptr<const DistPlan> al_plan;
+  std::vector<int> al_sbi, al_sbj;
   std::vector<unsigned char> lam_own_h;  // per pose: this rank adds lambda to its diagonal block of S
   DevBuf<unsigned char> d_lam_own;
   void align_shards();

@@ -688,7 +688,11 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
     // vector-memory operations then), B1 / B3 the records k+1 / k+3.
     // The index loads are raw (clamped addresses, no select on the loaded value: a select right behind the load would
     // wait for it); entries past the batch's counts are never read, and the slot CSR is rebased at the store.
-    constexpr int NIDX = 2 * SCH_NI + 1;  // vector loads of one idx_load3 (always issued)
+    // vector loads of one idx_load3: SCH_NI of st_obs + SCH_NI of pairs + 1 of the slot CSR, all unconditional (clamped
+    // addresses). The counted waits below rely on exactly this count: a change to idx_load3 must change NIDX with it
+    // (the batch records rec() are uniform scalar loads and do not count). Checked against PIPE 0 bitwise by
+    // tests/test_gpu_parity.py::test_schur_rows_pipe_bitwise.
+    constexpr int NIDX = 2 * SCH_NI + 1;
     int rpr0 = 0;
     auto idx_load3 = [&](const launch::SchurBatch B, int k) {
 #pragma unroll
@@ -1422,8 +1426,13 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
                 int nzero, const long long* zr, double* fronts, hipStream_t s) {
   if (ntasks <= 0 && nzero <= 0) return;
-  static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;  // dev A/B only
-  static const int pipe = getenv("G2OHIP_SCHUR_PIPE") ? atoi(getenv("G2OHIP_SCHUR_PIPE")) : 1;
+#ifdef G2OHIP_DEV  // development build only: 1 no pair products, 2 no staging, 3 neither (wrong S, timing splits)
+  static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;
+#else
+  constexpr int mode = 0;
+#endif
+  static EnvKnob pipe_k{"G2OHIP_SCHUR_PIPE", 1};  // 0: two index buffers (A/B; tests/test_gpu_parity.py)
+  const int pipe = pipe_k.get();
   const int nz = nzero > 0 ? nzero : 0;
   pl_dispatch(pd, ld, [&](auto P, auto L) {
     constexpr int pv = decltype(P)::value, lv = decltype(L)::value;
@@ -1448,7 +1457,8 @@ void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, con
 void backsub_g(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* G, const double* Ufac,
                const double* cl_all, int size_poses, int lm0, double* x, hipStream_t s) {
   if (nl <= 0) return;
-  static const int lanes = getenv("G2OHIP_BACKSUB_LANES") ? atoi(getenv("G2OHIP_BACKSUB_LANES")) : 8;  // dev A/B (8: C4 48.5 -> 45.3 us)
+  static EnvKnob lanes_k{"G2OHIP_BACKSUB_LANES", 8};
+  const int lanes = lanes_k.get();  // dev A/B (8: C4 48.5 -> 45.3 us)
   pl_dispatch(pd, ld, [&](auto P, auto L) {
     if (lanes == 8)
       hipLaunchKernelGGL((k_backsub_g<decltype(P)::value, decltype(L)::value, 8>), grid_for((size_t)nl * 8, 256), 256,

@@ -158,8 +158,14 @@ long long g2ohip_solver_vector_size(g2ohip_graph* g);           /* Solver::vecto
 /* BlockSolver<p, l> traits after build_structure: dims = [PoseDim, LandmarkDim, pose blocks, landmark blocks]
  * (block_solver.h:44-60; Solver::additionalVectorSpace etc. not needed) */
 int g2ohip_solver_block_dims(g2ohip_graph* g, int* dims);
-int g2ohip_solver_get_x(g2ohip_graph* g, double* x);            /* Solver::x() (host copy) */
-int g2ohip_solver_get_b(g2ohip_graph* g, double* b);            /* Solver::b() (host copy) */
+/* Solver::x() / Solver::b() (host copies) in the Hessian order: poses, then the free landmarks. On one rank the
+ * landmarks follow buildIndexMapping's id order (block_solver.hpp, sparse_optimizer.cpp:207-241). With landmark shards
+ * aligned to the factorization's cut (g2ohip_set_comm, N > 1) the landmarks are regrouped by owning rank (stable in
+ * id order within a rank). The vectors keep a slot for every landmark, but on a sharded rank only its own landmarks'
+ * slots hold this rank's values: one contiguous range of the landmark part, whose landmark ids g2ohip_local_landmarks
+ * lists in the order x / b carry them. */
+int g2ohip_solver_get_x(g2ohip_graph* g, double* x);
+int g2ohip_solver_get_b(g2ohip_graph* g, double* b);
 /* BlockSolverBase::multiplyHessian (core/block_solver.h:94,146; used by OptimizationAlgorithmDogleg
  * optimization_algorithm_dogleg.cpp:100,179): dest = Hpp src with the upper blocks mirrored (+ lambda on the
  * diagonal while a setLambda is active), host arrays of hessianPoseDimension. Single rank only. */

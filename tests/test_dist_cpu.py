@@ -83,3 +83,45 @@ def test_landmark_shard_partition():
         assert sum(s.num_edges for s in subs) == prob.num_edges
         ids = np.concatenate([s.vertices[1].ids for s in subs])
         assert np.array_equal(ids, prob.vertices[1].ids)
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p, (json.loads(lines[-1]) if lines else None)
+
+
+def test_bench_spawns_ranks_dry_run():
+    """`bench.py --gpus 2` without a launcher starts two ranks itself (before any HIP call) and the line reports
+    n_gpus 2 with one record per rank; --dry-run stops before the GPU."""
+    p, out = _run_bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out is not None and out["dry_run"] is True
+    assert out["n_gpus"] == 2
+    assert [r["rank"] for r in out["ranks"]] == [0, 1]
+    assert [r["device"] for r in out["ranks"]] == [0, 1]
+    assert len({r["pid"] for r in out["ranks"]}) == 2
+    assert all(r["world_size_env"] == 2 for r in out["ranks"])
+    assert out["config"]["parallelism"] == "landmark-shard2"
+    assert out["ms_per_step"] >= 20.0  # max over ranks: rank 1 sleeps 20 ms inside the bracketed region
+    for k in ("metric", "unit", "steps", "warmup", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"):
+        assert k in out
+    assert out["steps"] == 3 and out["warmup"] == 1
+
+
+def test_bench_single_rank_dry_run():
+    p, out = _run_bench(["--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert out["n_gpus"] == 1 and len(out["ranks"]) == 1
+
+
+def test_bench_refuses_world_mismatch():
+    """Under a launcher whose WORLD_SIZE differs from --gpus the bench refuses instead of reporting the wrong N."""
+    p, out = _run_bench(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and out is None
+    assert "WORLD_SIZE=1" in p.stderr

@@ -110,34 +110,23 @@ def test_c3_full_trajectory(g2o_amd_mod):
 
 
 def test_c4_bench_sequence(g2o_amd_mod):
-    """C4 (the headline config) over exactly the iterations bench.py runs and times: optimize_step from iteration 0
-    (structure + lambda init), the warmup at full statistics, then the timed steps at stats level 1, every
-    iteration's chi2, lambda and trial count against the oracle + reference CSparse fixture, and the final state."""
-    fx = _fixture("C4")
-    prob = synth.by_name("C4")
-    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
-    opt.set_algorithm(ALG["C4"])
-    chi0 = opt.chi2()
-    assert abs(chi0 - float(fx["chi2_0"])) <= 1e-9 * float(fx["chi2_0"])
-    n = int(fx["iterations"])
-    st = []
-    for it in range(n):
-        if it == 5:  # bench.py: warmup done, the timed region runs at stats level 1
-            opt.set_stats_level(1)
-        r, s = opt.optimize_step(it)
-        st.append(s)
-        assert r == 0, (it, r)
-    _check_trajectory(fx, st, n, chi0)
-    x, xr = opt.minimal_state(), fx["state"]
+    """C4 (the headline config) over exactly the iterations the driver's `bench.py --steps 20 --warmup 5` runs: 5 warmup
+    at full statistics, 20 timed at stats level 1 with the chol_factor timer (bench.py's roofline timer), then the two
+    stage iterations with every kernel timer on at stats level 2 (the speculative next assembly is off while assembly
+    kernels are timed); the fixture's last 3 iterations follow with the same timers. Every iteration's chi2, lambda
+    and trial count against the oracle + reference CSparse fixture, then the final state."""
+    prob, opt = _bench_sequence(g2o_amd_mod, "C4", 5, 20, "chol_factor", extra=3)
+    x, xr = opt.minimal_state(), _fixture("C4")["state"]
     assert np.linalg.norm(x - xr) <= RTOL * np.linalg.norm(xr)
 
 
-def _bench_sequence(g2o_amd_mod, name, warmup, timed, first_timer, stage_timer=None):
+def _bench_sequence(g2o_amd_mod, name, warmup, timed, first_timer, stage_timer=None, extra=0):
     """optimize_step from iteration 0 through exactly the iterations a bench.py leg runs: `warmup` at the default
     statistics, `timed` at stats level 1 (with `first_timer` kernel timing, as the leg's timed region), then the leg's
     two stage iterations with every kernel timer on at stats level 2 — each switch where the leg makes it, since the
     kernel timers change what the LM loop enqueues (the speculative next assembly is off while assembly kernels are
-    timed). Every iteration's chi2, lambda and trial count against the fixture, then the final state."""
+    timed), and `extra` further iterations with those timers. Every iteration's chi2, lambda and trial count against the
+    fixture, then the final state."""
     fx = _fixture(name)
     prob = synth.by_name(name)
     opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
@@ -145,7 +134,7 @@ def _bench_sequence(g2o_amd_mod, name, warmup, timed, first_timer, stage_timer=N
     chi0 = opt.chi2()
     assert abs(chi0 - float(fx["chi2_0"])) <= 1e-9 * float(fx["chi2_0"])
     n = int(fx["iterations"])
-    assert n == warmup + timed + 2, (name, n)
+    assert n == warmup + timed + 2 + extra, (name, n)
     st = []
     for it in range(n):
         if it == warmup:

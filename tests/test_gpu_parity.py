@@ -354,6 +354,18 @@ SCHEDULES = {
     "no_leaf_absorption": {"G2OHIP_ND_ABSORB": "0"},
     # the Schur split's back-substitution from the stored G blocks (default: Jacobians recomputed per observation)
     "backsub_from_g": {"G2OHIP_BACKSUB_RECOMPUTE": "0"},
+    # the Schur row pass with two index buffers drained by each batch's barrier (default: three, counted vmcnt)
+    "schur_rows_pipe0": {"G2OHIP_SCHUR_PIPE": "0"},
+    # contribution / trailing GEMM tiles: the register-staged GemmNT (default: the LDS-DMA ring GemmNTd (16, 2))
+    "syrk_register_staged": {"G2OHIP_SYRK_DMA": "0"},
+    "syrk_dma_32x2": {"G2OHIP_SYRK_DMA": "1"},
+    # in-place extend-add column buffers of 512 / 2048 rows (default 1024)
+    "extend_add_512": {"G2OHIP_EA_BIG": "512"},
+    "extend_add_2048": {"G2OHIP_EA_BIG": "2048"},
+    # recomputing back-substitution with 4 / 8 / 16 lanes per landmark (default 2)
+    "backsub_j_lanes4": {"G2OHIP_BACKSUB_J_LANES": "4"},
+    "backsub_j_lanes8": {"G2OHIP_BACKSUB_J_LANES": "8"},
+    "backsub_j_lanes16": {"G2OHIP_BACKSUB_J_LANES": "16"},
 }
 
 
@@ -383,3 +395,21 @@ def test_factor_schedules(g2o_amd_mod, oracle, monkeypatch, name, mode):
     assert opt.linear_residual() <= 1e-10
     opt.restore_diagonal()
     _check(*_run_both(g2o_amd_mod, oracle, prob, 4))
+
+
+@pytest.mark.parametrize("name", ["C4", "C5"])
+def test_schur_rows_pipe_bitwise(g2o_amd_mod, monkeypatch, name):
+    """k_schur_rows' pipelined index loads (PIPE 1: three index buffers, counted vmcnt waits that trust the number of
+    index loads idx_load3 issues) against the plain double-buffered pass (PIPE 0): both are deterministic with the same
+    summation order, so the reduced camera system must be BITWISE equal; a miscounted wait would read G blocks before
+    they land."""
+    prob = synth.by_name(name, "small")
+    out = {}
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("G2OHIP_SCHUR_PIPE", pipe)
+        opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+        out[pipe] = opt.stage(1e-3)
+        opt.close()
+    assert np.array_equal(out["0"]["Hschur"], out["1"]["Hschur"])
+    assert np.array_equal(out["0"]["bschur"], out["1"]["bschur"])
+    assert np.array_equal(out["0"]["x"], out["1"]["x"])

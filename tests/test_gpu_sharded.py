@@ -14,7 +14,16 @@ from g2o_amd import synth
 from shard_util import gather_sharded_state
 
 pytestmark = pytest.mark.gpu
-os.environ.setdefault("G2OHIP_COMM_CHECK", "1")  # RcclComm verifies every collective's (call, length, op) across ranks
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _comm_check_every_call():
+    """RcclComm verifies every collective's (call, length, op) across ranks in this module only (the library reads the
+    variable when a communicator is made, so other modules keep the default check of the first calls)."""
+    with pytest.MonkeyPatch.context() as mp:
+        if "G2OHIP_COMM_CHECK" not in os.environ:
+            mp.setenv("G2OHIP_COMM_CHECK", "1")
+        yield
 
 RTOL = 1e-6
 

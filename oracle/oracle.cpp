@@ -1945,6 +1945,32 @@ int oracle_push(OracleGraph* og) { push(og->g); return 0; }
 int oracle_pop(OracleGraph* og) { pop(og->g); return 0; }
 int oracle_discard_top(OracleGraph* og) { discardTop(og->g); return 0; }
 
+// The rotation / isometry mappings of isometry3d_mappings.{h,cpp} and the SE2 constructors, for the CPU pins of the
+// reference's own unit tests (unit_test/slam3d/mappings_slam3d.cpp, orthogonal_matrix.cpp, slam2d/mappings_se2.cpp).
+// Matrices col-major (Eigen), an isometry as [R (9) | t (3)]. Returns the number of doubles written, -1 for an unknown op.
+int oracle_mapping(int op, const double* in, double* out) {
+  auto getR = [](const double* p) { M3 R; for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) R.m[r][c] = p[c * 3 + r]; return R; };
+  auto putR = [](const M3& R, double* p) { for (int c = 0; c < 3; ++c) for (int r = 0; r < 3; ++r) p[c * 3 + r] = R.m[r][c]; return 9; };
+  auto getI = [&](const double* p) { Iso3 a; a.R = getR(p); a.t = {p[9], p[10], p[11]}; return a; };
+  auto putI = [&](const Iso3& a, double* p) { putR(a.R, p); p[9] = a.t.x; p[10] = a.t.y; p[11] = a.t.z; return 12; };
+  switch (op) {
+    case 0: return putR(fromEuler(V3{in[0], in[1], in[2]}), out);
+    case 1: { const V3 e = toEuler(getR(in)); out[0] = e.x; out[1] = e.y; out[2] = e.z; return 3; }
+    case 2: { const V3 q = toCompactQuaternion(getR(in)); out[0] = q.x; out[1] = q.y; out[2] = q.z; return 3; }
+    case 3: return putR(fromCompactQuaternion(V3{in[0], in[1], in[2]}), out);
+    case 4: return putI(fromVectorET(in), out);
+    case 5: toVectorET(getI(in), out); return 6;
+    case 6: toVectorMQT(getI(in), out); return 6;
+    case 7: return putI(fromVectorMQT(in), out);
+    case 8: toVectorQT(getI(in), out); return 7;
+    case 9: return putI(fromVectorQT(in), out);
+    case 10: { M3 R = getR(in); approximateNearestOrthogonalMatrix(R); return putR(R, out); }
+    case 11: { M3 R = getR(in); nearestOrthogonalMatrix(R); return putR(R, out); }
+    case 12: { const SE2 s = se2FromIso(in, in + 4); out[0] = s.x; out[1] = s.y; out[2] = s.th; return 3; }
+    default: return -1;
+  }
+}
+
 int oracle_ref_available(void) { return refcs().ok() ? 1 : 0; }
 const char* oracle_ref_path(void) { return refcs().path.c_str(); }
 

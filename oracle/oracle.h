@@ -110,6 +110,8 @@ int oracle_push(OracleGraph* g);
 int oracle_pop(OracleGraph* g);
 int oracle_discard_top(OracleGraph* g);
 int oracle_ref_available(void);
+/* isometry3d_mappings / SE2 mappings (op codes in oracle.cpp), for the reference unit-test pins */
+int oracle_mapping(int op, const double* in, double* out);
 const char* oracle_ref_path(void);
 
 #ifdef __cplusplus

@@ -10,6 +10,7 @@
 // Every function cites the reference file:line it follows
 // (paths relative to /root/reference).
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -252,6 +253,83 @@ inline void approximateNearestOrthogonalMatrix(M3& R) {
   R = madd(R, mmul(R, E), -0.5);
 }
 
+// isometry3d_mappings.cpp:48-58 toEuler (roll, pitch, yaw) from the quaternion of R
+inline V3 toEuler(const M3& R) {
+  const Quat q = qFromR(R);
+  const double q0 = q.w, q1 = q.x, q2 = q.y, q3 = q.z;
+  return {std::atan2(2 * (q0 * q1 + q2 * q3), 1 - 2 * (q1 * q1 + q2 * q2)), std::asin(2 * (q0 * q2 - q3 * q1)),
+          std::atan2(2 * (q0 * q3 + q1 * q2), 1 - 2 * (q2 * q2 + q3 * q3))};
+}
+// isometry3d_mappings.cpp:60-76 fromEuler: the quaternion of roll / pitch / yaw half angles, then toRotationMatrix
+inline M3 fromEuler(V3 v) {
+  const double sy = std::sin(v.z * 0.5), cy = std::cos(v.z * 0.5);
+  const double sp = std::sin(v.y * 0.5), cp = std::cos(v.y * 0.5);
+  const double sr = std::sin(v.x * 0.5), cr = std::cos(v.x * 0.5);
+  return qToR(Quat{cr * cp * cy + sr * sp * sy, sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy,
+                   cr * cp * sy - sr * sp * cy});
+}
+// isometry3d_mappings.cpp:102-107 toVectorET, :125-130 fromVectorET: (x y z roll pitch yaw)
+inline void toVectorET(const Iso3& a, double* v) {
+  const V3 e = toEuler(a.R);
+  v[0] = a.t.x; v[1] = a.t.y; v[2] = a.t.z; v[3] = e.x; v[4] = e.y; v[5] = e.z;
+}
+inline Iso3 fromVectorET(const double* v) {
+  Iso3 r;
+  r.R = fromEuler(V3{v[3], v[4], v[5]});
+  r.t = {v[0], v[1], v[2]};
+  return r;
+}
+inline double det3(const M3& a) {
+  return a.m[0][0] * (a.m[1][1] * a.m[2][2] - a.m[1][2] * a.m[2][1]) -
+         a.m[0][1] * (a.m[1][0] * a.m[2][2] - a.m[1][2] * a.m[2][0]) +
+         a.m[0][2] * (a.m[1][0] * a.m[2][1] - a.m[1][1] * a.m[2][0]);
+}
+// isometry3d_mappings.h:64-73 nearestOrthogonalMatrix: R = U' V^T from the SVD R = U S V^T (Eigen JacobiSVD, an
+// unvendored dependency: restated as a one-sided Jacobi SVD with singular values sorted decreasing, as Eigen returns
+// them), with U's first column divided by det(U V^T). Not on the solver path (VertexSE3::oplusImpl uses the approximate
+// form below); restated to pin the reference's own orthogonal_matrix.cpp test.
+inline void nearestOrthogonalMatrix(M3& R) {
+  M3 A = R, V = meye();
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0;
+    for (int p = 0; p < 2; ++p)
+      for (int q = p + 1; q < 3; ++q) {
+        double a = 0, b = 0, g = 0;
+        for (int i = 0; i < 3; ++i) {
+          a += A.m[i][p] * A.m[i][p];
+          b += A.m[i][q] * A.m[i][q];
+          g += A.m[i][p] * A.m[i][q];
+        }
+        if (std::fabs(g) <= 1e-300) continue;
+        off = std::max(off, std::fabs(g) / std::sqrt(a * b));
+        const double zeta = (b - a) / (2 * g);
+        const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1 + zeta * zeta));
+        const double c = 1 / std::sqrt(1 + t * t), s = c * t;
+        for (int i = 0; i < 3; ++i) {
+          const double x = A.m[i][p], y = A.m[i][q];
+          A.m[i][p] = c * x - s * y;
+          A.m[i][q] = s * x + c * y;
+          const double vx = V.m[i][p], vy = V.m[i][q];
+          V.m[i][p] = c * vx - s * vy;
+          V.m[i][q] = s * vx + c * vy;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  double sg[3];
+  int ord[3] = {0, 1, 2};
+  for (int k = 0; k < 3; ++k) sg[k] = std::sqrt(A.m[0][k] * A.m[0][k] + A.m[1][k] * A.m[1][k] + A.m[2][k] * A.m[2][k]);
+  std::sort(ord, ord + 3, [&](int a, int b) { return sg[a] > sg[b]; });
+  M3 U, Vs;
+  for (int k = 0; k < 3; ++k)
+    for (int i = 0; i < 3; ++i) {
+      U.m[i][k] = A.m[i][ord[k]] / sg[ord[k]];
+      Vs.m[i][k] = V.m[i][ord[k]];
+    }
+  const double det = det3(mmul(U, mT(Vs)));
+  for (int i = 0; i < 3; ++i) U.m[i][0] /= det;
+  R = mmul(U, mT(Vs));
+}
 // ---- dq/dR (dquat2mat.cpp:63-86) -------------------------------------------
 // Derivative of the (x,y,z) part of the quaternion extracted from R (with the
 // w>=0 sign convention) w.r.t. the 9 entries of R in column-major order
@@ -353,6 +431,16 @@ inline SE2 se2inv(const SE2& a) {  // se2.h:84-94
   const double tx = -a.x, ty = -a.y;
   r.x = c * tx - s * ty;
   r.y = s * tx + c * ty;
+  return r;
+}
+
+// se2.h:45-47 SE2(const Isometry2&): translation, and Rotation2D's angle of the linear part (Eigen
+// Rotation2D::fromRotationMatrix: atan2(R(1,0), R(0,0)))
+inline SE2 se2FromIso(const double* R2 /* col-major 2x2 */, const double* t) {
+  SE2 r;
+  r.x = t[0];
+  r.y = t[1];
+  r.th = std::atan2(R2[1], R2[0]);
   return r;
 }
 

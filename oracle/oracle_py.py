@@ -78,6 +78,8 @@ def lib():
         L.oracle_pop.argtypes = [P]
         L.oracle_discard_top.argtypes = [P]
         L.oracle_ref_available.restype = I
+        L.oracle_mapping.argtypes = [I, P, P]
+        L.oracle_mapping.restype = I
         L.oracle_ref_path.restype = C.c_char_p
         _lib = L
     return _lib
@@ -85,6 +87,21 @@ def lib():
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+MAPPING_OPS = {"fromEuler": 0, "toEuler": 1, "toCompactQuaternion": 2, "fromCompactQuaternion": 3, "fromVectorET": 4,
+               "toVectorET": 5, "toVectorMQT": 6, "fromVectorMQT": 7, "toVectorQT": 8, "fromVectorQT": 9,
+               "approximateNearestOrthogonalMatrix": 10, "nearestOrthogonalMatrix": 11, "SE2fromIsometry2": 12}
+
+
+def mapping(name: str, x) -> np.ndarray:
+    """isometry3d_mappings / SE2 as the oracle restates them: matrices col-major (9), isometries [R col-major | t]
+    (12), vectors as the reference orders them."""
+    x = np.ascontiguousarray(x, np.float64).ravel()
+    out = np.zeros(16)
+    n = lib().oracle_mapping(MAPPING_OPS[name], x.ctypes.data_as(C.c_void_p), out.ctypes.data_as(C.c_void_p))
+    assert n > 0, name
+    return out[:n].copy()
 
 
 def ref_available() -> bool:

@@ -236,3 +236,148 @@ def test_oracle_block_symbolic_natural_order(oracle):
         L[np.ix_(rows, rows)] |= np.tril(np.ones((len(rows), len(rows)), bool))
     cnt = L.sum(axis=0)
     assert lnz == cnt.sum() and fl == float((cnt.astype(np.float64) ** 2).sum())
+
+
+# ---- the reference's own mapping tests, restated against the oracle's mappings (oracle_math.hpp) ----
+# EXPECT_DOUBLE_EQ is gtest's 4-ulp comparison; EXPECT_NEAR / EXPECT_EQ / EXPECT_LE / EXPECT_GE as written.
+
+def _double_eq(a, b):
+    a, b = float(a), float(b)
+    if a == b:
+        return True
+    ia = np.array([a]).view(np.int64)[0]
+    ib = np.array([b]).view(np.int64)[0]
+    ia = ia if ia >= 0 else -(ia & 0x7FFFFFFFFFFFFFFF)  # sign-magnitude -> biased, as gtest's FloatingPoint
+    ib = ib if ib >= 0 else -(ib & 0x7FFFFFFFFFFFFFFF)
+    return abs(int(ia) - int(ib)) <= 4
+
+
+def _R(v9):
+    return np.asarray(v9).reshape(3, 3).T  # col-major -> matrix
+
+
+def _flat(R):
+    return np.asarray(R).T.ravel()
+
+
+EULER = np.array([.1, .2, .3])
+ET = np.array([1., 2., 3., .1, .2, .3])
+
+
+def test_mappings_slam3d_euler_conversion(oracle):
+    """unit_test/slam3d/mappings_slam3d.cpp:35-42 (EulerConversion): toEuler(fromEuler(e)) == e to 4 ulps."""
+    m1 = oracle.mapping("fromEuler", EULER)
+    back = oracle.mapping("toEuler", m1)
+    for i in range(3):
+        assert _double_eq(EULER[i], back[i]), (i, EULER[i], back[i])
+
+
+def test_mappings_slam3d_quaternion_conversion(oracle):
+    """mappings_slam3d.cpp:44-53 (QuaternionConversion): fromCompactQuaternion(toCompactQuaternion(R)) == R to 4 ulps
+    entry by entry — the compact (x, y, z; w >= 0) quaternion EdgeSE3's error (toVectorMQT) is built on."""
+    m1 = oracle.mapping("fromEuler", EULER)
+    q = oracle.mapping("toCompactQuaternion", m1)
+    m2 = oracle.mapping("fromCompactQuaternion", q)
+    for k in range(9):
+        assert _double_eq(m1[k], m2[k]), (k, m1[k], m2[k])
+
+
+def test_mappings_slam3d_et(oracle):
+    """mappings_slam3d.cpp:55-72 (ET): fromVectorET keeps the translation exactly and the rotation of fromEuler to 1e-6;
+    toVectorET inverts it to 1e-6."""
+    m1 = _R(oracle.mapping("fromEuler", EULER))
+    i1 = oracle.mapping("fromVectorET", ET)
+    for r in range(3):
+        assert ET[r] == i1[9 + r]
+    assert np.abs(_R(i1[:9]) - m1).max() <= 1e-6
+    et2 = oracle.mapping("toVectorET", i1)
+    assert np.abs(ET - et2).max() <= 1e-6
+
+
+def test_mappings_slam3d_mqt(oracle):
+    """mappings_slam3d.cpp:74-88 (MQT): fromVectorMQT(toVectorMQT(T)) == T to 1e-6 (rotation and translation)."""
+    i1 = oracle.mapping("fromVectorET", ET)
+    qt1 = oracle.mapping("toVectorMQT", i1)
+    assert qt1.size == 6
+    i2 = oracle.mapping("fromVectorMQT", qt1)
+    assert np.abs(_R(i1[:9]) - _R(i2[:9])).max() <= 1e-6
+    assert np.abs(i1[9:] - i2[9:]).max() <= 1e-6
+
+
+def test_mappings_slam3d_qt(oracle):
+    """mappings_slam3d.cpp:90-104 (QT): fromVectorQT(toVectorQT(T)) == T to 1e-6 — the (x y z qx qy qz qw) layout of the
+    VERTEX_SE3:QUAT / EDGE_SE3:QUAT tags."""
+    i1 = oracle.mapping("fromVectorET", ET)
+    qt2 = oracle.mapping("toVectorQT", i1)
+    assert qt2.size == 7
+    assert abs(np.linalg.norm(qt2[3:]) - 1.0) <= 1e-15
+    i2 = oracle.mapping("fromVectorQT", qt2)
+    assert np.abs(_R(i1[:9]) - _R(i2[:9])).max() <= 1e-6
+    assert np.abs(i1[9:] - i2[9:]).max() <= 1e-6
+
+
+def _angle_axis(angle, axis):
+    """Eigen AngleAxis::toRotationMatrix (Rodrigues) for a unit axis — the test's input construction."""
+    a = np.asarray(axis, float)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    return np.eye(3) * math.cos(angle) + math.sin(angle) * K + (1 - math.cos(angle)) * np.outer(a, a)
+
+
+def test_orthogonal_matrix(oracle):
+    """unit_test/slam3d/orthogonal_matrix.cpp:33-77 (Slam3D.OrthogonalMatrix): 10000 products of a small rotation
+    drift off orthogonality; nearestOrthogonalMatrix brings det and R R^T back to 1e-7, and the approximate form that
+    VertexSE3::oplusImpl applies every 1000 updates (vertex_se3.h:110-113) to 1e-6, never closer than the exact one."""
+    R = np.eye(3)
+    rot = _angle_axis(0.01, [0, 0, 1]) @ _angle_axis(0.01, [1, 0, 0])
+    initial = np.abs(R @ R.T - np.eye(3)).max()
+    assert _double_eq(0.0, initial)
+    for _ in range(10000):
+        R = R @ rot
+    after = np.abs(R @ R.T - np.eye(3)).max()
+    assert after >= initial
+    inaccurate_det = np.linalg.det(R)
+    approx = _R(oracle.mapping("approximateNearestOrthogonalMatrix", _flat(R)))
+    Rn = _R(oracle.mapping("nearestOrthogonalMatrix", _flat(R)))
+    assert abs(np.linalg.det(Rn) - 1.0) <= abs(inaccurate_det - 1.0)
+    assert abs(1.0 - np.linalg.det(Rn)) <= 1e-7
+    assert np.abs(Rn @ Rn.T - np.eye(3)).max() <= 1e-7
+    for i in range(3):
+        assert abs(1.0 - np.linalg.norm(Rn[:, i])) <= 1e-7
+    assert np.abs(approx @ approx.T - np.eye(3)).max() <= 1e-6
+    assert abs(np.linalg.det(Rn) - 1.0) <= abs(np.linalg.det(approx) - 1.0)
+    assert abs(1.0 - np.linalg.det(approx)) <= 1e-6
+    for i in range(3):
+        assert abs(1.0 - np.linalg.norm(approx[:, i])) <= 1e-6
+
+
+def test_nearest_orthogonal_matrix_is_the_polar_factor(oracle):
+    """The restated one-sided Jacobi SVD behind nearestOrthogonalMatrix: for det > 0 the result is the orthogonal polar
+    factor U V^T (numpy's SVD), for det < 0 U's first column (largest singular value) flips, as the reference divides
+    it by det(U V^T) = -1."""
+    rng = np.random.default_rng(3)
+    for k in range(200):
+        A = rng.normal(size=(3, 3))
+        U, s, Vt = np.linalg.svd(A)
+        d = np.linalg.det(U @ Vt)
+        U[:, 0] /= d
+        want = U @ Vt
+        got = _R(oracle.mapping("nearestOrthogonalMatrix", _flat(A)))
+        assert np.abs(got - want).max() <= 1e-12, (k, np.abs(got - want).max())
+
+
+def test_mappings_se2(oracle, tmp_path):
+    """unit_test/slam2d/mappings_se2.cpp:34-55 (MappingsSlam2D.SE2): the three SE2 constructors. From three values and
+    from a vector the (x, y, theta) are kept exactly — checked through the oracle's VERTEX_SE2 reader / writer, the path
+    those values take into the oracle; from an Isometry2 of Rotation2D(1) the angle comes back as 1 (4 ulps) and the
+    translation as 0."""
+    for vals in ((0., 1., 2.), (0.1, 0.2, 0.3)):
+        path = tmp_path / "se2.g2o"
+        path.write_text(f"VERTEX_SE2 0 {vals[0]!r} {vals[1]!r} {vals[2]!r}\nFIX 0\n")
+        g = oracle.OracleGraph.load(str(path))
+        est = g.estimates(synth.V_SE2)
+        for k in range(3):
+            assert _double_eq(vals[k], est[0][k]), (vals, est)
+    c, s = math.cos(1.0), math.sin(1.0)
+    s3 = oracle.mapping("SE2fromIsometry2", [c, s, -s, c, 0.0, 0.0])
+    assert _double_eq(0., s3[0]) and _double_eq(0., s3[1])
+    assert _double_eq(1., s3[2]), s3

@@ -40,10 +40,12 @@ __device__ __forceinline__ void copy_out(double* __restrict__ dst, const double*
 }
 
 // error, Jacobians and the (robust-weighted) information of one edge (base_binary_edge.hpp:104-135)
-template <class F>
-__device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err, double* A, double* B, double* Om) {
+template <class F, bool PC = false>
+__device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err, double* A, double* B, double* Om,
+                                           double* pc = nullptr) {
   constexpr int D = F::D;
-  F::linearize(d, e, err, A, B);
+  if constexpr (PC) F::linearize(d, e, err, A, B, pc);
+  else F::linearize(d, e, err, A, B);
   load_info<D>(info_rec(d, e, F::INFO), Om);
   if (d.rk) {
     double chi = 0;
@@ -62,7 +64,16 @@ __device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err
 }
 }  // namespace
 
-template <class F, bool FG>
+// KX (with FG, BA only): instead of G = Hpl U^-T (18 doubles) each observation stores the 10-double record the Schur
+// row pass rebuilds G from: Kt = diag(fx, fy) Omega A U^-T (2 x 3 col-major), then (u, v, w) = (x/z, y/z, 1/z) of the
+// point in the camera frame, then a pad. The camera Jacobian is B = diag(fx, fy) Bt(u, v, w) with
+//   Bt = [ u v   -(1 + u^2)   v   -w    0   u w ]
+//        [ 1+v^2   -u v      -u    0   -w   v w ]    (types_six_dof_expmap.cpp linearizeOplus, z-scaled)
+// so Hpl = B^T Omega A = Bt^T diag(f) Omega A and G = Bt^T Kt. Split landmarks store Kt before U^-T (k_lm_fixup
+// applies it).
+constexpr int KXB = 10;
+
+template <class F, bool FG, bool KX = false>
 __global__ void __launch_bounds__(256)
     k_linearize_fused(EdgeData d, const int4* __restrict__ chunks, int nchunks, const int* __restrict__ h0,
                       const int* __restrict__ h1, const long long* __restrict__ off_dst,
@@ -86,8 +97,8 @@ __global__ void __launch_bounds__(256)
   const int pv = in ? d.v0[e] : -1;
   const int hA = in ? h0[pv] : -1;
   const bool nfA = hA >= 0, nfB = in && h1[d.v1[e]] >= 0;
-  double err[D], A[D * DA], B[D * DB], Om[D * D];
-  if (nfA || nfB) edge_terms<F>(d, e, err, A, B, Om);
+  double err[D], A[D * DA], B[D * DB], Om[D * D], pc[3];
+  if (nfA || nfB) edge_terms<F, KX>(d, e, err, A, B, Om, pc);
   double wr[D];
 #pragma unroll
   for (int r = 0; r < D; ++r) {
@@ -113,16 +124,38 @@ __global__ void __launch_bounds__(256)
     constexpr long long SLOT_BIT = 1LL << 62;
     const long long od_raw = (nfA && nfB) ? off_dst[e] : -1;
     const bool in_slot = od_raw >= 0 && (od_raw & SLOT_BIT);
-    const long long od = od_raw >= 0 ? (od_raw & ~SLOT_BIT) - (FG ? sp.hpl_base : 0) : -1;
+    constexpr int BS = KX ? KXB : SH;  // doubles per stored block
+    long long od = od_raw >= 0 ? (od_raw & ~SLOT_BIT) - (FG ? sp.hpl_base : 0) : -1;
+    if constexpr (KX) od = od >= 0 ? od / SH * KXB : -1;  // no duplicate (landmark, camera) edges in KX mode: no slots
     double* base = FG ? sp.G : off_base;
     const bool tr = nfA && nfB && off_tr[e];
     const long long od0 = __shfl(od, 0, 64);
     const bool tr0 = __shfl((int)tr, 0, 64) != 0;
     const bool slot0f = __shfl((int)in_slot, 0, 64) != 0;
-    const bool run = __all(!in || (od >= 0 && od0 >= 0 && od == od0 + (long long)lane * SH && tr == tr0 && in_slot == slot0f));
+    const bool run = __all(!in || (od >= 0 && od0 >= 0 && od == od0 + (long long)lane * BS && tr == tr0 && in_slot == slot0f));
     if (od >= 0) {
-      double* H = run ? sw + lane * SH : (in_slot ? off_slot : base) + od;
-      if (FG || tr) {  // (pose, landmark) block, column-major: H[i * DB + j] = (A^T Omega B)(i, j)
+      double* H = run ? sw + lane * BS : (in_slot ? off_slot : base) + od;
+      if constexpr (KX) {  // Kt = diag(f) Omega A (U^-T unless the landmark is split), then (x/z, y/z, 1/z)
+        const double* Kp = param_rec(d, e, 4);
+        double W[D * DA];
+#pragma unroll
+        for (int a2 = 0; a2 < DA; ++a2)
+#pragma unroll
+          for (int r = 0; r < D; ++r) {
+            double s = 0;
+#pragma unroll
+            for (int c = 0; c < D; ++c) s += Om[r * D + c] * A[c * DA + a2];
+            W[a2 * D + r] = Kp[r] * s;
+          }
+        if (ch.z < 0) form_G<D, DA>(W, U);
+        const double iz = 1.0 / pc[2];
+#pragma unroll
+        for (int k = 0; k < D * DA; ++k) H[k] = W[k];
+        H[6] = pc[0] * iz;
+        H[7] = pc[1] * iz;
+        H[8] = iz;
+        H[9] = 0.0;
+      } else if (FG || tr) {  // (pose, landmark) block, column-major: H[i * DB + j] = (A^T Omega B)(i, j)
         double g[SH];
 #pragma unroll
         for (int i = 0; i < DA; ++i)
@@ -152,7 +185,7 @@ __global__ void __launch_bounds__(256)
     }
     if (run) {
       wsync();
-      copy_out((slot0f ? off_slot : base) + od0, sw, nw * SH, lane);
+      copy_out((slot0f ? off_slot : base) + od0, sw, nw * BS, lane);
     }
     wsync();
   };
@@ -248,7 +281,7 @@ __global__ void __launch_bounds__(256)
 
 // split landmarks: fix = (hessian index, first partial, count); partials added in chunk order. With a Schur split the
 // landmark's U, c follow, and its G blocks (stored as Hpl by the linearize chunks) are formed in place.
-template <bool FG>
+template <bool FG, bool KX = false>
 __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restrict__ fix, const double* __restrict__ lpart,
                                                   double* __restrict__ Hll, double* __restrict__ bvec, int num_poses,
                                                   int size_poses, int lm_begin, launch::SchurSplit sp) {
@@ -294,6 +327,18 @@ __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restri
     for (int j = 0; j < 6; ++j) sp.Ufac[(size_t)l * 6 + j] = U[j];
 #pragma unroll
     for (int j = 0; j < 3; ++j) sp.cl[(size_t)(f.x - num_poses) * 3 + j] = cl[j];
+    if constexpr (KX) {  // Kt U^-T in place; (u, v, w) as the linearize chunks stored them
+      for (int a2 = sp.lm_ptr[l]; a2 < sp.lm_ptr[l + 1]; ++a2) {
+        double g[6];
+        double* gp = sp.G + (size_t)a2 * KXB;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) g[j] = gp[j];
+        form_G<2, 3>(g, U);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) gp[j] = g[j];
+      }
+      return;
+    }
     for (int a2 = sp.lm_ptr[l]; a2 < sp.lm_ptr[l + 1]; ++a2) {
       double g[18];
       double* gp = sp.G + (size_t)a2 * 18;
@@ -524,7 +569,10 @@ void linearize_fused(const EdgeArgs& a, const int4* chunks, int nchunks, const i
   if (nchunks <= 0) return;
   const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
   const SchurSplit z = sp ? *sp : SchurSplit{};
-  if (sp)
+  if (sp && sp->kx)
+    hipLaunchKernelGGL((k_linearize_fused<FamilyBA, true, true>), grid_for(nchunks, 4), 256, 0, s, d, chunks, nchunks, h0,
+                       h1, off_dst, off_tr, off_base, off_slot, Hll, b, num_poses, size_poses, lm_begin, lpart, z);
+  else if (sp)
     hipLaunchKernelGGL((k_linearize_fused<FamilyBA, true>), grid_for(nchunks, 4), 256, 0, s, d, chunks, nchunks, h0, h1,
                        off_dst, off_tr, off_base, off_slot, Hll, b, num_poses, size_poses, lm_begin, lpart, z);
   else
@@ -536,7 +584,10 @@ void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, doubl
               int lm_begin, const SchurSplit* sp, hipStream_t s) {
   if (nfix <= 0) return;
   const SchurSplit z = sp ? *sp : SchurSplit{};
-  if (sp)
+  if (sp && sp->kx)
+    hipLaunchKernelGGL((k_lm_fixup<true, true>), grid_for(nfix, 256), 256, 0, s, nfix, fix, lpart, Hll, b, num_poses,
+                       size_poses, lm_begin, z);
+  else if (sp)
     hipLaunchKernelGGL(k_lm_fixup<true>, grid_for(nfix, 256), 256, 0, s, nfix, fix, lpart, Hll, b, num_poses,
                        size_poses, lm_begin, z);
   else

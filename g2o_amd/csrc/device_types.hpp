@@ -353,11 +353,15 @@ struct FamilyBA {
     err[1] = d.meas[(size_t)e * 2 + 1] - (pc[1] / pc[2] * K[1] + K[3]);
   }
   DI static void linearize(const EdgeData& d, int e, double* err, double* A, double* B) {
+    double pc[3];
+    linearize(d, e, err, A, B, pc);
+  }
+  // ... and the point in the camera frame (x, y, z): the camera Jacobian is B = diag(fx, fy) Bt(x/z, y/z, 1/z)
+  DI static void linearize(const EdgeData& d, int e, double* err, double* A, double* B, double* pc) {
     const double* c = d.s1 + (size_t)d.v1[e] * 8;
     const double* p = d.s0 + (size_t)d.v0[e] * 3;
     const double q[4] = {c[3], c[4], c[5], c[6]};
     const double pv[3] = {p[0], p[1], p[2]};
-    double pc[3];
     qrot(q, pv, pc);
     pc[0] += c[0]; pc[1] += c[1]; pc[2] += c[2];
     const double* K = param_rec(d, e, 4);

@@ -2002,6 +2002,13 @@ void Engine::align_shards() {
   dist_aligned = true;
 }
 
+// staged Kt records per Schur row batch (G2OHIP_SCHUR_SB_KX: 128, 192 or 256; A/B)
+int Engine::kx_batch_size() {
+  const char* v = getenv("G2OHIP_SCHUR_SB_KX");
+  const int sb = v ? atoi(v) : launch::SCHUR_SB_KX;
+  return sb == 128 || sb == 192 || sb == 256 ? sb : launch::SCHUR_SB_KX;
+}
+
 int Engine::build_structure() {  // block_solver.hpp:102-256
   knob_epoch().fetch_add(1, std::memory_order_relaxed);  // launch-time knobs re-read from here on
   if (!initialized) {
@@ -2249,9 +2256,22 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       sch_obs_lm.upload(obs_lm, stream);
       sch_sdiag.upload(sdiag, stream);
 
-      std::vector<launch::SchurTask> tasks;
-      std::vector<launch::SchurBatch> batches;
-      std::vector<int> st_obs, st_obs_h, prs, pp;
+      // one batch set per staged-block size: SB blocks per batch (G blocks: launch::SCHUR_SB; the split's 80-byte Kt
+      // records: G2OHIP_SCHUR_SB_KX, default launch::SCHUR_SB_KX)
+      struct BatchSet {
+        std::vector<launch::SchurTask> tasks;
+        std::vector<launch::SchurBatch> batches;
+        std::vector<int> st_obs, st_obs_h, prs, pp;
+        long long npairs = 0;
+      };
+      auto build_batches = [&](int SB, BatchSet& bs) {
+      auto& tasks = bs.tasks;
+      auto& batches = bs.batches;
+      auto& st_obs = bs.st_obs;
+      auto& st_obs_h = bs.st_obs_h;
+      auto& prs = bs.prs;
+      auto& pp = bs.pp;
+      long long& npairs = bs.npairs;
       std::vector<int> camslot(num_poses, -1);
       struct P3 { int ls, a, b; };
       std::vector<P3> cur;
@@ -2316,16 +2336,35 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         }
         for (int k = s_lo; k < s_hi; ++k) camslot[s_bj[k]] = -1;
       }
-      nsch_tasks = (int)tasks.size();
-      nstaged = (long long)st_obs.size();
-      auto nz = [](std::vector<int>& v) -> std::vector<int>& { if (v.empty()) v.push_back(0); return v; };
-      sch_tasks.upload(tasks.empty() ? std::vector<launch::SchurTask>(1) : tasks, stream);
       batches.push_back(launch::SchurBatch{});  // trailing dummy: k_schur_rows reads one record ahead
-      sch_batches.upload(batches, stream);
-      sch_st_obs.upload(nz(st_obs), stream);
-      sch_st_obs_h.upload(nz(st_obs_h), stream);
-      sch_pairs.upload(nz(prs), stream);
-      sch_pp.upload(nz(pp), stream);
+      };
+      auto nz = [](std::vector<int>& v) -> std::vector<int>& { if (v.empty()) v.push_back(0); return v; };
+      {
+        BatchSet bs;
+        build_batches(SB, bs);
+        npairs = bs.npairs;
+        nsch_tasks = (int)bs.tasks.size();
+        nstaged = (long long)bs.st_obs.size();
+        sch_tasks.upload(bs.tasks.empty() ? std::vector<launch::SchurTask>(1) : bs.tasks, stream);
+        sch_batches.upload(bs.batches, stream);
+        sch_st_obs.upload(nz(bs.st_obs), stream);
+        sch_st_obs_h.upload(nz(bs.st_obs_h), stream);
+        sch_pairs.upload(nz(bs.prs), stream);
+        sch_pp.upload(nz(bs.pp), stream);
+      }
+      // the Kt-record set (BA split; decided with the split below): another block size needs its own batches
+      kx_sb = kx_batch_size();
+      nsch_tasks_kx = 0;
+      if (kx_sb != SB && ba_fused && pd == 6 && ld == 3) {
+        BatchSet bs;
+        build_batches(kx_sb, bs);
+        nsch_tasks_kx = (int)bs.tasks.size();
+        sch_tasks_kx.upload(bs.tasks.empty() ? std::vector<launch::SchurTask>(1) : bs.tasks, stream);
+        sch_batches_kx.upload(bs.batches, stream);
+        sch_st_obs_kx.upload(nz(bs.st_obs_h), stream);
+        sch_pairs_kx.upload(nz(bs.prs), stream);
+        sch_pp_kx.upload(nz(bs.pp), stream);
+      }
     }
     std::vector<int> shpp(nS, -1);
     nHppUsed = 0;
@@ -2346,6 +2385,12 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     {  // landmark side of the Schur complement formed during assembly (G2OHIP_SCHUR_SPLIT=0: the plain passes, A/B)
       const char* ev = getenv("G2OHIP_SCHUR_SPLIT");
       fz_split_ok = ba_fused && nslotd == 0 && pd == 6 && ld == 3 && !use_cgls() && !(ev && atoi(ev) == 0);
+      // the split stores 10-double Kt records instead of G (assembly.hip KXB): 80 instead of 144 bytes written per
+      // observation and staged by the Schur row pass (G2OHIP_SCHUR_KX=0: G, A/B). The stored-G back-substitution
+      // (G2OHIP_BACKSUB_RECOMPUTE=0) needs G.
+      const char* kx = getenv("G2OHIP_SCHUR_KX");
+      const char* bsr = getenv("G2OHIP_BACKSUB_RECOMPUTE");
+      fz_kx = fz_split_ok && !(kx && atoi(kx) == 0) && !(bsr && atoi(bsr) == 0);
       fz_lambda = std::numeric_limits<double>::quiet_NaN();
     }
     if (use_cgls()) {  // the fork's JacobiSolver_6_3: CGLS on J, no reduced system to factor
@@ -2505,6 +2550,7 @@ int Engine::build_system_split(double lambda, const double* lamp) {  // block_so
       sp.Ufac = dUfac.get();
       sp.cl = dCl.get();
       sp.G = dG.get();
+      sp.kx = fz_kx ? 1 : 0;
       sp.hpl_base = (long long)nHpp * pd * pd;
       sp.lm_ptr = d_lm_ptr.get();
       sp.hl = d_hidx[g.vtA].get();
@@ -2636,10 +2682,15 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   // last factorization), off the factorization's own chain
   const bool zero_here = !use_pcg() && chol.nzero > 0;
   timer.begin("schur_rows", stream);
-  launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(),
-                     split ? sch_st_obs_h.get() : sch_st_obs.get(), sch_pairs.get(), sch_pp.get(), dG.get(),
-                     ds_hpp.get(), dH.get(), S, zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(),
-                     stream);
+  if (split && fz_kx && nsch_tasks_kx > 0)  // Kt records in batches of their own block size
+    launch::schur_rows(pd, ld, nsch_tasks_kx, sch_tasks_kx.get(), sch_batches_kx.get(), sch_st_obs_kx.get(),
+                       sch_pairs_kx.get(), sch_pp_kx.get(), dG.get(), ds_hpp.get(), dH.get(), S,
+                       zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(), stream, true, kx_sb);
+  else
+    launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(),
+                       split ? sch_st_obs_h.get() : sch_st_obs.get(), sch_pairs.get(), sch_pp.get(), dG.get(),
+                       ds_hpp.get(), dH.get(), S, zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(),
+                       stream, split && fz_kx, launch::SCHUR_SB);
   timer.end(stream);
   const bool rs = !use_pcg() && chol.rs_on;  // distributed factorization: each rank's blocks reduce-scattered to it
   if (rs) chol.reduce_input(dS.get(), stream);
@@ -2666,7 +2717,7 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   // (k_backsub_j: C5 4.58 -> 4.48 ms per iteration, profiles/r04_ab_backsub_recompute.log); G2OHIP_BACKSUB_RECOMPUTE=0
   // reads G (k_backsub_g, dev A/B)
   const char* bsr = getenv("G2OHIP_BACKSUB_RECOMPUTE");
-  const bool bs_recompute = !(bsr && atoi(bsr) == 0);
+  const bool bs_recompute = !(bsr && atoi(bsr) == 0) || fz_kx;  // Kt records: no G to read
   if (split && bs_recompute && ld == 3 && pd == 6)
     launch::backsub_j(group_args(groups[0]), nLloc, d_bs_erng.get(), d_hidx[groups[0].vtB].get(), dUfac.get(),
                       dCl.get(), size_poses, lm_begin, dx.get(), stream);
@@ -3341,9 +3392,11 @@ int Engine::local_landmarks(int* ids, int cap) const {
 double Engine::kernel_bytes(const std::string& name) const {
   // algorithmic bytes per launch (SURVEY.md §8d formulas)
   const double npl = nHpl, pb = (double)pd * ld * 8;
-  // Schur row pass (off-diagonal blocks): G of every observation once, the off-diagonal Hpp blocks
+  // the BA split's per-observation record: the 80-byte Kt record instead of the G block (assembly.hip KXB)
+  const double ob = fz_kx ? 80.0 : pb;
+  // Schur row pass (off-diagonal blocks): G (or its Kt record) of every observation once, the off-diagonal Hpp blocks
   // present in S, the off-diagonal S blocks written once
-  if (name == "schur_rows") return npl * pb + (double)(nHppUsed - num_poses) * pd * pd * 8 +
+  if (name == "schur_rows") return npl * ob + (double)(nHppUsed - num_poses) * pd * pd * 8 +
                                    (double)(nS - num_poses) * pd * pd * 8;
   // diagonal blocks: Hpl, U and c per observation's landmark, G written, Hpp diagonal, S diagonal + bschur
   if (name == "schur_diag") return 2 * npl * pb + local_lm.size() * 9 * 8.0 + (double)num_poses * pd * pd * 8 * 2 +
@@ -3353,7 +3406,7 @@ double Engine::kernel_bytes(const std::string& name) const {
     double by = 0;
     for (const EGroup& g : groups)
       if (g.family == FAM_BA)
-        by += g.ne * ((2 + 3 + 4) * 8.0 + 8 + (ba_fused ? 0.0 : 9.0 + 27.0) * 8 + pd * ld * 8.0) +
+        by += g.ne * ((2 + 3 + 4) * 8.0 + 8 + (ba_fused ? 0.0 : 9.0 + 27.0) * 8 + ob) +
               (ba_fused ? local_lm.size() * 12 * 8.0 : 0.0);
     return by;
   }

@@ -373,6 +373,7 @@ class Engine {
   // Schur split at assembly: eligible graphs (fused BA, no shared off-diagonal blocks, a Cholesky / PCG on S), and the
   // lambda the stored G = Hpl U^-T, S(i,i) and bschur were formed with (NaN: Hpl stored, the plain Schur passes run)
   bool fz_split_ok = false;
+  bool fz_kx = false;  // the split stores Kt records (assembly.hip KXB) instead of G
   double fz_lambda = std::numeric_limits<double>::quiet_NaN();
   DevBuf<int> cm_ptr, cm_v0, cm_v1;
   DevBuf<double> cm_meas, cm_info, cm_params;
@@ -398,6 +399,12 @@ class Engine {
   DevBuf<int> sch_st_obs, sch_pairs, sch_pp;
   DevBuf<int> sch_st_obs_h;  // the same staged blocks as Hpl block indices (G in Hpl's order, Schur split)
   int nsch_tasks = 0;
+  // the BA split's Kt-record batches (k_schur_rows<..., KX>) when their block size differs from launch::SCHUR_SB
+  DevBuf<launch::SchurTask> sch_tasks_kx;
+  DevBuf<launch::SchurBatch> sch_batches_kx;
+  DevBuf<int> sch_st_obs_kx, sch_pairs_kx, sch_pp_kx;
+  int nsch_tasks_kx = 0, kx_sb = launch::SCHUR_SB;
+  static int kx_batch_size();
   // diagonal Schur blocks (k_schur_diag): per camera row its observations in landmark order
   DevBuf<int> sch_rptr, sch_robs, sch_obs_lm, sch_sdiag;
   std::vector<int> s_bi, s_bj, hpp_bi, hpp_bj;

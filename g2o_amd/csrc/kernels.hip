@@ -565,6 +565,65 @@ __device__ __forceinline__ void schur_pairs(const double* Gs, const int* sp, con
     }
   }
 }
+// The same pairs from the BA split's 10-double records (assembly.hip KXB: Kt = diag(f) Omega A U^-T, 2 x 3 col-major,
+// then u = x/z, v = y/z, w = 1/z): G = Bt^T Kt, so G_a G_b^T = Bt_a^T (Kt_a Kt_b^T) Bt_b. Per pair a thread forms the
+// 2 x 2 M = Kt_a Kt_b^T, T = M Bt_b(:, c0 .. c0 + 2) and acc(j, r) += Bt_a(:, r) . T(:, j): 18 staged doubles read
+// instead of 27, the camera Jacobians rebuilt from three numbers each.
+__device__ __forceinline__ void schur_pairs_kx(const double* Gs, const int* sp, const int* spp, int noff, int ls, int q,
+                                               double (&acc)[18]) {
+  constexpr int GB = 10;
+  const int par = q >> 1;
+  const bool hi = q & 1;  // columns 3..5 of the block
+  if (ls >= noff) return;
+  const int p1 = spp[ls + 1];
+  for (int p = spp[ls] + par; p < p1; p += 2) {
+    const int pr = sp[p];
+    const double* ga = &Gs[(pr & 0xffff) * GB];
+    const double* gb = &Gs[(pr >> 16) * GB];
+    double ka[6], kb[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double2 x = *reinterpret_cast<const double2*>(ga + 2 * k);
+      const double2 y = *reinterpret_cast<const double2*>(gb + 2 * k);
+      ka[2 * k] = x.x; ka[2 * k + 1] = x.y;
+      kb[2 * k] = y.x; kb[2 * k + 1] = y.y;
+    }
+    const double2 ua2 = *reinterpret_cast<const double2*>(ga + 6), ub2 = *reinterpret_cast<const double2*>(gb + 6);
+    const double ua = ua2.x, va = ua2.y, wa = ga[8], ub = ub2.x, vb = ub2.y, wb = gb[8];
+    // M = Kt_a Kt_b^T (2 x 2)
+    double M[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) M[r][s] = ka[r] * kb[s] + ka[2 + r] * kb[2 + s] + ka[4 + r] * kb[4 + s];
+    // Bt_b columns c0 .. c0 + 2 (rows 0, 1)
+    double b0[3], b1[3];
+    if (!hi) {
+      b0[0] = ub * vb; b0[1] = -(1.0 + ub * ub); b0[2] = vb;
+      b1[0] = 1.0 + vb * vb; b1[1] = -(ub * vb); b1[2] = -ub;
+    } else {
+      b0[0] = -wb; b0[1] = 0.0; b0[2] = ub * wb;
+      b1[0] = 0.0; b1[1] = -wb; b1[2] = vb * wb;
+    }
+    double T0[3], T1[3];  // T = M Bt_b(:, cols)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      T0[j] = M[0][0] * b0[j] + M[0][1] * b1[j];
+      T1[j] = M[1][0] * b0[j] + M[1][1] * b1[j];
+    }
+    // Bt_a, all six columns
+    const double a0[6] = {ua * va, -(1.0 + ua * ua), va, -wa, 0.0, ua * wa};
+    const double a1[6] = {1.0 + va * va, -(ua * va), -ua, 0.0, -wa, va * wa};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        if (r == 4) acc[j * 6 + r] += a1[r] * T1[j];
+        else if (r == 3) acc[j * 6 + r] += a0[r] * T0[j];
+        else acc[j * 6 + r] += a0[r] * T0[j] + a1[r] * T1[j];
+      }
+  }
+}
 // Even + odd pairs (fixed order) and the S block store: thread (h, par) stores rows [0, CW) (par 0) or [CW, PD) (par 1)
 // of its columns; S(i, j) = Hpp(i, j) - sum
 template <int PD>
@@ -602,10 +661,8 @@ __device__ __forceinline__ void schur_row_store(double (&acc)[((PD + 1) / 2) * P
 // one fixed shuffle: every output has one owner and a fixed summation order (no atomics, bitwise
 // reproducible).
 namespace {
-constexpr int SCH_SB = launch::SCHUR_SB;  // staged G blocks per batch
 constexpr int SCH_SL = launch::SCHUR_SL;  // off-diagonal slots per task
 constexpr int SCH_PPB = SCH_SL + 1;       // slot-CSR entries per batch
-constexpr int SCH_NI = (SCH_SB + 255) / 256;
 }  // namespace
 
 // PIPE 1 (default): three index buffers, so a batch's indices are loaded one whole iteration before they are stored to
@@ -614,14 +671,17 @@ constexpr int SCH_NI = (SCH_SB + 255) / 256;
 // (G2OHIP_SCHUR_PIPE=0, A/B). A variant issuing the next batch's staging right after the barrier and storing the
 // indices behind the products (two register sets, the staging as inline assembly) measured the same (C4 142 vs 139 us,
 // profiles/r04_ab_schur_pipe2.log) and was dropped.
-template <int PD, int LD, int PIPE>
-__global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
+// SCH_SB: staged blocks per batch (launch::SCHUR_SB for G blocks, launch::SCHUR_SB_KX for the 80-byte Kt records)
+template <int PD, int LD, int PIPE, bool KX = false, int SCH_SB = launch::SCHUR_SB>
+__global__ void __launch_bounds__(256, 4)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
                  const int* st_obs, const int* pairs, const int* pp,
                  const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,
                  double* __restrict__ S, int mode, int ntasks, const long long* __restrict__ zr,
                  double* __restrict__ fronts) {
-  constexpr int GB = PD * LD;                        // doubles per staged block: G, PD x LD col-major
+  static_assert(!KX || (PD == 6 && LD == 3), "Kt records: BA blocks");
+  constexpr int SCH_NI = (SCH_SB + 255) / 256;
+  constexpr int GB = KX ? 10 : PD * LD;              // doubles per staged block: G, PD x LD col-major (or a Kt record)
   constexpr int NPC = GB / 2;                        // 16-B pieces per block
   constexpr int NC = (SCH_SB * NPC + 255) / 256;     // 16-B pieces per thread per batch
   constexpr int CW = (PD + 1) / 2;                   // output columns (and rows) per half
@@ -676,7 +736,10 @@ __global__ void __launch_bounds__(256, launch::SCHUR_SB <= 128 ? 4 : 2)
       }
     }
   };
-  auto compute = [&](int buf, int ib) { schur_pairs<PD, LD>(Gs[buf], sp[ib], spp[ib], t.noff, ls, q, acc); };
+  auto compute = [&](int buf, int ib) {
+    if constexpr (KX) schur_pairs_kx(Gs[buf], sp[ib], spp[ib], t.noff, ls, q, acc);
+    else schur_pairs<PD, LD>(Gs[buf], sp[ib], spp[ib], t.noff, ls, q, acc);
+  };
   // index loads the pipelined passes count with vmcnt. Their pointers are not __restrict__ and every counted wait is
   // an inline-assembly memory clobber, so the compiler can neither sink them below the wait nor hoist them above the
   // staging (read-only restrict loads may move across assembly and barriers).
@@ -1424,7 +1487,7 @@ void schur_diag(int pd, int ld, int nrows, const int* rptr, const int* robs, con
 }
 void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
-                int nzero, const long long* zr, double* fronts, hipStream_t s) {
+                int nzero, const long long* zr, double* fronts, hipStream_t s, bool kx, int sb) {
   if (ntasks <= 0 && nzero <= 0) return;
 #ifdef G2OHIP_DEV  // development build only: 1 no pair products, 2 no staging, 3 neither (wrong S, timing splits)
   static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;
@@ -1434,6 +1497,24 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
   static EnvKnob pipe_k{"G2OHIP_SCHUR_PIPE", 1};  // 0: two index buffers (A/B; tests/test_gpu_parity.py)
   const int pipe = pipe_k.get();
   const int nz = nzero > 0 ? nzero : 0;
+  if (kx) {  // BA split: G rebuilt from the Kt records
+    if (pd != 6 || ld != 3) throw DeviceError("schur_rows: Kt records need BlockSolver_6_3 blocks");
+    auto go = [&](auto SBc) {
+      constexpr int SBK = decltype(SBc)::value;
+      if (pipe == 0)
+        hipLaunchKernelGGL((k_schur_rows<6, 3, 0, true, SBK>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs,
+                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
+      else
+        hipLaunchKernelGGL((k_schur_rows<6, 3, 1, true, SBK>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs,
+                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
+    };
+    if (sb == 128) go(std::integral_constant<int, 128>{});
+    else if (sb == 192) go(std::integral_constant<int, 192>{});
+    else if (sb == 256) go(std::integral_constant<int, 256>{});
+    else throw DeviceError("schur_rows: unsupported Kt batch size " + std::to_string(sb));
+    KERNEL_CHECK();
+    return;
+  }
   pl_dispatch(pd, ld, [&](auto P, auto L) {
     constexpr int pv = decltype(P)::value, lv = decltype(L)::value;
     if (pipe == 0)

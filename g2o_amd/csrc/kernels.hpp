@@ -48,7 +48,8 @@ struct SchurSplit {
                                  // instead of lam_rank
   double* Ufac;          // per local landmark U record (6 doubles)
   double* cl;            // c = U^-1 b_l, global landmark index
-  double* G;             // Hpl's block order
+  double* G;             // Hpl's block order: G (PD x LD) per observation, or with kx its 10-double Kt | x/z y/z 1/z record
+  int kx;                // BA: store the Kt record instead of G (assembly.hip KXB; k_schur_rows rebuilds G from it)
   long long hpl_base;    // offset of the first Hpl block in off_base (the Hessian)
   const int* lm_ptr;     // local landmark -> its Hpl/G block range (split landmarks' fixup)
   const int* hl;         // landmark vertex (local id) -> hessian index (-1 fixed), for the camera pass
@@ -81,6 +82,12 @@ void schur_diag(int pd, int ld, int nrows, const int* rptr, const int* robs, con
 // row-stationary off-diagonal Schur pass (k_schur_rows): task = (camera row, <= SCHUR_SL off-diagonal
 // slots), batch = <= SCHUR_SB staged observation blocks of the row's landmarks
 constexpr int SCHUR_SB = 128, SCHUR_SL = 64;  // 128: 4 workgroups per CU (LDS), 150 vs 172 us at C4
+// batches of the BA split's 80-byte Kt records (assembly.hip KXB): 192 blocks are 30 KB of staging, still 4 workgroups
+// per CU, and a third fewer batches per row task than 128
+#ifndef G2OHIP_SCHUR_SB_KX
+#define G2OHIP_SCHUR_SB_KX 192
+#endif
+constexpr int SCHUR_SB_KX = G2OHIP_SCHUR_SB_KX;
 struct SchurTask {
   int row, noff;  // camera row, number of off-diagonal slots of this task
   int b0, b1;     // batches
@@ -95,7 +102,8 @@ struct SchurBatch {
 // factorization's pre-scattered fronts, cleared beside the Schur pass instead of by a launch of the factor's own
 void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
-                int nzero, const long long* zr, double* fronts, hipStream_t s);
+                int nzero, const long long* zr, double* fronts, hipStream_t s, bool kx = false,
+                int sb = SCHUR_SB);
 void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv,
              const double* b, int size_poses, int lm0, double* x, hipStream_t s);
 // back-substitution from the G blocks of an assembly-time Schur split: x_l = U^-T (c_l - G^T x_p)

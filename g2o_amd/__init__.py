@@ -475,7 +475,7 @@ class SparseOptimizer:
                         "distributed", "reduce_scatter", "rs_segment_doubles", "rs_tail_doubles", "model_input_s",
                         "model_input_allreduce_s", None,  # None: retired slots (always 0), kept for the ABI layout
                         "band_leaf", "aligned_shards", "local_block_doubles", "exchange_bytes_per_rank",
-                        "local_landmarks", "model_shard_s")
+                        "local_landmarks", "model_shard_s", "deferred_l21_fronts")
 
     def factor_info(self) -> dict:
         out = np.zeros(len(self.FACTOR_INFO_KEYS))

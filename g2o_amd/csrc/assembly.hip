@@ -81,8 +81,10 @@ __global__ void __launch_bounds__(256)
                       double* __restrict__ off_slot, double* __restrict__ Hll, double* __restrict__ bvec,
                       int num_poses, int size_poses, int lm_begin, double* __restrict__ lpart, launch::SchurSplit sp) {
   constexpr int D = F::D, DA = F::DA, DB = F::DB;
-  constexpr int SA = DA * (DA + 1) / 2 + DA, SH = DA * DB, SM = SA > SH ? SA : SH;
   constexpr int UF = 2 * DA;  // U record of a DA = 3 landmark (FG instantiations are BA only)
+  // per-lane LDS image: landmark terms (+ U records with a split), or the lane's stored block (G / Hpl, or a Kt record)
+  constexpr int SA = DA * (DA + 1) / 2 + DA, SH = DA * DB, SB0 = KX ? 10 : SH, SL0 = FG ? SA + UF : SA;
+  constexpr int SM = SL0 > SB0 ? SL0 : SB0;
   static_assert(!FG || (DA == 3 && 64 * SA + 64 * UF <= 64 * SM), "U records live behind the landmark terms");
   __shared__ __attribute__((aligned(16))) double stage[4][64 * SM];
   __shared__ int lmid[4][64];
@@ -126,7 +128,14 @@ __global__ void __launch_bounds__(256)
     const bool in_slot = od_raw >= 0 && (od_raw & SLOT_BIT);
     constexpr int BS = KX ? KXB : SH;  // doubles per stored block
     long long od = od_raw >= 0 ? (od_raw & ~SLOT_BIT) - (FG ? sp.hpl_base : 0) : -1;
-    if constexpr (KX) od = od >= 0 ? od / SH * KXB : -1;  // no duplicate (landmark, camera) edges in KX mode: no slots
+    if constexpr (KX) {  // no duplicate (landmark, camera) edges in KX mode: no slots
+      od = od >= 0 ? od / SH * KXB : -1;
+      // an observation of a fixed landmark by a free camera gets a record of its own (Kt = 0) for the camera pass
+      if (in && !nfA && nfB) {
+        const int x = sp.kx_extra[e];
+        od = x >= 0 ? (long long)x * KXB : -1;
+      }
+    }
     double* base = FG ? sp.G : off_base;
     const bool tr = nfA && nfB && off_tr[e];
     const long long od0 = __shfl(od, 0, 64);
@@ -145,15 +154,14 @@ __global__ void __launch_bounds__(256)
             double s = 0;
 #pragma unroll
             for (int c = 0; c < D; ++c) s += Om[r * D + c] * A[c * DA + a2];
-            W[a2 * D + r] = Kp[r] * s;
+            W[a2 * D + r] = nfA ? Kp[r] * s : 0.0;
           }
-        if (ch.z < 0) form_G<D, DA>(W, U);
-        const double iz = 1.0 / pc[2];
+        if (ch.z < 0 && nfA) form_G<D, DA>(W, U);
 #pragma unroll
         for (int k = 0; k < D * DA; ++k) H[k] = W[k];
-        H[6] = pc[0] * iz;
-        H[7] = pc[1] * iz;
-        H[8] = iz;
+        H[6] = pc[0] / pc[2];  // as the projection divides (the camera pass rebuilds the error from these)
+        H[7] = pc[1] / pc[2];
+        H[8] = 1.0 / pc[2];
         H[9] = 0.0;
       } else if (FG || tr) {  // (pose, landmark) block, column-major: H[i * DB + j] = (A^T Omega B)(i, j)
         double g[SH];
@@ -357,7 +365,11 @@ __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restri
 // landmark, G G^T = B^T M B and G c_l = B^T W c_l with W = Omega A U^-T (D x LD), M = W W^T = Omega A (Hll + lambda I)^-1
 // A^T Omega, so S(i,i) = lambda I + sum B^T (Omega - M) B and bschur_i = sum B^T (omega_r - W c_l), beside b_i
 // (block_solver.hpp:361-400's j == i terms in 33 accumulators; Hpp is left to a plain buildSystem).
-template <class F, bool FG>
+// KX (with FG): an observation of a free landmark reads the 10-double Kt record the linearize wave left instead of
+// re-linearising the edge: with B = diag(f) Bt(u, v, w) and Kt = diag(f) W,
+//   B^T (Omega - W W^T) B = Bt^T (F Omega F - Kt Kt^T) Bt,   B^T (omega_r - W c_l) = Bt^T (F omega_r - Kt c_l),
+// the error from (u, v) = (x/z, y/z) exactly as the projection computes it (robust weight from its chi2).
+template <class F, bool FG, bool KX = false>
 __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* __restrict__ cm_ptr, int npose,
                                                       double* __restrict__ Hpp, double* __restrict__ bvec,
                                                       int num_poses, int lm_begin, launch::SchurSplit sp) {
@@ -375,6 +387,55 @@ __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* 
   for (int p = cm_ptr[i] + tid; p < p1; p += 256) {
     int hl = -1;
     if constexpr (FG) hl = sp.hl[d.v0[p]];
+    if constexpr (KX) {  // every camera-major observation has a record (fixed landmarks: Kt = 0)
+      const int a = sp.cm_hpl[p];
+      {
+        const double* rec = sp.G + (size_t)a * KXB;
+        double Kt[6];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const double2 x = *reinterpret_cast<const double2*>(rec + 2 * q);
+          Kt[2 * q] = x.x; Kt[2 * q + 1] = x.y;
+        }
+        const double2 uv = *reinterpret_cast<const double2*>(rec + 6);
+        const double u = uv.x, v = uv.y, wz = rec[8];
+        const double* cp = sp.cl + (size_t)(hl >= 0 ? hl - num_poses : 0) * DA;
+        const double c0 = hl >= 0 ? cp[0] : 0.0, c1 = hl >= 0 ? cp[1] : 0.0, c2 = hl >= 0 ? cp[2] : 0.0;
+        const double* Kp = param_rec(d, p, 4);
+        const double fx = Kp[0], fy = Kp[1];
+        const double e0 = d.meas[(size_t)p * 2 + 0] - (u * fx + Kp[2]);
+        const double e1 = d.meas[(size_t)p * 2 + 1] - (v * fy + Kp[3]);
+        double Om[4];
+        load_info<2>(info_rec(d, p, F::INFO), Om);
+        if (d.rk) {
+          const double chi = e0 * (Om[0] * e0 + Om[1] * e1) + e1 * (Om[2] * e0 + Om[3] * e1);
+          double r0, r1;
+          robustify(d.rk, d.rk_delta, chi, r0, r1);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Om[q] *= r1;
+        }
+        const double w0 = -(Om[0] * e0 + Om[1] * e1), w1 = -(Om[2] * e0 + Om[3] * e1);
+        const double h0 = fx * w0, h1 = fy * w1;  // F omega_r
+        const double g0 = h0 - (Kt[0] * c0 + Kt[2] * c1 + Kt[4] * c2);
+        const double g1 = h1 - (Kt[1] * c0 + Kt[3] * c1 + Kt[5] * c2);
+        const double n00 = fx * Om[0] * fx - (Kt[0] * Kt[0] + Kt[2] * Kt[2] + Kt[4] * Kt[4]);
+        const double n01 = fx * Om[1] * fy - (Kt[0] * Kt[1] + Kt[2] * Kt[3] + Kt[4] * Kt[5]);
+        const double n11 = fy * Om[3] * fy - (Kt[1] * Kt[1] + Kt[3] * Kt[3] + Kt[5] * Kt[5]);
+        const double b0[6] = {u * v, -(1.0 + u * u), v, -wz, 0.0, u * wz};
+        const double b1[6] = {1.0 + v * v, -(u * v), -u, 0.0, -wz, v * wz};
+        int k = 0;
+#pragma unroll
+        for (int c = 0; c < DB; ++c) {  // column c of (N Bt): t0, t1
+          const double t0 = n00 * b0[c] + n01 * b1[c], t1 = n01 * b0[c] + n11 * b1[c];
+#pragma unroll
+          for (int r = 0; r <= c; ++r) acc[k++] += b0[r] * t0 + b1[r] * t1;
+        }
+#pragma unroll
+        for (int j = 0; j < DB; ++j) acc[k++] += b0[j] * h0 + b1[j] * h1;
+#pragma unroll
+        for (int j = 0; j < DB; ++j) acc[k++] += b0[j] * g0 + b1[j] * g1;
+      }
+    } else {
     double err[D], A[D * DA], B[D * DB], Om[D * D];
     edge_terms<F>(d, p, err, A, B, Om);
     double wr[D];
@@ -464,6 +525,7 @@ __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* 
         for (int r = 0; r < D; ++r) s += B[r * DB + j] * v[r];
         acc[k++] += s;
       }
+    }
     }
   }
 #pragma unroll
@@ -623,7 +685,10 @@ void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, 
   if (npose <= 0) return;
   const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
   const SchurSplit z = sp ? *sp : SchurSplit{};
-  if (sp)
+  if (sp && sp->kx && sp->cm_hpl)
+    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
+                       lm_begin, z);
+  else if (sp)
     hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
                        lm_begin, z);
   else

@@ -551,12 +551,13 @@ struct MfmaTile {  // 64x64 tile, 4 waves x (2x2) v_mfma_f64_16x16x4f64 tiles, K
 };
 
 // C tile entries owned by a thread: idx = tid + 256 u -> (r = idx % 64, c = idx / 64)
-__device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J0, int climit, int tid, double (&cv)[16]) {
+__device__ __forceinline__ void load_ctile(const double* F, int m, int rlim, int I0, int J0, int climit, int tid,
+                                           double (&cv)[16]) {
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
     const int gi = I0 + r, gj = J0 + c;
-    cv[u] = ld0(F, gj * m + gi, gi < m && gj < climit && gi >= gj);
+    cv[u] = ld0(F, gj * m + gi, gi < rlim && gj < climit && gi >= gj);
   }
 }
 
@@ -566,6 +567,8 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int I0, int J
 // 64 lagged pair (odd steps of a lagged front, DeviceCholesky::setup): the update also applies the PREVIOUS
 //    panel (k0 - 32, whose L rows the strip tiles of the even step stored), so the trailing columns are read and
 //    written once per two panels (rank-64); the even steps update only the next panel's strip (clim = r0 + kbn).
+// 128 own rows only (deferred L21, DeviceCholesky::setup): the tile's rows stop at ns; L21 and the front vector's
+//    rows below come from k_l21 and the contribution pass.
 // Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
 // PAIRS: the launch may hold lagged-pair tasks (flag 64); without them the pair code is compiled out (166 instead of
 // ~180 VGPRs: three workgroups per CU instead of two)
@@ -758,14 +761,15 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
 
   // ---- lagged pair: the previous panel's L rows of I and J (stored by the even step's strip tiles) go first
   const bool pair = PAIRS && (t.flags & 64) && upd;
+  const int rlim = (t.flags & 128) ? ns : m;  // rows this tile owns
   MfmaTile T;
   T.zero();
   double xpa[8], xpb[8];  // issued with the current panel's loads (one round trip), staged before the C prefetch
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-    xpa[u] = ld0(L, (k0 - NB + q) * m + I0 + r, pair && I0 + r < m);
-    xpb[u] = ld0(L, (k0 - NB + q) * m + J0 + r, pair && J0 + r < m);
+    xpa[u] = ld0(L, (k0 - NB + q) * m + I0 + r, pair && I0 + r < rlim);
+    xpb[u] = ld0(L, (k0 - NB + q) * m + J0 + r, pair && J0 + r < rlim);
   }
   // ---- stage L_kk^-1, y_k, the raw panel rows of I (and J), prefetch the C tile: every global
   // load is issued before the first LDS store so the whole batch is in flight at once
@@ -776,8 +780,8 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-    pav[u] = ld0(F, (k0 + q) * m + I0 + r, q < kb && I0 + r < m);
-    pbv[u] = ld0(F, (k0 + q) * m + J0 + r, upd && q < kb && J0 + r < m);
+    pav[u] = ld0(F, (k0 + q) * m + I0 + r, q < kb && I0 + r < rlim);
+    pbv[u] = ld0(F, (k0 + q) * m + J0 + r, upd && q < kb && J0 + r < rlim);
   }
   const int climit = t.clim;  // ns; m when the contribution block is fused; the big-panel end when blocked
   if (pair) {  // C[I, J] -= X_prev,I X_prev,J^T into the accumulators first, the current panel's loads in flight
@@ -791,7 +795,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
     T.step(Pa, Pb, lane, w);
     __syncthreads();  // Pa / Pb free for the current panel
   }
-  if (upd) load_ctile(F, m, I0, J0, climit, tid, cv);
+  if (upd) load_ctile(F, m, rlim, I0, J0, climit, tid, cv);
 #pragma unroll
   for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
     const int e = tid + 256 * u_;
@@ -836,7 +840,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   // rows/columns of the next diagonal block, [r0, r0 + kbn): this step's diagonal task reads their
   // raw values at its start and applies the panel update itself, so tile tasks never write them
   const int kbn = (t.flags & 32) ? 0 : max(0, min(NB, ns - r0));
-  if (writer && tid < 64 && I0 + tid < m && I0 + tid >= r0 + kbn) {  // forward-solve update: v_i -= x_i y_k
+  if (writer && tid < 64 && I0 + tid < rlim && I0 + tid >= r0 + kbn) {  // forward-solve update: v_i -= x_i y_k
     double s2 = 0.0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) s2 += Pa[tid * PS + q] * yk[q];
@@ -848,7 +852,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
-      if (q < kb && I0 + r < m) L[(k0 + q) * m + I0 + r] = Pa[r * PS + q];
+      if (q < kb && I0 + r < rlim) L[(k0 + q) * m + I0 + r] = Pa[r * PS + q];
     }
   }
   PH1(3)
@@ -864,7 +868,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
     const int idx = tid + 256 * u, r = idx & (TT - 1), c = idx >> 6;
     const int gi = I0 + r, gj = J0 + c;
     const bool dblk = gi < r0 + kbn && gj < r0 + kbn;
-    if (gi < m && gj < climit && gi >= gj && !dblk) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
+    if (gi < rlim && gj < climit && gi >= gj && !dblk) F[(size_t)gj * m + gi] = cv[u] - sh[r * CS + c];
   }
   PH1(4)
   PH1R(7)
@@ -876,20 +880,43 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
 // The same kernel is the trailing update of a blocked front after each big panel: rows >= kb, columns
 // [kb, ns), K = the big panel's columns [ka, kb) of the finished factor.
 // Tile: GemmNT (register-staged double buffer) or GemmNTd (LDS-DMA ring, G2OHIP_SYRK_DMA)
+// Task bit 31 of b (contribution passes of deferred-L21 fronts, diagonal tiles): the tile also applies the forward
+// solve's update to the front vector's rows below the supernode, v_i -= L21(i, :) y1 (the panel steps of such fronts
+// update only the supernode's own rows).
 template <class SyrkTile>
 __global__ void __launch_bounds__(256) k_syrk(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                              double* __restrict__ fronts, const double* __restrict__ lbuf) {
+                                              double* __restrict__ fronts, const double* __restrict__ lbuf,
+                                              const double* __restrict__ ysol, double* __restrict__ vecs) {
   __shared__ __attribute__((aligned(16))) double sh[SyrkTile::LDS_DOUBLES];
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int m = me.ns + me.nr, ns = me.ns;
-  const int ti = t.b & 0xffff, tj = t.b >> 16;
+  const bool vec = t.b < 0;
+  const int ti = t.b & 0xffff, tj = (t.b >> 16) & 0x7fff;
   const int ka = t.a, kb = t.c ? t.c : ns, climit = kb == ns ? m : ns;
   // a childless front's contribution block holds nothing before this pass (its rows and columns are ancestors'
   // variables: no input entries, no children): written, not read
   const bool overwrite = t.c == 0 && me.child_begin == me.child_end;
-  SyrkTile::run(lbuf + me.l_off, m, fronts + me.front_off, m, m, climit, kb + ti * TT, kb + tj * TT, ka, kb, sh,
-                overwrite);
+  SyrkTile::run(lbuf + me.l_off, m, fronts + me.front_off, m, m, climit, kb + ti * SyrkTile::ROWS, kb + tj * TT, ka,
+                kb, sh, overwrite, vec ? ysol + me.c0 : nullptr, vec ? vecs + me.vec_off : nullptr);
+}
+
+// Deferred L21 (wide throughput-bound levels, DeviceCholesky::setup): after a front's panel steps, which factored only
+// its own rows, L21 = A21 L11^-T = A21 X^T with the explicit inverse X = L11^-1 the inverse tasks built (diagonal blocks
+// copied in by a per-level k_xdiag): one GEMM tile per (row tile ti of the nr rows below, column tile tj), K = [0, 64 tj
+// + 64) since X(j, k) = 0 for k > j. A21 is the front's raw rows below the supernode (no panel step touched them).
+using L21Tile = GemmNTd<TT, TT, 2, 2, 16, 2>;
+__global__ void __launch_bounds__(256) k_l21(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+                                             const double* __restrict__ fronts, const double* __restrict__ xinv,
+                                             double* __restrict__ lbuf) {
+  __shared__ __attribute__((aligned(16))) double sh[L21Tile::LDS_DOUBLES];
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int m = me.ns + me.nr, ns = me.ns, nr = me.nr;
+  const int ti = t.b & 0xffff, tj = t.b >> 16;
+  const int I0 = ti * TT, J0 = tj * TT, kb = min(ns, J0 + TT);
+  L21Tile::run_ab(fronts + me.front_off + ns, m, nr, xinv + me.x_off, ns, ns, lbuf + me.l_off + ns, m, nr, ns, I0, J0,
+                  0, kb, sh, 2);
 }
 
 __global__ void k_permute(int n, const int* __restrict__ perm, const double* __restrict__ in, double* __restrict__ out) {
@@ -1129,7 +1156,24 @@ void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* 
     hipLaunchKernelGGL(k_step<false>, grid, 256, 0, s, tasks, head, fronts, lbuf, vecs, ysol, linv, xinv, fail);
   KERNEL_CHECK();
 }
-void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s) {
+void chol_l21(int ntasks, const Task* tasks, const FrontDesc* fd, const double* fronts, const double* xinv, double* lbuf,
+              hipStream_t s) {
+  if (ntasks <= 0) return;
+  hipLaunchKernelGGL(k_l21, ntasks, 256, 0, s, tasks, fd, fronts, xinv, lbuf);
+  KERNEL_CHECK();
+}
+// G2OHIP_SYRK_DMA (dev A/B): 1-4 the 64 x 64 LDS-DMA tiles below, 5 / 6 a 128 x 64 tile (K chunks 16 x 2 / 8 x 3
+// stages), 0 the register-staged GemmNT; the task lists are built for the variant's row-tile height (syrk_tile_rows)
+int syrk_variant() {
+  static EnvKnob dma_k{"G2OHIP_SYRK_DMA", 4};
+  return dma_k.get();
+}
+int syrk_tile_rows() {
+  const int v = syrk_variant();
+  return v == 5 || v == 6 ? 2 * TT : TT;
+}
+void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf,
+               const double* ysol, double* vecs, hipStream_t s) {
   if (ntasks <= 0) return;
   // G2OHIP_SYRK_DMA=k (dev A/B): the LDS-DMA tile GemmNTd with (K chunk, stages) = (32, 2), (16, 3), (8, 4), (16, 2)
   // for k = 1..4. Alone on one 4096^2 SYRK at K = 2048 the (32, 2) ring reaches 47.9 against 41.2 TF/s for the
@@ -1138,14 +1182,15 @@ void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* front
   // (profiles/r04_ab_c3_syrk.log; 74 KB of LDS leave 2 workgroups per CU against 3). The (16, 2) ring (37 KB, four
   // workgroups per CU) is the one that wins there: C3 factor 29.07 -> 28.54 ms (profiles/r04_ab_c3_knobs.log), the
   // default; G2OHIP_SYRK_DMA=0 is the register-staged GemmNT.
-  static EnvKnob dma_k{"G2OHIP_SYRK_DMA", 4};
-  const int dma = dma_k.get();
+  const int dma = syrk_variant();
   switch (dma) {
-    case 1: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 32, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
-    case 2: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 16, 3>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
-    case 3: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 8, 4>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
-    case 4: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 16, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf); break;
-    default: hipLaunchKernelGGL((k_syrk<GemmNT<TT, TT>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf);
+    case 5: hipLaunchKernelGGL((k_syrk<GemmNTd<2 * TT, TT, 2, 2, 16, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;
+    case 6: hipLaunchKernelGGL((k_syrk<GemmNTd<2 * TT, TT, 2, 2, 8, 3>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;
+    case 1: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 32, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;
+    case 2: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 16, 3>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;
+    case 3: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 8, 4>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;
+    case 4: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 16, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;
+    default: hipLaunchKernelGGL((k_syrk<GemmNT<TT, TT>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs);
   }
   KERNEL_CHECK();
 }

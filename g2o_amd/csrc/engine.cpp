@@ -469,6 +469,10 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       return f;
     };
     auto tile_nz = [&](int sn, int r, int kend) { return tile_fnz(sn, r) < kend; };
+    // k_syrk's row tiles: SR rows (64, or 128 for the 128 x 64 tile variants)
+    const int SR = launch::syrk_tile_rows();
+    auto rows_fnz = [&](int sn, int r) { return SR == TT ? tile_fnz(sn, r) : std::min(tile_fnz(sn, r), tile_fnz(sn, r + TT)); };
+    auto rows_nz = [&](int sn, int r, int kend) { return rows_fnz(sn, r) < kend; };
     std::vector<Task> tk;
     std::vector<launch::StepTask> stk;
     std::vector<int> sn_pb(sym.sn.size(), 0);  // big-panel width of blocked fronts (0: unblocked)
@@ -504,6 +508,16 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     // level, 183 -> 161 us; the 1- and 2-front levels are bound by the diagonal chain and lose ~6 us each)
     const char* lfm = getenv("G2OHIP_CHOL_LAG_FUSED_MIN");
     const long long lag_fused_min = lag_mode >= 2 ? 0 : (lfm ? atoll(lfm) : 256);
+    // deferred L21 on wide throughput-bound levels: the panel steps factor only each front's own rows (the trailing tiles
+    // below the supernode are most of a lagged step's load burst), then L21 = A21 X^T in one GEMM launch (k_l21, with
+    // the explicit X = L11^-1 the inverse tasks build) and the contribution pass updates the front vector's lower rows
+    // (G2OHIP_CHOL_DEFER_L21: 0 off, 1 levels of >= G2OHIP_CHOL_DEFER_MIN fronts (default 16), 2 every eligible level)
+    const char* dlv = getenv("G2OHIP_CHOL_DEFER_L21");
+    const int dl_mode = dlv ? atoi(dlv) : 1;
+    const char* dlm = getenv("G2OHIP_CHOL_DEFER_MIN");
+    const int dl_min = dlm ? atoi(dlm) : 16;
+    std::vector<unsigned char> sn_dl(sym.sn.size(), 0);
+    n_deferred_l21 = 0;
     const char* eb = getenv("G2OHIP_EA_BIG");
     const int ea_big = eb ? atoi(eb) : 1024;  // C3 factor 28.29 (2048) -> 27.71 ms (1024), 28.31 (512)
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
@@ -591,6 +605,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       const bool wide = (int)lv.size() >= wide_fronts;
       const int lpb = wide ? wide_pb : block_pb, lmin = wide ? wide_pb : block_min;
       auto blocked = [&](const Supernode& q) { return !fused_contrib && q.ns > lmin; };
+      const bool dl_level = dl_mode != 0 && !fused_contrib && !distributed() && (dl_mode == 2 || (int)lv.size() >= dl_min);
+      for (int sn : lv) {
+        const Supernode& q = sym.sn[sn];
+        sn_dl[sn] = dl_level && !blocked(q) && q.nr > 0 && q.env_off < 0 ? 1 : 0;
+        n_deferred_l21 += sn_dl[sn];
+      }
       for (int p = 0; p < maxp; ++p) {
         Op st{2, (int)stk.size(), 0};
         // task order inside the launch (= dispatch order): every front's next-diagonal task first (the
@@ -614,8 +634,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           // step is latency-bound on the diagonal chain, the extra tiles run in its shadow); lagged even steps
           // stop at the next panel's strip
           const int clim = strip ? std::min(q.ns, r0 + NB) : (fused_contrib ? m : pend);
-          const int T = (m - r0 + TT - 1) / TT, TJ = (clim - r0 + TT - 1) / TT;
-          const int fl = (fused_contrib ? 8 : 0) | (bnd ? 32 : 0) | (pair ? 64 : 0);
+          const int rows = sn_dl[sn] ? q.ns : m;  // deferred L21: the supernode's own rows only
+          const int T = (rows - r0 + TT - 1) / TT, TJ = (clim - r0 + TT - 1) / TT;
+          const int fl = (fused_contrib ? 8 : 0) | (bnd ? 32 : 0) | (pair ? 64 : 0) | (sn_dl[sn] ? 128 : 0);
           auto mk = [&](int tile, int flags) {
             return launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns, q.c0,
                                     k0 | (kb << 16), tile, flags, clim};
@@ -657,11 +678,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           const Supernode& q = sym.sn[sn];
           const int kb = (p + 1) * NB, ka = kb - lpb, m = q.ns + q.nr;
           if (!blocked(q) || kb >= q.ns) continue;
-          const int T = (m - kb + TT - 1) / TT, TJ = (q.ns - kb + TT - 1) / TT;
+          const int T = (m - kb + SR - 1) / SR, TJ = (q.ns - kb + TT - 1) / TT;
           for (int tj = 0; tj < TJ; ++tj) {
             if (!tile_nz(sn, kb + TT * tj, kb)) continue;
-            for (int ti = tj; ti < T; ++ti)
-              if (tile_nz(sn, kb + TT * ti, kb)) tk.push_back(Task{sn, ka, ti | (tj << 16), kb});
+            for (int ti = TT * tj / SR; ti < T; ++ti)
+              if (rows_nz(sn, kb + SR * ti, kb)) tk.push_back(Task{sn, ka, ti | (tj << 16), kb});
           }
           stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns,
                                          q.c0, kb, 0, 4, q.ns});
@@ -671,19 +692,39 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         if (gm.count) { ops.push_back(gm); ++n_syrk_ops; }
         if (d0.count) { ops.push_back(d0); }
       }
+      {  // deferred L21: X's diagonal blocks for the level's fronts, then L21 = A21 X^T
+        Op xd{11, (int)tk.size(), 0};
+        for (int sn : lv)
+          if (sn_dl[sn])
+            for (int a = 0; a < sym.sn[sn].ns; a += NB) tk.push_back(Task{sn, a, 0, 0});
+        xd.count = (int)tk.size() - xd.off;
+        if (xd.count) ops.push_back(xd);
+        Op gl{12, (int)tk.size(), 0};
+        for (int sn : lv) {
+          if (!sn_dl[sn]) continue;
+          const Supernode& q = sym.sn[sn];
+          for (int ti = 0; ti < (q.nr + TT - 1) / TT; ++ti)
+            for (int tj = 0; tj < (q.ns + TT - 1) / TT; ++tj) tk.push_back(Task{sn, 0, ti | (tj << 16), 0});
+        }
+        gl.count = (int)tk.size() - gl.off;
+        if (gl.count) ops.push_back(gl);
+      }
       Op sy{3, (int)tk.size(), 0};
       for (int sn : lv) {
         if (fused_contrib) break;
         const Supernode& q = sym.sn[sn];
-        const int T = (q.nr + TT - 1) / TT;
+        const int T = (q.nr + SR - 1) / SR, TJ = (q.nr + TT - 1) / TT;
         const bool childless = sym.children_ptr[sn + 1] == sym.children_ptr[sn];
-        for (int tj = 0; tj < T; ++tj)
-          for (int ti = tj; ti < T; ++ti) {
+        for (int tj = 0; tj < TJ; ++tj)
+          for (int ti = TT * tj / SR; ti < T; ++ti) {
             // band supernodes: K starts where both tile row sets have structural nonzeros; a tile with none only keeps
             // its entries (childless fronts' contribution blocks are written, not read: an empty K writes the zeros)
-            const int ka = std::max(tile_fnz(sn, q.ns + TT * ti), tile_fnz(sn, q.ns + TT * tj));
+            const int ka = std::max(rows_fnz(sn, q.ns + SR * ti), tile_fnz(sn, q.ns + TT * tj));
             if (ka >= q.ns && !childless) continue;
-            tk.push_back(Task{sn, std::min(ka, q.ns), ti | (tj << 16), 0});
+            // deferred L21: the first tile of each row tile (its diagonal) also applies the forward solve to the
+            // vector's rows below
+            const int vb = sn_dl[sn] && ti == TT * tj / SR && (TT * tj) % SR == 0 ? (int)0x80000000 : 0;
+            tk.push_back(Task{sn, std::min(ka, q.ns), ti | (tj << 16) | vb, 0});
           }
       }
       sy.count = (int)tk.size() - sy.off;
@@ -810,7 +851,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     xdiag_off = (int)tk.size();
     for (const auto& lv : fplan)
       for (int sn : lv)
-        for (int a = 0; a < sym.sn[sn].ns; a += NB) tk.push_back(Task{sn, a, 0, 0});
+        if (!sn_dl[sn])  // deferred-L21 fronts: copied by their level's own k_xdiag launch
+          for (int a = 0; a < sym.sn[sn].ns; a += NB) tk.push_back(Task{sn, a, 0, 0});
     n_xdiag = (int)tk.size() - xdiag_off;
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
@@ -876,14 +918,17 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
   relmap.upload(sym.relmap.empty() ? std::vector<int>{0} : sym.relmap, s);
   rows.upload(sym.rows.empty() ? std::vector<int>{0} : sym.rows, s);
   perm.upload(sym.perm, s);
-  fronts.resize(std::max<int64_t>(sym.front_pool, 1));
+  fronts.resize(std::max<int64_t>(sym.front_pool, 1) + 2);  // + a 16-byte piece of slack (k_l21 reads A21 by GemmNTd)
   vecs.resize(std::max<int64_t>(sym.vec_pool, 1));
   rhs_p.resize(std::max(sym.n, 1));
   y_p.resize(std::max(sym.n, 1));
   lbuf.resize(std::max<long long>(lpool, 1) + 2);  // + one 16-byte piece of slack after the last front (GemmNTd)
   if (!sym.fnz.empty()) lbuf.zero(s);  // band supernodes: the L rows of skipped tiles are read as zeros
   linv.resize((size_t)(sym.n + launch::CHOL_NB) * launch::CHOL_NB * launch::CHOL_NB);  // one 32x32 L_kk^-1 per panel start
-  xinv.resize(std::max<long long>(xoff, 1));
+  xinv.resize(std::max<long long>(xoff, 1) + 2);  // + slack: k_l21 stages X by GemmNTd
+  // X's blocks above the diagonal are never written (the inverse tasks and k_xdiag fill the lower part, the diagonal
+  // blocks with their zeros above): zero once, so a full-tile read of X (k_l21's B operand) sees an exact triangle
+  xinv.zero(s);
   t_p.resize(std::max(sym.n, 1));
   x_p.resize(std::max(sym.n, 1));
 }
@@ -930,7 +975,9 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
                                  vecs.get(), s);
         break;
       }
-      default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), s); break;
+      case 11: launch::chol_xdiag(op.count, t, fd.get(), linv.get(), xinv.get(), s); break;
+      case 12: launch::chol_l21(op.count, t, fd.get(), fronts.get(), xinv.get(), lbuf.get(), s); break;
+      default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), y_p.get(), vecs.get(), s); break;
     }
   }
   launch::chol_xdiag(n_xdiag, tasks.get() + xdiag_off, fd.get(), linv.get(), xinv.get(), s);
@@ -2157,6 +2204,23 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     if (od.empty()) { od.push_back(-1); tr.push_back(0); }
     g.off_dst.upload(od, stream);
     g.off_tr.upload(tr, stream);
+    if (gi == 0 && ba_fused) {
+      // the split's Kt records: one per Hpl block, plus one per observation of a fixed landmark by a free camera (Kt = 0)
+      // behind them; camera-major observation -> its record
+      std::vector<int> xe(std::max(g.ne, 1), -1), ch(std::max<size_t>(cm_e_h.size(), 1), -1);
+      n_kx_extra = 0;
+      for (int k = 0; k < g.ne; ++k) {
+        const int e2 = g.edges[k];
+        if (hidx[hg.esets[g.set].ev0[e2]] < 0 && hidx[hg.esets[g.set].ev1[e2]] >= 0) xe[k] = nHpl + n_kx_extra++;
+      }
+      for (size_t p = 0; p < cm_e_h.size(); ++p) {
+        const long long o = od[cm_e_h[p]];
+        if (o >= 0 && !(o & SLOT_BIT)) ch[p] = (int)((o - hpl_base) / ((long long)pd * ld));
+        else ch[p] = xe[cm_e_h[p]];
+      }
+      cm_hpl.upload(ch, stream);
+      kx_extra.upload(xe, stream);
+    }
   }
   // storage
   dH.resize(std::max<long long>((long long)nHpp * pd * pd + (long long)nHpl * pd * ld, 1));
@@ -2379,7 +2443,8 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     ds_hpp.upload(shpp, stream);
     dDinv.resize(std::max(nLloc * ld * ld, 1));
     dUfac.resize(std::max(nLloc * launch::schur_ufac_stride(ld), 1));
-    dG.resize(std::max<long long>((long long)nHpl * pd * ld, 1));  // G = Hpl U^-T per observation (pd x ld)
+    // G = Hpl U^-T per observation (pd x ld), or the split's 10-double Kt records (+ the fixed-landmark ones)
+    dG.resize(std::max<long long>(std::max((long long)nHpl * pd * ld, ((long long)nHpl + n_kx_extra) * 10), 1));
     dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
     {  // landmark side of the Schur complement formed during assembly (G2OHIP_SCHUR_SPLIT=0: the plain passes, A/B)
@@ -2425,7 +2490,9 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       // no-op exchanges — the kernel chain rank r would run, on this GPU; the solution is not meaningful
       const char* sim = getenv("G2OHIP_DIST_SIMULATE");
       int sr = 0, sn = 0;
+      bool sim_on = false;
       if (!dist && sim && sscanf(sim, "%d/%d", &sr, &sn) == 2 && sn > 1 && sr >= 0 && sr < sn) {
+        sim_on = true;
         chol.dist_rank = sr;
         chol.dist_nranks = sn;
         chol.dist_force = true;
@@ -2436,7 +2503,15 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       }
       chol.aligned = dist_aligned && dist;
       chol.blk_local.clear();
-      if (chol.aligned) {
+      // the simulated rank plays the aligned cut the product would take (landmark shards follow the cut: every block of
+      // its subtrees is complete locally, only the shared blocks are exchanged); G2OHIP_DIST_SIMULATE_ALIGNED=0: the
+      // uniform-shard cut
+      const char* sal = getenv("G2OHIP_DIST_SIMULATE_ALIGNED");
+      if (sim_on && !(sal && atoi(sal) == 0) && do_schur) {
+        chol.aligned = true;
+        chol.blk_local.assign(nS, 1);
+      }
+      if (chol.aligned && !sim_on) {
         // blocks written by a rank other than the one whose subtrees read them: those of edges without a free
         // landmark (assembled by rank 0: pose-pose edges, edges to fixed landmarks) — both endpoints' diagonal blocks
         // and their off-diagonal block — where the reading rank is not rank 0. Landmark blocks and lambda (lam_own)
@@ -2551,6 +2626,15 @@ int Engine::build_system_split(double lambda, const double* lamp) {  // block_so
       sp.cl = dCl.get();
       sp.G = dG.get();
       sp.kx = fz_kx ? 1 : 0;
+      // the camera pass from the Kt records while they stay cache-resident (the pass gathers them in camera order; C4's
+      // 80 MB: 52 -> 48 us), else re-linearising every observation from the per-landmark point, U and c (C5's 800 MB of
+      // records: 0.42 -> 0.49 ms, where the per-landmark gathers are 96 MB; profiles/r05_ab_c5_dl_camkx.log).
+      // G2OHIP_CAM_KX=0 / 1 forces either (A/B)
+      static EnvKnob cam_kx{"G2OHIP_CAM_KX", -1};
+      const int ck = cam_kx.get();
+      const bool use_ck = ck == 1 || (ck < 0 && ((double)nHpl + n_kx_extra) * 80.0 <= 192.0 * (1 << 20));
+      sp.cm_hpl = fz_kx && use_ck ? cm_hpl.get() : nullptr;
+      sp.kx_extra = fz_kx ? kx_extra.get() : nullptr;
       sp.hpl_base = (long long)nHpp * pd * pd;
       sp.lm_ptr = d_lm_ptr.get();
       sp.hl = d_hidx[g.vtA].get();
@@ -3363,7 +3447,8 @@ int Engine::factor_info(double* out, int n) {
                       chol.dist_model[2], chol.dist_model[3], chol.dist_model[4], chol.rs_on ? 1.0 : 0.0,
                       (double)chol.rs_seg, (double)chol.rs_tail_len, chol.rs_model[0], chol.rs_model[1],
                       0.0 /* retired: 64-column-step levels */, (double)S.band_leaf, dist_aligned ? 1.0 : 0.0,
-                      (double)chol.rs_local, exchange_bytes(), (double)local_lm.size(), chol.shard_model};
+                      (double)chol.rs_local, exchange_bytes(), (double)local_lm.size(), chol.shard_model,
+                      (double)chol.n_deferred_l21};
   const int m = (int)(sizeof v / sizeof v[0]);
   for (int k = 0; k < std::min(n, m); ++k) out[k] = v[k];
   return m;

@@ -112,6 +112,7 @@ struct DeviceCholesky {
   // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
   // trailing-update (k_syrk) launches, big-panel backward rounds
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
+  int n_deferred_l21 = 0;  // fronts whose L21 comes from the k_l21 GEMM after their panel steps
   struct Op { int kind, off, count; long long sc0 = 0, sc1 = 0; };  // sc: deferred scatter range (extend-add ops)  // kind 0 extend-add (pre-scattered level), 4 / 5 assembly + extend-add,
                                         // 2 panel step (6: with lagged-pair tasks), 3 syrk, 8 root exchange
   // ---- distributed factorization (landmark-sharded BA). Set dist_rank / dist_nranks / allreduce before
@@ -374,6 +375,9 @@ class Engine {
   // lambda the stored G = Hpl U^-T, S(i,i) and bschur were formed with (NaN: Hpl stored, the plain Schur passes run)
   bool fz_split_ok = false;
   bool fz_kx = false;  // the split stores Kt records (assembly.hip KXB) instead of G
+  DevBuf<int> cm_hpl;    // per camera-major observation its Kt record (the camera pass reads it)
+  DevBuf<int> kx_extra;  // per BA edge of a fixed landmark and a free camera its extra Kt record, else -1
+  int n_kx_extra = 0;
   double fz_lambda = std::numeric_limits<double>::quiet_NaN();
   DevBuf<int> cm_ptr, cm_v0, cm_v1;
   DevBuf<double> cm_meas, cm_info, cm_params;

@@ -18,6 +18,7 @@ typedef double gdx4 __attribute__((ext_vector_type(4)));
 
 template <int BM, int BN, int WM = 2, int WN = 2, int KC_ = 16>
 struct GemmNT {
+  static constexpr int ROWS = BM;          // rows of C per tile (k_syrk's row-tile unit)
   static constexpr int NT = 64 * WM * WN;  // threads
   static constexpr int KC = KC_;
   static constexpr int SA = BM + 16;  // k-major LDS strides (doubles), = 16 mod 32: the four k rows of a
@@ -32,9 +33,12 @@ struct GemmNT {
   // Short-K tiles (their time is the C traffic) stage the tile in LDS (once it holds no K chunk) and move C a column
   // per wave instruction: 16-lane segments of the MFMA layout would touch 16 columns 32 bytes at a time.
   static constexpr bool LDS_EPILOGUE = (long long)BM * (BN + 1) <= LDS_DOUBLES && NT % BM == 0;
+  // yv / vout (diagonal tiles of a contribution pass): also vout[r] -= sum_k A(I0 + r, k) yv[k] for the tile's rows
   __device__ static void run(const double* __restrict__ A, int lda, double* __restrict__ C, int ldc, int mrows,
-                             int climit, int I0, int J0, int ka, int kb, double* lds, bool overwrite = false) {
+                             int climit, int I0, int J0, int ka, int kb, double* lds, bool overwrite = false,
+                             const double* yv = nullptr, double* vout = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    double vdot = 0.0;
     const int wr = w % WM, wc = w / WM;
     const int lr = lane & 15, lk = lane >> 4;
     constexpr int BUF = KC * (SA + SB);  // buffer b: A image at lds + b BUF, B image after it
@@ -99,9 +103,14 @@ struct GemmNT {
 #pragma unroll
           for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
       }
+      if (yv && tid < BM) {  // masked entries (k >= kb) were stashed as zeros
+        const int k0 = ka + c * KC;
+        for (int k = 0; k < KC && k0 + k < kb; ++k) vdot += lds[b * BUF + k * SA + tid] * yv[k0 + k];
+      }
       stash(b ^ 1);
       __syncthreads();
     }
+    if (yv && tid < BM && I0 + tid < mrows) vout[I0 + tid] -= vdot;
     // (short K only: with a long K loop the tile's own epilogue measured faster, C4 K = 384 pass 48 vs 51 us)
     if (LDS_EPILOGUE && (overwrite || kb - ka <= 2 * KC)) {
       // acc -> LDS tile (row-major, stride BN + 1), then thread t owns row t % BM of columns t / BM, + NT / BM, ...
@@ -164,6 +173,7 @@ struct GemmNT {
 // 16-byte piece of slack after A).
 template <int BM, int BN, int WM = 2, int WN = 2, int KC_ = 16, int NS = 3>
 struct GemmNTd {
+  static constexpr int ROWS = BM;  // rows of C per tile (k_syrk's row-tile unit)
   static constexpr int NT = 64 * WM * WN, NW = WM * WN;
   static constexpr int KC = KC_;
   static_assert(BM == 64 || BM == 128, "BM: one or two columns per DMA instruction");
@@ -175,7 +185,10 @@ struct GemmNTd {
   static_assert(IA % NW == 0 && IB % NW == 0, "every wave issues the same number of DMA instructions");
   static constexpr int JA = IA / NW, JB = IB / NW;             // per wave (= per thread)
   static constexpr int STAGE = IA * GA + IB * GB;              // doubles per stage
-  static constexpr int LDS_DOUBLES = NS * STAGE > BM * (BN + 1) ? NS * STAGE : BM * (BN + 1);
+  // the LDS epilogue (short K, or a written-only C) needs a BM x (BN + 1) image: 64-row tiles only (a 128-row tile
+  // would double its LDS and halve the workgroups per CU; it stores from the MFMA layout instead)
+  static constexpr bool LDS_EPI = BM == 64;
+  static constexpr int LDS_DOUBLES = LDS_EPI && BM * (BN + 1) > NS * STAGE ? BM * (BN + 1) : NS * STAGE;
   static constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;
   static constexpr int G = JA + JB;                            // DMA instructions per thread per chunk
 
@@ -183,7 +196,19 @@ struct GemmNTd {
   __device__ static double* bptr(double* st, int k, int r) { return st + IA * GA + (k / CPB) * GB + (k % CPB) * BN + r; }
 
   __device__ __forceinline__ static void run(const double* __restrict__ A, int lda, double* __restrict__ C, int ldc, int mrows,
-                             int climit, int I0, int J0, int ka, int kb, double* lds, bool overwrite = false) {
+                             int climit, int I0, int J0, int ka, int kb, double* lds, bool overwrite = false,
+                             const double* yv = nullptr, double* vout = nullptr) {
+    run_ab(A, lda, mrows, A, lda, mrows, C, ldc, mrows, climit, I0, J0, ka, kb, lds, overwrite ? 1 : 0, yv, vout);
+  }
+  // General form: C(I, J) op A(I, K) B(J, K)^T with A (rows < arows, leading dimension lda) and B (rows < brows, ldb)
+  // column-major. mode 0: C -= A B^T on the lower triangle (rows < mrows, columns < climit); 1: the same with C known
+  // to be zero (not read); 2: C = A B^T on the whole tile (no triangle). yv / vout (mode 0 / 1, diagonal tiles): also
+  // vout[r] -= sum_k A(I0 + r, k) yv[k] for the tile's rows (the front vector's rows below the supernode).
+  __device__ __forceinline__ static void run_ab(const double* __restrict__ A, int lda, int arows, const double* __restrict__ Bm,
+                                                int ldb, int brows, double* __restrict__ C, int ldc, int mrows, int climit,
+                                                int I0, int J0, int ka, int kb, double* lds, int mode,
+                                                const double* yv = nullptr, double* vout = nullptr) {
+    const bool overwrite = mode == 1, full = mode == 2;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w % WM, wc = w / WM;
     const int lr = lane & 15, lk = lane >> 4;
@@ -192,15 +217,15 @@ struct GemmNTd {
 #pragma unroll
       for (int j = 0; j < JA; ++j) {
         const int g = j * NW + w, col = g * CPA + lane / (BM / 2), row = 2 * (lane % (BM / 2));
-        const int k = min(kc + col, kb - 1), r = min(I0 + row, mrows - 1);  // (row mrows - 1, mrows): see below
+        const int k = min(kc + col, kb - 1), r = min(I0 + row, arows - 1);  // (row arows - 1, arows): see below
         __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)k * lda + r),
                                          (__attribute__((address_space(3))) void*)(st + g * GA), 16, 0, 0);
       }
 #pragma unroll
       for (int j = 0; j < JB; ++j) {
         const int g = j * NW + w, col = g * CPB + lane / (BN / 2), row = 2 * (lane % (BN / 2));
-        const int k = min(kc + col, kb - 1), r = min(J0 + row, mrows - 1);
-        __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)k * lda + r),
+        const int k = min(kc + col, kb - 1), r = min(J0 + row, brows - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(Bm + (size_t)k * ldb + r),
                                          (__attribute__((address_space(3))) void*)(st + IA * GA + g * GB), 16, 0, 0);
       }
     };
@@ -210,6 +235,7 @@ struct GemmNTd {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = gdx4{0.0, 0.0, 0.0, 0.0};
     const int nch = (kb - ka + KC - 1) / KC;
+    double vdot = 0.0;
 #pragma unroll
     for (int c = 0; c < NS - 1; ++c)
       if (c < nch) issue(ka + c * KC, lds + c * STAGE);
@@ -254,9 +280,14 @@ struct GemmNTd {
             for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
       }
+      if (yv && tid < BM) {  // the tile's rows of A times the chunk of y (workgroup-uniform branch per launch task)
+        const double* yc = yv + ka + c * KC;
+        for (int k = 0; k < kv; ++k) vdot += *aptr(st, k, tid) * yc[k];
+      }
     }
+    if (yv && tid < BM && I0 + tid < arows) vout[I0 + tid] -= vdot;
     // every DMA retired (the last chunk waited vmcnt(0)); the LDS epilogue reuses the ring after a barrier
-    if ((overwrite || kb - ka <= 2 * KC) && NT % BM == 0) {
+    if (LDS_EPI && !full && (overwrite || kb - ka <= 2 * KC) && NT % BM == 0) {
       __syncthreads();
       constexpr int CS = BN + 1, CPI = NT / BM;
 #pragma unroll
@@ -279,6 +310,20 @@ struct GemmNTd {
       for (int u = 0; u < NP; ++u) {
         const int c = tid / BM + CPI * u, gj = J0 + c;
         if (gi < mrows && gj < climit && gi >= gj) C[(size_t)gj * ldc + gi] = cv[u] - lds[r * CS + c];
+      }
+      return;
+    }
+    if (full) {  // C = A B^T, every entry of the tile in range
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int gj = J0 + wc * (BN / WN) + 16 * j + lr;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int gi = I0 + wr * (BM / WM) + 16 * i + lk + 4 * q;
+            if (gi < mrows && gj < climit) C[(size_t)gj * ldc + gi] = acc[i][j][q];
+          }
       }
       return;
     }

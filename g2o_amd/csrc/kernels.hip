@@ -672,8 +672,8 @@ constexpr int SCH_PPB = SCH_SL + 1;       // slot-CSR entries per batch
 // indices behind the products (two register sets, the staging as inline assembly) measured the same (C4 142 vs 139 us,
 // profiles/r04_ab_schur_pipe2.log) and was dropped.
 // SCH_SB: staged blocks per batch (launch::SCHUR_SB for G blocks, launch::SCHUR_SB_KX for the 80-byte Kt records)
-template <int PD, int LD, int PIPE, bool KX = false, int SCH_SB = launch::SCHUR_SB>
-__global__ void __launch_bounds__(256, 4)
+template <int PD, int LD, int PIPE, bool KX = false, int SCH_SB = launch::SCHUR_SB, int OCC = 4>
+__global__ void __launch_bounds__(256, OCC)
     k_schur_rows(const launch::SchurTask* __restrict__ tasks, const launch::SchurBatch* __restrict__ batches,
                  const int* st_obs, const int* pairs, const int* pp,
                  const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,
@@ -1499,6 +1499,7 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
   const int nz = nzero > 0 ? nzero : 0;
   if (kx) {  // BA split: G rebuilt from the Kt records
     if (pd != 6 || ld != 3) throw DeviceError("schur_rows: Kt records need BlockSolver_6_3 blocks");
+    // (108 VGPRs: four workgroups per CU; a register budget for five or six spills 8 / 35 VGPRs at 128-block batches)
     auto go = [&](auto SBc) {
       constexpr int SBK = decltype(SBc)::value;
       if (pipe == 0)

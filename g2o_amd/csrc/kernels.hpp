@@ -50,6 +50,8 @@ struct SchurSplit {
   double* cl;            // c = U^-1 b_l, global landmark index
   double* G;             // Hpl's block order: G (PD x LD) per observation, or with kx its 10-double Kt | x/z y/z 1/z record
   int kx;                // BA: store the Kt record instead of G (assembly.hip KXB; k_schur_rows rebuilds G from it)
+  const int* cm_hpl;     // kx: per camera-major observation its record (Hpl block, or an extra one: fixed landmark)
+  const int* kx_extra;   // kx: per (landmark-major) edge of a fixed landmark and a free camera its extra record, else -1
   long long hpl_base;    // offset of the first Hpl block in off_base (the Hessian)
   const int* lm_ptr;     // local landmark -> its Hpl/G block range (split landmarks' fixup)
   const int* hl;         // landmark vertex (local id) -> hessian index (-1 fixed), for the camera pass
@@ -229,7 +231,12 @@ void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* 
                                                                                     // + head's scatter workgroups
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
 // the contribution block, K = [0, ns)); columns stop at ns unless kb = ns (then m)
-void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf, hipStream_t s);
+void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf,
+               const double* ysol, double* vecs, hipStream_t s);
+int syrk_variant();    // the k_syrk tile (G2OHIP_SYRK_DMA)
+int syrk_tile_rows();  // rows per k_syrk tile of that variant (64 or 128): the task lists' row-tile unit
+void chol_l21(int ntasks, const Task* tasks, const FrontDesc* fd, const double* fronts, const double* xinv, double* lbuf,
+              hipStream_t s);
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]
 void chol_ipermute(int n, const int* perm, const double* in, double* out, hipStream_t s);  // out[perm[k]] = in[k]
 void chol_bwd_gemv(int ntasks, const Task* tasks, const FrontDesc* fd, const int* rows, const double* lbuf,

@@ -472,3 +472,17 @@ def landmark_shard(prob: Problem, rank: int, nranks: int) -> Problem:
     ev = EdgeSet(e.etype, e.v0[m].copy(), e.v1[m].copy(), e.meas[m].copy(), e.info[m].copy(),
                  None if e.params is None else e.params[m].copy())
     return Problem(f"{prob.name}/shard{rank}of{nranks}", [cams, pv], [ev], prob.pose_dim, prob.landmark_dim)
+
+
+def landmark_subset(prob: Problem, ids, name: str = "subset") -> Problem:
+    """Sub-problem of every camera and the landmarks whose ids are in ``ids`` (any subset, e.g. the aligned shard a rank
+    holds, SparseOptimizer.local_landmark_ids), with the observations of those landmarks."""
+    cams, pts = prob.vertices
+    e = prob.edges[0]
+    keep = np.isin(pts.ids, np.asarray(ids))
+    m = np.isin(e.v0, pts.ids[keep])
+    pv = VertexSet(pts.vtype, pts.ids[keep].copy(), pts.est[keep].copy(), pts.fixed[keep].copy(),
+                   pts.marginalized[keep].copy())
+    ev = EdgeSet(e.etype, e.v0[m].copy(), e.v1[m].copy(), e.meas[m].copy(), e.info[m].copy(),
+                 None if e.params is None else e.params[m].copy())
+    return Problem(f"{prob.name}/{name}", [cams, pv], [ev], prob.pose_dim, prob.landmark_dim)

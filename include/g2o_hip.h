@@ -199,7 +199,8 @@ int g2ohip_solver_linear_residual(g2ohip_graph* g, double* rel);
  * out[29] = doubles of this rank's subtree blocks read from its own partial reduced system (never exchanged), out[30] =
  * bytes this rank sends per LM trial through the reduced system's and the factorization's collectives (ring
  * algorithms), out[31] = free landmarks in this rank's shard, out[32] = the modelled sharded work (s) of the busiest
- * rank under this layout. Returns the number of entries available. */
+ * rank under this layout, out[33] = fronts whose panel steps factor only their own rows, L21 then formed as one GEMM
+ * with the explicit L11^-1 (deferred L21, G2OHIP_CHOL_DEFER_L21). Returns the number of entries available. */
 int g2ohip_solver_factor_info(g2ohip_graph* g, double* out, int n);
 /* Landmark shards (g2ohip_set_comm / _set_comm_local): the ids of the free landmarks this rank holds (their estimates
  * are current on this rank only); ids may be NULL. Returns the count. With the distributed factorization the shards

@@ -359,9 +359,19 @@ SCHEDULES = {
     # contribution / trailing GEMM tiles: the register-staged GemmNT (default: the LDS-DMA ring GemmNTd (16, 2))
     "syrk_register_staged": {"G2OHIP_SYRK_DMA": "0"},
     "syrk_dma_32x2": {"G2OHIP_SYRK_DMA": "1"},
+    # 128 x 64 contribution / trailing tiles (row tiles of 128 in the task lists), blocked fronts forced
+    "syrk_128x64_blocked": {"G2OHIP_SYRK_DMA": "6", "G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64",
+                            "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
+    "syrk_128x64_deferred_l21": {"G2OHIP_SYRK_DMA": "5", "G2OHIP_CHOL_DEFER_L21": "2", "G2OHIP_CHOL_FUSED_MAX": "0"},
     # in-place extend-add column buffers of 512 / 2048 rows (default 1024)
     "extend_add_512": {"G2OHIP_EA_BIG": "512"},
     "extend_add_2048": {"G2OHIP_EA_BIG": "2048"},
+    # deferred L21 forced on every eligible level (default: levels of >= 16 fronts) and switched off
+    "deferred_l21_all": {"G2OHIP_CHOL_DEFER_L21": "2", "G2OHIP_CHOL_FUSED_MAX": "0"},
+    "deferred_l21_off": {"G2OHIP_CHOL_DEFER_L21": "0"},
+    # the Schur split storing G blocks instead of the Kt records
+    "schur_g_blocks": {"G2OHIP_SCHUR_KX": "0"},
+    "schur_kx_batch128": {"G2OHIP_SCHUR_SB_KX": "128"},
     # recomputing back-substitution with 4 / 8 / 16 lanes per landmark (default 2)
     "backsub_j_lanes4": {"G2OHIP_BACKSUB_J_LANES": "4"},
     "backsub_j_lanes8": {"G2OHIP_BACKSUB_J_LANES": "8"},
@@ -389,6 +399,8 @@ def test_factor_schedules(g2o_amd_mod, oracle, monkeypatch, name, mode):
     info = opt.factor_info()
     if mode == "blocked_separate_contrib" and name in ("C1", "C3"):
         assert info["blocked_fronts"] > 0, info
+    if mode == "deferred_l21_all" and info["levels"] > 1:  # every front below the root has rows below its supernode
+        assert info["deferred_l21_fronts"] > 0, info
     opt.build_system()
     opt.set_lambda(1e-3)
     assert opt.solve()

@@ -92,3 +92,45 @@ def test_split_hpp_consumers_after_optimize(g2o_amd_mod, oracle):
     r = ref.stage(0.0)  # buildSystem at the optimized state
     Hpp, _, _ = ref.hessian_dense(r["np"], r["nl"])
     assert np.linalg.norm(y - Hpp @ v) <= 1e-8 * np.linalg.norm(Hpp @ v)
+
+
+def _ba_fixed_points_varied_intrinsics(seed=5):
+    """BA where every 7th point is fixed (observations of a fixed landmark only feed the camera's blocks: the Kt
+    record of such an observation is zero), intrinsics differ per edge (no shared record: the Kt record folds each
+    edge's fx, fy) and a few gross outliers for a robust kernel."""
+    base = synth.ba(num_cameras=30, num_points=900, obs_per_point=6, window=16, seed=seed)
+    cams, pts = base.vertices
+    fixed = pts.fixed.copy()
+    fixed[::7] = 1
+    pv = synth.VertexSet(pts.vtype, pts.ids, pts.est, fixed, pts.marginalized)
+    e = base.edges[0]
+    rng = np.random.default_rng(seed)
+    par = e.params * (1.0 + 0.02 * rng.standard_normal(e.params.shape))
+    meas = e.meas.copy()
+    out = rng.random(len(meas)) < 0.05
+    meas[out] += rng.standard_normal((int(out.sum()), 2)) * 30.0
+    ev = synth.EdgeSet(e.etype, e.v0, e.v1, meas, e.info, par)
+    return synth.Problem(base.name + "_fixedpts", [cams, pv], [ev], 6, 3)
+
+
+@pytest.mark.parametrize("kx,cam", [("1", "1"), ("1", "0"), ("0", "0")])
+def test_split_fixed_points_varied_intrinsics_robust(g2o_amd_mod, oracle, monkeypatch, kx, cam):
+    """The Schur split with Kt records (default; the camera pass from the records or re-linearising, G2OHIP_CAM_KX) and
+    with G blocks (G2OHIP_SCHUR_KX=0): stage-level reduced system and a Huber-robustified LM trajectory against the
+    oracle on a graph with fixed points and per-edge intrinsics."""
+    monkeypatch.setenv("G2OHIP_SCHUR_KX", kx)
+    monkeypatch.setenv("G2OHIP_CAM_KX", cam)
+    prob = _ba_fixed_points_varied_intrinsics()
+    _stage(g2o_amd_mod, oracle, prob, 1e-3, monkeypatch)
+    opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    opt.set_robust_kernel(synth.E_SE3_PROJECT_XYZ, "Huber", 2.447)
+    ref = oracle.OracleGraph(prob)
+    ref.set_robust_kernel(synth.E_SE3_PROJECT_XYZ, 1, 2.447)
+    n, st = opt.optimize(6)
+    nr, sr = ref.optimize(6, oracle.make_config(threads=8))
+    assert n == nr
+    for a, b in zip(st, sr):
+        assert abs(a.chi2 - b.chi2) <= 1e-6 * abs(b.chi2), (a.chi2, b.chi2)
+        assert a.levenbergIterations == b.levenbergIterations
+    xg, xr = opt.minimal_state(), ref.minimal_state()
+    assert np.linalg.norm(xg - xr) <= 1e-6 * np.linalg.norm(xr)

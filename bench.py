@@ -254,8 +254,10 @@ def posegraph_leg(local, steps=5, warmup=1):
     fms = opt.kernel_ms("chol_factor")
     own = opt.kernel_flops("chol_factor")
     ref = load_json("chol_flops.json").get("C3", {}).get("ref_cs_amd", {}).get("flops")
-    flops = ref or own
-    tf = flops / (fms * 1e-3) / 1e12 if fms > 0 else 0.0
+    # C3's fronts are dense enough that the executed flops are what the MFMA pipes see: the primary figure is on them,
+    # the reference-ordering count (sum c_k^2 of cs_amd) is reported beside it, labelled
+    tf = own / (fms * 1e-3) / 1e12 if fms > 0 else 0.0
+    tref = ref / (fms * 1e-3) / 1e12 if fms > 0 and ref else None
     lin = [1e3 * s.timeLinearSolution / max(s.levenbergIterations, 1) for s in timed]
     return {
         "workload": f"C3: {prob.name} ({prob.num_vertices} poses, {prob.num_edges} edges), {solver_name(prob)}",
@@ -265,11 +267,11 @@ def posegraph_leg(local, steps=5, warmup=1):
         "steps": steps,
         "final_chi2": timed[-1].chi2,
         "factor": with_peaks({"bound": "mfma", "achieved": tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                   "frac": tf / PEAK_FP64_TFLOPS, "flops_per_launch": flops,
-                   "flops_convention": "reference cs_amd sum c_k^2" if ref else "backend ordering",
-                   "backend_ordering_flops": own,
-                   "backend_ordering_achieved": own / (fms * 1e-3) / 1e12 if fms > 0 else 0.0,
-                   "backend_ordering_frac": own / (fms * 1e-3) / 1e12 / PEAK_FP64_TFLOPS if fms > 0 else 0.0,
+                   "frac": tf / PEAK_FP64_TFLOPS, "flops_per_launch": own,
+                   "flops_convention": "executed (backend nested-dissection ordering, supernodal)",
+                   "ref_order_flops": ref, "ref_order_convention": "reference cs_amd sum c_k^2",
+                   "ref_order_achieved": tref,
+                   "ref_order_frac": tref / PEAK_FP64_TFLOPS if tref is not None else None,
                    "avg_launch_ms": fms, "traffic": traffic_lookup("C3")("chol_factor")}),
     }
 

@@ -252,33 +252,36 @@ struct GemmNTd {
       if (c + NS - 1 < nch) issue(ka + (c + NS - 1) * KC, lds + ((c + NS - 1) % NS) * STAGE);
       double* st = lds + (c % NS) * STAGE;
       const int kv = min(KC, kb - ka - c * KC);  // valid columns of this chunk
-      if (kv == KC) {
-#pragma unroll
-        for (int kk = 0; kk < KC / 4; ++kk) {
-          const int k = kk * 4 + lk;
-          double fa[MI], fb[NJ];
-#pragma unroll
-          for (int i = 0; i < MI; ++i) fa[i] = *aptr(st, k, wr * (BM / WM) + 16 * i + lr);
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) fb[j] = *bptr(st, k, wc * (BN / WN) + 16 * j + lr);
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if (kv < KC) {
+        // the tail chunk (uniform): its columns past kv hold clamped copies of column kb - 1; zero them so the
+        // full-chunk products below apply unchanged (one path through the chunk loop: a predicated tail path made
+        // the compiler carry the accumulators in two register sets and copy them at every chunk's end)
+        for (int e = tid; e < (KC - kv) * (BM + BN); e += NT) {
+          const int k = kv + e / (BM + BN), r = e % (BM + BN);
+          *(r < BM ? aptr(st, k, r) : bptr(st, k, r - BM)) = 0.0;
         }
-      } else {
-        for (int kk = 0; kk < (kv + 3) / 4; ++kk) {
-          const int k = kk * 4 + lk;
-          double fa[MI], fb[NJ];
+        __syncthreads();
+      }
+      // fragments double-buffered in registers: k-step kk + 1's LDS reads are in flight under k-step kk's MFMAs
+      double fa[2][MI], fb[2][NJ];
+      auto frag = [&](int kk, int s) {
+        const int k = kk * 4 + lk;
 #pragma unroll
-          for (int i = 0; i < MI; ++i) fa[i] = k < kv ? *aptr(st, k, wr * (BM / WM) + 16 * i + lr) : 0.0;
+        for (int i = 0; i < MI; ++i) fa[s][i] = *aptr(st, k, wr * (BM / WM) + 16 * i + lr);
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) fb[j] = k < kv ? *bptr(st, k, wc * (BN / WN) + 16 * j + lr) : 0.0;
+        for (int j = 0; j < NJ; ++j) fb[s][j] = *bptr(st, k, wc * (BN / WN) + 16 * j + lr);
+      };
+      frag(0, 0);
 #pragma unroll
-          for (int i = 0; i < MI; ++i)
+      for (int kk = 0; kk < KC / 4; ++kk) {
+        if (kk + 1 < KC / 4) frag(kk + 1, (kk + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);  // keep the next reads ahead of these MFMAs (the scheduler sinks them)
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        }
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[kk & 1][i], fb[kk & 1][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
       if (yv && tid < BM) {  // the tile's rows of A times the chunk of y (workgroup-uniform branch per launch task)
         const double* yc = yv + ka + c * KC;

@@ -314,6 +314,7 @@ int main(int argc, char** argv) {
   check("d64", [&](int r, double* f) { return run_d<64, 64>(dA, dC, m, K, r, f); });
   check("d128x64", [&](int r, double* f) { return run_d<128, 64, 4, 2, 1>(dA, dC, m, K, r, f); });
   check("d128", [&](int r, double* f) { return run_d<128, 128, 4, 2, 1>(dA, dC, m, K, r, f); });
+  report("d64x64k16s2o4", run_d<64, 64, 2, 2, 4, 16, 2>(dA, dC, m, K, reps, &fl));  // the k_syrk default
   report("d64x64o2", run_d<64, 64, 2, 2, 2>(dA, dC, m, K, reps, &fl));
   report("d64x64o3", run_d<64, 64, 2, 2, 3>(dA, dC, m, K, reps, &fl));
   report("d64x64s4", run_d<64, 64, 2, 2, 2, 16, 4>(dA, dC, m, K, reps, &fl));

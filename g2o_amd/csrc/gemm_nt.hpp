@@ -236,6 +236,10 @@ struct GemmNTd {
       for (int j = 0; j < NJ; ++j) acc[i][j] = gdx4{0.0, 0.0, 0.0, 0.0};
     const int nch = (kb - ka + KC - 1) / KC;
     double vdot = 0.0;
+    // a wave whose output block lies wholly above the diagonal (the upper quadrant of a diagonal tile; lower-triangle
+    // modes only) skips its products: nothing of it is stored, and its SIMD serves the other workgroups meanwhile
+    const bool upper_w = !full && I0 + wr * (BM / WM) + BM / WM <= J0 + wc * (BN / WN);
+    const bool lds_epi = LDS_EPI && !full && (overwrite || kb - ka <= 2 * KC) && NT % BM == 0;
 #pragma unroll
     for (int c = 0; c < NS - 1; ++c)
       if (c < nch) issue(ka + c * KC, lds + c * STAGE);
@@ -271,17 +275,19 @@ struct GemmNTd {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) fb[s][j] = *bptr(st, k, wc * (BN / WN) + 16 * j + lr);
       };
-      frag(0, 0);
+      if (!upper_w) {
+        frag(0, 0);
 #pragma unroll
-      for (int kk = 0; kk < KC / 4; ++kk) {
-        if (kk + 1 < KC / 4) frag(kk + 1, (kk + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);  // keep the next reads ahead of these MFMAs (the scheduler sinks them)
+        for (int kk = 0; kk < KC / 4; ++kk) {
+          if (kk + 1 < KC / 4) frag(kk + 1, (kk + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);  // keep the next reads ahead of these MFMAs (the scheduler sinks them)
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+          for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[kk & 1][i], fb[kk & 1][j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+            for (int j = 0; j < NJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[kk & 1][i], fb[kk & 1][j], acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       if (yv && tid < BM) {  // the tile's rows of A times the chunk of y (workgroup-uniform branch per launch task)
         const double* yc = yv + ka + c * KC;
@@ -290,7 +296,7 @@ struct GemmNTd {
     }
     if (yv && tid < BM && I0 + tid < arows) vout[I0 + tid] -= vdot;
     // every DMA retired (the last chunk waited vmcnt(0)); the LDS epilogue reuses the ring after a barrier
-    if (LDS_EPI && !full && (overwrite || kb - ka <= 2 * KC) && NT % BM == 0) {
+    if (lds_epi) {
       __syncthreads();
       constexpr int CS = BN + 1, CPI = NT / BM;
 #pragma unroll

@@ -595,7 +595,12 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   }
   PH_BEGIN(2)
   PH1_BEGIN(3)
-  const StepTask t = (int)blockIdx.x < head.n ? head.t[blockIdx.x] : tasks[blockIdx.x];
+  // the task: the chain's tasks ride in the kernel arguments, the rest in a global list; both read with scalar loads
+  // (the kernel-argument one at a clamped index, then replaced by VALUE): a select of the two POINTERS made the compiler
+  // fetch the task with a flat vector load, a full memory round trip on every step's chain before the first data load
+  // could issue
+  StepTask t = head.t[min((int)blockIdx.x, launch::CHOL_HEAD - 1)];
+  if ((int)blockIdx.x >= head.n) t = tasks[blockIdx.x];  // (the chain's tasks wait for no global load)
   const int m = t.m, ns = t.ns;
   double* F = fronts + t.f_off;
   double* L = lbuf + t.l_off;

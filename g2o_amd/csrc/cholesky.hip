@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
       Dn[r * DS + c] = cdv[u_];
       Pb[r * PS + c] = xpv[u_];
     }
-    if (tid < NB) yk[tid] = ykv;
+    *(tid < NB ? &yk[tid] : &col[tid & (4 * NB - 1)]) = ykv;  // unconditional: keeps the ysol load in the first batch
     __syncthreads();
     const int lr = lane & 15, lk = lane >> 4;
     {  // X = P L_kk^-T: wave w owns the 16x16 tile (w & 1, w >> 1), one MFMA pipe per tile
@@ -789,6 +789,13 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
     pbv[u] = ld0(F, (k0 + q) * m + J0 + r, upd && q < kb && J0 + r < rlim);
   }
   const int climit = t.clim;  // ns; m when the contribution block is fused; the big-panel end when blocked
+  // rows/columns of the next diagonal block, [r0, r0 + kbn): this step's diagonal task reads their raw values at its
+  // start and applies the panel update itself, so tile tasks never write them
+  const int kbn = (t.flags & 32) ? 0 : max(0, min(NB, ns - r0));
+  // the writer's forward-solve row of v, read with this first batch (a read at its update, after the TRSM, would be
+  // one more memory round trip on the writer tiles)
+  const bool vupd = writer && tid < 64 && I0 + tid < rlim && I0 + tid >= r0 + kbn;
+  const double vold = ld0(v, I0 + tid, vupd);
   if (pair) {  // C[I, J] -= X_prev,I X_prev,J^T into the accumulators first, the current panel's loads in flight
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -806,7 +813,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
     const int e = tid + 256 * u_;
     Li[(e >> 5) * PS + (e & (NB - 1))] = lv[u_];
   }
-  if (tid < NB) yk[tid] = ykv;
+  *(tid < NB ? &yk[tid] : &col[tid & (4 * NB - 1)]) = ykv;  // unconditional: keeps the ysol load in the first batch
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = tid + 256 * u, r = e & (TT - 1), q = e >> 6;
@@ -842,14 +849,11 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
     }
   }
   __syncthreads();
-  // rows/columns of the next diagonal block, [r0, r0 + kbn): this step's diagonal task reads their
-  // raw values at its start and applies the panel update itself, so tile tasks never write them
-  const int kbn = (t.flags & 32) ? 0 : max(0, min(NB, ns - r0));
-  if (writer && tid < 64 && I0 + tid < rlim && I0 + tid >= r0 + kbn) {  // forward-solve update: v_i -= x_i y_k
+  if (vupd) {  // forward-solve update: v_i -= x_i y_k
     double s2 = 0.0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) s2 += Pa[tid * PS + q] * yk[q];
-    v[I0 + tid] -= s2;
+    v[I0 + tid] = vold - s2;
   }
 
   // ---- writers store the L21 rows of block I

@@ -584,6 +584,13 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   __shared__ double Dn[NB * DS];      // next diagonal block
   __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
   __shared__ double vn[NB];
+  // the task: the chain's tasks ride in the kernel arguments, the rest in a global list; both read with scalar loads
+  // (the kernel-argument one at a clamped index, then replaced by VALUE): a select of the two POINTERS made the compiler
+  // fetch the task with a flat vector load, a full memory round trip on every step's chain before the first data load
+  // could issue. The kernel-argument task is read with ntask, before the scatter branch: read after it, the two were
+  // dependent scalar round trips (plus a third for head.n; a task index below ntask is in the head iff < CHOL_HEAD)
+  StepTask t = head.t[min((int)blockIdx.x, launch::CHOL_HEAD - 1)];
+  asm volatile("" ::"s"(t.m), "s"(t.f_off));  // (both halves: the compiler sinks loads used past the branch)
   if ((int)blockIdx.x >= head.ntask) {  // deferred input scatter of a later level (off this step's chain)
     const long long k = head.sc0 + (long long)((int)blockIdx.x - head.ntask) * 256 + threadIdx.x;
     if (k < head.sc1) {
@@ -595,12 +602,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   }
   PH_BEGIN(2)
   PH1_BEGIN(3)
-  // the task: the chain's tasks ride in the kernel arguments, the rest in a global list; both read with scalar loads
-  // (the kernel-argument one at a clamped index, then replaced by VALUE): a select of the two POINTERS made the compiler
-  // fetch the task with a flat vector load, a full memory round trip on every step's chain before the first data load
-  // could issue
-  StepTask t = head.t[min((int)blockIdx.x, launch::CHOL_HEAD - 1)];
-  if ((int)blockIdx.x >= head.n) t = tasks[blockIdx.x];  // (the chain's tasks wait for no global load)
+  if ((int)blockIdx.x >= launch::CHOL_HEAD) t = tasks[blockIdx.x];  // (the chain's tasks wait for no global load)
   const int m = t.m, ns = t.ns;
   double* F = fronts + t.f_off;
   double* L = lbuf + t.l_off;

@@ -860,12 +860,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     for (size_t k = 0; k < ops.size(); ++k) {
       if (ops[k].kind != 2 && ops[k].kind != 6) continue;
       launch::StepHead& h = heads[k];
-      h.n = 0;
       h.ntask = ops[k].count;
-      while (h.n < launch::CHOL_HEAD && h.n < ops[k].count) {  // the first workgroups (diagonal tasks among them)
-        h.t[h.n] = stk[ops[k].off + h.n];
-        ++h.n;
-      }
+      for (int i = 0; i < launch::CHOL_HEAD && i < ops[k].count; ++i)  // the first workgroups (diagonal tasks among them)
+        h.t[i] = stk[ops[k].off + i];
     }
     // Deferred input scatter: a pre-scattered level's entries are needed only from its own extend-add on, so they ride
     // as extra workgroups in the previous level's first panel-step launch (chain-bound: the chip is mostly idle beside

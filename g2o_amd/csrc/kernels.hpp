@@ -192,8 +192,7 @@ struct StepTask {  // k_step work item, self-contained so a workgroup needs one 
 // read their task with the kernel arguments instead of one more dependent global load
 constexpr int CHOL_HEAD = 8;
 struct StepHead {
-  StepTask t[CHOL_HEAD];
-  int n;
+  StepTask t[CHOL_HEAD];  // the launch's first min(CHOL_HEAD, ntask) tasks
   // deferred input scatter (DeviceCholesky::factor): workgroups past the launch's ntask tasks scatter the input entries
   // [sc0, sc1) of a later level's pre-scattered fronts (as k_chol_scatter: fronts[dst[k]] = vals[src[k] & 0x7fffffff],
   // + lambda when src[k] < 0), 256 entries each

@@ -1,0 +1,12 @@
+# k_step: kernel-argument task read with ntask before the scatter branch (no dependent head.n load): parity, A/B, C4 level split
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out; mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "factor_schedules or c5_bench or c4_bench or c3_bench or sharded or marginals" > $O/r05s_tests.log 2>&1; rc=$?; echo TESTS_RC=$rc; tail -2 $O/r05s_tests.log
+[ $rc -eq 0 ] || exit 1
+B=G2OHIP_LIB=/root/repo/g2o_amd/libg2o_hip_base.so
+bash tools/gpu_ab.sh r05s_ab "C4 - $B - $B --steps 20 --warmup 3" "C5 - $B - $B --steps 8 --warmup 2" "C3 - $B --steps 3 --warmup 1" || exit 1
+D=$O/r05s_C4
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python bench.py --config C4 --steps 3 --warmup 1 --no-cpu-baseline --no-posegraph --no-c5 > $D.json 2> $D.err || { echo PROF_FAIL; tail -5 $D.err; exit 1; }
+F=$(find $D -name '*kernel_trace.csv' | head -1)
+python tools/factor_levels.py $F

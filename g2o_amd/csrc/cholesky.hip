@@ -41,6 +41,8 @@
 
 namespace g2ohip {
 
+using launch::B0Child;
+using launch::B0Front;
 using launch::FrontDesc;
 using launch::StepTask;
 using launch::Task;
@@ -301,7 +303,8 @@ __device__ __forceinline__ double input_entry(const double* vals, const int* ent
 // ASM: the level's fronts are assembled here (EAC: rows per LDS column chunk); else they were pre-zeroed and
 // scattered
 template <bool ASM, int EAC>
-__global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
+__global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tasks, const B0Front* __restrict__ b0f,
+                                                    const B0Child* __restrict__ b0c, const FrontDesc* __restrict__ fd,
                                                     const int* __restrict__ children, const int* __restrict__ relmap,
                                                     const int* __restrict__ jtab, const int* __restrict__ cmptr,
                                                     const longlong2* __restrict__ cment, const int* __restrict__ colptr, const int* __restrict__ ent_row,
@@ -311,6 +314,10 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
                                                     double* __restrict__ ysol, double* __restrict__ linv,
                                                     double* __restrict__ xinv, int* __restrict__ fail,
                                                     const launch::ScatterJob sj) {
+  // a block-0 task's front: the head's by value (clamped index, read with ntask before the scatter branch), past
+  // EA_HEAD from b0f
+  B0Front bf = sj.b0[min((int)blockIdx.x, launch::EA_HEAD - 1)];
+  asm volatile("" ::"s"(bf.front_off), "s"(bf.ce));  // (both halves: the compiler sinks loads used past the branch)
   if ((int)blockIdx.x >= sj.ntask) {  // deferred input scatter of a later level (the launch's chip is mostly idle)
     const long long k = sj.sc0 + (long long)((int)blockIdx.x - sj.ntask) * 256 + threadIdx.x;
     if (k < sj.sc1) {
@@ -320,31 +327,37 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     }
     return;
   }
-  const Task t = tasks[blockIdx.x];
-  const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr, kb0 = min(NB, me.ns);
-  double* F = fronts + me.front_off;
-  double* v = vecs + me.vec_off;
   const int tid = threadIdx.x;
-  if (t.c == 1) {
+  if ((int)blockIdx.x < sj.nb0) {
+    if ((int)blockIdx.x >= launch::EA_HEAD) bf = b0f[blockIdx.x];
+    const int m = bf.m, kb0 = bf.kb0;
+    double* F = fronts + bf.front_off;
+    double* v = vecs + bf.vec_off;
     __shared__ double D[NB * DS];
     __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
     __shared__ double vy[NB];
     PH_BEGIN(1)
     if constexpr (!ASM) {
+      // every store unconditional (zeros outside the block's lower triangle, v past 32 into col's scratch): a
+      // predicated store kept its load in the same branch, one dependent round trip per load
+      double x[NB * NB / 256];
 #pragma unroll
       for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
         const int e = tid + 256 * u_;
         const int r = e & (NB - 1), c = e >> 5;
-        const bool ok = r < kb0 && c < kb0 && r >= c;
-        const double x = ld0(F, c * m + r, ok);
-        if (ok) D[r * DS + c] = x;
+        x[u_] = ld0(F, c * m + r, r < kb0 && c < kb0 && r >= c);
       }
-      if (tid < kb0) vy[tid] = v[tid];
+      const double yv = ld0(v, tid, tid < kb0);
+#pragma unroll
+      for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+        const int e = tid + 256 * u_;
+        D[(e & (NB - 1)) * DS + (e >> 5)] = x[u_];
+      }
+      *(tid < NB ? &vy[tid] : &col[tid & (4 * NB - 1)]) = yv;
     } else {
       __shared__ int cp[NB + 1];
       for (int i = tid; i < NB * DS; i += 256) D[i] = 0.0;
-      if (tid <= kb0) cp[tid] = colptr[me.c0 + tid];
+      if (tid <= kb0) cp[tid] = colptr[bf.c0 + tid];
       if (tid < kb0) vy[tid] = v[tid];
       __syncthreads();
       // input entries of the block's columns (one contiguous range), the whole workgroup striding over it
@@ -357,51 +370,82 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
       }
     }
     __syncthreads();
-    // children in groups of B0C: every load of a group (descriptors, n0, rel, update entries) is issued
-    // before the first add, so a group costs three dependent round trips instead of three per child;
-    // the adds then run child by child in the fixed order (bitwise reproducible)
+    // children in groups of B0C: every load of a group (records, rel, update entries) is issued before the
+    // first add, so a group costs two dependent round trips instead of two per child; the adds then run
+    // child by child in the fixed order (bitwise reproducible)
     constexpr int B0C = 4;
-    for (int kc = me.child_begin; kc < me.child_end; kc += B0C) {
+    for (int kc = bf.cb; kc < bf.ce; kc += B0C) {
       double val[B0C][NB * NB / 256], vv[B0C];
       int dst[B0C][NB * NB / 256], vdst[B0C];
+      B0Child cds[B0C];
+#pragma unroll
+      for (int c = 0; c < B0C; ++c) cds[c] = b0c[kc + c < bf.ce ? kc + c : kc];
+      // the group's records in one round trip (left to itself the compiler interleaved them with the data loads)
+      asm volatile("" ::"s"(cds[0].u_off), "s"(cds[1].u_off), "s"(cds[2].u_off), "s"(cds[3].u_off));
+      // the update entries first, then the row maps: the destinations computed from the maps then wait for the
+      // last loads only (computed in the same loop, they made the compiler wait for the maps before the entries)
+      int ri[B0C], rj[B0C][NB * NB / 256], rt[B0C];
 #pragma unroll
       for (int c = 0; c < B0C; ++c) {
-        const bool has = kc + c < me.child_end;
-        const FrontDesc cd = fd[children[has ? kc + c : kc]];
-        const int mc = cd.ns + cd.nr, nrc = cd.nr;
-        const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;
-        const int* rel = relmap + cd.rows_off;
-        const int n0 = has ? jtab[cd.jt_off] : 0;  // child rows mapping into the block (rel is increasing)
+        const B0Child& cd = cds[c];
 #pragma unroll
         for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
           const int e = tid + 256 * u_;
           const int i = e & (NB - 1), j = e >> 5;
-          const bool in = i < nrc && j <= i;  // independent of n0: issued together with it
-          val[c][u_] = ld0(U, j * mc + i, in);
-          const int ri = ld0(rel, i, in), rj = ld0(rel, j, in);
-          dst[c][u_] = (in && i < n0) ? ri * DS + rj : -1;
+          val[c][u_] = ld0(fronts + cd.u_off, j * cd.mc + i, i < cd.nrc && j <= i);
         }
-        vv[c] = ld0(vecs + cd.vec_off + cd.ns, tid, tid < nrc && tid < NB);
-        const int rt = ld0(rel, tid, tid < nrc && tid < NB);
-        vdst[c] = tid < n0 ? rt : -1;
+        vv[c] = ld0(vecs + cd.vv_off, tid, tid < cd.nrc && tid < NB);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < B0C; ++c) {
+        const B0Child& cd = cds[c];
+        const int* rel = relmap + cd.rel_off;
+        const int i = tid & (NB - 1);  // (the row of every entry of this thread)
+        ri[c] = ld0(rel, i, i < cd.nrc);
+#pragma unroll
+        for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+          const int j = (tid + 256 * u_) >> 5;
+          rj[c][u_] = ld0(rel, j, i < cd.nrc && j <= i);
+        }
+        rt[c] = ld0(rel, tid, tid < cd.nrc && tid < NB);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < B0C; ++c) {
+        const B0Child& cd = cds[c];
+        const int n0 = kc + c < bf.ce ? cd.n0 : 0;  // child rows mapping into the block (rel is increasing)
+        const int i = tid & (NB - 1);
+#pragma unroll
+        for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
+          const int j = (tid + 256 * u_) >> 5;
+          dst[c][u_] = (i < cd.nrc && j <= i && i < n0) ? ri[c] * DS + rj[c][u_] : -1;
+        }
+        vdst[c] = tid < n0 ? rt[c] : -1;
       }
 #pragma unroll
       for (int c = 0; c < B0C; ++c) {
-        if (kc + c >= me.child_end) break;
+        if (kc + c >= bf.ce) break;
 #pragma unroll
-        for (int u_ = 0; u_ < NB * NB / 256; ++u_)
-          if (dst[c][u_] >= 0) D[dst[c][u_]] += val[c][u_];
-        if (vdst[c] >= 0) vy[vdst[c]] += vv[c];
+        for (int u_ = 0; u_ < NB * NB / 256; ++u_) *(dst[c][u_] >= 0 ? &D[dst[c][u_]] : &col[tid & (4 * NB - 1)]) += val[c][u_];
+        // unconditional adds (entries outside the block go into col's scratch, unused until the factor): a
+        // predicated add had the compiler sink the entry's load into its branch, a dependent round trip each
+        *(vdst[c] >= 0 ? &vy[vdst[c]] : &col[tid & (4 * NB - 1)]) += vv[c];
         __syncthreads();
       }
     }
     PH(2)
     // L_00^-1 straight from wave 0's registers to linv (X's diagonal blocks: k_xdiag after the factorization)
-    if (tid < 64) factor_block(D, kb0, vy, col, tid, fail, ysol + me.c0, PH_REC, nullptr, linv + (size_t)me.c0 * (NB * NB));
+    if (tid < 64) factor_block(D, kb0, vy, col, tid, fail, ysol + bf.c0, PH_REC, nullptr, linv + (size_t)bf.c0 * (NB * NB));
     PH(3)
     PH(4)
     return;
   }
+  const Task t = tasks[blockIdx.x];
+  const FrontDesc me = fd[t.s];
+  const int m = me.ns + me.nr, kb0 = min(NB, me.ns);
+  double* F = fronts + me.front_off;
+  double* v = vecs + me.vec_off;
   const int a = t.a, b = t.b;
   const int lane = tid & 63, w = tid >> 6;
   if constexpr (ASM) {
@@ -1137,16 +1181,19 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
     KERNEL_CHECK();
   }
 }
-void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
+void chol_extend_add(int ntasks, int nb0, const Task* tasks, const B0Front* b0f, const B0Child* b0c, const FrontDesc* fd,
+                     const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const longlong2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv,
                      int* fail, int assemble, hipStream_t s, const ScatterJob* sj) {
   if (ntasks <= 0) return;
-  ScatterJob job{ntasks, 0, 0, nullptr, nullptr};
-  if (sj && sj->sc1 > sj->sc0) job = ScatterJob{ntasks, sj->sc0, sj->sc1, sj->dst, sj->src};
+  if (!sj || sj->ntask != ntasks || sj->nb0 != nb0 || nb0 > ntasks)
+    throw DeviceError("chol_extend_add: launch arguments do not match the task counts");
+  ScatterJob job = *sj;
+  if (job.sc1 <= job.sc0) job.sc0 = job.sc1 = 0;
   const int grid = ntasks + (int)((job.sc1 - job.sc0 + 255) / 256);
 #define G2OHIP_EA(A_, E_)                                                                                        \
-  hipLaunchKernelGGL((k_extend_add<A_, E_>), grid, 256, 0, s, tasks, fd, children, relmap, jtab, cmptr, cment, \
+  hipLaunchKernelGGL((k_extend_add<A_, E_>), grid, 256, 0, s, tasks, b0f, b0c, fd, children, relmap, jtab, cmptr, cment, \
                      colptr, ent_row, ent_src, vals, lam, fronts, vecs, lbuf, ysol, linv, xinv, fail, job)
   // assemble 2: fronts up to 512 rows (a small column buffer keeps more workgroups per CU)
   if (assemble == 2) G2OHIP_EA(true, 512);

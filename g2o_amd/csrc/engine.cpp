@@ -434,6 +434,17 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     xoff += (long long)q.ns * q.ns;  // X = L11^-1, column-major
   }
   lpool = loff;
+  {  // block-0 child records, in the children array's order (k_extend_add's block-0 tasks)
+    std::vector<launch::B0Child> hb0c;
+    for (int c : sym.children) {
+      const Supernode& cq = sym.sn[c];
+      const long long mc = cq.ns + cq.nr;
+      if (cq.rows_off >= (1LL << 31)) throw DeviceError("block-0 record overflow");
+      hb0c.push_back(launch::B0Child{cq.front_off + cq.ns * mc + cq.ns, cq.vec_off + cq.ns, (int)mc, cq.nr,
+                                     (int)cq.rows_off, hjt[hfd[c].jt_off]});
+    }
+    b0child.upload(hb0c.empty() ? std::vector<launch::B0Child>(1) : hb0c, s);
+  }
   fd.upload(hfd, s);
   jtab.upload(hjt.empty() ? std::vector<int>{0} : hjt, s);
   cmptr.upload(hcmp.empty() ? std::vector<int>{0} : hcmp, s);
@@ -475,6 +486,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     auto rows_nz = [&](int sn, int r, int kend) { return rows_fnz(sn, r) < kend; };
     std::vector<Task> tk;
     std::vector<launch::StepTask> stk;
+    std::vector<launch::B0Front> hb0;
     std::vector<int> sn_pb(sym.sn.size(), 0);  // big-panel width of blocked fronts (0: unblocked)
     ops.clear();
     // contribution blocks: fused into the panel steps (each step's rank-32 update also reaches the
@@ -580,8 +592,16 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       // column buffer of the in-place assembly: 512 rows (five workgroups per CU) up to m = 512, else ea_big rows
       // (G2OHIP_EA_BIG, dev A/B: 512 / 1024 / 2048; profiles/r04_ab_c3_ea.log)
       Op ea{pre ? 0 : (lmaxm <= 512 || ea_big == 512 ? 5 : ea_big == 1024 ? 9 : 4), (int)tk.size(), 0};
-      // first diagonal blocks: assembled and factored beside the slabs
-      for (int sn : lv) tk.push_back(Task{sn, 0, 0, 1});
+      // first diagonal blocks: assembled and factored beside the slabs (the launch's first nb0 workgroups, records
+      // in b0front from ea.b0)
+      ea.b0 = (int)hb0.size();
+      ea.nb0 = (int)lv.size();
+      for (int sn : lv) {
+        tk.push_back(Task{sn, 0, 0, 1});
+        const Supernode& q = sym.sn[sn];
+        hb0.push_back(launch::B0Front{q.front_off, q.vec_off, q.ns + q.nr, std::min(NB, q.ns), q.c0,
+                                      sym.children_ptr[sn], sym.children_ptr[sn + 1]});
+      }
       // every front is assembled here (input entries, zeros, children); slabs of EA columns where the level
       // has enough of them to fill the chip several times over, else 4 (latency-bound upper levels)
       const int slab = level_slab[sn_level[lv[0]]];
@@ -856,6 +876,16 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     n_xdiag = (int)tk.size() - xdiag_off;
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
+    b0front.upload(hb0.empty() ? std::vector<launch::B0Front>(1) : hb0, s);
+    ea_jobs.assign(ops.size(), launch::ScatterJob{});
+    for (size_t k = 0; k < ops.size(); ++k) {
+      const int kd = ops[k].kind;
+      if (kd != 0 && kd != 4 && kd != 5 && kd != 9) continue;
+      launch::ScatterJob& j = ea_jobs[k];
+      j.ntask = ops[k].count;
+      j.nb0 = ops[k].nb0;
+      for (int i = 0; i < launch::EA_HEAD && i < ops[k].nb0; ++i) j.b0[i] = hb0[ops[k].b0 + i];
+    }
     heads.assign(ops.size(), launch::StepHead{});
     for (size_t k = 0; k < ops.size(); ++k) {
       if (ops[k].kind != 2 && ops[k].kind != 6) continue;
@@ -942,8 +972,13 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       case 4:
       case 5:
       case 9: {
-        const launch::ScatterJob sj{op.count, op.sc0, op.sc1, pre_dst.get(), pre_src.get()};
-        launch::chol_extend_add(op.count, t, fd.get(), children.get(), relmap.get(), jtab.get(), cmptr.get(),
+        launch::ScatterJob sj = ea_jobs[&op - ops.data()];
+        sj.sc0 = op.sc0;
+        sj.sc1 = op.sc1;
+        sj.dst = pre_dst.get();
+        sj.src = pre_src.get();
+        launch::chol_extend_add(op.count, op.nb0, t, b0front.get() + op.b0, b0child.get(), fd.get(), children.get(),
+                                relmap.get(), jtab.get(), cmptr.get(),
                                 cment.get(), colptr.get(), ent_row.get(), ent_src.get(), vals, lam, fronts.get(),
                                 vecs.get(), lbuf.get(), y_p.get(), linv.get(), xinv.get(), fail,
                                 op.kind == 0 ? 0 : op.kind == 5 ? 2 : op.kind == 9 ? 3 : 1, s, &sj);

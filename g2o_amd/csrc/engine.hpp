@@ -113,7 +113,7 @@ struct DeviceCholesky {
   // trailing-update (k_syrk) launches, big-panel backward rounds
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
   int n_deferred_l21 = 0;  // fronts whose L21 comes from the k_l21 GEMM after their panel steps
-  struct Op { int kind, off, count; long long sc0 = 0, sc1 = 0; };  // sc: deferred scatter range (extend-add ops)  // kind 0 extend-add (pre-scattered level), 4 / 5 assembly + extend-add,
+  struct Op { int kind, off, count; long long sc0 = 0, sc1 = 0; int b0 = 0, nb0 = 0; };  // b0/nb0: extend-add block-0 records  // sc: deferred scatter range (extend-add ops)  // kind 0 extend-add (pre-scattered level), 4 / 5 assembly + extend-add,
                                         // 2 panel step (6: with lagged-pair tasks), 3 syrk, 8 root exchange
   // ---- distributed factorization (landmark-sharded BA). Set dist_rank / dist_nranks / allreduce before
   // setup. The elimination tree is cut: every front below the cut belongs to one rank (whole subtrees, balanced by
@@ -177,6 +177,9 @@ struct DeviceCholesky {
   std::vector<Op> ops;
   int xdiag_off = 0, n_xdiag = 0;  // k_xdiag tasks (in `tasks`): X's diagonal blocks from linv after the factor
   std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
+  std::vector<launch::ScatterJob> ea_jobs;  // per extend-add op: its leading block-0 fronts (kernel arguments)
+  DevBuf<launch::B0Front> b0front;          // per extend-add op (Op::b0): its fronts' block-0 records
+  DevBuf<launch::B0Child> b0child;          // parallel to `children`: each child's record for its parent's block 0
   DevBuf<launch::Task> tasks;
   DevBuf<launch::StepTask> step_tasks;
   DevBuf<double> fronts, vecs, rhs_p, y_p, x_p, t_p, lbuf, linv, xinv;

@@ -203,13 +203,31 @@ struct StepHead {
   const int* sc_src;
   const double* sc_lam;
 };
-// deferred input scatter riding in an extend-add launch (DeviceCholesky::factor): workgroups past its ntask tasks
-// scatter entries [sc0, sc1) as k_chol_scatter does, 256 each
+// k_extend_add's block-0 tasks (the launch's first nb0 workgroups, one per front: its first diagonal block assembled
+// and factored) read their front and children from these self-contained records, built at setup, instead of the chain
+// task -> FrontDesc -> children[] -> child FrontDesc -> jtab (four dependent round trips before the first data load)
+struct B0Front {
+  long long front_off, vec_off;
+  int m, kb0, c0;
+  int cb, ce;  // the front's children: B0Child records [cb, ce) (= FrontDesc::child_begin / child_end)
+};
+struct B0Child {      // one child, in the order of the children array
+  long long u_off;    // its update matrix U = fronts + u_off (leading dimension mc)
+  long long vv_off;   // its update vector vecs + vv_off
+  int mc, nrc, rel_off;
+  int n0;             // its rows mapping into the parent's first diagonal block (jtab[jt_off])
+};
+constexpr int EA_HEAD = 16;
+// extend-add launch arguments: the first EA_HEAD block-0 fronts by value (no global load at all on the level's
+// chain), and the deferred input scatter riding in the launch (DeviceCholesky::factor): workgroups past its ntask
+// tasks scatter entries [sc0, sc1) as k_chol_scatter does, 256 each
 struct ScatterJob {
   int ntask;
+  int nb0;  // block-0 tasks (the first nb0 workgroups)
   long long sc0, sc1;
   const long long* dst;
   const int* src;
+  B0Front b0[EA_HEAD];
 };
 // zero ranges (offset, length pairs) of the front pool, then scatter input entries: fronts[dst[k]] =
 // vals[src[k] & 0x7fffffff] (+ lambda when src[k] < 0), and the front vectors v_s = [rhs(perm[c0 ..]) (own
@@ -220,7 +238,8 @@ void chol_prescatter(int nzero, const long long* zr, long long nent, const doubl
 // assembly + extend-add of a level (slab tasks, t.c == 0: columns [a, b)) with every front's first
 // diagonal block assembled, factored and forward-solved beside it (t.c == 1). Input entries of scalar
 // column c (permuted): ent_row/ent_src[colptr[c] .. colptr[c+1]) = row in the front | diag << 30, index in vals
-void chol_extend_add(int ntasks, const Task* tasks, const FrontDesc* fd, const int* children, const int* relmap,
+void chol_extend_add(int ntasks, int nb0, const Task* tasks, const B0Front* b0f, const B0Child* b0c, const FrontDesc* fd,
+                     const int* children, const int* relmap,
                      const int* jtab, const int* cmptr, const longlong2* cment, const int* colptr, const int* ent_row, const int* ent_src, const double* vals, const double* lam,
                      double* fronts, double* vecs, double* lbuf, double* ysol, double* linv, double* xinv,
                      int* fail, int assemble, hipStream_t s,  // assemble: 0 pre-scattered level, 1 in place,

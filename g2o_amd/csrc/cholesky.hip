@@ -522,36 +522,55 @@ __global__ void __launch_bounds__(256) k_extend_add(const Task* __restrict__ tas
     }
     return;
   }
-  // 2. children in fixed order
+  // 2. children in fixed order, from their block-0 records (the next child's read while this one is added). Every
+  // read-modify-write batch reads all its old values (and the entries) before its first store: the rows of one batch
+  // are distinct, but the compiler cannot know it and kept each store's load behind the previous store, and it sank
+  // the loads of predicated adds into their branches — a dependent round trip per entry (the pins below)
+  B0Child nx = b0c[me.child_begin < me.child_end ? me.child_begin : 0];
   for (int k = me.child_begin; k < me.child_end; ++k) {
-    const FrontDesc cd = fd[children[k]];
-    const int mc = cd.ns + cd.nr, nrc = cd.nr;
-    const double* U = fronts + cd.front_off + (size_t)cd.ns * mc + cd.ns;  // U(i,j) = U[j*mc + i]
-    const double* u = vecs + cd.vec_off + cd.ns;
-    const int* rel = relmap + cd.rows_off;
+    const B0Child cd = nx;
+    if (k + 1 < me.child_end) nx = b0c[k + 1];
+    const int mc = cd.mc, nrc = cd.nrc;
+    const double* U = fronts + cd.u_off;  // U(i,j) = U[j*mc + i]
+    const double* u = vecs + cd.vv_off;
+    const int* rel = relmap + cd.rel_off;
     // child columns whose parent column lies in [a, b) (rel is increasing; precomputed per slab)
     const int j0 = jtab[cd.jt_off + t.c - 1], j1 = jtab[cd.jt_off + t.c];
-    for (int j = j0 + tid; j < j1; j += 256)
-      if (rel[j] >= kb0) v[rel[j]] += u[j];
+    for (int j = j0 + tid; j < j1; j += 256) {
+      const int rr = rel[j];
+      const double uu = u[j];
+      const double vo = v[rr >= kb0 ? rr : 0];
+      asm volatile("" ::"v"(uu), "v"(vo));
+      if (rr >= kb0) v[rr] = vo + uu;
+    }
     // lower triangle: one wave per child column, lanes run down the rows (coalesced U reads,
-    // mostly-contiguous F writes), 4 independent loads in flight per lane
+    // mostly-contiguous F writes), 4 entries per lane and batch
     for (int j = j0 + w; j < j1; j += 4) {
       const double* Uj = U + (size_t)j * mc;
-      double* Fj = F + (size_t)rel[j] * m;
-      const int rlo = rel[j] < kb0 ? kb0 : 0;  // rows of the first diagonal block: block-0 task
+      int rj = 0;  // the parent column, rel[j]: lane 0's first row map of the first batch (i = j), no load of its own
       for (int i0 = j + lane; i0 < nrc; i0 += 256) {
-        double val[4];
+        double val[4], old[4];
         int ri[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int i = i0 + q * 64;
           const bool ok = i < nrc;
-          val[q] = ld0(Uj, i, ok);
-          ri[q] = ok ? ld0(rel, i, ok) : -1;
+          val[q] = Uj[ok ? i : 0];
+          ri[q] = rel[ok ? i : 0];
         }
+        __builtin_amdgcn_sched_barrier(0);  // the batch's entries and row maps all in flight before the first wait
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ri[q] = i0 + q * 64 < nrc ? ri[q] : -1;
+        if (i0 == j + lane) rj = __builtin_amdgcn_readfirstlane(ri[0]);
+        double* Fj = F + (size_t)rj * m;
+        const int rlo = rj < kb0 ? kb0 : 0;  // rows of the first diagonal block: block-0 task
+#pragma unroll
+        for (int q = 0; q < 4; ++q) old[q] = Fj[ri[q] >= rlo ? ri[q] : rj];  // (Fj[rj]: a valid address)
+        asm volatile("" ::"v"(val[0]), "v"(val[1]), "v"(val[2]), "v"(val[3]), "v"(old[0]), "v"(old[1]), "v"(old[2]),
+                     "v"(old[3]));
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (ri[q] >= rlo) Fj[ri[q]] += val[q];
+          if (ri[q] >= rlo) Fj[ri[q]] = old[q] + val[q];
       }
     }
     __syncthreads();
@@ -667,24 +686,30 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
     // and forward solve. Only the critical chain of the panel step lives here.
     const int kbn = min(NB, ns - r0);
     const bool pair = PAIRS && (t.flags & 64);  // the block also lacks the previous panel's update (lagged, odd step)
+    // the loads at selected addresses (index 0 when masked: ld0 split in two), the masks applied after a sched_barrier:
+    // with ld0's select beside its load the scheduler placed the first select (and its wait) amid the batch, a round
+    // trip before the rest of the loads issued
     double lv[NB * NB / 256], pv[NB * NB / 256], cdv[NB * NB / 256], xpv[NB * NB / 256];
 #pragma unroll
     for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
       const int e = tid + 256 * u_, r = e & (NB - 1), c = e >> 5;
-      lv[u_] = ld0(Lin, e, kb > 0);  // kb = 0: first block of a big panel, already fully updated
-      pv[u_] = ld0(F, (k0 + c) * m + r0 + r, c < kb);
-      cdv[u_] = ld0(F, (r0 + c) * m + r0 + r, r >= c && r < kbn);
-      xpv[u_] = ld0(L, (k0 - NB + c) * m + r0 + r, pair);  // L rows of the block in the previous panel
+      lv[u_] = Lin[kb > 0 ? e : 0];  // kb = 0: first block of a big panel, already fully updated
+      pv[u_] = F[c < kb ? (k0 + c) * m + r0 + r : 0];
+      cdv[u_] = F[r >= c && r < kbn ? (r0 + c) * m + r0 + r : 0];
+      xpv[u_] = L[pair ? (k0 - NB + c) * m + r0 + r : 0];  // L rows of the block in the previous panel
     }
-    const double ykv = ld0(ysol, t.c0 + k0 + tid, tid < kb);
-    const double vo = ld0(v, r0 + tid, tid < kbn);
+    double ykv = ysol[tid < kb ? t.c0 + k0 + tid : 0];
+    double vo = v[tid < kbn ? r0 + tid : 0];
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(tid < kb)) ykv = 0.0;
+    if (!(tid < kbn)) vo = 0.0;
 #pragma unroll
     for (int u_ = 0; u_ < NB * NB / 256; ++u_) {
       const int e = tid + 256 * u_, r = e & (NB - 1), c = e >> 5;
-      Li[c * PS + r] = lv[u_];  // e = row * 32 + col of the row-major inverse: (c, r) = (row, col)
-      Pa[r * PS + c] = pv[u_];
-      Dn[r * DS + c] = cdv[u_];
-      Pb[r * PS + c] = xpv[u_];
+      Li[c * PS + r] = kb > 0 ? lv[u_] : 0.0;  // e = row * 32 + col of the row-major inverse: (c, r) = (row, col)
+      Pa[r * PS + c] = c < kb ? pv[u_] : 0.0;
+      Dn[r * DS + c] = r >= c && r < kbn ? cdv[u_] : 0.0;
+      Pb[r * PS + c] = pair ? xpv[u_] : 0.0;
     }
     *(tid < NB ? &yk[tid] : &col[tid & (4 * NB - 1)]) = ykv;  // unconditional: keeps the ysol load in the first batch
     __syncthreads();
@@ -1082,10 +1107,17 @@ __global__ void __launch_bounds__(256) k_xdiag(const Task* __restrict__ tasks, c
   const int a = t.a, kb = min(NB, me.ns - a);
   const double* L = linv + (size_t)(me.c0 + a) * (NB * NB);
   double* X = xinv + me.x_off + (size_t)a * me.ns + a;
+  double x[NB * NB / 256];  // (the padded 32 x 32 block is always readable: every load issued before the first store)
+#pragma unroll
+  for (int u = 0; u < NB * NB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u, c = e >> 5, i = e & (NB - 1);
+    x[u] = L[i * NB + c];
+  }
+  asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));  // else each load is sunk into its store's branch
 #pragma unroll
   for (int u = 0; u < NB * NB / 256; ++u) {
     const int e = threadIdx.x + 256 * u, c = e >> 5, i = e & (NB - 1);  // X(i, c): consecutive threads down a column
-    if (c < kb && i < kb) X[(size_t)c * me.ns + i] = L[i * NB + c];
+    if (c < kb && i < kb) X[(size_t)c * me.ns + i] = x[u];
   }
 }
 

@@ -441,7 +441,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       const long long mc = cq.ns + cq.nr;
       if (cq.rows_off >= (1LL << 31)) throw DeviceError("block-0 record overflow");
       hb0c.push_back(launch::B0Child{cq.front_off + cq.ns * mc + cq.ns, cq.vec_off + cq.ns, (int)mc, cq.nr,
-                                     (int)cq.rows_off, hjt[hfd[c].jt_off]});
+                                     (int)cq.rows_off, hjt[hfd[c].jt_off], hfd[c].jt_off});
     }
     b0child.upload(hb0c.empty() ? std::vector<launch::B0Child>(1) : hb0c, s);
   }

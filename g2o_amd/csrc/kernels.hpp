@@ -211,11 +211,12 @@ struct B0Front {
   int m, kb0, c0;
   int cb, ce;  // the front's children: B0Child records [cb, ce) (= FrontDesc::child_begin / child_end)
 };
-struct B0Child {      // one child, in the order of the children array
+struct B0Child {      // one child, in the order of the children array (also read by the pre-scattered slab tasks)
   long long u_off;    // its update matrix U = fronts + u_off (leading dimension mc)
   long long vv_off;   // its update vector vecs + vv_off
   int mc, nrc, rel_off;
   int n0;             // its rows mapping into the parent's first diagonal block (jtab[jt_off])
+  int jt_off;         // FrontDesc::jt_off
 };
 constexpr int EA_HEAD = 16;
 // extend-add launch arguments: the first EA_HEAD block-0 fronts by value (no global load at all on the level's

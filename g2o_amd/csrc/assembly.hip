@@ -62,6 +62,30 @@ __device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err
     for (int i = 0; i < D * D; ++i) Om[i] *= r1;
   }
 }
+// the same with the edge's vertex indices given: a caller that reads them ahead (software pipeline) starts the state
+// loads without a dependent index load (FamilyBA)
+template <class F>
+__device__ __forceinline__ void edge_terms_at(const EdgeData& d, int e, int v0, int v1, double* err, double* A, double* B,
+                                              double* Om) {
+  constexpr int D = F::D;
+  double pc[3];
+  F::linearize_at(d, e, v0, v1, err, A, B, pc);
+  load_info<D>(info_rec(d, e, F::INFO), Om);
+  if (d.rk) {
+    double chi = 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double r = 0;
+#pragma unroll
+      for (int j = 0; j < D; ++j) r += Om[i * D + j] * err[j];
+      chi += err[i] * r;
+    }
+    double r0, r1;
+    robustify(d.rk, d.rk_delta, chi, r0, r1);
+#pragma unroll
+    for (int i = 0; i < D * D; ++i) Om[i] *= r1;
+  }
+}
 }  // namespace
 
 // KX (with FG, BA only): instead of G = Hpl U^-T (18 doubles) each observation stores the 10-double record the Schur
@@ -383,10 +407,21 @@ __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* 
   double acc[NS];
 #pragma unroll
   for (int k = 0; k < NS; ++k) acc[k] = 0.0;
-  const int p1 = cm_ptr[i + 1];
-  for (int p = cm_ptr[i] + tid; p < p1; p += 256) {
+  const int p0 = cm_ptr[i] + tid, p1 = cm_ptr[i + 1];
+  // software pipeline over the thread's observations (recomputing path): the vertex indices are read two observations
+  // ahead and the landmark's Hessian index one ahead, so an observation's state / U / c loads depend on no load of the
+  // same iteration (three dependent round trips per observation before)
+  int v0a = 0, v1a = 0, v0b = 0, v1b = 0, hla = -1;
+  if constexpr (!KX) {
+    v0a = d.v0[p0 < p1 ? p0 : 0];
+    v1a = d.v1[p0 < p1 ? p0 : 0];
+    v0b = d.v0[p0 + 256 < p1 ? p0 + 256 : 0];
+    v1b = d.v1[p0 + 256 < p1 ? p0 + 256 : 0];
+    if constexpr (FG) hla = sp.hl[v0a];
+  }
+  for (int p = p0; p < p1; p += 256) {
     int hl = -1;
-    if constexpr (FG) hl = sp.hl[d.v0[p]];
+    if constexpr (FG && KX) hl = sp.hl[d.v0[p]];
     if constexpr (KX) {  // every camera-major observation has a record (fixed landmarks: Kt = 0)
       const int a = sp.cm_hpl[p];
       {
@@ -436,8 +471,17 @@ __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* 
         for (int j = 0; j < DB; ++j) acc[k++] += b0[j] * g0 + b1[j] * g1;
       }
     } else {
+    const int v0 = v0a, v1 = v1a;
+    if constexpr (FG) hl = hla;
+    {  // the next observations' indices (two ahead: streaming; one ahead: the Hessian index of a loaded vertex)
+      const int pn = p + 512 < p1 ? p + 512 : 0;
+      const int v0c = d.v0[pn], v1c = d.v1[pn];
+      if constexpr (FG) hla = sp.hl[v0b];
+      v0a = v0b; v1a = v1b;
+      v0b = v0c; v1b = v1c;
+    }
     double err[D], A[D * DA], B[D * DB], Om[D * D];
-    edge_terms<F>(d, p, err, A, B, Om);
+    edge_terms_at<F>(d, p, v0, v1, err, A, B, Om);
     double wr[D];
 #pragma unroll
     for (int r = 0; r < D; ++r) {
@@ -581,11 +625,24 @@ __global__ void __launch_bounds__(256)
   for (int k = 0; k < DA; ++k) y[k] = 0.0;
   if (active) {
     const int2 r = erng[l];
-    for (int e = r.x + q; e < r.y; e += LANES) {
-      const int hc = hcam[d.v1[e]];
+    // software pipeline over the lane's edges: vertex indices two edges ahead, the camera's Hessian index one ahead (an
+    // edge's state and x loads then wait for no load of their own iteration)
+    const int e0 = r.x + q;
+    int v0a = d.v0[e0 < r.y ? e0 : 0], v1a = d.v1[e0 < r.y ? e0 : 0];
+    int v0b = d.v0[e0 + LANES < r.y ? e0 + LANES : 0], v1b = d.v1[e0 + LANES < r.y ? e0 + LANES : 0];
+    int hca = hcam[v1a];
+    for (int e = e0; e < r.y; e += LANES) {
+      const int v0 = v0a, v1 = v1a, hc = hca;
+      {
+        const int en = e + 2 * LANES < r.y ? e + 2 * LANES : 0;
+        const int v0c = d.v0[en], v1c = d.v1[en];
+        hca = hcam[v1b];
+        v0a = v0b; v1a = v1b;
+        v0b = v0c; v1b = v1c;
+      }
       if (hc < 0) continue;  // fixed camera: no Hpl block
       double err[D], A[D * DA], B[D * DB], Om[D * D];
-      edge_terms<F>(d, e, err, A, B, Om);
+      edge_terms_at<F>(d, e, v0, v1, err, A, B, Om);
       const double* xp = x + (size_t)hc * DB;
       double u[D];
 #pragma unroll

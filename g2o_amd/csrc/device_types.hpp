@@ -358,8 +358,12 @@ struct FamilyBA {
   }
   // ... and the point in the camera frame (x, y, z): the camera Jacobian is B = diag(fx, fy) Bt(x/z, y/z, 1/z)
   DI static void linearize(const EdgeData& d, int e, double* err, double* A, double* B, double* pc) {
-    const double* c = d.s1 + (size_t)d.v1[e] * 8;
-    const double* p = d.s0 + (size_t)d.v0[e] * 3;
+    linearize_at(d, e, d.v0[e], d.v1[e], err, A, B, pc);
+  }
+  // the same with the edge's vertex indices given (a caller that prefetched them: no dependent index load)
+  DI static void linearize_at(const EdgeData& d, int e, int v0, int v1, double* err, double* A, double* B, double* pc) {
+    const double* c = d.s1 + (size_t)v1 * 8;
+    const double* p = d.s0 + (size_t)v0 * 3;
     const double q[4] = {c[3], c[4], c[5], c[6]};
     const double pv[3] = {p[0], p[1], p[2]};
     qrot(q, pv, pc);

@@ -174,6 +174,16 @@ void minimal_from_state(int vt, const double* st, double* out) {
 }
 
 // ------------------------------------------------------------------ KernelTimer
+// Events that only time work (read after a stream synchronisation, never waited on for data): without the system-scope
+// fence an event record costs no L2 writeback / invalidate between the kernels it brackets (the default record added
+// ~4 us of idle GPU per record to the LM iteration). G2OHIP_EVENT_FENCE=1 restores default events (A/B).
+static unsigned timing_event_flags() {
+  static const unsigned f = [] {
+    const char* v = getenv("G2OHIP_EVENT_FENCE");
+    return (v && atoi(v) != 0) ? (unsigned)hipEventDefault : (unsigned)hipEventDisableSystemFence;
+  }();
+  return f;
+}
 hipEvent_t KernelTimer::get() {
   if (!pool.empty()) {
     hipEvent_t e = pool.back();
@@ -181,7 +191,7 @@ hipEvent_t KernelTimer::get() {
     return e;
   }
   hipEvent_t e;
-  HIP_CHECK(hipEventCreate(&e));
+  HIP_CHECK(hipEventCreateWithFlags(&e, timing_event_flags()));
   return e;
 }
 void KernelTimer::begin(const std::string& name, hipStream_t s) {
@@ -613,6 +623,23 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       }
       ea.count = (int)tk.size() - ea.off;
       ops.push_back(ea);
+      if (getenv("G2OHIP_PRINT_LEVELS")) {  // diagnostics (stderr): the level's shape and its extend-add launch
+        int mm = 0, mns = 0, nch = 0, mnrc = 0;
+        long long cb = 0;
+        for (int sn : lv) {
+          const Supernode& q = sym.sn[sn];
+          mm = std::max(mm, q.ns + q.nr);
+          mns = std::max(mns, q.ns);
+          for (int ci = sym.children_ptr[sn]; ci < sym.children_ptr[sn + 1]; ++ci) {
+            const Supernode& cq = sym.sn[sym.children[ci]];
+            ++nch;
+            mnrc = std::max(mnrc, cq.nr);
+            cb += (long long)cq.nr * (cq.nr + 1) / 2;
+          }
+        }
+        fprintf(stderr, "level %zu: fronts %zu max_m %d max_ns %d children %d max_child_nr %d child_cb_MB %.1f slab %d %s ea_tasks %d\n",
+                l, lv.size(), mm, mns, nch, mnrc, cb * 8e-6, slab, pre ? "pre" : "inplace", ea.count);
+      }
      
       int maxp = 0;
       for (int sn : lv) maxp = std::max(maxp, (sym.sn[sn].ns + NB - 1) / NB);
@@ -1068,8 +1095,8 @@ Engine::Engine(int dev) : device(dev) {
   // [13] next lambda (rank 0) [14] accepted [15] rho (lm_decide)
   dscal.resize(16);
   dscal.zero(stream);
-  for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
-  for (auto& e : lm_ev_) HIP_CHECK(hipEventCreate(&e));
+  for (auto& e : ev_) HIP_CHECK(hipEventCreateWithFlags(&e, timing_event_flags()));
+  for (auto& e : lm_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, timing_event_flags()));
   HIP_CHECK(hipEventCreateWithFlags(&rb_ev_, hipEventDisableTiming));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hscal_), 16 * sizeof(double), hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hdec_), 16 * sizeof(double),

@@ -111,7 +111,7 @@ def test_c3_full_trajectory(g2o_amd_mod):
 
 def test_c4_bench_sequence(g2o_amd_mod):
     """C4 (the headline config) over exactly the iterations the driver's `bench.py --steps 20 --warmup 5` runs: 5 warmup
-    at full statistics, 20 timed at stats level 1 with the chol_factor timer (bench.py's roofline timer), then the two
+    at full statistics, 20 timed at stats level 0 with the chol_factor timer (bench.py's roofline timer), then the two
     stage iterations with every kernel timer on at stats level 2 (the speculative next assembly is off while assembly
     kernels are timed); the fixture's last 3 iterations follow with the same timers. Every iteration's chi2, lambda
     and trial count against the oracle + reference CSparse fixture, then the final state."""
@@ -122,7 +122,7 @@ def test_c4_bench_sequence(g2o_amd_mod):
 
 def _bench_sequence(g2o_amd_mod, name, warmup, timed, first_timer, stage_timer=None, extra=0):
     """optimize_step from iteration 0 through exactly the iterations a bench.py leg runs: `warmup` at the default
-    statistics, `timed` at stats level 1 (with `first_timer` kernel timing, as the leg's timed region), then the leg's
+    statistics, `timed` at stats level 0 (with `first_timer` kernel timing, as the leg's timed region), then the leg's
     two stage iterations with every kernel timer on at stats level 2 — each switch where the leg makes it, since the
     kernel timers change what the LM loop enqueues (the speculative next assembly is off while assembly kernels are
     timed), and `extra` further iterations with those timers. Every iteration's chi2, lambda and trial count against the
@@ -140,7 +140,7 @@ def _bench_sequence(g2o_amd_mod, name, warmup, timed, first_timer, stage_timer=N
         if it == warmup:
             if first_timer:
                 opt.enable_kernel_timing(True, only=first_timer)
-            opt.set_stats_level(1)
+            opt.set_stats_level(0)
         if it == warmup + timed:
             if stage_timer:
                 opt.enable_kernel_timing(True, only=stage_timer)

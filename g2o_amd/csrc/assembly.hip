@@ -120,11 +120,34 @@ __global__ void __launch_bounds__(256)
   const int e = ebase + lane;
   const bool in = lane < nw;
   double* sw = stage[w];
-  const int pv = in ? d.v0[e] : -1;
-  const int hA = in ? h0[pv] : -1;
-  const bool nfA = hA >= 0, nfB = in && h1[d.v1[e]] >= 0;
+  // the edge's terms are formed unconditionally (lanes past the chunk on its first edge), so the state loads issue
+  // beside the Hessian-index loads instead of behind them (v0 -> h0 -> states was three dependent round trips); an
+  // edge with both vertices fixed is masked below as before
+  const int ec = in ? e : ebase;
+  const int pv0 = d.v0[ec], pv1 = d.v1[ec];
+  const int hA0 = h0[pv0], hB0 = h1[pv1];
   double err[D], A[D * DA], B[D * DB], Om[D * D], pc[3];
-  if (nfA || nfB) edge_terms<F, KX>(d, e, err, A, B, Om, pc);
+  {
+    F::linearize_at(d, ec, pv0, pv1, err, A, B, pc);
+    load_info<D>(info_rec(d, ec, F::INFO), Om);
+    if (d.rk) {
+      double chi = 0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        double r = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) r += Om[i * D + j] * err[j];
+        chi += err[i] * r;
+      }
+      double r0, r1;
+      robustify(d.rk, d.rk_delta, chi, r0, r1);
+#pragma unroll
+      for (int i = 0; i < D * D; ++i) Om[i] *= r1;
+    }
+  }
+  const int pv = in ? pv0 : -1;
+  const int hA = in ? hA0 : -1;
+  const bool nfA = hA >= 0, nfB = in && hB0 >= 0;
   double wr[D];
 #pragma unroll
   for (int r = 0; r < D; ++r) {

@@ -1,0 +1,8 @@
+# linearize: the edge terms formed beside the Hessian-index loads (not behind them): parity subset, A/B C4 / C5
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out; mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "split or c5 or c4 or sharded or assembly or robust or ba_ or fixed or dist" > $O/r05z4_tests.log 2>&1; rc=$?; echo TESTS_RC=$rc; tail -2 $O/r05z4_tests.log
+[ $rc -eq 0 ] || exit 1
+B=G2OHIP_LIB=/root/repo/g2o_amd/libg2o_hip_base.so
+bash tools/gpu_ab.sh r05z4_ab "C4 - $B - $B --steps 20 --warmup 3" "C5 - $B - $B --steps 8 --warmup 2" || exit 1

@@ -1147,6 +1147,29 @@ __global__ void k_scale_terms(long long n, const double* __restrict__ x, const d
   out[i] = x[i] * (l * x[i] + b[i]);
 }
 
+// one thread's RED_PER_THREAD edges of a chi2 chunk, summed in edge order into s: the edges' errors are formed in groups
+// of four with every index and state load of a group in flight together (a guarded edge per iteration cost two dependent
+// round trips each, 32 per thread: the whole kernel time at C4); edges past ne read edge 0 and are not added
+template <class F>
+__device__ __forceinline__ void error_chunk_sum(const EdgeData& d, int ne, long long base, double& s) {
+  constexpr int GK = 4;
+#pragma unroll
+  for (int k0 = 0; k0 < RED_PER_THREAD; k0 += GK) {
+    double err[GK][F::D];
+#pragma unroll
+    for (int u = 0; u < GK; ++u) {  // errors first (no branches: the group's loads can interleave)
+      const long long e = base + (long long)(k0 + u) * RED_BLOCK + threadIdx.x;
+      F::error(d, e < ne ? (int)e : 0, err[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < GK; ++u) {  // then the (robustified) chi2 terms in edge order
+      const long long e = base + (long long)(k0 + u) * RED_BLOCK + threadIdx.x;
+      const double c = edge_chi<F>(d, e < ne ? (int)e : 0, err[u]);
+      if (e < ne) s += c;
+    }
+  }
+}
+
 // computeActiveErrors + activeRobustChi2 fused with the first pass of the deterministic sum: the
 // same fixed chunking and tree as k_sum_partial over a chi2 array, without the array
 template <class F>
@@ -1154,14 +1177,7 @@ __global__ void __launch_bounds__(RED_BLOCK) k_error_partial(EdgeData d, int ne,
   __shared__ double sh[RED_BLOCK];
   const long long base = (long long)blockIdx.x * RED_BLOCK * RED_PER_THREAD;
   double s = 0;
-  for (int k = 0; k < RED_PER_THREAD; ++k) {
-    const long long e = base + (long long)k * RED_BLOCK + threadIdx.x;
-    if (e < ne) {
-      double err[F::D];
-      F::error(d, (int)e, err);
-      s += edge_chi<F>(d, (int)e, err);
-    }
-  }
+  error_chunk_sum<F>(d, ne, base, s);
   sh[threadIdx.x] = s;
   __syncthreads();
   for (int m = RED_BLOCK / 2; m > 0; m >>= 1) {
@@ -1182,24 +1198,24 @@ __global__ void __launch_bounds__(RED_BLOCK) k_error_scale_partial(EdgeData d, i
   __shared__ double sh[RED_BLOCK];
   double s = 0;
   if ((int)blockIdx.x < npe) {
-    const long long base = (long long)blockIdx.x * RED_BLOCK * RED_PER_THREAD;
-    for (int k = 0; k < RED_PER_THREAD; ++k) {
-      const long long e = base + (long long)k * RED_BLOCK + threadIdx.x;
-      if (e < ne) {
-        double err[F::D];
-        F::error(d, (int)e, err);
-        s += edge_chi<F>(d, (int)e, err);
-      }
-    }
+    error_chunk_sum<F>(d, ne, (long long)blockIdx.x * RED_BLOCK * RED_PER_THREAD, s);
   } else {
     const double lp = lam[4], ll = lam[0];
     const long long base = (long long)(blockIdx.x - npe) * RED_BLOCK * RED_PER_THREAD;
+    // every load of the chunk issued before the first term (a guarded load per term was a round trip each)
+    double xv[RED_PER_THREAD], bv[RED_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < RED_PER_THREAD; ++k) {
+      const long long i = base + (long long)k * RED_BLOCK + threadIdx.x;
+      xv[k] = x[i < n ? i : 0];
+      bv[k] = b[i < n ? i : 0];
+    }
 #pragma unroll
     for (int k = 0; k < RED_PER_THREAD; ++k) {
       const long long i = base + (long long)k * RED_BLOCK + threadIdx.x;
       if (i < n) {
         const double l = i < npose ? lp : ll;
-        s += x[i] * (l * x[i] + b[i]);
+        s += xv[k] * (l * xv[k] + bv[k]);
       }
     }
   }

@@ -1153,7 +1153,7 @@ __global__ void k_scale_terms(long long n, const double* __restrict__ x, const d
 template <class F>
 __device__ __forceinline__ void error_chunk_sum(const EdgeData& d, int ne, long long base, double& s) {
   constexpr int GK = 4;
-#pragma unroll
+#pragma unroll 1  // (the group loop stays rolled: unrolled, every family's instance was 4x the code)
   for (int k0 = 0; k0 < RED_PER_THREAD; k0 += GK) {
     double err[GK][F::D];
 #pragma unroll

@@ -50,38 +50,60 @@ def make_problem(cfg):
     return synth.by_name(cfg)
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, deadline_s=None):
     """`--gpus N` (N > 1) without a launcher: start N child ranks of this same command line, one process per GPU, with
     the torch.distributed.run environment (RANK / LOCAL_RANK / WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free port), and
     return the worst exit code. Runs before this process makes any HIP call (nothing here loads libg2o_hip.so). Rank
     0's stdout is this process's (it prints the one JSON line); the other ranks print nothing on stdout. If a rank
-    fails, the others are terminated (by their own PIDs) so no rank is left waiting in a collective."""
+    fails, the others are terminated (by their own PIDs) so no rank is left waiting in a collective. A wall-clock
+    deadline (G2OHIP_BENCH_DEADLINE seconds, default 1800) ends a job whose ranks hang: every rank is killed and the
+    exit code is 124. The port is probed by bind-and-close, which can race with another process: a job whose ranks
+    all fail within 30 s (the rendezvous) is retried once on a fresh port."""
     import socket
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
-    rc = 0
-    pending = set(range(n))
-    while pending:
-        for r in sorted(pending):
-            c = procs[r].poll()
-            if c is None:
-                continue
-            pending.discard(r)
-            if c != 0 and rc == 0:
-                rc = c if c > 0 else 128 - c
-                print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr, flush=True)
+    if deadline_s is None:
+        deadline_s = float(os.environ.get("G2OHIP_BENCH_DEADLINE", "1800"))
+
+    def attempt():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        procs = []
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                          stdout=None if r == 0 else subprocess.DEVNULL))
+        rc = 0
+        t0 = time.monotonic()
+        pending = set(range(n))
+        while pending:
+            if time.monotonic() - t0 > deadline_s:
+                print(f"bench.py: deadline of {deadline_s:.0f} s passed; killing ranks {sorted(pending)}",
+                      file=sys.stderr, flush=True)
                 for q in pending:
-                    procs[q].terminate()
-        time.sleep(0.05)
+                    procs[q].kill()
+                for q in pending:
+                    procs[q].wait()
+                return 124, time.monotonic() - t0, False
+            for r in sorted(pending):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                pending.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr, flush=True)
+                    for q in pending:
+                        procs[q].terminate()
+            time.sleep(0.05)
+        return rc, time.monotonic() - t0, all(p.returncode != 0 for p in procs)
+
+    rc, dt, all_failed = attempt()
+    if rc != 0 and rc != 124 and all_failed and dt < 30:
+        print("bench.py: every rank failed during start-up; retrying once on a fresh port", file=sys.stderr, flush=True)
+        rc, _, _ = attempt()
     return rc
 
 

@@ -1258,11 +1258,10 @@ int syrk_variant() {
   static EnvKnob dma_k{"G2OHIP_SYRK_DMA", 4};
   return dma_k.get();
 }
-int syrk_tile_rows() {
-  const int v = syrk_variant();
-  return v == 5 || v == 6 ? 2 * TT : TT;
-}
-void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf,
+int syrk_tile_rows(int v) { return v == 5 || v == 6 ? 2 * TT : TT; }
+// variant: the one DeviceCholesky::setup read and built its row-tile lists for (never re-read here: the knob may change
+// between optimizers, and a tile of another height would miss or double-apply rows of those lists)
+void chol_syrk(int variant, int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf,
                const double* ysol, double* vecs, hipStream_t s) {
   if (ntasks <= 0) return;
   // G2OHIP_SYRK_DMA=k (dev A/B): the LDS-DMA tile GemmNTd with (K chunk, stages) = (32, 2), (16, 3), (8, 4), (16, 2)
@@ -1272,8 +1271,7 @@ void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* front
   // (profiles/r04_ab_c3_syrk.log; 74 KB of LDS leave 2 workgroups per CU against 3). The (16, 2) ring (37 KB, four
   // workgroups per CU) is the one that wins there: C3 factor 29.07 -> 28.54 ms (profiles/r04_ab_c3_knobs.log), the
   // default; G2OHIP_SYRK_DMA=0 is the register-staged GemmNT.
-  const int dma = syrk_variant();
-  switch (dma) {
+  switch (variant) {
     case 5: hipLaunchKernelGGL((k_syrk<GemmNTd<2 * TT, TT, 2, 2, 16, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;
     case 6: hipLaunchKernelGGL((k_syrk<GemmNTd<2 * TT, TT, 2, 2, 8, 3>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;
     case 1: hipLaunchKernelGGL((k_syrk<GemmNTd<TT, TT, 2, 2, 32, 2>>), ntasks, 256, 0, s, tasks, fd, fronts, lbuf, ysol, vecs); break;

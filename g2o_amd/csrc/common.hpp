@@ -86,16 +86,20 @@ inline std::atomic<int>& knob_epoch() {
 struct EnvKnob {
   const char* name;
   int dflt;
-  std::atomic<int> epoch{-1}, val{0};
+  // (epoch + 1) << 32 | value in one word, so a reader on another host thread never pairs a new epoch with an old
+  // value (0: never read). An unset or EMPTY variable gives the default (not atoi("") = 0).
+  std::atomic<unsigned long long> state{0};
   EnvKnob(const char* n, int d) : name(n), dflt(d) {}
   int get() {
-    const int e = knob_epoch().load(std::memory_order_relaxed);
-    if (epoch.load(std::memory_order_relaxed) != e) {
+    const unsigned long long e = (unsigned long long)(unsigned)knob_epoch().load(std::memory_order_acquire) + 1;
+    unsigned long long st = state.load(std::memory_order_acquire);
+    if ((st >> 32) != e) {
       const char* v = std::getenv(name);
-      val.store(v && *v ? std::atoi(v) : dflt, std::memory_order_relaxed);
-      epoch.store(e, std::memory_order_relaxed);
+      const int x = v && *v ? std::atoi(v) : dflt;
+      st = e << 32 | (unsigned)x;
+      state.store(st, std::memory_order_release);
     }
-    return val.load(std::memory_order_relaxed);
+    return (int)(unsigned)(st & 0xffffffffULL);
   }
 };
 

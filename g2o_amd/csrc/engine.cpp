@@ -491,7 +491,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     };
     auto tile_nz = [&](int sn, int r, int kend) { return tile_fnz(sn, r) < kend; };
     // k_syrk's row tiles: SR rows (64, or 128 for the 128 x 64 tile variants)
-    const int SR = launch::syrk_tile_rows();
+    syrk_var = launch::syrk_variant();  // pinned: chol_syrk launches this tile for these row-tile lists
+    const int SR = launch::syrk_tile_rows(syrk_var);
     auto rows_fnz = [&](int sn, int r) { return SR == TT ? tile_fnz(sn, r) : std::min(tile_fnz(sn, r), tile_fnz(sn, r + TT)); };
     auto rows_nz = [&](int sn, int r, int kend) { return rows_fnz(sn, r) < kend; };
     std::vector<Task> tk;
@@ -901,6 +902,23 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         if (!sn_dl[sn])  // deferred-L21 fronts: copied by their level's own k_xdiag launch
           for (int a = 0; a < sym.sn[sn].ns; a += NB) tk.push_back(Task{sn, a, 0, 0});
     n_xdiag = (int)tk.size() - xdiag_off;
+    if (getenv("G2OHIP_PRINT_OPS")) {  // diagnostics (stderr): the factor's launch list in order, k_syrk with its flops
+      for (size_t k = 0; k < ops.size(); ++k) {
+        const Op& op = ops[k];
+        double fma = 0;
+        int kmin = 1 << 30, kmax = 0;
+        if (op.kind == 3)
+          for (int i = op.off; i < op.off + op.count; ++i) {
+            const Task& t = tk[i];
+            const int K = t.c ? t.c - t.a : sym.sn[t.s].ns - t.a;
+            kmin = std::min(kmin, K);
+            kmax = std::max(kmax, K);
+            fma += (double)SR * TT * std::max(K, 0);
+          }
+        fprintf(stderr, "op %zu kind %d count %d%s", k, op.kind, op.count, op.kind == 3 ? "" : "\n");
+        if (op.kind == 3) fprintf(stderr, " K %d..%d tile_gflop %.4f\n", kmin, kmax, 2 * fma * 1e-9);
+      }
+    }
     tasks.upload(tk.empty() ? std::vector<Task>{Task{0, 0, 0, 0}} : tk, s);
     step_tasks.upload(stk.empty() ? std::vector<launch::StepTask>(1) : stk, s);
     b0front.upload(hb0.empty() ? std::vector<launch::B0Front>(1) : hb0, s);
@@ -1036,7 +1054,7 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       }
       case 11: launch::chol_xdiag(op.count, t, fd.get(), linv.get(), xinv.get(), s); break;
       case 12: launch::chol_l21(op.count, t, fd.get(), fronts.get(), xinv.get(), lbuf.get(), s); break;
-      default: launch::chol_syrk(op.count, t, fd.get(), fronts.get(), lbuf.get(), y_p.get(), vecs.get(), s); break;
+      default: launch::chol_syrk(syrk_var, op.count, t, fd.get(), fronts.get(), lbuf.get(), y_p.get(), vecs.get(), s); break;
     }
   }
   launch::chol_xdiag(n_xdiag, tasks.get() + xdiag_off, fd.get(), linv.get(), xinv.get(), s);
@@ -2116,7 +2134,7 @@ int Engine::kx_batch_size() {
 }
 
 int Engine::build_structure() {  // block_solver.hpp:102-256
-  knob_epoch().fetch_add(1, std::memory_order_relaxed);  // launch-time knobs re-read from here on
+  knob_epoch().fetch_add(1, std::memory_order_acq_rel);  // launch-time knobs re-read from here on
   if (!initialized) {
     int r = initialize();
     if (r) return r;

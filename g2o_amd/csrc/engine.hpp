@@ -109,6 +109,7 @@ struct DeviceCholesky {
   };
   std::vector<BwdLevel> bwd_ops;
   int max_ns = 0;
+  int syrk_var = 4;  // the k_syrk tile variant the task lists were built for (G2OHIP_SYRK_DMA at setup)
   // schedule summary (g2ohip_solver_factor_info): blocked fronts, levels assembled in place / pre-scattered,
   // trailing-update (k_syrk) launches, big-panel backward rounds
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;

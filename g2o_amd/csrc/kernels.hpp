@@ -250,10 +250,10 @@ void chol_step(int ntasks, const StepTask* tasks, const StepHead& head, double* 
                                                                                     // + head's scatter workgroups
 // C -= L(:, ka:kb) L(:, ka:kb)^T over rows/columns >= kb of a front (task: s, a = ka, b = tile, c = kb; c = 0 is
 // the contribution block, K = [0, ns)); columns stop at ns unless kb = ns (then m)
-void chol_syrk(int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf,
+void chol_syrk(int variant, int ntasks, const Task* tasks, const FrontDesc* fd, double* fronts, const double* lbuf,
                const double* ysol, double* vecs, hipStream_t s);
 int syrk_variant();    // the k_syrk tile (G2OHIP_SYRK_DMA)
-int syrk_tile_rows();  // rows per k_syrk tile of that variant (64 or 128): the task lists' row-tile unit
+int syrk_tile_rows(int variant);  // rows per k_syrk tile of a variant (64 or 128): the task lists' row-tile unit
 void chol_l21(int ntasks, const Task* tasks, const FrontDesc* fd, const double* fronts, const double* xinv, double* lbuf,
               hipStream_t s);
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]

@@ -425,3 +425,26 @@ def test_schur_rows_pipe_bitwise(g2o_amd_mod, monkeypatch, name):
     assert np.array_equal(out["0"]["Hschur"], out["1"]["Hschur"])
     assert np.array_equal(out["0"]["bschur"], out["1"]["bschur"])
     assert np.array_equal(out["0"]["x"], out["1"]["x"])
+
+
+def test_syrk_variant_pinned_per_factorization(g2o_amd_mod, monkeypatch):
+    """The k_syrk tile variant is read once, when a factorization builds its row-tile task lists, and kept with them:
+    optimizer A is built with the 128 x 64 tile (G2OHIP_SYRK_DMA=5, row tiles of 128), the knob then changes and optimizer
+    B is built with the 64 x 64 tile (row tiles of 64); A's next solve must still launch the tile its lists were built for
+    (a 64-row tile over 128-row lists would skip half the rows, the reverse would apply rows twice)."""
+    prob = synth.by_name("C3", "small")
+    sched = {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"}
+    for k, v in sched.items():
+        monkeypatch.setenv(k, v)
+    ref = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    r0 = ref.stage(1e-3)
+    monkeypatch.setenv("G2OHIP_SYRK_DMA", "5")
+    a = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    ga = a.stage(1e-3)
+    monkeypatch.setenv("G2OHIP_SYRK_DMA", "4")
+    b = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+    gb = b.stage(1e-3)
+    ga2 = a.stage(1e-3)  # A again, after B's build bumped the knob epoch
+    for g in (ga, gb, ga2):
+        assert g["ok"] == 1
+        assert np.linalg.norm(g["x"] - r0["x"]) <= 1e-9 * np.linalg.norm(r0["x"])

@@ -1072,10 +1072,10 @@ __global__ void __launch_bounds__(256) k_bpd(const StepTask* __restrict__ tasks,
     }
   }
   __syncthreads();
-  // ---- right-looking over the block columns
-#pragma unroll
-  for (int j = 0; j < NBK; ++j) {
-    if (j >= nbk) break;
+  // ---- right-looking over the block columns. The column loop stays rolled: one inlined factor_block (chol32 is
+  //      ~20 KB of straight-line code) instead of NBK copies that the instruction cache cannot hold together
+#pragma unroll 1
+  for (int j = 0; j < nbk; ++j) {
     if (!(j == 0 && pre0)) {
       if (tid < 64)
         factor_block(slot(j, j), kbk(j), vb + NB * j, col, tid, fail, ysol + t.c0 + ka + NB * j, nullptr, yb + NB * j,
@@ -1083,29 +1083,30 @@ __global__ void __launch_bounds__(256) k_bpd(const StepTask* __restrict__ tasks,
       __syncthreads();
     }
     // TRSM: L_ij = A_ij L_jj^-T for every block below (wave w: the 16 x 16 tile (tr, tc) of each)
+    const double* Dj = slot(j, j);
     dx4 acc[NBK > 1 ? NBK - 1 : 1];
 #pragma unroll
-    for (int i = j + 1; i < NBK; ++i) {
-      acc[i - j - 1] = dx4{0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < NBK - 1; ++q) {
+      const int i = j + 1 + q;
+      acc[q] = dx4{0.0, 0.0, 0.0, 0.0};
       if (i >= nbk) continue;
       const double* Ai = slot(i, j);
-      const double* Dj = slot(j, j);
 #pragma unroll
       for (int kk = 0; kk < NB / 4; ++kk) {
         const int k = kk * 4 + lk;
-        acc[i - j - 1] =
-            __builtin_amdgcn_mfma_f64_16x16x4f64(Ai[(16 * tr + lr) * DS + k], Dj[k * DS + 16 * tc + lr], acc[i - j - 1], 0, 0, 0);
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(Ai[(16 * tr + lr) * DS + k], Dj[k * DS + 16 * tc + lr], acc[q], 0, 0, 0);
       }
     }
     __syncthreads();  // every read of the A_ij done
 #pragma unroll
-    for (int i = j + 1; i < NBK; ++i) {
+    for (int q = 0; q < NBK - 1; ++q) {
+      const int i = j + 1 + q;
       if (i >= nbk) continue;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) slot(i, j)[(16 * tr + lk + 4 * q) * DS + 16 * tc + lr] = acc[i - j - 1][q];
+      for (int e = 0; e < 4; ++e) slot(i, j)[(16 * tr + lk + 4 * e) * DS + 16 * tc + lr] = acc[q][e];
     }
     __syncthreads();
-    // rhs of the later blocks, v_i -= L_ij y_j (same wave order as the tiles' v update: one row per thread)
+    // rhs of the later blocks, v_i -= L_ij y_j (one row per thread)
     if (tid < (nbk - 1 - j) * NB) {
       const int i = j + 1 + tid / NB, r = tid & (NB - 1);
       const double* Li = slot(i, j) + r * DS;
@@ -1116,9 +1117,10 @@ __global__ void __launch_bounds__(256) k_bpd(const StepTask* __restrict__ tasks,
     }
     // SYRK: A_ik -= L_ij L_kj^T, j < k <= i (reads column j, writes columns > j)
 #pragma unroll
-    for (int i = j + 1; i < NBK; ++i)
+    for (int qi = 0; qi < NBK - 1; ++qi)
 #pragma unroll
-      for (int k = j + 1; k <= i; ++k) {
+      for (int qk = 0; qk <= qi; ++qk) {
+        const int i = j + 1 + qi, k = j + 1 + qk;
         if (i >= nbk) continue;
         const double* Li = slot(i, j);
         const double* Lk = slot(k, j);
@@ -1130,7 +1132,7 @@ __global__ void __launch_bounds__(256) k_bpd(const StepTask* __restrict__ tasks,
         }
         double* Aik = slot(i, k);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) Aik[(16 * tr + lk + 4 * q) * DS + 16 * tc + lr] -= s4[q];
+        for (int e = 0; e < 4; ++e) Aik[(16 * tr + lk + 4 * e) * DS + 16 * tc + lr] -= s4[e];
       }
     __syncthreads();
   }
@@ -1148,22 +1150,28 @@ __global__ void __launch_bounds__(256) k_bpd(const StepTask* __restrict__ tasks,
     }
   // ---- X_bp = L_bp^-1 in place of the L blocks, column block by column block (X_ij = -L_ii^-1 sum_{k=j}^{i-1} L_ik X_kj;
   //      column j reads L_ik only for k >= j, which later columns never overwrite before they read them)
-#pragma unroll
-  for (int j = 0; j < NBK - 1; ++j)
-#pragma unroll
-    for (int i = j + 1; i < NBK; ++i) {
-      if (i >= nbk) continue;
+#pragma unroll 1
+  for (int j = 0; j < nbk - 1; ++j)
+#pragma unroll 1
+    for (int i = j + 1; i < nbk; ++i) {
       dx4 s4 = {0.0, 0.0, 0.0, 0.0};
+      {  // k = j: X_jj = L_jj^-1, stored transposed in the diagonal slot
+        const double* Lik = slot(i, j);
+        const double* Xk = slot(j, j);
 #pragma unroll
-      for (int k = j; k < i; ++k) {
+        for (int kk = 0; kk < NB / 4; ++kk) {
+          const int c = kk * 4 + lk;
+          s4 = __builtin_amdgcn_mfma_f64_16x16x4f64(Lik[(16 * tr + lr) * DS + c], Xk[(16 * tc + lr) * DS + c], s4, 0, 0, 0);
+        }
+      }
+#pragma unroll 1
+      for (int k = j + 1; k < i; ++k) {  // X_kj (k > j) row-major
         const double* Lik = slot(i, k);
         const double* Xk = slot(k, j);
 #pragma unroll
         for (int kk = 0; kk < NB / 4; ++kk) {
           const int c = kk * 4 + lk;
-          // B(c, n) = X_kj(c, n): X_jj = L_jj^-1 is stored transposed in the diagonal slot, X_kj (k > j) row-major
-          const double b = k == j ? Xk[(16 * tc + lr) * DS + c] : Xk[c * DS + 16 * tc + lr];
-          s4 = __builtin_amdgcn_mfma_f64_16x16x4f64(Lik[(16 * tr + lr) * DS + c], b, s4, 0, 0, 0);
+          s4 = __builtin_amdgcn_mfma_f64_16x16x4f64(Lik[(16 * tr + lr) * DS + c], Xk[c * DS + 16 * tc + lr], s4, 0, 0, 0);
         }
       }
       __syncthreads();  // every read of L_ij done

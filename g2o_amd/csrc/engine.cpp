@@ -553,6 +553,8 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const int bpd_min = bpm ? atoi(bpm) : 0;
     std::vector<unsigned char> sn_bpd(sym.sn.size(), 0);
     n_bpd_fronts = 0;
+    const char* cbk = getenv("G2OHIP_EA_CB_ZERO");  // dev A/B: 1 = in-place assembly also zeroes childless fronts' CBs
+    const bool cb_keep = cbk && atoi(cbk) == 1;
     const char* eb = getenv("G2OHIP_EA_BIG");
     const int ea_big = eb ? atoi(eb) : 1024;  // C3 factor 28.29 (2048) -> 27.71 ms (1024), 28.31 (512)
     const char* pm = getenv("G2OHIP_CHOL_PRE_MAX");  // dev A/B: largest level (bytes) pre-scattered
@@ -631,8 +633,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
         const int m = q.ns + q.nr;
-        if (pre && sym.children_ptr[sn + 1] == sym.children_ptr[sn]) continue;  // nothing left to assemble
-        for (int a = 0; a < m; a += slab) tk.push_back(Task{sn, a, std::min(a + slab, m), 2 + a / slab});
+        const bool childless = sym.children_ptr[sn + 1] == sym.children_ptr[sn];
+        if (pre && childless) continue;  // nothing left to assemble
+        // a childless front's contribution block is written (not read) by its level's separate k_syrk pass
+        // (overwrite): its own columns only (the pre-scattered levels skip those zeros the same way)
+        const int mcols = childless && !fused_contrib && !cb_keep ? q.ns : m;
+        for (int a = 0; a < mcols; a += slab) tk.push_back(Task{sn, a, std::min(a + slab, mcols), 2 + a / slab});
       }
       ea.count = (int)tk.size() - ea.off;
       ops.push_back(ea);

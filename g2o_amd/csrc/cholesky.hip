@@ -999,244 +999,6 @@ __global__ void __launch_bounds__(256) k_l21(const Task* __restrict__ tasks, con
                   0, kb, sh, 2);
 }
 
-// ---------------------------------------------------------------------------- big-panel diagonal blocks (BPD)
-// Blocked fronts (DeviceCholesky::setup, G2OHIP_BPD): a big panel [ka, ka + pb), pb <= 32 NBK, is factored by two
-// launches instead of pb / 32 panel steps:
-//  * k_bpd, one workgroup per (front, big panel): the whole pb x pb diagonal block in LDS (its lower 32 x 32 blocks,
-//    row stride DS). Per block column j: factor_block on wave 0 (L_jj^-1 -> linv, y_j -> ysol, exactly as a panel
-//    step's diagonal task), then with the four waves on v_mfma_f64_16x16x4f64 the TRSM of the blocks below it,
-//    L_ij = A_ij L_jj^-T, the rhs of the later blocks v_i -= L_ij y_j and the SYRK A_ik -= L_ij L_kj^T (j < k <= i).
-//    Then X_bp = L_bp^-1 (the big panel's diagonal block of X = L11^-1, in place of the L blocks once those are
-//    stored), and z = X_bp^T y_bp, written into the front-vector rows [ka, ka + pb) (their rhs is consumed).
-//    Block 0 of a front's first big panel was factored by the extend-add's block-0 task: its L^-1 and y come from
-//    linv / ysol (task flag 1).
-//  * k_bpl21, one workgroup per (64-row tile below the big panel, 64-column tile of it): L21 = A21 X_bp^T (the deferred
-//    L21 product of k_l21, restricted to the big panel), and on the tile whose K range is the whole panel the forward
-//    solve's update of the rows below, v2 -= L21 y_bp = A21 z.
-// The trailing update of the supernode's later columns stays the k_syrk pass (K = the big panel). Against the panel
-// steps: one kernel boundary per big panel on the diagonal chain instead of pb / 32, and the rows below are read and
-// written once (TRSM as one product with X_bp) instead of once per 32-column step.
-template <int NBK>
-__global__ void __launch_bounds__(256) k_bpd(const StepTask* __restrict__ tasks, double* __restrict__ fronts,
-                                             double* __restrict__ lbuf, double* __restrict__ vecs,
-                                             double* __restrict__ ysol, double* __restrict__ linv,
-                                             double* __restrict__ xinv, int* __restrict__ fail) {
-  constexpr int NSLOT = NBK * (NBK + 1) / 2, BS = NB * DS;
-  __shared__ double A[NSLOT * BS];
-  __shared__ __attribute__((aligned(16))) double col[4 * NB];
-  __shared__ double vb[NBK * NB], yb[NBK * NB];
-  const StepTask t = tasks[blockIdx.x];
-  const int m = t.m, ns = t.ns, ka = t.k0kb & 0xffff, pb = t.k0kb >> 16;
-  const bool pre0 = t.flags & 1;
-  const int nbk = (pb + NB - 1) / NB;
-  double* F = fronts + t.f_off;
-  double* L = lbuf + t.l_off;
-  double* v = vecs + t.v_off;
-  double* Xf = xinv + t.x_off;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lk = lane >> 4;
-  const int tr = w & 1, tc = w >> 1;
-  auto slot = [&](int i, int j) { return A + (i * (i + 1) / 2 + j) * BS; };
-  auto kbk = [&](int i) { return min(NB, pb - NB * i); };
-  // ---- load every lower block of the diagonal block (entries past pb as zeros; block (0, 0) of a pre-factored panel
-  //      as its L^-1, transposed as factor_block leaves it: D[c DS + i] = L^-1(i, c)), the rhs rows and y_0
-  {
-    double av[NSLOT][4];
-#pragma unroll
-    for (int i = 0; i < NBK; ++i)
-#pragma unroll
-      for (int j = 0; j <= i; ++j)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = tid + 256 * u, r = e & (NB - 1), c = e >> 5;
-          const bool p0 = pre0 && i == 0 && j == 0;
-          const bool ok = NB * i + r < pb && NB * j + c < pb && (i > j || r >= c);
-          av[i * (i + 1) / 2 + j][u] = p0 ? linv[(size_t)(t.c0 + ka) * (NB * NB) + e]  // row-major L^-1(c, r)
-                                          : ld0(F, (ka + NB * j + c) * m + ka + NB * i + r, ok);
-        }
-    const double vv = ld0(v, ka + tid, tid < pb);
-    const double y0 = ld0(ysol, t.c0 + ka + tid, pre0 && tid < kbk(0));
-#pragma unroll
-    for (int i = 0; i < NBK; ++i)
-#pragma unroll
-      for (int j = 0; j <= i; ++j)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = tid + 256 * u, r = e & (NB - 1), c = e >> 5;
-          // pre-factored block 0: e = c' * 32 + r' indexes L^-1(c', r') row-major, stored at D[r' DS + c']
-          if (pre0 && i == 0 && j == 0) slot(0, 0)[r * DS + c] = av[0][u];
-          else slot(i, j)[r * DS + c] = av[i * (i + 1) / 2 + j][u];
-        }
-    if (tid < NBK * NB) {
-      vb[tid] = vv;
-      yb[tid] = y0;
-    }
-  }
-  __syncthreads();
-  // ---- right-looking over the block columns. The column loop stays rolled: one inlined factor_block (chol32 is
-  //      ~20 KB of straight-line code) instead of NBK copies that the instruction cache cannot hold together
-#pragma unroll 1
-  for (int j = 0; j < nbk; ++j) {
-    if (!(j == 0 && pre0)) {
-      if (tid < 64)
-        factor_block(slot(j, j), kbk(j), vb + NB * j, col, tid, fail, ysol + t.c0 + ka + NB * j, nullptr, yb + NB * j,
-                     linv + (size_t)(t.c0 + ka + NB * j) * (NB * NB));
-      __syncthreads();
-    }
-    // TRSM: L_ij = A_ij L_jj^-T for every block below (wave w: the 16 x 16 tile (tr, tc) of each)
-    const double* Dj = slot(j, j);
-    dx4 acc[NBK > 1 ? NBK - 1 : 1];
-#pragma unroll
-    for (int q = 0; q < NBK - 1; ++q) {
-      const int i = j + 1 + q;
-      acc[q] = dx4{0.0, 0.0, 0.0, 0.0};
-      if (i >= nbk) continue;
-      const double* Ai = slot(i, j);
-#pragma unroll
-      for (int kk = 0; kk < NB / 4; ++kk) {
-        const int k = kk * 4 + lk;
-        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(Ai[(16 * tr + lr) * DS + k], Dj[k * DS + 16 * tc + lr], acc[q], 0, 0, 0);
-      }
-    }
-    __syncthreads();  // every read of the A_ij done
-#pragma unroll
-    for (int q = 0; q < NBK - 1; ++q) {
-      const int i = j + 1 + q;
-      if (i >= nbk) continue;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) slot(i, j)[(16 * tr + lk + 4 * e) * DS + 16 * tc + lr] = acc[q][e];
-    }
-    __syncthreads();
-    // rhs of the later blocks, v_i -= L_ij y_j (one row per thread)
-    if (tid < (nbk - 1 - j) * NB) {
-      const int i = j + 1 + tid / NB, r = tid & (NB - 1);
-      const double* Li = slot(i, j) + r * DS;
-      double s = 0.0;
-#pragma unroll
-      for (int c = 0; c < NB; ++c) s += Li[c] * yb[NB * j + c];
-      vb[NB * i + r] -= s;
-    }
-    // SYRK: A_ik -= L_ij L_kj^T, j < k <= i (reads column j, writes columns > j)
-#pragma unroll
-    for (int qi = 0; qi < NBK - 1; ++qi)
-#pragma unroll
-      for (int qk = 0; qk <= qi; ++qk) {
-        const int i = j + 1 + qi, k = j + 1 + qk;
-        if (i >= nbk) continue;
-        const double* Li = slot(i, j);
-        const double* Lk = slot(k, j);
-        dx4 s4 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < NB / 4; ++kk) {
-          const int c = kk * 4 + lk;
-          s4 = __builtin_amdgcn_mfma_f64_16x16x4f64(Li[(16 * tr + lr) * DS + c], Lk[(16 * tc + lr) * DS + c], s4, 0, 0, 0);
-        }
-        double* Aik = slot(i, k);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) Aik[(16 * tr + lk + 4 * e) * DS + 16 * tc + lr] -= s4[e];
-      }
-    __syncthreads();
-  }
-  // ---- the L blocks below the diagonal blocks -> lbuf (coalesced columns)
-#pragma unroll
-  for (int i = 1; i < NBK; ++i)
-#pragma unroll
-    for (int j = 0; j < i; ++j) {
-      if (i >= nbk) continue;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = tid + 256 * u, r = e & (NB - 1), c = e >> 5;
-        if (r < kbk(i) && c < kbk(j)) L[(size_t)(ka + NB * j + c) * m + ka + NB * i + r] = slot(i, j)[r * DS + c];
-      }
-    }
-  // ---- X_bp = L_bp^-1 in place of the L blocks, column block by column block (X_ij = -L_ii^-1 sum_{k=j}^{i-1} L_ik X_kj;
-  //      column j reads L_ik only for k >= j, which later columns never overwrite before they read them)
-#pragma unroll 1
-  for (int j = 0; j < nbk - 1; ++j)
-#pragma unroll 1
-    for (int i = j + 1; i < nbk; ++i) {
-      dx4 s4 = {0.0, 0.0, 0.0, 0.0};
-      {  // k = j: X_jj = L_jj^-1, stored transposed in the diagonal slot
-        const double* Lik = slot(i, j);
-        const double* Xk = slot(j, j);
-#pragma unroll
-        for (int kk = 0; kk < NB / 4; ++kk) {
-          const int c = kk * 4 + lk;
-          s4 = __builtin_amdgcn_mfma_f64_16x16x4f64(Lik[(16 * tr + lr) * DS + c], Xk[(16 * tc + lr) * DS + c], s4, 0, 0, 0);
-        }
-      }
-#pragma unroll 1
-      for (int k = j + 1; k < i; ++k) {  // X_kj (k > j) row-major
-        const double* Lik = slot(i, k);
-        const double* Xk = slot(k, j);
-#pragma unroll
-        for (int kk = 0; kk < NB / 4; ++kk) {
-          const int c = kk * 4 + lk;
-          s4 = __builtin_amdgcn_mfma_f64_16x16x4f64(Lik[(16 * tr + lr) * DS + c], Xk[c * DS + 16 * tc + lr], s4, 0, 0, 0);
-        }
-      }
-      __syncthreads();  // every read of L_ij done
-      double* Wij = slot(i, j);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Wij[(16 * tr + lk + 4 * q) * DS + 16 * tc + lr] = s4[q];
-      __syncthreads();
-      const double* Di = slot(i, i);  // L_ii^-1 transposed: L_ii^-1(r, c) = Di[c DS + r]
-      dx4 x4 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int kk = 0; kk < NB / 4; ++kk) {
-        const int c = kk * 4 + lk;
-        x4 = __builtin_amdgcn_mfma_f64_16x16x4f64(Di[c * DS + 16 * tr + lr], Wij[c * DS + 16 * tc + lr], x4, 0, 0, 0);
-      }
-      __syncthreads();  // every read of W done
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Wij[(16 * tr + lk + 4 * q) * DS + 16 * tc + lr] = -x4[q];
-      __syncthreads();
-    }
-  // ---- X_bp -> X (the whole pb x pb block, zeros above the diagonal: k_bpl21 reads full 64 x 64 tiles of it), and
-  //      z = X_bp^T y -> v[ka, ka + pb)
-#pragma unroll
-  for (int i = 0; i < NBK; ++i)
-#pragma unroll
-    for (int j = 0; j < NBK; ++j) {
-      if (i >= nbk || j >= nbk) continue;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = tid + 256 * u, r = e & (NB - 1), c = e >> 5;
-        double x = 0.0;
-        if (i > j) x = slot(i, j)[r * DS + c];
-        else if (i == j) x = slot(j, j)[c * DS + r];
-        if (r < kbk(i) && c < kbk(j)) Xf[(size_t)(ka + NB * j + c) * ns + ka + NB * i + r] = x;
-      }
-    }
-  if (tid < pb) {
-    const int jb = tid / NB, cc = tid & (NB - 1);
-    double z = 0.0;
-#pragma unroll
-    for (int i = 0; i < NBK; ++i) {
-      if (i < jb || i >= nbk) continue;
-      const double* S = slot(i, jb);
-#pragma unroll 8
-      for (int r = 0; r < NB; ++r) z += (i == jb ? S[cc * DS + r] : S[r * DS + cc]) * yb[NB * i + r];
-    }
-    v[ka + tid] = z;
-  }
-}
-
-__global__ void __launch_bounds__(256) k_bpl21(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                               const double* __restrict__ fronts, const double* __restrict__ xinv,
-                                               double* __restrict__ lbuf, double* vecs) {
-  __shared__ __attribute__((aligned(16))) double sh[L21Tile::LDS_DOUBLES];
-  const Task t = tasks[blockIdx.x];
-  const FrontDesc me = fd[t.s];
-  const int m = me.ns + me.nr, ns = me.ns, ka = t.a, pb = t.c;
-  const int ti = t.b & 0xffff, tj = t.b >> 16;
-  const int I0 = ka + pb + ti * TT, J0 = tj * TT, kb = min(pb, J0 + TT);  // X_bp(j, k) = 0 for k > j
-  double* v = vecs + me.vec_off;
-  const bool vupd = kb == pb;  // the tile whose K range is the whole big panel: v2 -= A21 z (z in v[ka, ka + pb))
-  L21Tile::run_ab(fronts + me.front_off + (size_t)ka * m, m, m, xinv + me.x_off + (size_t)ka * ns + ka, ns, pb,
-                  lbuf + me.l_off + (size_t)ka * m, m, m, pb, I0, J0, 0, kb, sh, 2, vupd ? v + ka : nullptr,
-                  vupd ? v : nullptr);
-}
-
 __global__ void k_permute(int n, const int* __restrict__ perm, const double* __restrict__ in, double* __restrict__ out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) out[k] = in[perm[k]];
@@ -1488,23 +1250,6 @@ void chol_l21(int ntasks, const Task* tasks, const FrontDesc* fd, const double* 
               hipStream_t s) {
   if (ntasks <= 0) return;
   hipLaunchKernelGGL(k_l21, ntasks, 256, 0, s, tasks, fd, fronts, xinv, lbuf);
-  KERNEL_CHECK();
-}
-void chol_bpd(int nbk, int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
-              double* linv, double* xinv, int* fail, hipStream_t s) {
-  if (ntasks <= 0) return;
-  switch (nbk) {
-    case 2: hipLaunchKernelGGL(k_bpd<2>, ntasks, 256, 0, s, tasks, fronts, lbuf, vecs, ysol, linv, xinv, fail); break;
-    case 3: hipLaunchKernelGGL(k_bpd<3>, ntasks, 256, 0, s, tasks, fronts, lbuf, vecs, ysol, linv, xinv, fail); break;
-    case 4: hipLaunchKernelGGL(k_bpd<4>, ntasks, 256, 0, s, tasks, fronts, lbuf, vecs, ysol, linv, xinv, fail); break;
-    default: throw DeviceError("chol_bpd: big panels of 2, 3 or 4 blocks of 32 columns");
-  }
-  KERNEL_CHECK();
-}
-void chol_bpl21(int ntasks, const Task* tasks, const FrontDesc* fd, const double* fronts, const double* xinv, double* lbuf,
-                double* vecs, hipStream_t s) {
-  if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_bpl21, ntasks, 256, 0, s, tasks, fd, fronts, xinv, lbuf, vecs);
   KERNEL_CHECK();
 }
 // G2OHIP_SYRK_DMA (dev A/B): 1-4 the 64 x 64 LDS-DMA tiles below, 5 / 6 a 128 x 64 tile (K chunks 16 x 2 / 8 x 3

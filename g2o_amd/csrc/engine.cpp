@@ -541,18 +541,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const int dl_min = dlm ? atoi(dlm) : 16;
     std::vector<unsigned char> sn_dl(sym.sn.size(), 0);
     n_deferred_l21 = 0;
-    // big-panel diagonal blocks (k_bpd + k_bpl21, cholesky.hip) for the blocked fronts: a big panel of bpd_pb columns
-    // factored in one workgroup's LDS and its rows below in one GEMM pass, instead of one panel step per 32 columns
-    // (G2OHIP_BPD: 0 off, 1 blocked fronts; G2OHIP_BPD_PB: 64 / 96 / 128; G2OHIP_BPD_MIN > 0: also every dense front of a
-    // level with a separate contribution pass whose supernode is wider than that)
-    const char* bpv = getenv("G2OHIP_BPD");
-    const bool bpd_on = bpv ? atoi(bpv) != 0 : false;
-    const char* bpp = getenv("G2OHIP_BPD_PB");
-    const int bpd_pb = bpp ? std::max(64, std::min(128, atoi(bpp) / NB * NB)) : 128;
-    const char* bpm = getenv("G2OHIP_BPD_MIN");
-    const int bpd_min = bpm ? atoi(bpm) : 0;
-    std::vector<unsigned char> sn_bpd(sym.sn.size(), 0);
-    n_bpd_fronts = 0;
     const char* cbk = getenv("G2OHIP_EA_CB_ZERO");  // dev A/B: 1 = in-place assembly also zeroes childless fronts' CBs
     const bool cb_keep = cbk && atoi(cbk) == 1;
     const char* eb = getenv("G2OHIP_EA_BIG");
@@ -674,34 +662,19 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       const bool dl_level = dl_mode != 0 && !fused_contrib && !distributed() && (dl_mode == 2 || (int)lv.size() >= dl_min);
       for (int sn : lv) {
         const Supernode& q = sym.sn[sn];
-        sn_bpd[sn] = bpd_on && !fused_contrib && q.env_off < 0 && q.ns > NB &&
-                     (blocked(q) || (bpd_min > 0 && q.ns > bpd_min)) ? 1 : 0;
-        n_bpd_fronts += sn_bpd[sn];
-        if (sn_bpd[sn]) sn_pb[sn] = bpd_pb;  // backward solve in big-panel rounds (X holds the diagonal big-panel blocks)
-        sn_dl[sn] = dl_level && !blocked(q) && !sn_bpd[sn] && q.nr > 0 && q.env_off < 0 ? 1 : 0;
+        sn_dl[sn] = dl_level && !blocked(q) && q.nr > 0 && q.env_off < 0 ? 1 : 0;
         n_deferred_l21 += sn_dl[sn];
       }
       for (int p = 0; p < maxp; ++p) {
+        Op st{2, (int)stk.size(), 0};
         // task order inside the launch (= dispatch order): every front's next-diagonal task first (the
         // critical chain must start at once, on a CU of its own), then the tile tasks, then the
         // inverse tasks (X = L11^-1 for the backward solve), which have the most slack
-        std::vector<launch::StepTask> diag_t, tile_t, inv_t, bpd_t;
-        std::vector<Task> bl21_t;
+        std::vector<launch::StepTask> diag_t, tile_t, inv_t;
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
           const int k0 = p * NB;
           if (k0 >= q.ns) continue;
-          if (sn_bpd[sn]) {  // big-panel front: k_bpd + k_bpl21 at the start of each big panel, no panel steps
-            if (k0 % bpd_pb) continue;
-            const int pbw = std::min(bpd_pb, q.ns - k0), m = q.ns + q.nr, rb = k0 + pbw;
-            // block 0 of the first big panel was factored by the extend-add's block-0 task (flag 1)
-            bpd_t.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns,
-                                             q.c0, k0 | (pbw << 16), 0, k0 == 0 ? 1 : 0, q.ns});
-            const int T = (m - rb + TT - 1) / TT, TJ = (pbw + TT - 1) / TT;
-            for (int ti = 0; ti < T; ++ti)
-              for (int tj = 0; tj < TJ; ++tj) bl21_t.push_back(Task{sn, k0, ti | (tj << 16), pbw});
-            continue;
-          }
           const int kb = std::min(NB, q.ns - k0), r0 = k0 + kb, m = q.ns + q.nr;
           const bool blk = blocked(q);
           const int pend = blk ? std::min((k0 / lpb + 1) * lpb, q.ns) : q.ns;  // big-panel end
@@ -744,16 +717,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           for (int bp = p; bp < ib1 && p - 1 >= ib0 && !dev_noinv; ++bp)
             for (int j = ib0; j < p; ++j) inv_t.push_back(mk(j | (bp << 16), 16));
         }
-        if (!bpd_t.empty()) {
-          Op bd{13, (int)stk.size(), (int)bpd_t.size()};
-          bd.nb0 = bpd_pb / NB;
-          stk.insert(stk.end(), bpd_t.begin(), bpd_t.end());
-          ops.push_back(bd);
-          Op bl{14, (int)tk.size(), (int)bl21_t.size()};
-          tk.insert(tk.end(), bl21_t.begin(), bl21_t.end());
-          if (bl.count) ops.push_back(bl);
-        }
-        Op st{2, (int)stk.size(), 0};
         stk.insert(stk.end(), diag_t.begin(), diag_t.end());
         if (!dev_diagonly) stk.insert(stk.end(), tile_t.begin(), tile_t.end());
         if (!dev_diagonly) stk.insert(stk.end(), inv_t.begin(), inv_t.end());
@@ -761,25 +724,20 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         for (int k = st.off; k < st.off + st.count; ++k)
           if (stk[k].flags & 64) st.kind = 6;
         if (st.count) { ops.push_back(st); }
-        // end of a big panel: trailing update of the blocked fronts, then their next first blocks (big-panel fronts:
-        // their next k_bpd factors it)
+        if ((p + 1) * NB % lpb) continue;
+        // end of a big panel: trailing update of the blocked fronts, then their next first blocks
         Op gm{3, (int)tk.size(), 0};
         Op d0{2, (int)stk.size(), 0};
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
-          const bool bpf = sn_bpd[sn];
-          if (!blocked(q) && !bpf) continue;
-          const int pbw = bpf ? bpd_pb : lpb;
-          if ((p + 1) * NB % pbw) continue;
-          const int kb = (p + 1) * NB, ka = kb - pbw, m = q.ns + q.nr;
-          if (kb >= q.ns) continue;
+          const int kb = (p + 1) * NB, ka = kb - lpb, m = q.ns + q.nr;
+          if (!blocked(q) || kb >= q.ns) continue;
           const int T = (m - kb + SR - 1) / SR, TJ = (q.ns - kb + TT - 1) / TT;
           for (int tj = 0; tj < TJ; ++tj) {
             if (!tile_nz(sn, kb + TT * tj, kb)) continue;
             for (int ti = TT * tj / SR; ti < T; ++ti)
               if (rows_nz(sn, kb + SR * ti, kb)) tk.push_back(Task{sn, ka, ti | (tj << 16), kb});
           }
-          if (bpf) continue;
           stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns,
                                          q.c0, kb, 0, 4, q.ns});
         }
@@ -1102,11 +1060,6 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       }
       case 11: launch::chol_xdiag(op.count, t, fd.get(), linv.get(), xinv.get(), s); break;
       case 12: launch::chol_l21(op.count, t, fd.get(), fronts.get(), xinv.get(), lbuf.get(), s); break;
-      case 13:
-        launch::chol_bpd(op.nb0, op.count, step_tasks.get() + op.off, fronts.get(), lbuf.get(), vecs.get(), y_p.get(),
-                         linv.get(), xinv.get(), fail, s);
-        break;
-      case 14: launch::chol_bpl21(op.count, t, fd.get(), fronts.get(), xinv.get(), lbuf.get(), vecs.get(), s); break;
       default: launch::chol_syrk(syrk_var, op.count, t, fd.get(), fronts.get(), lbuf.get(), y_p.get(), vecs.get(), s); break;
     }
   }

@@ -114,7 +114,6 @@ struct DeviceCholesky {
   // trailing-update (k_syrk) launches, big-panel backward rounds
   int n_blocked = 0, n_inplace_levels = 0, n_pre_levels = 0, n_syrk_ops = 0, n_bwd_rounds = 0;
   int n_deferred_l21 = 0;  // fronts whose L21 comes from the k_l21 GEMM after their panel steps
-  int n_bpd_fronts = 0;    // fronts whose big panels are factored by k_bpd + k_bpl21
   struct Op { int kind, off, count; long long sc0 = 0, sc1 = 0; int b0 = 0, nb0 = 0; };  // b0/nb0: extend-add block-0 records  // sc: deferred scatter range (extend-add ops)  // kind 0 extend-add (pre-scattered level), 4 / 5 assembly + extend-add,
                                         // 2 panel step (6: with lagged-pair tasks), 3 syrk, 8 root exchange
   // ---- distributed factorization (landmark-sharded BA). Set dist_rank / dist_nranks / allreduce before

@@ -254,12 +254,6 @@ void chol_syrk(int variant, int ntasks, const Task* tasks, const FrontDesc* fd, 
                const double* ysol, double* vecs, hipStream_t s);
 int syrk_variant();    // the k_syrk tile (G2OHIP_SYRK_DMA)
 int syrk_tile_rows(int variant);  // rows per k_syrk tile of a variant (64 or 128): the task lists' row-tile unit
-// big-panel diagonal blocks (blocked fronts, G2OHIP_BPD): k_bpd<nbk> factors a front's pb x pb diagonal block of a big
-// panel (nbk = 2..4 blocks of 32) and forms X_bp, k_bpl21 the rows below (L21 = A21 X_bp^T, v2 -= A21 z)
-void chol_bpd(int nbk, int ntasks, const StepTask* tasks, double* fronts, double* lbuf, double* vecs, double* ysol,
-              double* linv, double* xinv, int* fail, hipStream_t s);
-void chol_bpl21(int ntasks, const Task* tasks, const FrontDesc* fd, const double* fronts, const double* xinv, double* lbuf,
-                double* vecs, hipStream_t s);
 void chol_l21(int ntasks, const Task* tasks, const FrontDesc* fd, const double* fronts, const double* xinv, double* lbuf,
               hipStream_t s);
 void chol_permute(int n, const int* perm, const double* in, double* out, hipStream_t s);   // out[k] = in[perm[k]]

@@ -95,9 +95,7 @@ def test_marginals_many_batches(g2o_amd_mod, oracle):
     {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
     {"G2OHIP_CHOL_LAG": "2"},
     {"G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_LAG": "1"},
-    {"G2OHIP_BPD": "1", "G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64",
-     "G2OHIP_CHOL_WIDE_PB": "64"},
-], ids=["blocked_fronts", "lagged_all_levels", "lagged_separate_contrib", "big_panel_blocks"])
+], ids=["blocked_fronts", "lagged_all_levels", "lagged_separate_contrib"])
 @pytest.mark.parametrize("name", ["C1", "C3"])
 def test_marginals_blocked_and_lagged_schedules(g2o_amd_mod, oracle, monkeypatch, knobs, name):
     """The marginal solves read the factor's layout (L21 per front, L_kk^-1 per panel, no stored diagonal blocks).

@@ -348,14 +348,8 @@ SCHEDULES = {
     "band_leaves": {"G2OHIP_BAND_LEAF": "24"},
     "band_leaves_blocked": {"G2OHIP_BAND_LEAF": "24", "G2OHIP_CHOL_FUSED_MAX": "0", "G2OHIP_CHOL_BLOCK_MIN": "64",
                             "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
-    # big-panel diagonal blocks (k_bpd + k_bpl21) for the blocked fronts: 128-, 96- and 64-column big panels, and on
-    # every dense front wider than 32 columns of the levels with a separate contribution pass
-    "bpd_blocked_128": {"G2OHIP_BPD": "1", "G2OHIP_BPD_PB": "128", "G2OHIP_CHOL_FUSED_MAX": "0",
-                        "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
-    "bpd_blocked_96": {"G2OHIP_BPD": "1", "G2OHIP_BPD_PB": "96", "G2OHIP_CHOL_FUSED_MAX": "0",
-                       "G2OHIP_CHOL_BLOCK_MIN": "64", "G2OHIP_CHOL_PB": "64", "G2OHIP_CHOL_WIDE_PB": "64"},
-    "bpd_all_64": {"G2OHIP_BPD": "1", "G2OHIP_BPD_PB": "64", "G2OHIP_BPD_MIN": "32", "G2OHIP_CHOL_FUSED_MAX": "0"},
-    "bpd_all_128": {"G2OHIP_BPD": "1", "G2OHIP_BPD_PB": "128", "G2OHIP_BPD_MIN": "32", "G2OHIP_CHOL_FUSED_MAX": "0"},
+    # the in-place assembly zeroing childless fronts' contribution blocks too (default: their k_syrk pass writes them)
+    "assembly_cb_zeroed": {"G2OHIP_EA_CB_ZERO": "1"},
     # every input entry scattered before the first level (default: later levels' entries ride in earlier launches)
     "scatter_up_front": {"G2OHIP_SCATTER_DEFER": "0"},
     # no small leaf absorption in the symbolic analysis (the r03 tree shapes)

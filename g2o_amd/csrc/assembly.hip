@@ -64,12 +64,13 @@ __device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err
 }
 // the same with the edge's vertex indices given: a caller that reads them ahead (software pipeline) starts the state
 // loads without a dependent index load (FamilyBA)
-template <class F>
+template <class F, bool NT = false>
 __device__ __forceinline__ void edge_terms_at(const EdgeData& d, int e, int v0, int v1, double* err, double* A, double* B,
                                               double* Om) {
   constexpr int D = F::D;
   double pc[3];
-  F::linearize_at(d, e, v0, v1, err, A, B, pc);
+  if constexpr (NT) F::template linearize_at<true>(d, e, v0, v1, err, A, B, pc);
+  else F::linearize_at(d, e, v0, v1, err, A, B, pc);
   load_info<D>(info_rec(d, e, F::INFO), Om);
   if (d.rk) {
     double chi = 0;
@@ -416,7 +417,8 @@ __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restri
 // re-linearising the edge: with B = diag(f) Bt(u, v, w) and Kt = diag(f) W,
 //   B^T (Omega - W W^T) B = Bt^T (F Omega F - Kt Kt^T) Bt,   B^T (omega_r - W c_l) = Bt^T (F omega_r - Kt c_l),
 // the error from (u, v) = (x/z, y/z) exactly as the projection computes it (robust weight from its chi2).
-template <class F, bool FG, bool KX = false>
+// NT (recomputing path): the per-observation streams (vertex indices, measurements) are read nontemporally
+template <class F, bool FG, bool KX = false, bool NT = false>
 __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* __restrict__ cm_ptr, int npose,
                                                       double* __restrict__ Hpp, double* __restrict__ bvec,
                                                       int num_poses, int lm_begin, launch::SchurSplit sp) {
@@ -498,13 +500,14 @@ __global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* 
     if constexpr (FG) hl = hla;
     {  // the next observations' indices (two ahead: streaming; one ahead: the Hessian index of a loaded vertex)
       const int pn = p + 512 < p1 ? p + 512 : 0;
-      const int v0c = d.v0[pn], v1c = d.v1[pn];
+      const int v0c = NT ? __builtin_nontemporal_load(d.v0 + pn) : d.v0[pn];
+      const int v1c = NT ? __builtin_nontemporal_load(d.v1 + pn) : d.v1[pn];
       if constexpr (FG) hla = sp.hl[v0b];
       v0a = v0b; v1a = v1b;
       v0b = v0c; v1b = v1c;
     }
     double err[D], A[D * DA], B[D * DB], Om[D * D];
-    edge_terms_at<F>(d, p, v0, v1, err, A, B, Om);
+    edge_terms_at<F, NT>(d, p, v0, v1, err, A, B, Om);
     double wr[D];
 #pragma unroll
     for (int r = 0; r < D; ++r) {
@@ -760,6 +763,11 @@ void backsub_j(const EdgeArgs& a, int nl, const int2* erng, const int* hcam, con
   KERNEL_CHECK();
 }
 
+// G2OHIP_CAM_NT (A/B): the recomputing camera pass with nontemporal per-observation streams
+static bool cam_nt() {
+  static EnvKnob k{"G2OHIP_CAM_NT", 0};
+  return k.get() != 0;
+}
 void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, int num_poses, int lm_begin,
                   const SchurSplit* sp, hipStream_t s) {
   if (npose <= 0) return;
@@ -768,6 +776,9 @@ void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, 
   if (sp && sp->kx && sp->cm_hpl)
     hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
                        lm_begin, z);
+  else if (sp && cam_nt())
+    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true, false, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b,
+                       num_poses, lm_begin, z);
   else if (sp)
     hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
                        lm_begin, z);

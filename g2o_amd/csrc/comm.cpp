@@ -170,6 +170,16 @@ struct LocalComm : Comm {
   void allgather(double* p, size_t count, hipStream_t s) override { reduce(p, count * g->nranks, s, OP_AG); }
 };
 
+// Timing-only transport (tools/dist_rank_times.py): one engine plays rank r of N alone, every collective a no-op. The
+// engine then runs exactly the kernels rank r would (its landmark shard, the global Schur pattern, its subtrees and the
+// shared top of the distributed factorization) on one GPU; its sums are partial, so its results are not meaningful.
+struct SoloComm : Comm {
+  void allreduce_sum(double*, size_t, hipStream_t) override { ++seq; }
+  void allreduce_max(double*, size_t, hipStream_t) override { ++seq; }
+  void reduce_scatter_sum(double*, size_t, hipStream_t) override { ++seq; }
+  void allgather(double*, size_t, hipStream_t) override { ++seq; }
+};
+
 }  // namespace
 
 Comm* make_rccl_comm(const unsigned char* uid128, int rank, int nranks, std::string& err) {
@@ -192,6 +202,7 @@ Comm* make_rccl_comm(const unsigned char* uid128, int rank, int nranks, std::str
 }
 
 Comm* make_local_comm(const std::string& key, int rank, int nranks) {
+  if (key.rfind("solo:", 0) == 0) return new SoloComm();  // timing only: no other rank exists
   auto* c = new LocalComm();
   c->g = group_for(key, nranks);
   c->rank = rank;

@@ -7,6 +7,8 @@
 //   LocalComm  test transport: N engines driven by N host threads of ONE process on one GPU;
 //              host-staged, summed in rank order. Lets the sharding logic run under pytest on
 //              a single-GPU box; never selected by the product path.
+//   SoloComm   timing transport (key "solo:..."): one engine plays rank r of N alone, every collective a no-op
+//              (tools/dist_rank_times.py); its results are not meaningful.
 //
 // Every collective carries a per-communicator call number. LocalComm always checks that all ranks
 // entered the same call (number, length, operation) and throws DeviceError on every rank otherwise (a

@@ -360,7 +360,9 @@ struct FamilyBA {
   DI static void linearize(const EdgeData& d, int e, double* err, double* A, double* B, double* pc) {
     linearize_at(d, e, d.v0[e], d.v1[e], err, A, B, pc);
   }
-  // the same with the edge's vertex indices given (a caller that prefetched them: no dependent index load)
+  // the same with the edge's vertex indices given (a caller that prefetched them: no dependent index load); NT: the
+  // measurement (streamed once per pass) is read nontemporally, so it does not push the reused landmark lines out of L2
+  template <bool NT = false>
   DI static void linearize_at(const EdgeData& d, int e, int v0, int v1, double* err, double* A, double* B, double* pc) {
     const double* c = d.s1 + (size_t)v1 * 8;
     const double* p = d.s0 + (size_t)v0 * 3;
@@ -371,8 +373,10 @@ struct FamilyBA {
     const double* K = param_rec(d, e, 4);
     const double fx = K[0], fy = K[1];
     const double x = pc[0], y = pc[1], z = pc[2], z2 = z * z;
-    err[0] = d.meas[(size_t)e * 2 + 0] - (x / z * fx + K[2]);
-    err[1] = d.meas[(size_t)e * 2 + 1] - (y / z * fy + K[3]);
+    const double m0 = NT ? __builtin_nontemporal_load(d.meas + (size_t)e * 2) : d.meas[(size_t)e * 2 + 0];
+    const double m1 = NT ? __builtin_nontemporal_load(d.meas + (size_t)e * 2 + 1) : d.meas[(size_t)e * 2 + 1];
+    err[0] = m0 - (x / z * fx + K[2]);
+    err[1] = m1 - (y / z * fy + K[3]);
     double R[9];
     quat_to_R(q[0], q[1], q[2], q[3], R);
     const double iz = -1. / z;

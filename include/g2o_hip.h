@@ -248,7 +248,9 @@ int g2ohip_comm_unique_id(unsigned char out[128]);
 int g2ohip_set_comm(g2ohip_graph* g, const unsigned char uid[128], int rank, int nranks);
 /* Test transport: `nranks` graphs in ONE process (one host thread each, same GPU) that share
  * `group_key` reduce through host memory in rank order instead of RCCL. Same sharding, same
- * call sequence as g2ohip_set_comm; used to test the sharded path on a single-GPU box. */
+ * call sequence as g2ohip_set_comm; used to test the sharded path on a single-GPU box. A `group_key` starting with
+ * "solo:" makes this graph play rank `rank` of `nranks` ALONE with every collective a no-op: the kernels rank `rank`
+ * would run, for timing (tools/dist_rank_times.py); its results are not meaningful. */
 int g2ohip_set_comm_local(g2ohip_graph* g, const char* group_key, int rank, int nranks);
 /* RCCL transport self-test on one device (a one-rank communicator from `uid`): the product's allreduce sum and max
  * (the calls g2ohip_set_comm's ranks make) over n doubles of `in` on a stream of `device`; out (2n doubles) =

@@ -112,12 +112,76 @@ print(json.dumps(dict(factor_ms=f, solve_ms=opt.kernel_ms("chol_solve"), info=op
     return run_child(code, {"G2OHIP_DIST_SIMULATE": sim} if sim else None)
 
 
+def solo_rank(config, rank, n):
+    """Rank `rank` of `n` as the product runs it: the full problem in one engine that plays that rank alone through the
+    timing transport (set_comm_local("solo:...")): its aligned landmark shard, the GLOBAL Schur pattern and task lists,
+    its subtrees + the shared top of the distributed factorization, every collective a no-op. Stage and factor / solve
+    timers of that engine (the sums are partial, so its LM decisions are not meaningful; the kernels are the rank's)."""
+    code = f"""
+import sys, json
+sys.path.insert(0, {ROOT!r})
+import g2o_amd
+from g2o_amd import synth
+prob = synth.by_name({config!r})
+opt = g2o_amd.SparseOptimizer(0).add_problem(prob)
+opt.set_algorithm("lm_hip_fix6_3")
+opt.set_comm_local("solo:dist_rank_times", {rank}, {n})
+def steps(a, b):
+    for it in range(a, b):
+        try:
+            opt.optimize_step(it)
+        except Exception:
+            pass
+steps(0, 2)
+opt.enable_kernel_timing(True)
+steps(2, 5)
+st = {{k: opt.kernel_ms(k) for k in {STAGES!r}}}
+opt.enable_kernel_timing(True, only="chol_factor")
+steps(5, 8)
+f = opt.kernel_ms("chol_factor")
+opt.enable_kernel_timing(True, only="chol_solve")
+steps(8, 10)
+print(json.dumps(dict(landmarks=len(opt.local_landmark_ids()), stages_ms=st, factor_ms=f,
+                      solve_ms=opt.kernel_ms("chol_solve"), info=opt.factor_info())))
+"""
+    return run_child(code)
+
+
+def main_solo(a):
+    """--solo: every rank measured on the product's own sharded engine (timing transport)."""
+    res = {"config": a.config, "method": "solo transport: each rank's engine alone on one GPU, collectives no-ops",
+           "by_ranks": {}}
+    for n in [int(x) for x in a.ranks.split(",")]:
+        per = []
+        for r in range(n):
+            m = solo_rank(a.config, r, n)
+            i = m["info"]
+            coll_ms = 1e3 * (i["model_exchange_s"] + i["model_input_s"])
+            st = sum(m["stages_ms"].values())
+            total = st + m["factor_ms"] + m["solve_ms"] + coll_ms
+            per.append(dict(rank=r, landmarks=m["landmarks"], stages_ms=m["stages_ms"], factor_ms=m["factor_ms"],
+                            solve_ms=m["solve_ms"], collectives_model_ms=coll_ms, total_ms=total,
+                            exchange_bytes_per_rank=i["exchange_bytes_per_rank"], owned_fronts=i["owned_fronts"]))
+            print(f"N={n} rank {r}: {m['landmarks']} landmarks, stages {st:.3f} ms "
+                  f"({', '.join(f'{k} {v:.3f}' for k, v in m['stages_ms'].items())}), factor {m['factor_ms']:.3f} + "
+                  f"solve {m['solve_ms']:.3f} ms, collectives (model) {coll_ms:.3f} ms -> {total:.3f} ms",
+                  file=sys.stderr, flush=True)
+        res["by_ranks"][str(n)] = {"per_rank": per, "max_rank_total_ms": max(p["total_ms"] for p in per),
+                                   "max_rank_stages_ms": max(sum(p["stages_ms"].values()) for p in per),
+                                   "max_rank_schur_rows_ms": max(p["stages_ms"]["schur_rows"] for p in per),
+                                   "max_rank_factor_ms": max(p["factor_ms"] for p in per)}
+    print(json.dumps(res))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C5")
     ap.add_argument("--ranks", default="2,4,8")
     ap.add_argument("--tmp", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--solo", action="store_true", help="measure each rank on the product's sharded engine")
     a = ap.parse_args()
+    if a.solo:
+        return main_solo(a)
     os.makedirs(a.tmp, exist_ok=True)
     single = factor_chain(a.config, None)
     full = shard_stages_full(a.config, a.tmp)

@@ -418,16 +418,20 @@ __global__ void __launch_bounds__(256) k_lm_fixup(int nfix, const int4* __restri
 //   B^T (Omega - W W^T) B = Bt^T (F Omega F - Kt Kt^T) Bt,   B^T (omega_r - W c_l) = Bt^T (F omega_r - Kt c_l),
 // the error from (u, v) = (x/z, y/z) exactly as the projection computes it (robust weight from its chi2).
 // NT (recomputing path): the per-observation streams (vertex indices, measurements) are read nontemporally
+// cams (landmark-sharded ranks): the npose cameras of this launch (those with local observations or a diagonal block
+// this rank's factorization reads); nullptr: cameras 0 .. npose - 1
 template <class F, bool FG, bool KX = false, bool NT = false>
-__global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* __restrict__ cm_ptr, int npose,
+__global__ void __launch_bounds__(256, 3) k_cam_assemble(EdgeData d, const int* __restrict__ cm_ptr,
+                                                      const int* __restrict__ cams, int npose,
                                                       double* __restrict__ Hpp, double* __restrict__ bvec,
                                                       int num_poses, int lm_begin, launch::SchurSplit sp) {
   constexpr int D = F::D, DA = F::DA, DB = F::DB;
   constexpr int SP = DB * (DB + 1) / 2, S = SP + DB, NS = FG ? S + DB : S;
   constexpr int UF = 2 * DA;
   __shared__ double red[4][NS];
-  const int i = xcd_item(blockIdx.x, npose);  // neighbouring cameras share landmarks: one L2
+  int i = xcd_item(blockIdx.x, npose);  // neighbouring cameras share landmarks: one L2
   if (i >= npose) return;  // workgroup-uniform
+  if (cams) i = cams[i];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   double acc[NS];
 #pragma unroll
@@ -769,21 +773,21 @@ static bool cam_nt() {
   return k.get() != 0;
 }
 void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, int num_poses, int lm_begin,
-                  const SchurSplit* sp, hipStream_t s) {
+                  const SchurSplit* sp, hipStream_t s, const int* cams) {
   if (npose <= 0) return;
   const EdgeData d{a.v0, a.v1, a.meas, a.info, a.params, a.s0, a.s1, a.rk, a.rk_delta, a.ue};
   const SchurSplit z = sp ? *sp : SchurSplit{};
   if (sp && sp->kx && sp->cm_hpl)
-    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
+    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true, true>), npose, 256, 0, s, d, cm_ptr, cams, npose, Hpp, b, num_poses,
                        lm_begin, z);
   else if (sp && cam_nt())
-    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true, false, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b,
+    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true, false, true>), npose, 256, 0, s, d, cm_ptr, cams, npose, Hpp, b,
                        num_poses, lm_begin, z);
   else if (sp)
-    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
+    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, true>), npose, 256, 0, s, d, cm_ptr, cams, npose, Hpp, b, num_poses,
                        lm_begin, z);
   else
-    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, false>), npose, 256, 0, s, d, cm_ptr, npose, Hpp, b, num_poses,
+    hipLaunchKernelGGL((k_cam_assemble<FamilyBA, false>), npose, 256, 0, s, d, cm_ptr, cams, npose, Hpp, b, num_poses,
                        lm_begin, z);
   KERNEL_CHECK();
 }

@@ -2409,8 +2409,23 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         std::vector<launch::SchurTask> tasks;
         std::vector<launch::SchurBatch> batches;
         std::vector<int> st_obs, st_obs_h, prs, pp;
-        long long npairs = 0;
+        std::vector<launch::SchurPartGroup> groups;  // row chunks split into parts (their partial sums' reduction)
+        long long npairs = 0, nparts_blocks = 0;
       };
+      // Per-rank task lists of the landmark-sharded BA (aligned shards + the distributed factorization reading only its
+      // own subtrees' and the shared blocks): a row chunk with no local pair whose slots all land in another rank's
+      // subtrees writes nothing anyone reads here, and is skipped (dS is zeroed once, so a skipped block reads 0).
+      // Chunks are split into parts (partial sums reduced by k_schur_part_sum) when the row tasks would not fill the
+      // chip twice: a task's batches are a serial chain, and a rank with an eighth of the rows would otherwise be
+      // bound by its longest row (G2OHIP_SCHUR_SPLIT_TASKS: the target task count, 0 off; default 2048 in the sharded
+      // path, off on one GPU).
+      const char* dvr = getenv("G2OHIP_DIST_RS");
+      const char* ssk = getenv("G2OHIP_SCHUR_SKIP");  // dev A/B: 0 = every rank runs every row chunk and camera
+      const bool sch_skip = dist_aligned && nranks > 1 && comm && !write_debug && !(dvr && atoi(dvr) == 0) &&
+                            !(ssk && atoi(ssk) == 0);
+      const char* sst = getenv("G2OHIP_SCHUR_SPLIT_TASKS");
+      const int split_target = sst ? atoi(sst) : (nranks > 1 && comm ? 2048 : 0);
+      auto blk_owner = [&](int i, int j) { return al_bowner[std::min(al_bpinv[i], al_bpinv[j])]; };
       auto build_batches = [&](int SB, BatchSet& bs) {
       auto& tasks = bs.tasks;
       auto& batches = bs.batches;
@@ -2424,17 +2439,63 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       std::vector<P3> cur;
       std::vector<std::pair<int, int>> tmp;
       npairs = 0;
+      // pass 1: per row chunk its staged blocks (0: no local pair) and whether it must run at all
+      std::vector<long long> ch_staged;
+      std::vector<unsigned char> ch_live;
+      for (int i = 0; i < num_poses; ++i) {
+        const int s_lo = srow_ptr[i], s_hi = srow_ptr[i + 1];
+        for (int k = s_lo; k < s_hi; ++k) camslot[s_bj[k]] = k - s_lo;
+        const int noff_total = s_hi - s_lo - 1;
+        for (int ch = 0; ch * SL < noff_total; ++ch) {
+          const int off_lo = 1 + ch * SL, noff = std::min(SL, noff_total - ch * SL);
+          long long st = 0;
+          for (int r = rptr[i]; r < rptr[i + 1]; ++r) {
+            const int a = robs[r], l = obs_lm[a];
+            int np = 0;
+            for (int a2 = a + 1; a2 < lm_ptr[l + 1]; ++a2) {
+              const int sl = camslot[blk_pose[a2]] - off_lo;
+              np += sl >= 0 && sl < noff;
+            }
+            if (np) st += 1 + np;
+          }
+          bool live = st > 0 || !sch_skip;
+          for (int k = 0; k < noff && !live; ++k) {
+            const int o = blk_owner(i, s_bj[s_lo + off_lo + k]);
+            live = o < 0 || o == rank;
+          }
+          ch_staged.push_back(st);
+          ch_live.push_back(live ? 1 : 0);
+        }
+        for (int k = s_lo; k < s_hi; ++k) camslot[s_bj[k]] = -1;
+      }
+      long long nlive = 0;
+      for (size_t c = 0; c < ch_live.size(); ++c) nlive += ch_live[c];
+      const int P = split_target > 0 && nlive > 0 ? (int)std::min<long long>(8, std::max<long long>(1, (split_target + nlive - 1) / nlive)) : 1;
+      size_t cidx = 0;
       for (int i = 0; i < num_poses; ++i) {
         const int s_lo = srow_ptr[i], s_hi = srow_ptr[i + 1];
         for (int k = s_lo; k < s_hi; ++k) camslot[s_bj[k]] = k - s_lo;  // slot 0 = the diagonal block
         const int noff_total = s_hi - s_lo - 1;
-        for (int ch = 0; ch * SL < noff_total; ++ch) {
+        for (int ch = 0; ch * SL < noff_total; ++ch, ++cidx) {
+          if (!ch_live[cidx]) continue;
+          const long long tot = ch_staged[cidx];
+          // parts of at least two batches each
+          const int np = (int)std::max<long long>(1, std::min<long long>(P, tot / (2LL * SB)));
           launch::SchurTask T{};
           T.row = i;
           const int off_lo = 1 + ch * SL;
           T.noff = std::min(SL, noff_total - ch * SL);
           T.soff = s_lo + off_lo;
           T.b0 = (int)batches.size();
+          long long xo = 0;
+          if (np > 1) {
+            xo = bs.nparts_blocks;
+            bs.nparts_blocks += (long long)np * T.noff;
+            bs.groups.push_back(launch::SchurPartGroup{T.soff, T.noff, (int)xo, np});
+            T.pad = (int)xo + 1;  // part 0's partial blocks (k_schur_rows stores acc there, not Hpp - acc)
+          }
+          int part = 0;
+          long long cum = 0;
           int bst0 = (int)st_obs.size();
           cur.clear();
           auto flush = [&]() {
@@ -2466,6 +2527,16 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
             }
             if (tmp.empty()) continue;
             const int need = 1 + (int)tmp.size();
+            const int want = np > 1 ? (int)std::min<long long>(np - 1, cum * np / tot) : 0;
+            while (part < want) {  // the next part: a task of its own (the same slots, its own partial blocks)
+              flush();
+              T.b1 = (int)batches.size();
+              tasks.push_back(T);
+              ++part;
+              T.b0 = (int)batches.size();
+              T.pad = (int)xo + part * T.noff + 1;
+            }
+            cum += need;
             if ((int)st_obs.size() - bst0 + need > SB) flush();
             const int posA = (int)st_obs.size() - bst0;
             st_obs.push_back(gpos[a]);
@@ -2480,18 +2551,40 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
           flush();
           T.b1 = (int)batches.size();
           tasks.push_back(T);
+          if (np > 1 && part != np - 1) {  // trailing parts without observations: their partial blocks are zeros
+            for (int q = part + 1; q < np; ++q) {
+              T.b0 = T.b1 = (int)batches.size();
+              T.pad = (int)xo + q * T.noff + 1;
+              tasks.push_back(T);
+            }
+          }
         }
         for (int k = s_lo; k < s_hi; ++k) camslot[s_bj[k]] = -1;
       }
       batches.push_back(launch::SchurBatch{});  // trailing dummy: k_schur_rows reads one record ahead
       };
       auto nz = [](std::vector<int>& v) -> std::vector<int>& { if (v.empty()) v.push_back(0); return v; };
+      // the split camera pass of a sharded rank: cameras with local observations or a diagonal block this rank reads
+      {
+        std::vector<int> cl;
+        if (sch_skip && (int)cm_ptr_h.size() == num_poses + 1)
+          for (int i = 0; i < num_poses; ++i) {
+            const int o = blk_owner(i, i);
+            if (cm_ptr_h[i + 1] > cm_ptr_h[i] || o < 0 || o == rank) cl.push_back(i);
+          }
+        ncam_list = (int)cl.size();
+        d_cam_list.upload(cl.empty() ? std::vector<int>{0} : cl, stream);
+      }
+      sch_part_blocks = 0;
       {
         BatchSet bs;
         build_batches(SB, bs);
         npairs = bs.npairs;
         nsch_tasks = (int)bs.tasks.size();
         nstaged = (long long)bs.st_obs.size();
+        nsch_groups = (int)bs.groups.size();
+        sch_groups.upload(bs.groups.empty() ? std::vector<launch::SchurPartGroup>(1) : bs.groups, stream);
+        sch_part_blocks = bs.nparts_blocks;
         sch_tasks.upload(bs.tasks.empty() ? std::vector<launch::SchurTask>(1) : bs.tasks, stream);
         sch_batches.upload(bs.batches, stream);
         sch_st_obs.upload(nz(bs.st_obs), stream);
@@ -2501,11 +2594,14 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       }
       // the Kt-record set (BA split; decided with the split below): another block size needs its own batches
       kx_sb = kx_batch_size();
-      nsch_tasks_kx = 0;
+      nsch_tasks_kx = nsch_groups_kx = 0;
       if (kx_sb != SB && ba_fused && pd == 6 && ld == 3) {
         BatchSet bs;
         build_batches(kx_sb, bs);
         nsch_tasks_kx = (int)bs.tasks.size();
+        nsch_groups_kx = (int)bs.groups.size();
+        sch_groups_kx.upload(bs.groups.empty() ? std::vector<launch::SchurPartGroup>(1) : bs.groups, stream);
+        sch_part_blocks = std::max(sch_part_blocks, bs.nparts_blocks);
         sch_tasks_kx.upload(bs.tasks.empty() ? std::vector<launch::SchurTask>(1) : bs.tasks, stream);
         sch_batches_kx.upload(bs.batches, stream);
         sch_st_obs_kx.upload(nz(bs.st_obs_h), stream);
@@ -2530,6 +2626,10 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
     dG.resize(std::max<long long>(std::max((long long)nHpl * pd * ld, ((long long)nHpl + n_kx_extra) * 10), 1));
     dCl.resize(std::max<long long>((long long)num_landmarks * ld, 1));  // c = U^-1 b_l (global landmark index)
     dS.resize((size_t)nS * pd * pd + size_poses);  // [S blocks | bschur] contiguous for one all-reduce
+    // blocks and rhs rows the per-rank task lists never write (sch_skip) must read as zeros in the whole-dS all-reduce of
+    // stage(): zero once per structure
+    dS.zero(stream);
+    dSchurPart.resize(std::max<long long>(sch_part_blocks * pd * pd, 1));
     {  // landmark side of the Schur complement formed during assembly (G2OHIP_SCHUR_SPLIT=0: the plain passes, A/B)
       const char* ev = getenv("G2OHIP_SCHUR_SPLIT");
       fz_split_ok = ba_fused && nslotd == 0 && pd == 6 && ld == 3 && !use_cgls() && !(ev && atoi(ev) == 0);
@@ -2746,8 +2846,12 @@ int Engine::build_system_split(double lambda, const double* lamp) {  // block_so
     ca.meas = cm_meas.get();
     ca.info = cm_info.get();
     ca.params = cm_params.get();
-    launch::cam_assemble(ca, cm_ptr.get(), num_poses, dH.get(), db.get(), num_poses, lm_begin, split ? &sp : nullptr,
-                         stream);
+    if (split && ncam_list > 0)  // a sharded rank's split pass: only the cameras it needs (the rest stay zero)
+      launch::cam_assemble(ca, cm_ptr.get(), ncam_list, dH.get(), db.get(), num_poses, lm_begin, &sp, stream,
+                           d_cam_list.get());
+    else
+      launch::cam_assemble(ca, cm_ptr.get(), num_poses, dH.get(), db.get(), num_poses, lm_begin, split ? &sp : nullptr,
+                           stream);
     timer.end(stream);
     if (use_cgls()) {  // JacobiSolver::buildSystem's J (jacobi_solver.hpp:479-700)
       timer.begin("cgls_jacobian", stream);
@@ -2849,15 +2953,19 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
   // last factorization), off the factorization's own chain
   const bool zero_here = !use_pcg() && chol.nzero > 0;
   timer.begin("schur_rows", stream);
-  if (split && fz_kx && nsch_tasks_kx > 0)  // Kt records in batches of their own block size
+  if (split && fz_kx && nsch_tasks_kx > 0) {  // Kt records in batches of their own block size
     launch::schur_rows(pd, ld, nsch_tasks_kx, sch_tasks_kx.get(), sch_batches_kx.get(), sch_st_obs_kx.get(),
                        sch_pairs_kx.get(), sch_pp_kx.get(), dG.get(), ds_hpp.get(), dH.get(), S,
-                       zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(), stream, true, kx_sb);
-  else
+                       zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(), stream, true, kx_sb,
+                       dSchurPart.get());
+    launch::schur_part_sum(pd, nsch_groups_kx, sch_groups_kx.get(), dSchurPart.get(), ds_hpp.get(), dH.get(), S, stream);
+  } else {
     launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(),
                        split ? sch_st_obs_h.get() : sch_st_obs.get(), sch_pairs.get(), sch_pp.get(), dG.get(),
                        ds_hpp.get(), dH.get(), S, zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(),
-                       stream, split && fz_kx, launch::SCHUR_SB);
+                       stream, split && fz_kx, launch::SCHUR_SB, dSchurPart.get());
+    launch::schur_part_sum(pd, nsch_groups, sch_groups.get(), dSchurPart.get(), ds_hpp.get(), dH.get(), S, stream);
+  }
   timer.end(stream);
   const bool rs = !use_pcg() && chol.rs_on;  // distributed factorization: each rank's blocks reduce-scattered to it
   if (rs) chol.reduce_input(dS.get(), stream);

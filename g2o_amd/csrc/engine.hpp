@@ -412,6 +412,13 @@ class Engine {
   DevBuf<launch::SchurBatch> sch_batches_kx;
   DevBuf<int> sch_st_obs_kx, sch_pairs_kx, sch_pp_kx;
   int nsch_tasks_kx = 0, kx_sb = launch::SCHUR_SB;
+  // row chunks split into parts (per-rank task lists): their reduction groups and the partial-block scratch
+  DevBuf<launch::SchurPartGroup> sch_groups, sch_groups_kx;
+  int nsch_groups = 0, nsch_groups_kx = 0;
+  long long sch_part_blocks = 0;
+  DevBuf<double> dSchurPart;
+  DevBuf<int> d_cam_list;  // the split camera pass's cameras on a sharded rank (ncam_list 0: every camera)
+  int ncam_list = 0;
   static int kx_batch_size();
   // diagonal Schur blocks (k_schur_diag): per camera row its observations in landmark order
   DevBuf<int> sch_rptr, sch_robs, sch_obs_lm, sch_sdiag;

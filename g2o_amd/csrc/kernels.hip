@@ -626,13 +626,27 @@ __device__ __forceinline__ void schur_pairs_kx(const double* Gs, const int* sp, 
 }
 // Even + odd pairs (fixed order) and the S block store: thread (h, par) stores rows [0, CW) (par 0) or [CW, PD) (par 1)
 // of its columns; S(i, j) = Hpp(i, j) - sum
+// pidx > 0 (one part of a split row chunk): the part's sums go to part blocks pidx - 1 + ls, not S (k_schur_part_sum)
 template <int PD>
 __device__ __forceinline__ void schur_row_store(double (&acc)[((PD + 1) / 2) * PD], int ls, int q, int noff, int soff,
-                                                const int* s_hpp, const double* Hpp, double* S) {
+                                                const int* s_hpp, const double* Hpp, double* S, int pidx = 0,
+                                                double* part = nullptr) {
   constexpr int CW = (PD + 1) / 2;
   const int c0 = (q & 1) * CW, par = q >> 1;
 #pragma unroll
   for (int k = 0; k < CW * PD; ++k) acc[k] += __shfl_xor(acc[k], 2, 4);
+  if (ls < noff && pidx > 0) {
+    double* Po = part + (size_t)(pidx - 1 + ls) * PD * PD;
+#pragma unroll
+    for (int j = 0; j < CW; ++j)
+#pragma unroll
+      for (int r = 0; r < PD; ++r) {
+        if ((r >= CW) != (par == 1)) continue;
+        if (PD % 2 != 0 && c0 + j >= PD) continue;
+        Po[(c0 + j) * PD + r] = acc[j * PD + r];
+      }
+    return;
+  }
   if (ls < noff) {
     const int sidx = soff + ls;
     const int hp = s_hpp[sidx];
@@ -678,7 +692,7 @@ __global__ void __launch_bounds__(256, OCC)
                  const int* st_obs, const int* pairs, const int* pp,
                  const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,
                  double* __restrict__ S, int mode, int ntasks, const long long* __restrict__ zr,
-                 double* __restrict__ fronts) {
+                 double* __restrict__ fronts, double* __restrict__ part) {
   static_assert(!KX || (PD == 6 && LD == 3), "Kt records: BA blocks");
   constexpr int SCH_NI = (SCH_SB + 255) / 256;
   constexpr int GB = KX ? 10 : PD * LD;              // doubles per staged block: G, PD x LD col-major (or a Kt record)
@@ -822,7 +836,7 @@ __global__ void __launch_bounds__(256, OCC)
       B2 = B3;
       B3 = B4;
     }
-    schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S);
+    schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S, t.pad, part);
     return;
   }
 
@@ -853,7 +867,7 @@ __global__ void __launch_bounds__(256, OCC)
     B1 = B2;
     B2 = B3;
   }
-  schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S);
+  schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S, t.pad, part);
 }
 
 // back-substitution: x_l = Dinv_l (b_l - sum_a Hpl_a^T x_pose(a)); LANES lanes per landmark stride over
@@ -1501,9 +1515,32 @@ void schur_diag(int pd, int ld, int nrows, const int* rptr, const int* robs, con
   });
   KERNEL_CHECK();
 }
+// S(soff + s) = Hpp - sum_p part(xo + p noff + s): one workgroup per group, parts summed in order
+template <int PD>
+__global__ void __launch_bounds__(256) k_schur_part_sum(const launch::SchurPartGroup* __restrict__ groups,
+                                                        const double* __restrict__ part, const int* __restrict__ s_hpp,
+                                                        const double* __restrict__ Hpp, double* __restrict__ S) {
+  const launch::SchurPartGroup g = groups[blockIdx.x];
+  constexpr int BB = PD * PD;
+  for (int e = threadIdx.x; e < g.noff * BB; e += 256) {
+    const int sl = e / BB, k = e - sl * BB;
+    double sum = 0.0;
+    for (int p = 0; p < g.np; ++p) sum += part[(size_t)(g.xo + p * g.noff + sl) * BB + k];
+    const int sidx = g.soff + sl, hp = s_hpp[sidx];
+    S[(size_t)sidx * BB + k] = (hp >= 0 ? Hpp[(size_t)hp * BB + k] : 0.0) - sum;
+  }
+}
+void schur_part_sum(int pd, int ngroups, const SchurPartGroup* groups, const double* part, const int* s_hpp,
+                    const double* Hpp, double* S, hipStream_t s) {
+  if (ngroups <= 0) return;
+  if (pd == 6) hipLaunchKernelGGL(k_schur_part_sum<6>, ngroups, 256, 0, s, groups, part, s_hpp, Hpp, S);
+  else if (pd == 3) hipLaunchKernelGGL(k_schur_part_sum<3>, ngroups, 256, 0, s, groups, part, s_hpp, Hpp, S);
+  else throw DeviceError("schur_part_sum: pose blocks of 3 or 6");
+  KERNEL_CHECK();
+}
 void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
-                int nzero, const long long* zr, double* fronts, hipStream_t s, bool kx, int sb) {
+                int nzero, const long long* zr, double* fronts, hipStream_t s, bool kx, int sb, double* part) {
   if (ntasks <= 0 && nzero <= 0) return;
 #ifdef G2OHIP_DEV  // development build only: 1 no pair products, 2 no staging, 3 neither (wrong S, timing splits)
   static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;
@@ -1520,10 +1557,10 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
       constexpr int SBK = decltype(SBc)::value;
       if (pipe == 0)
         hipLaunchKernelGGL((k_schur_rows<6, 3, 0, true, SBK>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs,
-                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
+                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts, part);
       else
         hipLaunchKernelGGL((k_schur_rows<6, 3, 1, true, SBK>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs,
-                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts);
+                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts, part);
     };
     if (sb == 128) go(std::integral_constant<int, 128>{});
     else if (sb == 192) go(std::integral_constant<int, 192>{});
@@ -1536,10 +1573,10 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
     constexpr int pv = decltype(P)::value, lv = decltype(L)::value;
     if (pipe == 0)
       hipLaunchKernelGGL((k_schur_rows<pv, lv, 0>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs, pp, G, s_hpp,
-                         Hpp, S, mode, ntasks, zr, fronts);
+                         Hpp, S, mode, ntasks, zr, fronts, part);
     else
       hipLaunchKernelGGL((k_schur_rows<pv, lv, 1>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs, pp, G, s_hpp,
-                         Hpp, S, mode, ntasks, zr, fronts);
+                         Hpp, S, mode, ntasks, zr, fronts, part);
   });
   KERNEL_CHECK();
 }

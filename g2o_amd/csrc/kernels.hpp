@@ -67,7 +67,7 @@ void linearize_fused(const EdgeArgs& a, const int4* chunks, int nchunks, const i
 void lm_fixup(int nfix, const int4* fix, const double* lpart, double* Hll, double* b, int num_poses, int size_poses,
               int lm_begin, const SchurSplit* sp, hipStream_t s);
 void cam_assemble(const EdgeArgs& a, const int* cm_ptr, int npose, double* Hpp, double* b, int num_poses, int lm_begin,
-                  const SchurSplit* sp, hipStream_t s);
+                  const SchurSplit* sp, hipStream_t s, const int* cams = nullptr);
 // back-substitution of the Schur split recomputing each observation's Jacobians (no G blocks read): per local landmark
 // its edge range erng (landmark-major group order), hcam = camera vertex -> hessian index (-1 fixed)
 void backsub_j(const EdgeArgs& a, int nl, const int2* erng, const int* hcam, const double* Ufac, const double* cl_all,
@@ -94,7 +94,11 @@ struct SchurTask {
   int row, noff;  // camera row, number of off-diagonal slots of this task
   int b0, b1;     // batches
   int soff;       // S index of the first off-diagonal slot
-  int pad;
+  int pad;        // 0: S = Hpp - sum; k > 0: one part of a split row chunk, its partial sums to part blocks k - 1 ...
+};
+// a row chunk split into parts: S(soff + s) = Hpp - sum over the np parts of part block (xo + p noff + s), parts in order
+struct SchurPartGroup {
+  int soff, noff, xo, np;
 };
 struct SchurBatch {
   int st0, nst;  // staged blocks (st_obs)
@@ -105,7 +109,10 @@ struct SchurBatch {
 void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
                 int nzero, const long long* zr, double* fronts, hipStream_t s, bool kx = false,
-                int sb = SCHUR_SB);
+                int sb = SCHUR_SB, double* part = nullptr);
+// the split row chunks' partial sums into S (fixed part order: bitwise reproducible)
+void schur_part_sum(int pd, int ngroups, const SchurPartGroup* groups, const double* part, const int* s_hpp,
+                    const double* Hpp, double* S, hipStream_t s);
 void backsub(int pd, int ld, int nl, const int* lm_ptr, const int* blk_pose, const double* Hpl, const double* Dinv,
              const double* b, int size_poses, int lm0, double* x, hipStream_t s);
 // back-substitution from the G blocks of an assembly-time Schur split: x_l = U^-T (c_l - G^T x_p)

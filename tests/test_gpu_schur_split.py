@@ -157,3 +157,23 @@ def test_split_kx_records_match_g_blocks(g2o_amd_mod, monkeypatch, which):
         x, y = np.asarray(a[k]), np.asarray(b[k])
         scale = np.abs(y).max()
         assert np.abs(x - y).max() <= 1e-13 * scale, (k, np.abs(x - y).max() / scale)
+
+
+@pytest.mark.parametrize("name", ["C4", "C5"])
+def test_split_row_parts(g2o_amd_mod, oracle, name, monkeypatch):
+    """Row chunks split into parts (G2OHIP_SCHUR_SPLIT_TASKS: the sharded path's default, forced here on one GPU): each
+    part's partial blocks, then k_schur_part_sum's fixed-order sum into S. The reduced system against the oracle, and
+    the LM trajectory against the unsplit pass."""
+    monkeypatch.setenv("G2OHIP_SCHUR_SPLIT_TASKS", "1000000")
+    prob = synth.by_name(name, "small")
+    _stage(g2o_amd_mod, oracle, prob, 1e-3, monkeypatch)
+    runs = []
+    for flag in ("1000000", "0"):
+        monkeypatch.setenv("G2OHIP_SCHUR_SPLIT_TASKS", flag)
+        opt = g2o_amd_mod.SparseOptimizer(0).add_problem(prob)
+        n, st = opt.optimize(5)
+        runs.append((n, [s.chi2 for s in st], [s.levenbergIterations for s in st], opt.minimal_state()))
+    (n1, c1, t1, x1), (n0, c0, t0, x0) = runs
+    assert n1 == n0 and t1 == t0
+    assert np.allclose(c1, c0, rtol=1e-10, atol=0)
+    assert np.linalg.norm(x1 - x0) <= 1e-10 * np.linalg.norm(x0)

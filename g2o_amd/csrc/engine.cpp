@@ -512,8 +512,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     const int block_pb = bp ? std::max(64, atoi(bp) / 64 * 64) : 256;
     const char* wf = getenv("G2OHIP_CHOL_WIDE_FRONTS");  // dev A/B: fronts per level that make it "wide"
     const int wide_fronts = wf ? atoi(wf) : 64;
+    // wide levels block only supernodes wider than 512 columns (r06: C3 factor 26.04 -> 25.22 ms against 128, its
+    // levels of >= 64 fronts, all <= 384 columns wide, then take the deferred-L21 path — panel steps over the own rows,
+    // the rows below in one k_l21 GEMM — instead of 128-column big panels whose steps re-read the rows below;
+    // profiles/r06_ab_defer_widepb.log, r06_ab_c3_blocking.log)
     const char* wp = getenv("G2OHIP_CHOL_WIDE_PB");
-    const int wide_pb = wp ? std::max(64, atoi(wp) / 64 * 64) : 128;
+    const int wide_pb = wp ? std::max(64, atoi(wp) / 64 * 64) : 512;
 #ifdef G2OHIP_DEV  // development build only (make dev): timing experiments that give a wrong result on purpose
     const bool dev_noinv = getenv("G2OHIP_DEV_NOINV") != nullptr;  // no inverse tasks (wrong solve)
     const bool dev_diagonly = getenv("G2OHIP_DEV_DIAGONLY") != nullptr;  // diagonal tasks only (wrong factor)

@@ -635,10 +635,6 @@ __device__ __forceinline__ void load_ctile(const double* F, int m, int rlim, int
 // Rows/columns of the tile: I0 = r0 + 64 ti, J0 = r0 + 64 tj, r0 = k0 + kb.
 // PAIRS: the launch may hold lagged-pair tasks (flag 64); without them the pair code is compiled out (166 instead of
 // ~180 VGPRs: three workgroups per CU instead of two)
-// 64 x 64 tile of a previous big panel's trailing update run inside the panel steps (flag 1024): the LDS-DMA ring with
-// 8-column K chunks (its 33 KB fit the step's panel buffers; the chunk loop computes the same products in the same
-// order as the k_syrk pass's 16-column chunks)
-using FarTile = GemmNTd<TT, TT, 2, 2, 8, 2>;
 template <bool PAIRS>
 __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ tasks, const launch::StepHead head,
                                               double* __restrict__ fronts,
@@ -647,7 +643,7 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
                                               double* __restrict__ xinv, int* __restrict__ fail) {
   __shared__ double Li[NB * PS];      // L_kk^-1, row-major, stride 34
   __shared__ double yk[NB];
-  __shared__ __attribute__((aligned(16))) double sh[2 * TT * PS];  // Pa | Pb; reused as the 64 x 65 result tile
+  __shared__ double sh[2 * TT * PS];  // Pa | Pb; reused as the 64 x 65 result tile
   __shared__ double Dn[NB * DS];      // next diagonal block
   __shared__ __attribute__((aligned(16))) double col[4 * NB];  // two 64-lane column buffers
   __shared__ double vn[NB];
@@ -684,15 +680,6 @@ __global__ void __launch_bounds__(256, 3) k_step(const StepTask* __restrict__ ta
   double* Pb = sh + TT * PS;
   const double* Lin = linv + (size_t)(t.c0 + k0) * (NB * NB);
 
-  if (t.flags & 1024) {
-    // ---- a far trailing-update tile of the PREVIOUS big panel (blocked fronts, DeviceCholesky::setup): columns past the
-    // current big panel, C -= L(:, ka:kb) L(:, ka:kb)^T, riding in this big panel's steps (their chip is mostly idle
-    // beside the diagonal chain, and no step touches those columns before the next trailing update). k0kb = ka | kb << 16
-    static_assert(FarTile::LDS_DOUBLES <= 2 * TT * PS, "the far tile's LDS ring fits the panel buffers");
-    const int fka = t.k0kb & 0xffff, fkb = t.k0kb >> 16;
-    FarTile::run(L, m, F, m, m, ns, fkb + ti * TT, fkb + tj * TT, fka, fkb, sh);
-    return;
-  }
   if (t.flags & 4) {
     // ---- dedicated next-diagonal task (runs beside the tile tasks of this step): the 32x32 block
     // D' = A(r0:r0+32, r0:r0+32) - X X^T with X = P(r0:r0+32) L_kk^-T, then its factor, inverse

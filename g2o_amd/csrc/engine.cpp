@@ -516,8 +516,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     // levels of >= 64 fronts, all <= 384 columns wide, then take the deferred-L21 path — panel steps over the own rows,
     // the rows below in one k_l21 GEMM — instead of 128-column big panels whose steps re-read the rows below;
     // profiles/r06_ab_defer_widepb.log, r06_ab_c3_blocking.log)
-    const char* fo = getenv("G2OHIP_CHOL_FAR");
-    const bool far_on = !(fo && atoi(fo) == 0);
     const char* wp = getenv("G2OHIP_CHOL_WIDE_PB");
     const int wide_pb = wp ? std::max(64, atoi(wp) / 64 * 64) : 512;
 #ifdef G2OHIP_DEV  // development build only (make dev): timing experiments that give a wrong result on purpose
@@ -671,15 +669,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         sn_dl[sn] = dl_level && !blocked(q) && q.nr > 0 && q.env_off < 0 ? 1 : 0;
         n_deferred_l21 += sn_dl[sn];
       }
-      // far trailing-update tiles of blocked fronts (columns past the next big panel): spread over the next big
-      // panel's step launches instead of the k_syrk pass on the chain (G2OHIP_CHOL_FAR=0: all in k_syrk, A/B)
-      std::vector<launch::StepTask> far_q;
-      int far_steps_left = 0;
       for (int p = 0; p < maxp; ++p) {
         Op st{2, (int)stk.size(), 0};
         // task order inside the launch (= dispatch order): every front's next-diagonal task first (the
         // critical chain must start at once, on a CU of its own), then the tile tasks, then the
-        // inverse tasks (X = L11^-1 for the backward solve), which have the most slack, then far trailing tiles
+        // inverse tasks (X = L11^-1 for the backward solve), which have the most slack
         std::vector<launch::StepTask> diag_t, tile_t, inv_t;
         for (int sn : lv) {
           const Supernode& q = sym.sn[sn];
@@ -730,19 +724,12 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         stk.insert(stk.end(), diag_t.begin(), diag_t.end());
         if (!dev_diagonly) stk.insert(stk.end(), tile_t.begin(), tile_t.end());
         if (!dev_diagonly) stk.insert(stk.end(), inv_t.begin(), inv_t.end());
-        if (!far_q.empty() && far_steps_left > 0) {
-          const size_t n = (far_q.size() + far_steps_left - 1) / far_steps_left;
-          stk.insert(stk.end(), far_q.begin(), far_q.begin() + n);
-          far_q.erase(far_q.begin(), far_q.begin() + n);
-          --far_steps_left;
-        }
         st.count = (int)stk.size() - st.off;
         for (int k = st.off; k < st.off + st.count; ++k)
           if (stk[k].flags & 64) st.kind = 6;
         if (st.count) { ops.push_back(st); }
         if ((p + 1) * NB % lpb) continue;
         // end of a big panel: trailing update of the blocked fronts, then their next first blocks
-        if (!far_q.empty()) throw DeviceError("chol setup: far trailing tiles left over at a big-panel end");
         Op gm{3, (int)tk.size(), 0};
         Op d0{2, (int)stk.size(), 0};
         for (int sn : lv) {
@@ -750,19 +737,11 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           const int kb = (p + 1) * NB, ka = kb - lpb, m = q.ns + q.nr;
           if (!blocked(q) || kb >= q.ns) continue;
           const int T = (m - kb + SR - 1) / SR, TJ = (q.ns - kb + TT - 1) / TT;
-          // columns past the next big panel (a full one: ns > kb + lpb) go to its steps as far tiles
-          const int TJn = far_on && q.env_off < 0 && SR == TT && q.ns > kb + lpb ? lpb / TT : TJ;
           for (int tj = 0; tj < TJ; ++tj) {
             if (!tile_nz(sn, kb + TT * tj, kb)) continue;
-            for (int ti = TT * tj / SR; ti < T; ++ti) {
-              if (!rows_nz(sn, kb + SR * ti, kb)) continue;
-              if (tj < TJn) tk.push_back(Task{sn, ka, ti | (tj << 16), kb});
-              else
-                far_q.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m,
-                                                 q.ns, q.c0, ka | (kb << 16), ti | (tj << 16), 1024, q.ns});
-            }
+            for (int ti = TT * tj / SR; ti < T; ++ti)
+              if (rows_nz(sn, kb + SR * ti, kb)) tk.push_back(Task{sn, ka, ti | (tj << 16), kb});
           }
-          if (!far_q.empty()) far_steps_left = lpb / NB;
           stk.push_back(launch::StepTask{hfd[sn].front_off, hfd[sn].l_off, hfd[sn].vec_off, hfd[sn].x_off, m, q.ns,
                                          q.c0, kb, 0, 4, q.ns});
         }

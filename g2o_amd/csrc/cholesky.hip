@@ -1045,10 +1045,12 @@ __global__ void __launch_bounds__(256) k_bwd_gemv(const Task* __restrict__ tasks
   if (lane == 0) tsol[me.c0 + j] = ysol[me.c0 + j] - acc;
 }
 
+// X's 32 x 32 diagonal blocks are read from linv (L_kk^-1, row-major, as the factorization published them): no copy of
+// them into X is needed for the solve (k_xdiag runs only for the deferred-L21 fronts' k_l21)
 __global__ void __launch_bounds__(256) k_bwd_x(const Task* __restrict__ tasks, const FrontDesc* __restrict__ fd,
-                                               const double* __restrict__ xinv, const double* __restrict__ tsol,
-                                               double* __restrict__ xsol, const int* __restrict__ perm,
-                                               double* __restrict__ xout) {
+                                               const double* __restrict__ xinv, const double* __restrict__ linv,
+                                               const double* __restrict__ tsol, double* __restrict__ xsol,
+                                               const int* __restrict__ perm, double* __restrict__ xout) {
   const Task t = tasks[blockIdx.x];
   const FrontDesc me = fd[t.s];
   const int ns = me.ns;
@@ -1057,8 +1059,10 @@ __global__ void __launch_bounds__(256) k_bwd_x(const Task* __restrict__ tasks, c
   const double* xc = xinv + me.x_off + (size_t)j * ns;  // column j of X (rows >= j are nonzero)
   const double* tt = tsol + me.c0;
   const int ie = t.c;  // X(j.., j) up to row ie: ns, or the end of a blocked front's big panel (X_bb)
+  const int b0 = j & ~(NB - 1), be = min(min(b0 + NB, ns), ie);  // j's diagonal block: rows [j, be) from L_kk^-1
   double a4[4] = {0.0, 0.0, 0.0, 0.0};
-  int i = j + lane;
+  if (j + lane < be) a4[0] = linv[(size_t)(me.c0 + b0) * (NB * NB) + (j + lane - b0) * NB + (j - b0)] * tt[j + lane];
+  int i = be + lane;
   for (; i + 192 < ie; i += 256) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) a4[u] += xc[i + 64 * u] * tt[i + 64 * u];
@@ -1309,10 +1313,10 @@ void chol_xdiag(int ntasks, const Task* tasks, const FrontDesc* fd, const double
   hipLaunchKernelGGL(k_xdiag, ntasks, 256, 0, s, tasks, fd, linv, xinv);
   KERNEL_CHECK();
 }
-void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,
-                const int* perm, double* xout, hipStream_t s) {
+void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* linv,
+                const double* tsol, double* xsol, const int* perm, double* xout, hipStream_t s) {
   if (ntasks <= 0) return;
-  hipLaunchKernelGGL(k_bwd_x, ntasks, 256, 0, s, tasks, fd, xinv, tsol, xsol, perm, xout);
+  hipLaunchKernelGGL(k_bwd_x, ntasks, 256, 0, s, tasks, fd, xinv, linv, tsol, xsol, perm, xout);
   KERNEL_CHECK();
 }
 

@@ -904,14 +904,9 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
       bwd_ops.push_back(bl);
       bwd_off.push_back((int)tk.size());
     }
-    // diagonal blocks of X = L11^-1 (the factorization publishes every L_kk^-1 to linv only): one k_xdiag task per
-    // block, after the factorization's last launch
-    xdiag_off = (int)tk.size();
-    for (const auto& lv : fplan)
-      for (int sn : lv)
-        if (!sn_dl[sn])  // deferred-L21 fronts: copied by their level's own k_xdiag launch
-          for (int a = 0; a < sym.sn[sn].ns; a += NB) tk.push_back(Task{sn, a, 0, 0});
-    n_xdiag = (int)tk.size() - xdiag_off;
+    // X's diagonal blocks stay in linv (the factorization publishes every L_kk^-1 there only): k_bwd_x reads them from
+    // it, so no copy runs after the factorization (the deferred-L21 fronts' level k_xdiag launches remain: k_l21 reads X
+    // whole)
     if (getenv("G2OHIP_PRINT_OPS")) {  // diagnostics (stderr): the factor's launch list in order, k_syrk with its flops
       for (size_t k = 0; k < ops.size(); ++k) {
         const Op& op = ops[k];
@@ -1067,7 +1062,6 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       default: launch::chol_syrk(syrk_var, op.count, t, fd.get(), fronts.get(), lbuf.get(), y_p.get(), vecs.get(), s); break;
     }
   }
-  launch::chol_xdiag(n_xdiag, tasks.get() + xdiag_off, fd.get(), linv.get(), xinv.get(), s);
 }
 
 void DeviceCholesky::reduce_input(const double* vals, hipStream_t s) {
@@ -1089,11 +1083,11 @@ void DeviceCholesky::solve(double* x, hipStream_t s) {
     const BwdLevel& bl = bwd_ops[l];
     launch::chol_bwd_gemv(bl.gemv.second, tasks.get() + bl.gemv.first, fd.get(), rows.get(), lbuf.get(), y_p.get(),
                           x_p.get(), t_p.get(), s);
-    launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), bl.t_is_y ? y_p.get() : t_p.get(),
+    launch::chol_bwd_x(bl.xall.second, tasks.get() + bl.xall.first, fd.get(), xinv.get(), linv.get(), bl.t_is_y ? y_p.get() : t_p.get(),
                        x_p.get(), perm.get(), xo, s);
     for (const auto& rd : bl.rounds) {
       launch::chol_bwd_inner(rd.first.second, tasks.get() + rd.first.first, fd.get(), lbuf.get(), x_p.get(), t_p.get(), s);
-      launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), t_p.get(), x_p.get(),
+      launch::chol_bwd_x(rd.second.second, tasks.get() + rd.second.first, fd.get(), xinv.get(), linv.get(), t_p.get(), x_p.get(),
                          perm.get(), xo, s);
     }
   }

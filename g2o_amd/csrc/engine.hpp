@@ -176,7 +176,6 @@ struct DeviceCholesky {
   // pack this rank's partial [blocks | rhs] (the caller's layout) and reduce; factor(rs_buf, ..., rs_buf + rs_rhs_off)
   void reduce_input(const double* vals, hipStream_t s);
   std::vector<Op> ops;
-  int xdiag_off = 0, n_xdiag = 0;  // k_xdiag tasks (in `tasks`): X's diagonal blocks from linv after the factor
   std::vector<launch::StepHead> heads;  // per op: its leading next-diagonal tasks (k_step kernel arguments)
   std::vector<launch::ScatterJob> ea_jobs;  // per extend-add op: its leading block-0 fronts (kernel arguments)
   DevBuf<launch::B0Front> b0front;          // per extend-add op (Op::b0): its fronts' block-0 records

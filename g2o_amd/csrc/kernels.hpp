@@ -271,8 +271,8 @@ void chol_bwd_inner(int ntasks, const Task* tasks, const FrontDesc* fd, const do
                     hipStream_t s);
 // x = X^T t per front column; each x also lands at xout[perm[k]] (the caller's order)
 void chol_xdiag(int ntasks, const Task* tasks, const FrontDesc* fd, const double* linv, double* xinv, hipStream_t s);
-void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* tsol, double* xsol,
-                const int* perm, double* xout, hipStream_t s);
+void chol_bwd_x(int ntasks, const Task* tasks, const FrontDesc* fd, const double* xinv, const double* linv,
+                const double* tsol, double* xsol, const int* perm, double* xout, hipStream_t s);
 int debug_phases(unsigned long long* out, int maxrec);  // -DG2OHIP_PHASES builds only
 constexpr int CHOL_NB = 32, CHOL_TT = 64, CHOL_EA = 16, CHOL_BW = 4;
 // distributed factorization glue: contiguous range copies (src, dst, len) in doubles; the distributed

@@ -493,12 +493,6 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
     // k_syrk's row tiles: SR rows (64, or 128 for the 128 x 64 tile variants)
     syrk_var = launch::syrk_variant();  // pinned: chol_syrk launches this tile for these row-tile lists
     const int SR = launch::syrk_tile_rows(syrk_var);
-    // a k_syrk pass with fewer tiles than one round of the chip at two workgroups per CU is a serial chain of K chunks
-    // per tile: the (32, 2) ring halves the chain (G2OHIP_SYRK_SMALL: the largest such pass in tiles, 0 off; 64-row
-    // tiles only, the same task lists)
-    const char* ssm = getenv("G2OHIP_SYRK_SMALL");
-    const int syrk_small = ssm ? atoi(ssm) : 0;
-    auto syrk_pick = [&](int ntiles) { return SR == TT && ntiles <= syrk_small ? 1 : syrk_var; };
     auto rows_fnz = [&](int sn, int r) { return SR == TT ? tile_fnz(sn, r) : std::min(tile_fnz(sn, r), tile_fnz(sn, r + TT)); };
     auto rows_nz = [&](int sn, int r, int kend) { return rows_fnz(sn, r) < kend; };
     std::vector<Task> tk;
@@ -753,7 +747,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
         }
         gm.count = (int)tk.size() - gm.off;
         d0.count = (int)stk.size() - d0.off;
-        if (gm.count) { gm.nb0 = syrk_pick(gm.count); ops.push_back(gm); ++n_syrk_ops; }
+        if (gm.count) { ops.push_back(gm); ++n_syrk_ops; }
         if (d0.count) { ops.push_back(d0); }
       }
       {  // deferred L21: X's diagonal blocks for the level's fronts, then L21 = A21 X^T
@@ -792,7 +786,7 @@ void DeviceCholesky::setup(int nblocks, int bdim, const std::vector<int>& bi, co
           }
       }
       sy.count = (int)tk.size() - sy.off;
-      if (sy.count) { sy.nb0 = syrk_pick(sy.count); ops.push_back(sy); ++n_syrk_ops; }
+      if (sy.count) { ops.push_back(sy); ++n_syrk_ops; }
       for (int sn : lv) n_blocked += blocked(sym.sn[sn]) ? 1 : 0;
     }
     // root exchange (distributed): per subtree root, the lower triangle of its contribution block column by column
@@ -1065,7 +1059,7 @@ void DeviceCholesky::factor(const double* vals, const double* lam, const double*
       }
       case 11: launch::chol_xdiag(op.count, t, fd.get(), linv.get(), xinv.get(), s); break;
       case 12: launch::chol_l21(op.count, t, fd.get(), fronts.get(), xinv.get(), lbuf.get(), s); break;
-      default: launch::chol_syrk(op.nb0, op.count, t, fd.get(), fronts.get(), lbuf.get(), y_p.get(), vecs.get(), s); break;
+      default: launch::chol_syrk(syrk_var, op.count, t, fd.get(), fronts.get(), lbuf.get(), y_p.get(), vecs.get(), s); break;
     }
   }
 }

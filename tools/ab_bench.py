@@ -38,7 +38,7 @@ def main(argv):
         print(f"{cfg} {s:60s} {d['value']:9.3f} LM it/s  {d['ms_per_step']:8.3f} ms/step  factor "
               f"{d['roofline']['avg_launch_ms']:8.3f} ms  schur_rows {st.get('schur_rows', 0):.3f}  "
               f"linearize {st.get('linearize', 0):.3f}  vreduce {st.get('vreduce', 0):.3f}  backsub {st.get('backsub', 0):.3f}  "
-              f"trials {d['config']['levenberg_trials']}", flush=True)
+              f"trials {d['config']['levenberg_trials']}  ms/linear-solve {d.get('ms_per_linear_solve', 0):.3f}", flush=True)
     return 0
 
 

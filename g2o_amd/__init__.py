@@ -107,6 +107,7 @@ def lib() -> C.CDLL:
         "g2ohip_minimal_state": ([P, P], I),
         "g2ohip_set_algorithm": ([P, C.c_char_p], I),
         "g2ohip_initialize": ([P], I),
+        "g2ohip_update_initialization": ([P], I),
         "g2ohip_chi2": ([P], D),
         "g2ohip_optimize": ([P, P, I, P], I),
         "g2ohip_optimize_step": ([P, P, I, P], I),
@@ -364,6 +365,11 @@ class SparseOptimizer:
 
     def initialize_optimization(self):
         _check(lib().g2ohip_initialize(self.h), "initializeOptimization")
+
+    def update_initialization(self):
+        """SparseOptimizer::updateInitialization (online mode, non-Schur): vertices / edges added since
+        initialize_optimization join with appended hessian indices; optimize() then continues from the current state."""
+        _check(lib().g2ohip_update_initialization(self.h), "updateInitialization")
 
     def chi2(self) -> float:
         return lib().g2ohip_chi2(self.h)

@@ -154,6 +154,16 @@ int g2ohip_initialize(g2ohip_graph* g) {
   if (!g) return G2OHIP_ERR_ARG;
   return guarded([&] { return g->e->initialize(); });
 }
+
+int g2ohip_update_initialization(g2ohip_graph* g) {
+  if (!g) return G2OHIP_ERR_ARG;
+  const int r = guarded([&] { return g->e->update_initialization(); });
+  if (r == G2OHIP_ERR_STATE) g_err = "updateInitialization: initializeOptimization first";
+  if (r == G2OHIP_ERR_UNSUPPORTED)
+    g_err = "updateInitialization: online updates of a Schur (marginalized) graph or of another pose block size are "
+            "not supported (block_solver.hpp:274-277)";
+  return r;
+}
 double g2ohip_chi2(g2ohip_graph* g) {
   if (!g) return std::nan("");
   try {

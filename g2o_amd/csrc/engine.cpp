@@ -1137,6 +1137,7 @@ Engine::~Engine() {
 
 int Engine::add_vertices(int type, int n, const int* ids, const double* est, const int* fixed, const int* marg) {
   if (vertex_dim(type) < 0 || n < 0) return G2OHIP_ERR_ARG;
+  sync_host_state();  // the appended states are uploaded with the rest: the optimized ones must be current here
   const int ed = vertex_est_dim(type), sd = vertex_state_stride(type);
   for (int k = 0; k < n; ++k) {
     if (hg.idmap.count(ids[k])) return G2OHIP_ERR_ARG;
@@ -1724,6 +1725,55 @@ int Engine::initialize() {  // sparse_optimizer.cpp:201-279 + buildIndexMapping 
       const int a = hidx[es.ev0[k]], b = hidx[es.ev1[k]];
       if (a >= num_poses && b >= num_poses) return G2OHIP_ERR_UNSUPPORTED;
     }
+  initialized = true;
+  structure_built = false;
+  edges_ready = false;
+  return G2OHIP_OK;
+}
+
+// SparseOptimizer::updateInitialization (sparse_optimizer.cpp:465-502) + BlockSolver::updateStructure
+// (block_solver.hpp:258-312). The vertices that gained edges since the last initialization join the running
+// optimization behind the existing ones: each free one takes the next hessian index (the reference numbers the
+// caller's vertex set in its iteration order; here the new vertices in id order), so the blocks of x, b, Hpp and the
+// marginals of the vertices already there keep their places. The structure (pattern, symbolic factorization) is
+// rebuilt on the next build, as the reference's updateStructure + LinearSolver::init do. Non-Schur only: the
+// reference refuses marginalized vertices here ("Schur not supported", block_solver.hpp:274-277; abort in
+// sparse_optimizer.cpp:491-492), this returns G2OHIP_ERR_UNSUPPORTED and leaves the graph's indexing unchanged.
+int Engine::update_initialization() {
+  if (ivmap.empty()) return G2OHIP_ERR_STATE;  // initializeOptimization first
+  if (do_schur) return G2OHIP_ERR_UNSUPPORTED;
+  std::vector<char> was(hg.verts.size(), 0), has(hg.verts.size(), 0);
+  for (int vi : active) was[vi] = 1;
+  bool hj = false;
+  for (const HEdgeSet& es : hg.esets) {
+    int vtA, vtB;
+    const int fam = family_of(es.type, vtA, vtB);
+    if (fam == FAM_NONE) return G2OHIP_ERR_UNSUPPORTED;
+    hj |= fam == FAM_HOSTJ;
+    for (size_t k = 0; k < es.ev0.size(); ++k) {
+      const HVertex &a = hg.verts[es.ev0[k]], &b = hg.verts[es.ev1[k]];
+      if (fam != FAM_HOSTJ && (a.type != vtA || b.type != vtB)) return G2OHIP_ERR_UNSUPPORTED;
+      has[es.ev0[k]] = has[es.ev1[k]] = 1;
+    }
+  }
+  std::vector<int> fresh;
+  for (size_t k = 0; k < hg.verts.size(); ++k)
+    if (has[k] && !was[k]) fresh.push_back((int)k);
+  std::sort(fresh.begin(), fresh.end(), [&](int a, int b) { return hg.verts[a].id < hg.verts[b].id; });
+  for (int vi : fresh) {
+    const HVertex& v = hg.verts[vi];
+    if (!v.fixed && (v.marg || v.dim != pd)) return G2OHIP_ERR_UNSUPPORTED;  // BlockSolver<p, l>: one pose size
+  }
+  hidx.resize(hg.verts.size(), -1);
+  for (int vi : fresh) {
+    active.push_back(vi);
+    if (hg.verts[vi].fixed) continue;
+    hidx[vi] = (int)ivmap.size();
+    ivmap.push_back(vi);
+    ++num_poses;
+  }
+  size_poses = num_poses * pd;
+  has_hostj = hj;
   initialized = true;
   structure_built = false;
   edges_ready = false;

@@ -264,6 +264,9 @@ class Engine {
 
   // ---- SparseOptimizer / Solver ----
   int initialize();
+  // SparseOptimizer::updateInitialization + BlockSolver::updateStructure (online mode, non-Schur): vertices and edges
+  // added after initialize() join with appended hessian indices; the existing vertices keep theirs
+  int update_initialization();
   double chi2();
   int optimize(const g2ohip_config* cfg, int iterations, g2ohip_batch_stats* stats);
   // one SparseOptimizer::optimize loop body (iteration 0 rebuilds structure + lambda init);

@@ -139,6 +139,14 @@ long long g2ohip_host_payload_len(g2ohip_graph* g, int edge_type);
 int g2ohip_set_algorithm(g2ohip_graph* g, const char* name);
 /* SparseOptimizer::initializeOptimization(0): active edges/vertices, index mapping */
 int g2ohip_initialize(g2ohip_graph* g);
+/* SparseOptimizer::updateInitialization(vset, eset) + BlockSolver::updateStructure (sparse_optimizer.cpp:465-502,
+ * block_solver.hpp:258-312), online mode: after g2ohip_initialize (and optimizing), vertices and edges added with
+ * g2ohip_add_vertices / g2ohip_add_edges join the optimization without re-indexing the existing ones — each new free
+ * vertex (one that has an edge) takes the next hessian index, new vertices in id order; the next optimize / build
+ * continues from the current (optimized) state with the grown structure. Non-Schur graphs only, as in the reference:
+ * G2OHIP_ERR_UNSUPPORTED when the graph or a new vertex is marginalized (the reference aborts), G2OHIP_ERR_STATE
+ * before g2ohip_initialize. Calling g2ohip_initialize instead re-indexes every vertex in id order. */
+int g2ohip_update_initialization(g2ohip_graph* g);
 /* computeActiveErrors + activeRobustChi2 on the device */
 double g2ohip_chi2(g2ohip_graph* g);
 /* SparseOptimizer::optimize(iterations) with the device-resident LM loop.

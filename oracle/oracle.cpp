@@ -844,6 +844,39 @@ void initializeOptimization(Graph& G) {  // sparse_optimizer.cpp:201-279 (level 
   G.structureBuilt = false;
 }
 
+// sparse_optimizer.cpp:465-502 (updateInitialization) + block_solver.hpp:258-312 (updateStructure), online mode: the
+// vertices that gained edges since the last initialization are appended to the index mapping (free ones take the next
+// hessian indices; the reference walks the caller's vertex set, here the new vertices in id order); the existing
+// vertices keep their indices. The next LM iteration 0 rebuilds Hpp over the grown mapping — the same blocks the
+// reference's updateStructure adds to its Hpp — and the linear solver re-analyses (LinearSolverCSparse::init).
+// Marginalized vertices: -3 (the reference aborts, sparse_optimizer.cpp:491-492; Schur unsupported :274-277).
+int updateInitialization(Graph& G) {
+  if (G.ivMap.empty()) return -1;
+  for (int vi : G.ivMap)
+    if (G.verts[vi].marginalized) return -3;
+  std::vector<char> was(G.verts.size(), 0);
+  for (int vi : G.activeVertices) was[vi] = 1;
+  std::vector<int> fresh;
+  for (size_t k = 0; k < G.verts.size(); ++k)
+    if (!was[k] && !G.verts[k].edges.empty()) fresh.push_back((int)k);
+  std::sort(fresh.begin(), fresh.end(), [&](int a, int b) { return G.verts[a].id < G.verts[b].id; });
+  for (int vi : fresh)
+    if (!G.verts[vi].fixed && G.verts[vi].marginalized) return -3;
+  for (int vi : fresh) {
+    G.activeVertices.push_back(vi);
+    Vertex& v = G.verts[vi];
+    if (v.fixed) {
+      v.hessianIndex = -1;
+      continue;
+    }
+    v.hessianIndex = (int)G.ivMap.size();
+    G.ivMap.push_back(vi);
+  }
+  G.initialized = true;
+  G.structureBuilt = false;
+  return 0;
+}
+
 void computeActiveErrors(Graph& G, int threads) {  // sparse_optimizer.cpp:63-90
   const int ne = (int)G.edges.size();
 #pragma omp parallel for num_threads(threads) if (ne > 50)
@@ -1663,6 +1696,8 @@ int oracle_initialize(OracleGraph* og) {
   initializeOptimization(og->g);
   return 0;
 }
+
+int oracle_update_initialization(OracleGraph* og) { return updateInitialization(og->g); }
 
 double oracle_chi2(OracleGraph* og) {
   computeActiveErrors(og->g, 1);

@@ -73,6 +73,8 @@ int oracle_get_estimates(OracleGraph* g, int type, double* out, int* ids_out);
 int oracle_minimal_state(OracleGraph* g, double* out);
 
 int oracle_initialize(OracleGraph* g);
+/* SparseOptimizer::updateInitialization + BlockSolver::updateStructure (online, non-Schur); -3 for Schur graphs */
+int oracle_update_initialization(OracleGraph* g);
 double oracle_chi2(OracleGraph* g); /* computeActiveErrors + activeRobustChi2 */
 int oracle_optimize(OracleGraph* g, const oracle_config* cfg, int iterations, oracle_batch_stats* stats);
 

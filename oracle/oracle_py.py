@@ -61,6 +61,7 @@ def lib():
         L.oracle_get_estimates.argtypes = [P, I, P, P]
         L.oracle_minimal_state.argtypes = [P, P]
         L.oracle_initialize.argtypes = [P]
+        L.oracle_update_initialization.argtypes = [P]
         L.oracle_chi2.argtypes = [P]
         L.oracle_chi2.restype = D
         L.oracle_optimize.argtypes = [P, P, I, P]
@@ -155,6 +156,28 @@ class OracleGraph:
     def chi2(self) -> float:
         lib().oracle_initialize(self.h)
         return lib().oracle_chi2(self.h)
+
+    def initialize(self):
+        lib().oracle_initialize(self.h)
+
+    def update_initialization(self) -> int:
+        """sparse_optimizer.cpp:465-502 + block_solver.hpp:258-312 (online, non-Schur): 0 ok, <0 refused."""
+        return lib().oracle_update_initialization(self.h)
+
+    def add_vertices(self, vs):
+        ids = np.ascontiguousarray(vs.ids, np.int32)
+        est = np.ascontiguousarray(vs.est, np.float64)
+        fx = np.ascontiguousarray(vs.fixed, np.int32)
+        mg = np.ascontiguousarray(vs.marginalized, np.int32)
+        assert lib().oracle_add_vertices(self.h, vs.vtype, len(ids), _p(ids), _p(est), _p(fx), _p(mg)) == 0
+
+    def add_edges(self, es):
+        v0 = np.ascontiguousarray(es.v0, np.int32)
+        v1 = np.ascontiguousarray(es.v1, np.int32)
+        meas = np.ascontiguousarray(es.meas, np.float64)
+        info = np.ascontiguousarray(es.info, np.float64)
+        par = None if es.params is None else np.ascontiguousarray(es.params, np.float64)
+        assert lib().oracle_add_edges(self.h, es.etype, len(v0), _p(v0), _p(v1), _p(meas), _p(info), _p(par)) == 0
 
     def optimize(self, iterations=10, cfg: Config | None = None):
         cfg = cfg or make_config()

@@ -1832,6 +1832,9 @@ void Engine::refresh_host_payload(bool jacobians) {
   }
 }
 
+// the Kt records of nrec observations stay cache-resident between the linearize and camera passes (MALL)
+static bool kx_records_cached(double nrec) { return nrec * 80.0 <= 192.0 * (1 << 20); }
+
 void Engine::setup_edges_device() {
   // landmark shards: contiguous ranges of the hessian order, aligned with the factorization's cut (align_shards) or
   // the uniform split
@@ -1992,11 +1995,38 @@ void Engine::setup_edges_device() {
     fz_chunks.upload(chunks.empty() ? std::vector<int4>{int4{0, 0, -1, 0}} : chunks, stream);
     fz_fix.upload(fix.empty() ? std::vector<int4>{int4{0, 0, 0, 0}} : fix, stream);
     fz_lpart.resize((size_t)std::max(npart, 1) * 9);
-    // camera-major copy of the observations of every free camera (edge order within a camera: landmark-major)
+    // camera-major copy of the observations of every free camera. Edge order within a camera (G2OHIP_CAM_ORDER, dev
+    // A/B): 1 (default for the re-linearising camera pass) by the landmark's first observing camera, then landmark-major — neighbouring cameras, which run
+    // side by side on one XCD, then sweep their landmarks in step and re-read them from that L2 (a landmark's observers
+    // lie in one window of cameras, its id anywhere); 0 landmark-major (the gathers of U, c and the point then land
+    // on lines no other in-flight camera touches soon; C5 camera pass 0.407-0.409 -> 0.374-0.376 ms, L2 hit rate 62 %
+    // before, profiles/r06_ab_camorder_c5.log, r06_pmc_c5_l2.csv)
     std::vector<std::vector<int>> lists(num_poses);
     for (int k = 0; k < g.ne; ++k) {
       const int h = hidx[es.ev1[g.edges[k]]];
       if (h >= 0 && h < num_poses) lists[h].push_back(k);
+    }
+    {
+      // (only where the camera pass re-linearises from the per-landmark data: the records path gathers the 80-byte
+      // records in camera order, which the landmark-major order keeps ascending; C4 0.047 vs 0.048-0.049 ms)
+      const char* co = getenv("G2OHIP_CAM_ORDER");
+      const int cam_order = co ? atoi(co) : (kx_records_cached((double)g.ne) ? 0 : 1);
+      if (cam_order != 0) {
+        std::vector<int> first(g.ne, INT_MAX);  // per edge: its landmark's first free observing camera
+        for (int k = 0; k < g.ne;) {           // the group is landmark-major: one run of edges per landmark
+          int k2 = k, mc = INT_MAX;
+          const int v = es.ev0[g.edges[k]];
+          while (k2 < g.ne && es.ev0[g.edges[k2]] == v) {
+            const int h = hidx[es.ev1[g.edges[k2]]];
+            if (h >= 0 && h < num_poses) mc = std::min(mc, h);
+            ++k2;
+          }
+          for (int j = k; j < k2; ++j) first[j] = mc;
+          k = k2;
+        }
+        for (auto& L : lists)
+          std::stable_sort(L.begin(), L.end(), [&](int x, int y) { return first[x] < first[y]; });
+      }
     }
     std::vector<int> ptr(num_poses + 1, 0), cv0, cv1;
     std::vector<double> cmeas, cinfo, cpar;
@@ -2863,7 +2893,7 @@ int Engine::build_system_split(double lambda, const double* lamp) {  // block_so
       // G2OHIP_CAM_KX=0 / 1 forces either (A/B)
       static EnvKnob cam_kx{"G2OHIP_CAM_KX", -1};
       const int ck = cam_kx.get();
-      const bool use_ck = ck == 1 || (ck < 0 && ((double)nHpl + n_kx_extra) * 80.0 <= 192.0 * (1 << 20));
+      const bool use_ck = ck == 1 || (ck < 0 && kx_records_cached((double)nHpl + n_kx_extra));
       sp.cm_hpl = fz_kx && use_ck ? cm_hpl.get() : nullptr;
       sp.kx_extra = fz_kx ? kx_extra.get() : nullptr;
       sp.hpl_base = (long long)nHpp * pd * pd;

@@ -99,6 +99,8 @@ __device__ __forceinline__ void edge_terms_at(const EdgeData& d, int e, int v0, 
 constexpr int KXB = 10;
 
 template <class F, bool FG, bool KX = false>
+// (KX: 20 KB of LDS and 70 VGPRs, seven waves per SIMD; C5 0.51 -> 0.46 ms, C4 53 -> 45 us against five with the U
+// records in LDS; eight, forced by __launch_bounds__, spill 20 B per lane and gain nothing: profiles/r06_ab_lin_c{4,5}.log)
 __global__ void __launch_bounds__(256)
     k_linearize_fused(EdgeData d, const int4* __restrict__ chunks, int nchunks, const int* __restrict__ h0,
                       const int* __restrict__ h1, const long long* __restrict__ off_dst,
@@ -108,11 +110,12 @@ __global__ void __launch_bounds__(256)
   constexpr int D = F::D, DA = F::DA, DB = F::DB;
   constexpr int UF = 2 * DA;  // U record of a DA = 3 landmark (FG instantiations are BA only)
   // per-lane LDS image: landmark terms (+ U records with a split), or the lane's stored block (G / Hpl, or a Kt record)
-  constexpr int SA = DA * (DA + 1) / 2 + DA, SH = DA * DB, SB0 = KX ? 10 : SH, SL0 = FG ? SA + UF : SA;
-  constexpr int SM = SL0 > SB0 ? SL0 : SB0;
-  static_assert(!FG || (DA == 3 && 64 * SA + 64 * UF <= 64 * SM), "U records live behind the landmark terms");
+  // (the U records reach the segment's lanes from the head lane's registers by __shfl: an LDS image of them behind
+  // the landmark terms made the stage 15 doubles per lane and left 5 waves per SIMD, LDS-bound)
+  constexpr int SA = DA * (DA + 1) / 2 + DA, SH = DA * DB, SB0 = KX ? 10 : SH;
+  constexpr int SM = SA > SB0 ? SA : SB0;
+  static_assert(!FG || DA == 3, "U records of DA = 3 landmarks");
   __shared__ __attribute__((aligned(16))) double stage[4][64 * SM];
-  __shared__ int lmid[4][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wave = blockIdx.x * 4 + w;
   if (wave >= nchunks) return;  // wave-uniform
@@ -266,15 +269,22 @@ __global__ void __launch_bounds__(256)
       for (int r = 0; r < D; ++r) s += A[r * DA + i] * wr[r];
       o[k++] = nfA ? s : 0.0;
     }
-    lmid[w][lane] = pv;
   }
   wsync();
-  const bool head = in && (lane == 0 || lmid[w][lane - 1] != pv);
+  // segment heads by shuffles (no LDS word per lane: the stage alone sets the occupancy, eight waves per SIMD)
+  const int pv_prev = __shfl_up(pv, 1, 64);
+  const bool head = in && (lane == 0 || pv_prev != pv);
+  const unsigned long long heads = __ballot(head);
+  const unsigned long long above = lane == 63 ? 0ull : heads & ~((2ull << lane) - 1);  // heads past this lane
+  const int seg_end = above ? __builtin_ctzll(above) : nw;
+  double Uh[FG ? UF : 1];  // a head lane's U record (split: its landmark's)
+#pragma unroll
+  for (int k = 0; k < (FG ? UF : 1); ++k) Uh[k] = 0.0;
   if (head && nfA) {
     double acc[SA];
 #pragma unroll
     for (int k = 0; k < SA; ++k) acc[k] = sw[lane * SA + k];
-    for (int j = lane + 1; j < nw && lmid[w][j] == pv; ++j)
+    for (int j = lane + 1; j < seg_end; ++j)
 #pragma unroll
       for (int k = 0; k < SA; ++k) acc[k] += sw[j * SA + k];
     if (ch.z < 0) {
@@ -311,7 +321,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int k2 = 0; k2 < UF; ++k2) {
           Uo[k2] = U[k2];
-          sw[64 * SA + lane * UF + k2] = U[k2];
+          if constexpr (FG) Uh[k2] = U[k2];
         }
 #pragma unroll
         for (int i = 0; i < DA; ++i) co[i] = cl[i];
@@ -324,13 +334,12 @@ __global__ void __launch_bounds__(256)
   if constexpr (FG) {
     wsync();
     // the lane's segment head: the highest head lane at or below it
-    const unsigned long long hm = __ballot(head);
     const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1);
-    const int hl = 63 - __clzll(hm & le);
+    const int hl = 63 - __clzll(heads & le);
     double U[UF];
 #pragma unroll
-    for (int k = 0; k < UF; ++k) U[k] = sw[64 * SA + (hl & 63) * UF + k];
-    wsync();  // every U read before the run image reuses the stage
+    for (int k = 0; k < UF; ++k) U[k] = __shfl(Uh[k], hl & 63, 64);
+    wsync();  // every lane's landmark terms read before the run image reuses the stage
     off_block(U);
   }
 }

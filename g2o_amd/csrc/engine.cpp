@@ -2501,6 +2501,9 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       const char* ssk = getenv("G2OHIP_SCHUR_SKIP");  // dev A/B: 0 = every rank runs every row chunk and camera
       const bool sch_skip = dist_aligned && nranks > 1 && comm && !write_debug && !(dvr && atoi(dvr) == 0) &&
                             !(ssk && atoi(ssk) == 0);
+      // G2OHIP_SCHUR_BALANCE (dev A/B): 1 slot-balanced batches (build_batches), 0 batches in landmark order
+      const char* sbal = getenv("G2OHIP_SCHUR_BALANCE");
+      const bool sch_balance = !(sbal && atoi(sbal) == 0);
       const char* sst = getenv("G2OHIP_SCHUR_SPLIT_TASKS");
       const int split_target = sst ? atoi(sst) : (nranks > 1 && comm ? 2048 : 0);
       auto blk_owner = [&](int i, int j) { return al_bowner[std::min(al_bpinv[i], al_bpinv[j])]; };
@@ -2516,6 +2519,8 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       struct P3 { int ls, a, b; };
       std::vector<P3> cur;
       std::vector<std::pair<int, int>> tmp;
+      std::vector<int3> bal_items;                   // (observation, first partner in bal_part, partners)
+      std::vector<std::pair<int, int>> bal_part;     // (partner observation, slot)
       npairs = 0;
       // pass 1: per row chunk its staged blocks (0: no local pair) and whether it must run at all
       std::vector<long long> ch_staged;
@@ -2596,6 +2601,70 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
             cur.clear();
             bst0 = (int)st_obs.size();
           };
+          if (np == 1 && sch_balance) {
+            // slot-balanced batches: a batch's pair loop lasts as long as its busiest slot's pair list (four lanes per
+            // slot, one barrier per batch), so the row's observations are dealt to the batches greedily — most partners
+            // first, each to the batch (of those with room, among a window of candidates) where its busiest slot stays
+            // lowest — instead of in landmark order; each batch keeps its observations in landmark order
+            bal_items.clear();
+            bal_part.clear();
+            long long stt = 0;
+            for (int r = rptr[i]; r < rptr[i + 1]; ++r) {
+              const int a = robs[r], l = obs_lm[a];
+              const int o0 = (int)bal_part.size();
+              for (int a2 = a + 1; a2 < lm_ptr[l + 1]; ++a2) {
+                const int sl = camslot[blk_pose[a2]] - off_lo;
+                if (sl >= 0 && sl < T.noff) bal_part.push_back({a2, sl});
+              }
+              const int n = (int)bal_part.size() - o0;
+              if (n) { bal_items.push_back(int3{a, o0, n}); stt += 1 + n; }
+            }
+            int nbt = (int)std::max<long long>(1, (stt + SB - 1) / SB);
+            std::vector<int> cap(nbt, 0), cnt((size_t)nbt * SL, 0), asg(bal_items.size(), -1), ord(bal_items.size());
+            std::iota(ord.begin(), ord.end(), 0);
+            std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return bal_items[x].z > bal_items[y].z; });
+            constexpr int WIN = 16;  // candidate batches per observation (a rotating window: bounded setup time)
+            for (size_t q = 0; q < ord.size(); ++q) {
+              const int3 it = bal_items[ord[q]];
+              const int need = 1 + it.z;
+              int best = -1, bv = INT_MAX, bc = INT_MAX;
+              auto consider = [&](int b) {
+                if (cap[b] + need > SB) return;
+                int v = 0;
+                for (int k = 0; k < it.z; ++k) v = std::max(v, cnt[(size_t)b * SL + bal_part[it.y + k].second] + 1);
+                if (v < bv || (v == bv && cap[b] < bc)) { bv = v; bc = cap[b]; best = b; }
+              };
+              const int w = std::min(WIN, nbt);
+              for (int k = 0; k < w; ++k) consider((int)((q + k) % nbt));
+              if (best < 0)
+                for (int b = 0; b < nbt; ++b) consider(b);
+              if (best < 0) {  // no batch has room: a new one
+                best = nbt++;
+                cap.push_back(0);
+                cnt.resize((size_t)nbt * SL, 0);
+              }
+              asg[ord[q]] = best;
+              cap[best] += need;
+              for (int k = 0; k < it.z; ++k) cnt[(size_t)best * SL + bal_part[it.y + k].second]++;
+            }
+            for (int b = 0; b < nbt; ++b) {
+              for (size_t k = 0; k < bal_items.size(); ++k) {
+                if (asg[k] != b) continue;
+                const int3 it = bal_items[k];
+                const int posA = (int)st_obs.size() - bst0;
+                st_obs.push_back(gpos[it.x]);
+                st_obs_h.push_back(it.x);
+                for (int m = 0; m < it.z; ++m) {
+                  const auto& pr = bal_part[it.y + m];
+                  const int posB = (int)st_obs.size() - bst0;
+                  st_obs.push_back(gpos[pr.first]);
+                  st_obs_h.push_back(pr.first);
+                  cur.push_back(P3{pr.second, posA, posB});
+                }
+              }
+              flush();
+            }
+          } else
           for (int r = rptr[i]; r < rptr[i + 1]; ++r) {
             const int a = robs[r], l = obs_lm[a];
             tmp.clear();

@@ -2210,6 +2210,56 @@ void Engine::align_shards() {
   dist_aligned = true;
 }
 
+// Slot-balanced batches of one Schur row chunk (Engine::build_structure): items = (observation, first partner in part,
+// partners), part = (partner observation, slot). A batch's pair loop lasts as long as its busiest slot's pair list (four
+// lanes per slot, one barrier per batch), so the observations are dealt greedily — most partners first, each to the
+// batch, among a rotating window of WIN batches with room, where its busiest slot stays lowest (ties: the emptier one) —
+// within batches of at most sb staged records. asg[k] = item k's batch; returns the batch count.
+static int balance_batches(const std::vector<int3>& items, const std::vector<std::pair<int, int>>& part, int sb, int sl,
+                           int* asg, std::vector<int>& cap, std::vector<int>& cnt, std::vector<int>& ord,
+                           std::vector<int>& opn) {
+  constexpr int WIN = 8;  // a model of C4's rows: 8 candidates and all open batches balance alike, 4 worse
+  long long stt = 0;
+  for (const int3& it : items) stt += 1 + it.z;
+  int nbt = (int)std::max<long long>(1, (stt + sb - 1) / sb);
+  cap.assign(nbt, 0);
+  cnt.assign((size_t)nbt * sl, 0);
+  ord.resize(items.size());
+  std::iota(ord.begin(), ord.end(), 0);
+  std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return items[x].z > items[y].z; });
+  opn.resize(nbt);
+  std::iota(opn.begin(), opn.end(), 0);
+  for (size_t q = 0; q < ord.size(); ++q) {
+    const int3 it = items[ord[q]];
+    const int need = 1 + it.z;
+    int best = -1, bv = INT_MAX, bc = INT_MAX;
+    auto consider = [&](int b) {
+      if (cap[b] + need > sb) return;
+      int v = 0;
+      for (int k = 0; k < it.z; ++k) v = std::max(v, cnt[(size_t)b * sl + part[it.y + k].second] + 1);
+      if (v < bv || (v == bv && cap[b] < bc)) { bv = v; bc = cap[b]; best = b; }
+    };
+    // candidates: a rotating window over the batches that still have room for the smallest observation
+    const int no = (int)opn.size(), w = std::min(WIN, no);
+    for (int k = 0; k < w; ++k) consider(opn[(q + k) % no]);
+    if (best < 0)
+      for (int k = 0; k < no; ++k) consider(opn[k]);
+    if (best < 0) {  // no batch has room: a new one
+      best = nbt++;
+      cap.push_back(0);
+      cnt.resize((size_t)nbt * sl, 0);
+      opn.push_back(best);
+    }
+    asg[ord[q]] = best;
+    cap[best] += need;
+    for (int k = 0; k < it.z; ++k) cnt[(size_t)best * sl + part[it.y + k].second]++;
+    if (cap[best] + 2 > sb)  // full for every observation (each stages itself and a partner at least)
+      for (int k = 0; k < (int)opn.size(); ++k)
+        if (opn[k] == best) { opn[k] = opn.back(); opn.pop_back(); break; }
+  }
+  return nbt;
+}
+
 // staged Kt records per Schur row batch (G2OHIP_SCHUR_SB_KX: 128, 192 or 256; A/B)
 int Engine::kx_batch_size() {
   const char* v = getenv("G2OHIP_SCHUR_SB_KX");
@@ -2521,9 +2571,11 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       std::vector<std::pair<int, int>> tmp;
       std::vector<int3> bal_items;                   // (observation, first partner in bal_part, partners)
       std::vector<std::pair<int, int>> bal_part;     // (partner observation, slot)
+      std::vector<int> bal_bptr, bal_seq, bal_fill;  // (reused across rows)
       npairs = 0;
       // pass 1: per row chunk its staged blocks (0: no local pair) and whether it must run at all
       std::vector<long long> ch_staged;
+      std::vector<int> ch_items;
       std::vector<unsigned char> ch_live;
       for (int i = 0; i < num_poses; ++i) {
         const int s_lo = srow_ptr[i], s_hi = srow_ptr[i + 1];
@@ -2532,6 +2584,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         for (int ch = 0; ch * SL < noff_total; ++ch) {
           const int off_lo = 1 + ch * SL, noff = std::min(SL, noff_total - ch * SL);
           long long st = 0;
+          int nit = 0;  // observations with a partner in the chunk
           for (int r = rptr[i]; r < rptr[i + 1]; ++r) {
             const int a = robs[r], l = obs_lm[a];
             int np = 0;
@@ -2539,7 +2592,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
               const int sl = camslot[blk_pose[a2]] - off_lo;
               np += sl >= 0 && sl < noff;
             }
-            if (np) st += 1 + np;
+            if (np) { st += 1 + np; ++nit; }
           }
           bool live = st > 0 || !sch_skip;
           for (int k = 0; k < noff && !live; ++k) {
@@ -2547,6 +2600,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
             live = o < 0 || o == rank;
           }
           ch_staged.push_back(st);
+          ch_items.push_back(nit);
           ch_live.push_back(live ? 1 : 0);
         }
         for (int k = s_lo; k < s_hi; ++k) camslot[s_bj[k]] = -1;
@@ -2554,6 +2608,58 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       long long nlive = 0;
       for (size_t c = 0; c < ch_live.size(); ++c) nlive += ch_live[c];
       const int P = split_target > 0 && nlive > 0 ? (int)std::min<long long>(8, std::max<long long>(1, (split_target + nlive - 1) / nlive)) : 1;
+      // slot-balanced batches (see the emission below): every balanced chunk's observation -> batch assignment, rows in
+      // parallel (host threads; the greedy is the structure build's largest host step at C5), stored per chunk item
+      std::vector<long long> bal_off(ch_items.size() + 1, 0);
+      for (size_t c = 0; c < ch_items.size(); ++c) bal_off[c + 1] = bal_off[c] + ch_items[c];
+      std::vector<int> bal_asg_all(sch_balance ? (size_t)std::max<long long>(bal_off.back(), 1) : 1, -1);
+      std::vector<int> bal_nb_all(sch_balance ? ch_items.size() : 0, 0);
+      if (sch_balance) {
+        std::vector<long long> row_c0(num_poses + 1, 0);  // first chunk index of each row
+        for (int i = 0; i < num_poses; ++i) {
+          const int noff_total = srow_ptr[i + 1] - srow_ptr[i] - 1;
+          row_c0[i + 1] = row_c0[i] + (noff_total > 0 ? (noff_total + SL - 1) / SL : 0);
+        }
+        const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::atomic<int> next_row{0};
+        auto work = [&]() {
+          std::vector<int> cs(num_poses, -1), cap, cnt, ord, opn;
+          std::vector<int3> items;
+          std::vector<std::pair<int, int>> part;
+          for (int i; (i = next_row.fetch_add(1)) < num_poses;) {
+            const int s_lo = srow_ptr[i], s_hi = srow_ptr[i + 1];
+            for (int k = s_lo; k < s_hi; ++k) cs[s_bj[k]] = k - s_lo;
+            const int noff_total = s_hi - s_lo - 1;
+            for (int ch = 0; ch * SL < noff_total; ++ch) {
+              const size_t cidx = (size_t)row_c0[i] + ch;
+              if (!ch_live[cidx]) continue;
+              const long long tot = ch_staged[cidx];
+              const int npart = (int)std::max<long long>(1, std::min<long long>(P, tot / (2LL * SB)));
+              if (npart != 1) continue;
+              const int off_lo = 1 + ch * SL, noff = std::min(SL, noff_total - ch * SL);
+              items.clear();
+              part.clear();
+              for (int r = rptr[i]; r < rptr[i + 1]; ++r) {
+                const int a = robs[r], l = obs_lm[a];
+                const int o0 = (int)part.size();
+                for (int a2 = a + 1; a2 < lm_ptr[l + 1]; ++a2) {
+                  const int sl = cs[blk_pose[a2]] - off_lo;
+                  if (sl >= 0 && sl < noff) part.push_back({a2, sl});
+                }
+                const int n = (int)part.size() - o0;
+                if (n) items.push_back(int3{a, o0, n});
+              }
+              int* asg = bal_asg_all.data() + bal_off[cidx];
+              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, asg, cap, cnt, ord, opn);
+            }
+            for (int k = s_lo; k < s_hi; ++k) cs[s_bj[k]] = -1;
+          }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nth; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+      }
       size_t cidx = 0;
       for (int i = 0; i < num_poses; ++i) {
         const int s_lo = srow_ptr[i], s_hi = srow_ptr[i + 1];
@@ -2608,7 +2714,6 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
             // lowest — instead of in landmark order; each batch keeps its observations in landmark order
             bal_items.clear();
             bal_part.clear();
-            long long stt = 0;
             for (int r = rptr[i]; r < rptr[i + 1]; ++r) {
               const int a = robs[r], l = obs_lm[a];
               const int o0 = (int)bal_part.size();
@@ -2617,40 +2722,23 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
                 if (sl >= 0 && sl < T.noff) bal_part.push_back({a2, sl});
               }
               const int n = (int)bal_part.size() - o0;
-              if (n) { bal_items.push_back(int3{a, o0, n}); stt += 1 + n; }
+              if (n) bal_items.push_back(int3{a, o0, n});
             }
-            int nbt = (int)std::max<long long>(1, (stt + SB - 1) / SB);
-            std::vector<int> cap(nbt, 0), cnt((size_t)nbt * SL, 0), asg(bal_items.size(), -1), ord(bal_items.size());
-            std::iota(ord.begin(), ord.end(), 0);
-            std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return bal_items[x].z > bal_items[y].z; });
-            constexpr int WIN = 16;  // candidate batches per observation (a rotating window: bounded setup time)
-            for (size_t q = 0; q < ord.size(); ++q) {
-              const int3 it = bal_items[ord[q]];
-              const int need = 1 + it.z;
-              int best = -1, bv = INT_MAX, bc = INT_MAX;
-              auto consider = [&](int b) {
-                if (cap[b] + need > SB) return;
-                int v = 0;
-                for (int k = 0; k < it.z; ++k) v = std::max(v, cnt[(size_t)b * SL + bal_part[it.y + k].second] + 1);
-                if (v < bv || (v == bv && cap[b] < bc)) { bv = v; bc = cap[b]; best = b; }
-              };
-              const int w = std::min(WIN, nbt);
-              for (int k = 0; k < w; ++k) consider((int)((q + k) % nbt));
-              if (best < 0)
-                for (int b = 0; b < nbt; ++b) consider(b);
-              if (best < 0) {  // no batch has room: a new one
-                best = nbt++;
-                cap.push_back(0);
-                cnt.resize((size_t)nbt * SL, 0);
-              }
-              asg[ord[q]] = best;
-              cap[best] += need;
-              for (int k = 0; k < it.z; ++k) cnt[(size_t)best * SL + bal_part[it.y + k].second]++;
+            const int nbt = bal_nb_all[cidx];
+            const int* asg = bal_asg_all.data() + bal_off[cidx];
+            // each batch's observations in landmark order: a counting sort of the items by batch (stable)
+            bal_bptr.assign(nbt + 1, 0);
+            for (size_t k = 0; k < bal_items.size(); ++k) bal_bptr[asg[k] + 1]++;
+            for (int b = 0; b < nbt; ++b) bal_bptr[b + 1] += bal_bptr[b];
+            bal_seq.resize(bal_items.size());
+            {
+              std::vector<int>& fillb = bal_fill;
+              fillb.assign(bal_bptr.begin(), bal_bptr.end() - 1);
+              for (size_t k = 0; k < bal_items.size(); ++k) bal_seq[fillb[asg[k]]++] = (int)k;
             }
             for (int b = 0; b < nbt; ++b) {
-              for (size_t k = 0; k < bal_items.size(); ++k) {
-                if (asg[k] != b) continue;
-                const int3 it = bal_items[k];
+              for (int kk = bal_bptr[b]; kk < bal_bptr[b + 1]; ++kk) {
+                const int3 it = bal_items[bal_seq[kk]];
                 const int posA = (int)st_obs.size() - bst0;
                 st_obs.push_back(gpos[it.x]);
                 st_obs_h.push_back(it.x);

@@ -2210,17 +2210,39 @@ void Engine::align_shards() {
   dist_aligned = true;
 }
 
+// Lane groups (pairs of lanes, 128 per k_schur_rows workgroup) per slot of a Kt-record Schur task, in proportion to the
+// slots' pairs in the task (T): every slot one, the rest one at a time to the slot with the most pairs per group (ties:
+// the lower slot). A batch's pair loop lasts as long as its slowest group.
+static void slot_groups(const long long* T, int noff, int* g) {
+  for (int s = 0; s < noff; ++s) g[s] = 1;
+  for (int extra = 128 - noff; extra > 0; --extra) {
+    int bs = 0;
+    double bv = -1.0;
+    for (int s = 0; s < noff; ++s) {
+      const double v = (double)T[s] / g[s];
+      if (v > bv) { bv = v; bs = s; }
+    }
+    ++g[bs];
+  }
+}
+
 // Slot-balanced batches of one Schur row chunk (Engine::build_structure): items = (observation, first partner in part,
 // partners), part = (partner observation, slot). A batch's pair loop lasts as long as its busiest slot's pair list (four
 // lanes per slot, one barrier per batch), so the observations are dealt greedily — most partners first, each to the
 // batch, among a rotating window of WIN batches with room, where its busiest slot stays lowest (ties: the emptier one) —
 // within batches of at most sb staged records. asg[k] = item k's batch; returns the batch count.
 static int balance_batches(const std::vector<int3>& items, const std::vector<std::pair<int, int>>& part, int sb, int sl,
-                           int* asg, std::vector<int>& cap, std::vector<int>& cnt, std::vector<int>& ord,
+                           int noff, int* asg, std::vector<int>& cap, std::vector<int>& cnt, std::vector<int>& ord,
                            std::vector<int>& opn) {
   constexpr int WIN = 8;  // a model of C4's rows: 8 candidates and all open batches balance alike, 4 worse
   long long stt = 0;
   for (const int3& it : items) stt += 1 + it.z;
+  // the slots' lane groups (slot_groups, as the task's lane map will have them): a batch's time on slot s is
+  // ceil(pairs / groups)
+  std::vector<long long> T(sl, 0);
+  for (const auto& pr : part) T[pr.second]++;
+  std::vector<int> gw(sl, 1);
+  slot_groups(T.data(), noff, gw.data());
   int nbt = (int)std::max<long long>(1, (stt + sb - 1) / sb);
   cap.assign(nbt, 0);
   cnt.assign((size_t)nbt * sl, 0);
@@ -2236,7 +2258,10 @@ static int balance_batches(const std::vector<int3>& items, const std::vector<std
     auto consider = [&](int b) {
       if (cap[b] + need > sb) return;
       int v = 0;
-      for (int k = 0; k < it.z; ++k) v = std::max(v, cnt[(size_t)b * sl + part[it.y + k].second] + 1);
+      for (int k = 0; k < it.z; ++k) {
+        const int q = part[it.y + k].second;
+        v = std::max(v, (cnt[(size_t)b * sl + q] + gw[q]) / gw[q]);  // ceil((count + 1) / groups)
+      }
       if (v < bv || (v == bv && cap[b] < bc)) { bv = v; bc = cap[b]; best = b; }
     };
     // candidates: a rotating window over the batches that still have room for the smallest observation
@@ -2538,6 +2563,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         std::vector<launch::SchurBatch> batches;
         std::vector<int> st_obs, st_obs_h, prs, pp;
         std::vector<launch::SchurPartGroup> groups;  // row chunks split into parts (their partial sums' reduction)
+        std::vector<int> gmap;  // per task 128 lane-group entries: slot | index << 8 | groups << 16 (Kt-record pass)
         long long npairs = 0, nparts_blocks = 0;
       };
       // Per-rank task lists of the landmark-sharded BA (aligned shards + the distributed factorization reading only its
@@ -2565,6 +2591,18 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       auto& prs = bs.prs;
       auto& pp = bs.pp;
       long long& npairs = bs.npairs;
+      // a task and its lane map (slot_groups over the pairs of its batches [b0, b1))
+      std::vector<long long> tslot(SL);
+      auto push_task = [&](const launch::SchurTask& T) {
+        std::fill(tslot.begin(), tslot.end(), 0);
+        for (int b = T.b0; b < T.b1; ++b)
+          for (int q = 0; q < SL; ++q) tslot[q] += pp[(size_t)b * (SL + 1) + q + 1] - pp[(size_t)b * (SL + 1) + q];
+        int g[SL];
+        slot_groups(tslot.data(), T.noff, g);
+        for (int q = 0; q < T.noff; ++q)
+          for (int k = 0; k < g[q]; ++k) bs.gmap.push_back(q | (k << 8) | (g[q] << 16));
+        tasks.push_back(T);
+      };
       std::vector<int> camslot(num_poses, -1);
       struct P3 { int ls, a, b; };
       std::vector<P3> cur;
@@ -2650,7 +2688,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
                 if (n) items.push_back(int3{a, o0, n});
               }
               int* asg = bal_asg_all.data() + bal_off[cidx];
-              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, asg, cap, cnt, ord, opn);
+              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, noff, asg, cap, cnt, ord, opn);
             }
             for (int k = s_lo; k < s_hi; ++k) cs[s_bj[k]] = -1;
           }
@@ -2766,7 +2804,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
             while (part < want) {  // the next part: a task of its own (the same slots, its own partial blocks)
               flush();
               T.b1 = (int)batches.size();
-              tasks.push_back(T);
+              push_task(T);
               ++part;
               T.b0 = (int)batches.size();
               T.pad = (int)xo + part * T.noff + 1;
@@ -2785,12 +2823,12 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
           }
           flush();
           T.b1 = (int)batches.size();
-          tasks.push_back(T);
+          push_task(T);
           if (np > 1 && part != np - 1) {  // trailing parts without observations: their partial blocks are zeros
             for (int q = part + 1; q < np; ++q) {
               T.b0 = T.b1 = (int)batches.size();
               T.pad = (int)xo + q * T.noff + 1;
-              tasks.push_back(T);
+              push_task(T);
             }
           }
         }
@@ -2826,6 +2864,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         sch_st_obs_h.upload(nz(bs.st_obs_h), stream);
         sch_pairs.upload(nz(bs.prs), stream);
         sch_pp.upload(nz(bs.pp), stream);
+        sch_gmap.upload(nz(bs.gmap), stream);
       }
       // the Kt-record set (BA split; decided with the split below): another block size needs its own batches
       kx_sb = kx_batch_size();
@@ -2842,6 +2881,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
         sch_st_obs_kx.upload(nz(bs.st_obs_h), stream);
         sch_pairs_kx.upload(nz(bs.prs), stream);
         sch_pp_kx.upload(nz(bs.pp), stream);
+        sch_gmap_kx.upload(nz(bs.gmap), stream);
       }
     }
     std::vector<int> shpp(nS, -1);
@@ -3192,13 +3232,13 @@ void Engine::solve_async(bool reset_fail) {  // block_solver.hpp:314-447
     launch::schur_rows(pd, ld, nsch_tasks_kx, sch_tasks_kx.get(), sch_batches_kx.get(), sch_st_obs_kx.get(),
                        sch_pairs_kx.get(), sch_pp_kx.get(), dG.get(), ds_hpp.get(), dH.get(), S,
                        zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(), stream, true, kx_sb,
-                       dSchurPart.get());
+                       dSchurPart.get(), sch_gmap_kx.get());
     launch::schur_part_sum(pd, nsch_groups_kx, sch_groups_kx.get(), dSchurPart.get(), ds_hpp.get(), dH.get(), S, stream);
   } else {
     launch::schur_rows(pd, ld, nsch_tasks, sch_tasks.get(), sch_batches.get(),
                        split ? sch_st_obs_h.get() : sch_st_obs.get(), sch_pairs.get(), sch_pp.get(), dG.get(),
                        ds_hpp.get(), dH.get(), S, zero_here ? chol.nzero : 0, chol.zero_rng.get(), chol.fronts.get(),
-                       stream, split && fz_kx, launch::SCHUR_SB, dSchurPart.get());
+                       stream, split && fz_kx, launch::SCHUR_SB, dSchurPart.get(), sch_gmap.get());
     launch::schur_part_sum(pd, nsch_groups, sch_groups.get(), dSchurPart.get(), ds_hpp.get(), dH.get(), S, stream);
   }
   timer.end(stream);

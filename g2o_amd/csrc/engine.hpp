@@ -407,6 +407,7 @@ class Engine {
   DevBuf<launch::SchurTask> sch_tasks;
   DevBuf<launch::SchurBatch> sch_batches;
   DevBuf<int> sch_st_obs, sch_pairs, sch_pp;
+  DevBuf<int> sch_gmap, sch_gmap_kx;  // per Schur task its 128 lane groups (slot_groups; the Kt-record pass)
   DevBuf<int> sch_st_obs_h;  // the same staged blocks as Hpl block indices (G in Hpl's order, Schur split)
   int nsch_tasks = 0;
   // the BA split's Kt-record batches (k_schur_rows<..., KX>) when their block size differs from launch::SCHUR_SB

@@ -624,6 +624,102 @@ __device__ __forceinline__ void schur_pairs_kx(const double* Gs, const int* sp, 
       }
   }
 }
+// The KX pair loop with a per-task lane map (gmap, built with the batches): lane pair (group) g of the task owns columns
+// 3 hi .. 3 hi + 2 of slot gs's block over the slot's pairs p = gk, gk + gn, ... of each batch (gn groups per slot, in
+// proportion to the slot's pairs in the task: a batch's pair loop lasts as long as its slowest group)
+__device__ __forceinline__ void schur_pairs_kx_g(const double* Gs, const int* sp, const int* spp, int gs, int gk, int gn,
+                                                 bool hi, double (&acc)[18]) {
+  constexpr int GB = 10;
+  const int p1 = spp[gs + 1];
+  for (int p = spp[gs] + gk; p < p1; p += gn) {
+    const int pr = sp[p];
+    const double* ga = &Gs[(pr & 0xffff) * GB];
+    const double* gb = &Gs[(pr >> 16) * GB];
+    double ka[6], kb[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double2 x = *reinterpret_cast<const double2*>(ga + 2 * k);
+      const double2 y = *reinterpret_cast<const double2*>(gb + 2 * k);
+      ka[2 * k] = x.x; ka[2 * k + 1] = x.y;
+      kb[2 * k] = y.x; kb[2 * k + 1] = y.y;
+    }
+    const double2 ua2 = *reinterpret_cast<const double2*>(ga + 6), ub2 = *reinterpret_cast<const double2*>(gb + 6);
+    const double ua = ua2.x, va = ua2.y, wa = ga[8], ub = ub2.x, vb = ub2.y, wb = gb[8];
+    double M[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) M[r][q] = ka[r] * kb[q] + ka[2 + r] * kb[2 + q] + ka[4 + r] * kb[4 + q];
+    double b0[3], b1[3];
+    if (!hi) {
+      b0[0] = ub * vb; b0[1] = -(1.0 + ub * ub); b0[2] = vb;
+      b1[0] = 1.0 + vb * vb; b1[1] = -(ub * vb); b1[2] = -ub;
+    } else {
+      b0[0] = -wb; b0[1] = 0.0; b0[2] = ub * wb;
+      b1[0] = 0.0; b1[1] = -wb; b1[2] = vb * wb;
+    }
+    double T0[3], T1[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      T0[j] = M[0][0] * b0[j] + M[0][1] * b1[j];
+      T1[j] = M[1][0] * b0[j] + M[1][1] * b1[j];
+    }
+    const double a0[6] = {ua * va, -(1.0 + ua * ua), va, -wa, 0.0, ua * wa};
+    const double a1[6] = {1.0 + va * va, -(ua * va), -ua, 0.0, -wa, va * wa};
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        if (r == 4) acc[j * 6 + r] += a1[r] * T1[j];
+        else if (r == 3) acc[j * 6 + r] += a0[r] * T0[j];
+        else acc[j * 6 + r] += a0[r] * T0[j] + a1[r] * T1[j];
+      }
+  }
+}
+// The grouped store: the gn groups of a slot add their sums in group order (through LDS, one column half at a time, red:
+// >= 128 x 18 doubles of free LDS), the slot's first group stores S(i, j) = Hpp(i, j) - sum (or the part block)
+__device__ __forceinline__ void schur_row_store_g(const double (&acc)[18], int gs, int gk, int gn, int noff, int soff,
+                                                  const int* s_hpp, const double* Hpp, double* S, int pidx, double* part,
+                                                  double* red) {
+  const int tid = threadIdx.x, g = tid >> 1, hi = tid & 1;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+    if (hi == h) {
+#pragma unroll
+      for (int e = 0; e < 18; ++e) red[g * 18 + e] = acc[e];
+    }
+    __syncthreads();
+    if (hi == h && gk == 0 && gs < noff) {
+      double sum[18];
+#pragma unroll
+      for (int e = 0; e < 18; ++e) sum[e] = red[g * 18 + e];
+      for (int k = 1; k < gn; ++k)
+#pragma unroll
+        for (int e = 0; e < 18; ++e) sum[e] += red[(g + k) * 18 + e];
+      const int c0 = 3 * h;
+      if (pidx > 0) {
+        double* Po = part + (size_t)(pidx - 1 + gs) * 36;
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int r = 0; r < 6; ++r) Po[(c0 + j) * 6 + r] = sum[j * 6 + r];
+      } else {
+        const int sidx = soff + gs;
+        const int hp = s_hpp[sidx];
+        const double* Hh = Hpp + (size_t)(hp >= 0 ? hp : 0) * 36;
+        double* So = S + (size_t)sidx * 36;
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+            const int k = (c0 + j) * 6 + r;
+            So[k] = (hp >= 0 ? Hh[k] : 0.0) - sum[j * 6 + r];
+          }
+      }
+    }
+  }
+}
 // Even + odd pairs (fixed order) and the S block store: thread (h, par) stores rows [0, CW) (par 0) or [CW, PD) (par 1)
 // of its columns; S(i, j) = Hpp(i, j) - sum
 // pidx > 0 (one part of a split row chunk): the part's sums go to part blocks pidx - 1 + ls, not S (k_schur_part_sum)
@@ -692,7 +788,7 @@ __global__ void __launch_bounds__(256, OCC)
                  const int* st_obs, const int* pairs, const int* pp,
                  const double* __restrict__ G, const int* __restrict__ s_hpp, const double* __restrict__ Hpp,
                  double* __restrict__ S, int mode, int ntasks, const long long* __restrict__ zr,
-                 double* __restrict__ fronts, double* __restrict__ part) {
+                 double* __restrict__ fronts, double* __restrict__ part, const int* __restrict__ gmap) {
   static_assert(!KX || (PD == 6 && LD == 3), "Kt records: BA blocks");
   constexpr int SCH_NI = (SCH_SB + 255) / 256;
   constexpr int GB = KX ? 10 : PD * LD;              // doubles per staged block: G, PD x LD col-major (or a Kt record)
@@ -710,7 +806,16 @@ __global__ void __launch_bounds__(256, OCC)
     for (long long i = threadIdx.x; i < len; i += 256) fronts[off + i] = 0.0;
     return;
   }
-  const launch::SchurTask t = tasks[xcd_item(blockIdx.x, ntasks)];  // XCD-contiguous rows
+  const int tix = xcd_item(blockIdx.x, ntasks);  // XCD-contiguous rows
+  const launch::SchurTask t = tasks[tix];
+  // KX: the task's lane map (slot, index among the slot's groups, groups of the slot) for this thread's lane pair
+  int gs = 0, gk = 0, gn = 1;
+  if constexpr (KX) {
+    const int gm = gmap[(size_t)tix * 128 + (threadIdx.x >> 1)];
+    gs = gm & 0xff;
+    gk = (gm >> 8) & 0xff;
+    gn = gm >> 16;
+  }
   const int nb = t.b1 - t.b0;
   const int tid = threadIdx.x, w = tid >> 6;
   const int ls = tid >> 2, q = tid & 3;
@@ -751,7 +856,7 @@ __global__ void __launch_bounds__(256, OCC)
     }
   };
   auto compute = [&](int buf, int ib) {
-    if constexpr (KX) schur_pairs_kx(Gs[buf], sp[ib], spp[ib], t.noff, ls, q, acc);
+    if constexpr (KX) schur_pairs_kx_g(Gs[buf], sp[ib], spp[ib], gs, gk, gn, threadIdx.x & 1, acc);
     else schur_pairs<PD, LD>(Gs[buf], sp[ib], spp[ib], t.noff, ls, q, acc);
   };
   // index loads the pipelined passes count with vmcnt. Their pointers are not __restrict__ and every counted wait is
@@ -836,7 +941,8 @@ __global__ void __launch_bounds__(256, OCC)
       B2 = B3;
       B3 = B4;
     }
-    schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S, t.pad, part);
+    if constexpr (KX) schur_row_store_g(acc, gs, gk, gn, t.noff, t.soff, s_hpp, Hpp, S, t.pad, part, &Gs[0][0]);
+    else schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S, t.pad, part);
     return;
   }
 
@@ -867,7 +973,8 @@ __global__ void __launch_bounds__(256, OCC)
     B1 = B2;
     B2 = B3;
   }
-  schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S, t.pad, part);
+  if constexpr (KX) schur_row_store_g(acc, gs, gk, gn, t.noff, t.soff, s_hpp, Hpp, S, t.pad, part, &Gs[0][0]);
+  else schur_row_store<PD>(acc, ls, q, t.noff, t.soff, s_hpp, Hpp, S, t.pad, part);
 }
 
 // back-substitution: x_l = Dinv_l (b_l - sum_a Hpl_a^T x_pose(a)); LANES lanes per landmark stride over
@@ -1540,7 +1647,8 @@ void schur_part_sum(int pd, int ngroups, const SchurPartGroup* groups, const dou
 }
 void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
-                int nzero, const long long* zr, double* fronts, hipStream_t s, bool kx, int sb, double* part) {
+                int nzero, const long long* zr, double* fronts, hipStream_t s, bool kx, int sb, double* part,
+                const int* gmap) {
   if (ntasks <= 0 && nzero <= 0) return;
 #ifdef G2OHIP_DEV  // development build only: 1 no pair products, 2 no staging, 3 neither (wrong S, timing splits)
   static const int mode = getenv("G2OHIP_SCHUR_MODE") ? atoi(getenv("G2OHIP_SCHUR_MODE")) : 0;
@@ -1552,15 +1660,16 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
   const int nz = nzero > 0 ? nzero : 0;
   if (kx) {  // BA split: G rebuilt from the Kt records
     if (pd != 6 || ld != 3) throw DeviceError("schur_rows: Kt records need BlockSolver_6_3 blocks");
+    if (!gmap && ntasks > 0) throw DeviceError("schur_rows: Kt records need the tasks' lane map");
     // (108 VGPRs: four workgroups per CU; a register budget for five or six spills 8 / 35 VGPRs at 128-block batches)
     auto go = [&](auto SBc) {
       constexpr int SBK = decltype(SBc)::value;
       if (pipe == 0)
         hipLaunchKernelGGL((k_schur_rows<6, 3, 0, true, SBK>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs,
-                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts, part);
+                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts, part, gmap);
       else
         hipLaunchKernelGGL((k_schur_rows<6, 3, 1, true, SBK>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs,
-                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts, part);
+                           pp, G, s_hpp, Hpp, S, mode, ntasks, zr, fronts, part, gmap);
     };
     if (sb == 128) go(std::integral_constant<int, 128>{});
     else if (sb == 192) go(std::integral_constant<int, 192>{});
@@ -1573,10 +1682,10 @@ void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurB
     constexpr int pv = decltype(P)::value, lv = decltype(L)::value;
     if (pipe == 0)
       hipLaunchKernelGGL((k_schur_rows<pv, lv, 0>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs, pp, G, s_hpp,
-                         Hpp, S, mode, ntasks, zr, fronts, part);
+                         Hpp, S, mode, ntasks, zr, fronts, part, gmap);
     else
       hipLaunchKernelGGL((k_schur_rows<pv, lv, 1>), ntasks + nz, 256, 0, s, tasks, batches, st_obs, pairs, pp, G, s_hpp,
-                         Hpp, S, mode, ntasks, zr, fronts, part);
+                         Hpp, S, mode, ntasks, zr, fronts, part, gmap);
   });
   KERNEL_CHECK();
 }

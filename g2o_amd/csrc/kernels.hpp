@@ -109,7 +109,7 @@ struct SchurBatch {
 void schur_rows(int pd, int ld, int ntasks, const SchurTask* tasks, const SchurBatch* batches, const int* st_obs,
                 const int* pairs, const int* pp, const double* G, const int* s_hpp, const double* Hpp, double* S,
                 int nzero, const long long* zr, double* fronts, hipStream_t s, bool kx = false,
-                int sb = SCHUR_SB, double* part = nullptr);
+                int sb = SCHUR_SB, double* part = nullptr, const int* gmap = nullptr);
 // the split row chunks' partial sums into S (fixed part order: bitwise reproducible)
 void schur_part_sum(int pd, int ngroups, const SchurPartGroup* groups, const double* part, const int* s_hpp,
                     const double* Hpp, double* S, hipStream_t s);

@@ -2232,17 +2232,17 @@ static void slot_groups(const long long* T, int noff, int* g) {
 // batch, among a rotating window of WIN batches with room, where its busiest slot stays lowest (ties: the emptier one) —
 // within batches of at most sb staged records. asg[k] = item k's batch; returns the batch count.
 static int balance_batches(const std::vector<int3>& items, const std::vector<std::pair<int, int>>& part, int sb, int sl,
-                           int noff, int* asg, std::vector<int>& cap, std::vector<int>& cnt, std::vector<int>& ord,
+                           int noff, bool prop, int* asg, std::vector<int>& cap, std::vector<int>& cnt, std::vector<int>& ord,
                            std::vector<int>& opn) {
   constexpr int WIN = 8;  // a model of C4's rows: 8 candidates and all open batches balance alike, 4 worse
   long long stt = 0;
   for (const int3& it : items) stt += 1 + it.z;
-  // the slots' lane groups (slot_groups, as the task's lane map will have them): a batch's time on slot s is
-  // ceil(pairs / groups)
+  // the slots' lane groups (prop: slot_groups, as the Kt-record pass's lane map will have them; else two pair streams per
+  // slot): a batch's time on slot s is ceil(pairs / groups)
   std::vector<long long> T(sl, 0);
   for (const auto& pr : part) T[pr.second]++;
-  std::vector<int> gw(sl, 1);
-  slot_groups(T.data(), noff, gw.data());
+  std::vector<int> gw(sl, 2);  // (the G-block pass: four lanes per slot, two pair streams)
+  if (prop) slot_groups(T.data(), noff, gw.data());
   int nbt = (int)std::max<long long>(1, (stt + sb - 1) / sb);
   cap.assign(nbt, 0);
   cnt.assign((size_t)nbt * sl, 0);
@@ -2583,7 +2583,8 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       const char* sst = getenv("G2OHIP_SCHUR_SPLIT_TASKS");
       const int split_target = sst ? atoi(sst) : (nranks > 1 && comm ? 2048 : 0);
       auto blk_owner = [&](int i, int j) { return al_bowner[std::min(al_bpinv[i], al_bpinv[j])]; };
-      auto build_batches = [&](int SB, BatchSet& bs) {
+      // kx_lanes: the set the Kt-record pass (per-task lane map) walks — balanced for its lanes, else for the G-block pass's
+      auto build_batches = [&](int SB, BatchSet& bs, bool kx_lanes) {
       auto& tasks = bs.tasks;
       auto& batches = bs.batches;
       auto& st_obs = bs.st_obs;
@@ -2688,7 +2689,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
                 if (n) items.push_back(int3{a, o0, n});
               }
               int* asg = bal_asg_all.data() + bal_off[cidx];
-              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, noff, asg, cap, cnt, ord, opn);
+              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, noff, kx_lanes, asg, cap, cnt, ord, opn);
             }
             for (int k = s_lo; k < s_hi; ++k) cs[s_bj[k]] = -1;
           }
@@ -2851,7 +2852,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       sch_part_blocks = 0;
       {
         BatchSet bs;
-        build_batches(SB, bs);
+        build_batches(SB, bs, kx_batch_size() == SB);
         npairs = bs.npairs;
         nsch_tasks = (int)bs.tasks.size();
         nstaged = (long long)bs.st_obs.size();
@@ -2871,7 +2872,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       nsch_tasks_kx = nsch_groups_kx = 0;
       if (kx_sb != SB && ba_fused && pd == 6 && ld == 3) {
         BatchSet bs;
-        build_batches(kx_sb, bs);
+        build_batches(kx_sb, bs, true);
         nsch_tasks_kx = (int)bs.tasks.size();
         nsch_groups_kx = (int)bs.groups.size();
         sch_groups_kx.upload(bs.groups.empty() ? std::vector<launch::SchurPartGroup>(1) : bs.groups, stream);

@@ -2232,9 +2232,11 @@ static void slot_groups(const long long* T, int noff, int* g) {
 // batch, among a rotating window of WIN batches with room, where its busiest slot stays lowest (ties: the emptier one) —
 // within batches of at most sb staged records. asg[k] = item k's batch; returns the batch count.
 static int balance_batches(const std::vector<int3>& items, const std::vector<std::pair<int, int>>& part, int sb, int sl,
-                           int noff, bool prop, int* asg, std::vector<int>& cap, std::vector<int>& cnt, std::vector<int>& ord,
+                           int noff, bool prop, bool local, int* asg, std::vector<int>& cap, std::vector<int>& cnt, std::vector<int>& ord,
                            std::vector<int>& opn) {
   constexpr int WIN = 8;  // a model of C4's rows: 8 candidates and all open batches balance alike, 4 worse
+  // local: +-6 batches (C5 Schur rows 0.80 -> 0.73 ms against the rotating window; +-4..16 alike, +-1 0.81)
+  constexpr int LOCAL_HW = 6;
   long long stt = 0;
   for (const int3& it : items) stt += 1 + it.z;
   // the slots' lane groups (prop: slot_groups, as the Kt-record pass's lane map will have them; else two pair streams per
@@ -2264,9 +2266,16 @@ static int balance_batches(const std::vector<int3>& items, const std::vector<std
       }
       if (v < bv || (v == bv && cap[b] < bc)) { bv = v; bc = cap[b]; best = b; }
     };
-    // candidates: a rotating window over the batches that still have room for the smallest observation
+    // candidates: local — the batches around the item's place in landmark order (neighbouring rows, which share
+    // landmarks, then stage them at about the same time: L2 hits); else a rotating window over the batches that still
+    // have room for the smallest observation
     const int no = (int)opn.size(), w = std::min(WIN, no);
-    for (int k = 0; k < w; ++k) consider(opn[(q + k) % no]);
+    if (local) {
+      const int nat = (int)((long long)ord[q] * nbt / std::max<size_t>(items.size(), 1));
+      for (int b = std::max(0, nat - LOCAL_HW); b <= std::min(nbt - 1, nat + LOCAL_HW); ++b) consider(b);
+    } else {
+      for (int k = 0; k < w; ++k) consider(opn[(q + k) % no]);
+    }
     if (best < 0)
       for (int k = 0; k < no; ++k) consider(opn[k]);
     if (best < 0) {  // no batch has room: a new one
@@ -2577,9 +2586,13 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       const char* ssk = getenv("G2OHIP_SCHUR_SKIP");  // dev A/B: 0 = every rank runs every row chunk and camera
       const bool sch_skip = dist_aligned && nranks > 1 && comm && !write_debug && !(dvr && atoi(dvr) == 0) &&
                             !(ssk && atoi(ssk) == 0);
-      // G2OHIP_SCHUR_BALANCE (dev A/B): 1 slot-balanced batches (build_batches), 0 batches in landmark order
+      // G2OHIP_SCHUR_BALANCE (dev A/B): 0 batches in landmark order; else slot-balanced batches (build_batches) whose
+      // candidates are the batches near the observation's landmark-order place or a rotating window over the open ones
       const char* sbal = getenv("G2OHIP_SCHUR_BALANCE");
       const bool sch_balance = !(sbal && atoi(sbal) == 0);
+      // local candidates for the Kt-record pass's batches (measured); the G-block pass keeps the rotating window (its
+      // measured default) unless 3 = local there too (dev A/B); 2 = rotating for both
+      const int sbal_mode = sbal ? atoi(sbal) : 1;
       const char* sst = getenv("G2OHIP_SCHUR_SPLIT_TASKS");
       const int split_target = sst ? atoi(sst) : (nranks > 1 && comm ? 2048 : 0);
       auto blk_owner = [&](int i, int j) { return al_bowner[std::min(al_bpinv[i], al_bpinv[j])]; };
@@ -2689,7 +2702,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
                 if (n) items.push_back(int3{a, o0, n});
               }
               int* asg = bal_asg_all.data() + bal_off[cidx];
-              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, noff, kx_lanes, asg, cap, cnt, ord, opn);
+              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, noff, kx_lanes, kx_lanes ? sbal_mode != 2 : sbal_mode == 3, asg, cap, cnt, ord, opn);
             }
             for (int k = s_lo; k < s_hi; ++k) cs[s_bj[k]] = -1;
           }

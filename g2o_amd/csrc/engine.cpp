@@ -2590,9 +2590,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
       // candidates are the batches near the observation's landmark-order place or a rotating window over the open ones
       const char* sbal = getenv("G2OHIP_SCHUR_BALANCE");
       const bool sch_balance = !(sbal && atoi(sbal) == 0);
-      // local candidates for the Kt-record pass's batches (measured); the G-block pass keeps the rotating window (its
-      // measured default) unless 3 = local there too (dev A/B); 2 = rotating for both
-      const int sbal_mode = sbal ? atoi(sbal) : 1;
+      const bool sch_bal_local = !(sbal && atoi(sbal) == 2);  // 2 = the rotating window
       const char* sst = getenv("G2OHIP_SCHUR_SPLIT_TASKS");
       const int split_target = sst ? atoi(sst) : (nranks > 1 && comm ? 2048 : 0);
       auto blk_owner = [&](int i, int j) { return al_bowner[std::min(al_bpinv[i], al_bpinv[j])]; };
@@ -2702,7 +2700,7 @@ int Engine::build_structure() {  // block_solver.hpp:102-256
                 if (n) items.push_back(int3{a, o0, n});
               }
               int* asg = bal_asg_all.data() + bal_off[cidx];
-              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, noff, kx_lanes, kx_lanes ? sbal_mode != 2 : sbal_mode == 3, asg, cap, cnt, ord, opn);
+              bal_nb_all[cidx] = balance_batches(items, part, SB, SL, noff, kx_lanes, sch_bal_local, asg, cap, cnt, ord, opn);
             }
             for (int k = s_lo; k < s_hi; ++k) cs[s_bj[k]] = -1;
           }

@@ -39,6 +39,25 @@ __device__ __forceinline__ void copy_out(double* __restrict__ dst, const double*
   if (lane == 0 && ((n - s) & 1)) dst[n - 1] = src[n - 1];
 }
 
+// copy_out with nontemporal 16-byte stores (no L2 / MALL allocation): streams that outgrow the caches
+__device__ __forceinline__ void copy_out_nt(double* __restrict__ dst, const double* src, int n, int lane) {
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  int s = 0;
+  if (reinterpret_cast<uintptr_t>(dst) & 15) {
+    if (lane == 0 && n > 0) __builtin_nontemporal_store(src[0], dst);
+    s = 1;
+  }
+  const int n2 = (n - s) >> 1;
+  dv2* d2 = reinterpret_cast<dv2*>(dst + s);
+  for (int i = lane; i < n2; i += 64) {
+    dv2 v;
+    v.x = src[s + 2 * i];
+    v.y = src[s + 2 * i + 1];
+    __builtin_nontemporal_store(v, d2 + i);
+  }
+  if (lane == 0 && ((n - s) & 1)) __builtin_nontemporal_store(src[n - 1], dst + n - 1);
+}
+
 // error, Jacobians and the (robust-weighted) information of one edge (base_binary_edge.hpp:104-135)
 template <class F, bool PC = false>
 __device__ __forceinline__ void edge_terms(const EdgeData& d, int e, double* err, double* A, double* B, double* Om,
@@ -244,7 +263,10 @@ __global__ void __launch_bounds__(256)
     }
     if (run) {
       wsync();
-      copy_out((slot0f ? off_slot : base) + od0, sw, nw * BS, lane);
+      if (KX && sp.kx == 2)
+        copy_out_nt((slot0f ? off_slot : base) + od0, sw, nw * BS, lane);
+      else
+        copy_out((slot0f ? off_slot : base) + od0, sw, nw * BS, lane);
     }
     wsync();
   };

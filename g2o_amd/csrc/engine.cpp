@@ -3096,6 +3096,13 @@ int Engine::build_system_split(double lambda, const double* lamp) {  // block_so
       sp.cl = dCl.get();
       sp.G = dG.get();
       sp.kx = fz_kx ? 1 : 0;
+      {  // Kt records that outgrow the caches are stored nontemporally (C5's 800 MB: linearize 0.458 -> 0.43 ms; C4's 80 MB
+         // stay cached for the camera pass, which NT stores slow 47 -> 53 us: profiles/r06_ab_lin_nts.log);
+         // G2OHIP_LIN_NTS (dev A/B): 0 never, 1 always
+        const char* nts = getenv("G2OHIP_LIN_NTS");
+        const int nt = nts ? atoi(nts) : (kx_records_cached((double)nHpl + n_kx_extra) ? 0 : 1);
+        if (fz_kx && nt == 1) sp.kx = 2;
+      }
       // the camera pass from the Kt records while they stay cache-resident (the pass gathers them in camera order; C4's
       // 80 MB: 52 -> 48 us), else re-linearising every observation from the per-landmark point, U and c (C5's 800 MB of
       // records: 0.42 -> 0.49 ms, where the per-landmark gathers are 96 MB; profiles/r05_ab_c5_dl_camkx.log).
